@@ -1,0 +1,197 @@
+"""Benchmark: Krylov iterations/s of the block-preconditioned GMRES hot path on MI355X.
+
+Workload (BASELINE.json metric "Krylov iters/sec + SpMV achieved HBM GB/s,
+3-field poroelastic 10M DoF"): the synthetic 3-field system of SURVEY.md 8(d)
+at 3-D N=59 (10,326,954 DoF, ~1.88 G nnz in A), generated in HBM; one step =
+one full outer solve from a zero guess exactly as the reference runs it
+(``Solver.solve``: right-preconditioned GMRES, rtol 1e-6, atol 1e-8, restart =
+maxit = 100, swelling-3d.py:64-66) with the 2-way block preconditioner
+(lib/Preconditioner.py:219-246) and inner PREONLY + BJACOBI(ILU(0)) blocks.
+
+value = whole-job Krylov iterations per second (sum over ranks of the outer
+iterations done in the timed steps / max-over-ranks wall time).  At N GPUs
+every rank solves its own N=59 system (weak scaling, "replicas" for round 1).
+
+roofline: the dominant kernel is the CSR SpMV with A (one per outer
+iteration).  achieved = algorithmic bytes per launch
+(12 nnz + 8 (n+1) + 8 n + 8 n: val + col + int64 row_ptr + x once + y once)
+divided by the mean SpMV duration measured with HIP events on the solver
+stream inside the timed solves; peak = 8000 GB/s (MI355X HBM3E).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "poroelasticity-linear-solvers_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "Krylov iters/sec + SpMV achieved HBM GB/s, 3-field poroelastic 10M DoF"
+HBM_PEAK_GBS = 8000.0
+SEED = 20261015
+DELTA = 0.05
+
+
+def solver_options(args):
+    params = {"solver type": "gmres", "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": args.maxit,
+              "pc type": "diagonal", "inner ksp type": "preonly", "inner pc type": args.inner,
+              "inner accel order": 0}
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right",
+          "s_ksp_type": "preonly", "s_pc_type": args.inner,
+          "fp_ksp_type": "preonly", "fp_pc_type": args.inner}
+    if args.inner == "bjacobi":
+        db["s_pc_bjacobi_blocks"] = str(args.blocks)
+        db["fp_pc_bjacobi_blocks"] = str(args.blocks)
+    return params, db
+
+
+def cpu_baseline(args, params, db):
+    """Oracle (CPU restatement) timed on host cores on a bounded sample."""
+    import numpy as np
+    from oracle import synthetic as S
+    from oracle.solver import OracleSolver
+    Ns = args.cpu_N
+    spec = S.SynthSpec(3, Ns, SEED, DELTA)
+    t0 = time.perf_counter()
+    A, P = S.matrix(spec, 0), S.matrix(spec, 1)
+    is_s, is_f, is_p = S.field_major_index_sets(spec)
+    p = dict(params)
+    p["solver maxiter"] = args.cpu_maxit
+    o = OracleSolver(A, P, None, is_s, is_f, is_p, p, db, [])
+    b = S.rhs(spec)
+    t_setup = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    o.solve(b)
+    dt = time.perf_counter() - t1
+    n_sample = spec.n
+    n_metric = S.SynthSpec(3, args.N).n if args.N != Ns else n_sample
+    rate = o.its / dt
+    return {"value": rate * n_sample / n_metric, "unit": "Krylov iters/s (scaled to the 10.33M-DoF system by DoF)",
+            "cores": 1, "kind": "port",
+            "sample": (f"oracle (numpy/scipy + C kernels, 1 thread) 2-way GMRES solve of the N={Ns} 3-D "
+                       f"system ({n_sample} DoF), {o.its} outer iterations in {dt:.1f}s "
+                       f"(setup {t_setup:.1f}s), maxit {args.cpu_maxit}; iters/s x {n_sample}/{n_metric}"),
+            "raw_iters_per_s": rate}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--N", type=int, default=59)
+    ap.add_argument("--inner", default="bjacobi", choices=["bjacobi", "ilu", "jacobi"])
+    ap.add_argument("--blocks", type=int, default=256)
+    ap.add_argument("--maxit", type=int, default=100)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-N", type=int, default=20)
+    ap.add_argument("--cpu-maxit", type=int, default=100)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    import lib._native as Nat
+    from lib.handle import Handle, params_to_options
+    Nat.check(Nat.lib().pls_set_device(local))
+
+    params, db = solver_options(args)
+    opts = dict(db)
+    opts.update(params_to_options(params))
+    t0 = time.perf_counter()
+    h = Handle.synthetic(3, args.N, SEED + rank, DELTA, opts)
+    h.setup()
+    h.create_solver()
+    t_setup = time.perf_counter() - t0
+    n, nnz = h.n, h.nnz_A
+    d_b = Nat.DeviceArray(n)
+    d_x = Nat.DeviceArray(n)
+    h.rhs_device(7, d_b.p)
+
+    for _ in range(args.warmup):
+        h.solve_device(d_b.p, d_x.p)
+    h.reset_timings()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t1 = time.perf_counter()
+    its = 0
+    reasons = []
+    for _ in range(args.steps):
+        r = h.solve_device(d_b.p, d_x.p)
+        its += r.its
+        reasons.append(r.reason)
+    dt = time.perf_counter() - t1
+    barrier()
+    tm = h.timings()
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        it_t = torch.tensor([float(its)], dtype=torch.float64)
+        dist.all_reduce(it_t, op=dist.ReduceOp.SUM)
+        its_all = float(it_t.item())
+    else:
+        its_all = float(its)
+
+    spmv_avg = tm["spmv_total"] / max(1, tm["spmv_calls"])
+    alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 8.0 * n + 8.0 * n
+    achieved = alg_bytes / spmv_avg / 1e9 if spmv_avg > 0 else 0.0
+    iso = h.bench_spmv(d_x.p, d_b.p, 10)
+    h.rhs_device(7, d_b.p)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": its_all / dt,
+            "unit": "Krylov iters/s (outer GMRES iterations on the 10.33M-DoF system, summed over ranks)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * dt / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded SPD 3-field block system, SURVEY.md 8(d); generated in HBM)",
+            "config": {
+                "workload": (f"swelling-3d-shaped 3-D N={args.N} ({n} DoF, nnz(A)={nnz}): outer GMRES right-PC "
+                             f"rtol 1e-6 atol 1e-8 restart=maxit={args.maxit}, 2-way block PC, inner preonly+"
+                             f"{args.inner}" + (f"(ILU(0), {args.blocks} blocks)" if args.inner == "bjacobi" else "")),
+                "dim": 3, "N": args.N, "dofs": n, "nnz_A": nnz,
+                "parallelism": f"replicas x{world}" if world > 1 else "single GPU",
+            },
+            "its_per_solve": its / args.steps,
+            "reasons": sorted(set(reasons)),
+            "setup_s": t_setup,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_spmv<64> (y = A x, outer MatMult)",
+                         "alg_bytes_per_launch": alg_bytes, "mean_launch_s": spmv_avg,
+                         "isolated_spmv_gbs": alg_bytes / iso / 1e9},
+            "timings_s": {k: v for k, v in tm.items()},
+        }
+        if not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(args, params, db)
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,162 @@
+/*
+ * pls.h -- C-ABI of the MI355X-native block-preconditioned Krylov solver
+ * ("pls" = poroelastic linear solver).  Plain pointers and sizes, no torch or
+ * PETSc types.  Every entry point returns 0 on success and a nonzero status on
+ * failure; pls_last_error() then returns a thread-local message (the Python
+ * facade raises RuntimeError with it).
+ *
+ * Which reference interface each entry point replaces (reference = the
+ * nabw/poroelasticity-linear-solvers tree):
+ *
+ *   pls_create          Preconditioner(index_map, A, P, P_diff, parameters,
+ *                       bcs_sub_pressure)      lib/Preconditioner.py:263-276
+ *                       + Solver(A, b, PC, parameters, index_map)
+ *                                               lib/Solver.py:54-62
+ *                       + IndexSet contract     lib/IndexSet.py:29-67
+ *   pls_setup           Preconditioner.get_pc() -> PreconditionerCC.setUp
+ *                                               lib/Preconditioner.py:120-139,282-291
+ *                       + Solver.create_solver  lib/Solver.py:64-103
+ *   pls_pc_apply        PreconditionerCC.apply(pc, x, y)
+ *                                               lib/Preconditioner.py:141-250
+ *   pls_solve           Solver.solve(b, x) -> KSPSolve / AAR.solve
+ *                                               lib/Solver.py:148-152, lib/AAR.py:46-128
+ *   pls_get_result      Solver.getIterationNumber / KSPGetConvergedReason /
+ *                       residual history        lib/Solver.py:145-146
+ *   pls_get_timings     PreconditionerCC.print_timings / Solver.print_timings
+ *                                               lib/Preconditioner.py:252-260, lib/Solver.py:154-155
+ *   pls_destroy         (object lifetime; PETSc XXXDestroy)
+ *
+ * Device-resident variants (inputs already in HBM, field-major order) exist
+ * for benchmarks and for the synthetic generator of SURVEY.md 8(d).
+ */
+#ifndef PLS_H
+#define PLS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PLS_ABI_VERSION 1
+
+/* Host CSR (local rows): row_ptr[nrows+1] int64, col[nnz] int32, val[nnz] f64.
+ * Columns inside a row must be sorted ascending (PETSc AIJ convention).       */
+typedef struct pls_csr {
+    int64_t nrows;
+    int64_t ncols;
+    const int64_t *row_ptr;
+    const int32_t *col;
+    const double *val;
+} pls_csr;
+
+typedef struct pls_handle pls_handle;
+
+/* Result of the last solve (KSPGetIterationNumber / KSPGetConvergedReason /
+ * residual history as KSPSetResidualHistory records it).                      */
+typedef struct pls_result {
+    int32_t its;          /* outer iterations                                   */
+    int32_t reason;       /* KSPConvergedReason value (AAR: 2 rtol, 3 atol, -3 its) */
+    double rnorm;         /* last residual norm the outer solver tested        */
+    int32_t pc_applies;   /* block-PC applications during the solve            */
+    int32_t history_len;  /* entries available through pls_get_history         */
+} pls_result;
+
+/* Accumulated timers in seconds (names of lib/Preconditioner.py:35-39 and
+ * lib/Solver.py:62), measured with HIP events on the solver stream.         */
+typedef struct pls_timings {
+    double pc_total;      /* t_total  */
+    double pc_solid;      /* t_solid  */
+    double pc_fluid;      /* t_fluid  */
+    double pc_press;      /* t_press  */
+    double pc_alloc;      /* t_alloc (field gathers/scatters; 0 in field-major layout) */
+    double solver_total;  /* Solver.t_total */
+    double spmv_total;    /* outer MatMult time */
+    int64_t spmv_calls;
+} pls_timings;
+
+/* Synthetic 3-field system; generated directly in HBM.     */
+typedef struct pls_synth_spec {
+    int32_t dim;          /* 2 or 3                                            */
+    int32_t N;            /* elements per side                                 */
+    uint64_t seed;
+    double delta;         /* diagonal shift                                    */
+} pls_synth_spec;
+
+int pls_abi_version(void);
+const char *pls_last_error(void);
+int pls_device_count(int *count);
+int pls_set_device(int device);
+
+/* Options: newline-separated "key value" (or "key") lines.  Keys prefixed
+ * "pls." are the reference's parameter dict entries ("pls.solver_type gmres",
+ * "pls.pc_type diagonal", "pls.inner_ksp_type preonly", ...); every other key
+ * is a PETSc options-database entry without its leading '-' ("s_pc_type ilu",
+ * "global_ksp_pc_side right", ...), resolved with setFromOptions precedence. */
+
+/* Build a solver from host CSR matrices in the caller's (e.g. dolfin
+ * interleaved) ordering plus the field index sets (sorted global indices of
+ * each field, lib/IndexSet.py:38-41).  Pdiff may be NULL unless pc type is a
+ * 3-way variant.  bcs_sub_p: positions inside the p sub-vector with pressure
+ * Dirichlet BCs (lib/Poromechanics.py:48-55).                               */
+int pls_create(const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff,
+               const int32_t *is_s, int64_t ns, const int32_t *is_f, int64_t nf,
+               const int32_t *is_p, int64_t np, const int32_t *bcs_sub_p, int64_t nbc,
+               const char *options, pls_handle **out);
+
+/* Build a solver whose A, P, P_diff, index sets and pressure BCs come from the
+ * seeded synthetic generator, directly on the device, field-major order.     */
+int pls_create_synthetic(const pls_synth_spec *spec, const char *options, pls_handle **out);
+
+int pls_setup(pls_handle *h);
+/* Set / override one option ("key", "value" or NULL for a flag).  Options of
+ * the outer solver ("pls.solver_*", "pls.aar_*", "global_*") may change until
+ * pls_create_solver (or the first solve); PC options until pls_setup.        */
+int pls_set_option(pls_handle *h, const char *key, const char *value);
+/* Solver.create_solver (lib/Solver.py:64-103): build the outer KSP / AAR.    */
+int pls_create_solver(pls_handle *h);
+int pls_destroy(pls_handle *h);
+
+/* Global size n and field sizes of a handle.                                 */
+int pls_get_sizes(pls_handle *h, int64_t *n, int64_t *ns, int64_t *nf, int64_t *np, int64_t *nnz_A);
+
+/* Host-vector entry points (caller's ordering, length n).                     */
+int pls_pc_apply(pls_handle *h, const double *x, double *y);
+int pls_solve(pls_handle *h, const double *b, double *x, pls_result *res);
+int pls_matmult(pls_handle *h, const double *x, double *y);
+
+/* Device-vector entry points: d_b / d_x are device pointers in the handle's
+ * internal field-major order (no host traffic, no permutation).             */
+int pls_solve_device(pls_handle *h, const double *d_b, double *d_x, pls_result *res);
+int pls_pc_apply_device(pls_handle *h, const double *d_x, double *d_y);
+int pls_matmult_device(pls_handle *h, const double *d_x, double *d_y);
+/* Synthetic right-hand side (field-major) written to a device vector.        */
+int pls_synthetic_rhs_device(pls_handle *h, uint64_t seed, double *d_b);
+/* Device buffer helpers (so hosts without a GPU runtime binding can drive it) */
+int pls_device_alloc(int64_t bytes, void **d_ptr);
+int pls_device_free(void *d_ptr);
+int pls_memcpy_h2d(void *d_dst, const void *h_src, int64_t bytes);
+int pls_memcpy_d2h(void *h_dst, const void *d_src, int64_t bytes);
+
+int pls_get_result(pls_handle *h, pls_result *res);
+int pls_get_history(pls_handle *h, double *hist, int32_t cap);
+int pls_get_timings(pls_handle *h, pls_timings *t);
+int pls_reset_timings(pls_handle *h);
+
+/* Export a device matrix of the handle to host CSR (tests / parity):
+ * which: 0 = A, 1 = P, 2 = P_diff (field-major order).  Call once with
+ * col == NULL to get nrows/nnz, then with buffers sized accordingly.        */
+int pls_export_matrix(pls_handle *h, int which, int64_t *nrows, int64_t *nnz,
+                      int64_t *row_ptr, int32_t *col, double *val);
+/* Export the field-major permutation: perm[internal] = caller index.         */
+int pls_get_permutation(pls_handle *h, int64_t *perm);
+
+/* Kernel micro-entry points used by bench.py's roofline leg (device ptrs):
+ * y = A x on the handle's A, repeated `reps` times; returns the mean device
+ * time per launch in seconds measured with HIP events on the solver stream. */
+int pls_bench_spmv(pls_handle *h, const double *d_x, double *d_y, int32_t reps, double *sec_per_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLS_H */

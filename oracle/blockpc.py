@@ -1,0 +1,112 @@
+"""Block preconditioner restatement (TEST INFRASTRUCTURE ONLY, see oracle/__init__.py).
+
+Follows the reference ``lib/Preconditioner.py``:
+
+* sub-blocks of **P** by ``createSubMatrix(isrow, iscol)`` (rows in isrow order,
+  columns in iscol order) -- ``allocate_submatrices`` 60-75;
+* inner KSPs with prefixes ``s_ f_ p_ diff_ fp_``, ``setType(inner ksp type)``,
+  ``pc.setType(inner pc type)`` then ``setFromOptions`` (options win), inner
+  tolerances left at PETSc defaults (the stored inner rtol/atol/maxiter are
+  never applied: ``__init__`` 22-27 vs ``setup_elliptic_solver`` 94-100);
+  ``fp_`` is an elliptic solver when inner pc type is ``lu``, otherwise GMRES +
+  fieldsplit (``setUp`` 134-138, ``setup_fieldsplit`` 102-118);
+* ``apply`` 141-250:
+  - 2-way: y_s = K_s^-1 x_s ; y_fp = K_fp^-1 (x_fp - P_fp,s y_s)       (221-234)
+  - 3-way: FS sweep p -> f -> s and DIFF sweep (pressure-BC rows of x_p zeroed,
+    K_p,diff from P_diff), y = w1 y_FS + w2 y_DIFF with w1 = 1, w2 = 0.1
+    (150-218; the temporaries are copies: x is never written back);
+  - inner Anderson mixing of y when ``inner accel order > 0`` (248-249).
+* the factory's pc-type validation and ``flag_3_way`` (263-291).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import petsc
+from .aar import AndersonAcceleration
+from .options import get as opt
+
+PC_TYPES = ("undrained", "undrained 3-way", "diagonal", "diagonal 3-way", "diagonal 3-way-II", "lu")
+
+
+def submatrix(M, isrow, iscol):
+    return M[np.asarray(isrow)][:, np.asarray(iscol)].tocsr()
+
+
+class BlockPC:
+    def __init__(self, P, P_diff, index_sets, dims, flag_3_way, db,
+                 inner_ksp_type="gmres", inner_pc_type="lu", w1=1.0, w2=0.1,
+                 accel_order=0, bcs_sub_pressure=()):
+        self.flag_3_way = flag_3_way
+        self.w1, self.w2 = w1, w2
+        self.ns, self.nf, self.np = dims
+        self.is_s, self.is_f, self.is_p, self.is_fp = [np.asarray(i, dtype=np.int64) for i in index_sets]
+        self.bcs = np.asarray(bcs_sub_pressure, dtype=np.int64)
+        self.anderson = AndersonAcceleration(accel_order)
+        Ms_s = submatrix(P, self.is_s, self.is_s)
+        self.ksp_s = petsc.ksp_from_options("s_", db, Ms_s, Ms_s, inner_ksp_type, inner_pc_type)
+        if flag_3_way:
+            self.Ms_f = submatrix(P, self.is_s, self.is_f)
+            self.Ms_p = submatrix(P, self.is_s, self.is_p)
+            self.Mf_p = submatrix(P, self.is_f, self.is_p)
+            Mf_f = submatrix(P, self.is_f, self.is_f)
+            Mp_p = submatrix(P, self.is_p, self.is_p)
+            Mp_diff = submatrix(P_diff, self.is_p, self.is_p)
+            self.ksp_f = petsc.ksp_from_options("f_", db, Mf_f, Mf_f, inner_ksp_type, inner_pc_type)
+            self.ksp_p = petsc.ksp_from_options("p_", db, Mp_p, Mp_p, inner_ksp_type, inner_pc_type)
+            self.ksp_p_diff = petsc.ksp_from_options("diff_", db, Mp_diff, Mp_diff,
+                                                     inner_ksp_type, inner_pc_type)
+        else:
+            self.Mfp_s = submatrix(P, self.is_fp, self.is_s)
+            Mfp_fp = submatrix(P, self.is_fp, self.is_fp)
+            if inner_pc_type == "lu":
+                self.ksp_fp = petsc.ksp_from_options("fp_", db, Mfp_fp, Mfp_fp, inner_ksp_type, "lu")
+            else:
+                # setup_fieldsplit: GMRES + fieldsplit unless the options override the pc type
+                ptype = opt(db, "fp_", "pc_type", "fieldsplit")
+                if ptype == "fieldsplit":
+                    raise NotImplementedError("fp_ fieldsplit (Schur) is not restated yet (SURVEY 8f rank 1)")
+                self.ksp_fp = petsc.ksp_from_options("fp_", db, Mfp_fp, Mfp_fp, "gmres", ptype)
+
+    def apply(self, x):
+        x = np.asarray(x, dtype=np.float64)
+        y = np.zeros_like(x)
+        x_s = x[self.is_s]
+        if self.flag_3_way:
+            x_f = x[self.is_f]
+            x_p = x[self.is_p]
+            y_p = self.ksp_p.solve(x_p)
+            x_pd = x_p.copy()
+            x_pd[self.bcs] = 0.0
+            y_pd = self.ksp_p_diff.solve(x_pd)
+            t_f = x_f - self.Mf_p @ y_p
+            y_f = self.ksp_f.solve(t_f)
+            t_f = x_f - self.Mf_p @ y_pd
+            y_fd = self.ksp_f.solve(t_f)
+            t_s = x_s - (self.Ms_f @ y_f + self.Ms_p @ y_p)
+            y_s = self.ksp_s.solve(t_s)
+            t_s = x_s - (self.Ms_f @ y_fd + self.Ms_p @ y_pd)
+            y_sd = self.ksp_s.solve(t_s)
+            y[self.is_p] = self.w1 * y_p + self.w2 * y_pd
+            y[self.is_f] = self.w1 * y_f + self.w2 * y_fd
+            y[self.is_s] = self.w1 * y_s + self.w2 * y_sd
+        else:
+            y_s = self.ksp_s.solve(x_s)
+            t = x[self.is_fp] - self.Mfp_s @ y_s
+            y_fp = self.ksp_fp.solve(t)
+            y[self.is_s] = y_s
+            y[self.is_fp] = y_fp
+        if self.anderson.order > 0:
+            y = self.anderson.get_next_vector(y)
+        return y
+
+
+def make_block_pc(P, P_diff, index_sets, dims, parameters, db, bcs_sub_pressure):
+    """Preconditioner(...).get_pc() restated (lib/Preconditioner.py:263-291)."""
+    pc_type = parameters["pc type"]
+    if pc_type not in PC_TYPES:
+        raise SystemExit("pc type must be one of lu, undrained, diagonal, diagonal 3-way, diagonal 3-way-II.")
+    flag_3_way = pc_type in ("diagonal 3-way", "undrained 3-way")
+    return BlockPC(P, P_diff, index_sets, dims, flag_3_way, db,
+                   parameters["inner ksp type"], parameters["inner pc type"], 1.0, 0.1,
+                   parameters["inner accel order"], bcs_sub_pressure)

@@ -1,0 +1,960 @@
+// capi.cpp -- the handle, the block preconditioner, AAR / Anderson
+// acceleration and the extern "C" entry points declared in include/pls.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <numeric>
+
+#include "../../include/pls.h"
+#include "runtime.hpp"
+
+namespace pls {
+
+static thread_local std::string g_last_error;
+
+// ===================================================== synthetic (host) ===
+// Offsets per forward block (SURVEY.md 8(d) spec; same definition as the CPU
+// oracle so both build the identical matrix).
+static inline uint64_t mix64h(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static inline uint64_t hash3h(uint64_t s, uint64_t a, uint64_t b) { return mix64h(mix64h(mix64h(s) ^ a) ^ b); }
+
+struct SynthHost {
+    int dim = 3, N = 1;
+    uint64_t seed = 0;
+    double delta = 0.05;
+    int64_t n[3] = {0, 0, 0}, off[3] = {0, 0, 0}, W[3] = {0, 0, 0};
+    int cnt[6] = {0};
+    std::vector<int32_t> offs[6];
+    void init(const pls_synth_spec &s) {
+        dim = s.dim;
+        N = s.N;
+        seed = s.seed;
+        delta = s.delta;
+        if (N < 1 || (dim != 2 && dim != 3)) throw Error("synthetic spec: dim must be 2 or 3 and N >= 1");
+        const int64_t q = 2 * (int64_t)N + 1, v = (int64_t)N + 1;
+        if (dim == 3) {
+            n[0] = n[1] = 3 * q * q * q;
+            n[2] = v * v * v;
+            W[0] = W[1] = 6 * q * q;
+            W[2] = v * v + v + 1;
+            const int c[6] = {85, 85, 8, 85, 8, 15};
+            std::copy(c, c + 6, cnt);
+        } else {
+            n[0] = n[1] = 2 * q * q;
+            n[2] = v * v;
+            W[0] = W[1] = 4 * q;
+            W[2] = v + 1;
+            const int c[6] = {23, 23, 5, 23, 5, 7};
+            std::copy(c, c + 6, cnt);
+        }
+        off[0] = 0;
+        off[1] = n[0];
+        off[2] = n[0] + n[1];
+        if (n[0] + n[1] + n[2] >= (int64_t)INT32_MAX) throw Error("synthetic system too large for int32 columns");
+        static const int colf[6] = {0, 1, 2, 1, 2, 2};
+        for (int b = 0; b < 6; ++b) {
+            const bool sym = (b == 0 || b == 1 || b == 3 || b == 5);
+            const int want = cnt[b];
+            const int half = sym ? want / 2 : want;
+            const int64_t Wb = W[colf[b]];
+            const uint64_t range = sym ? (uint64_t)Wb : (uint64_t)(2 * Wb + 1);
+            if ((uint64_t)half > range) throw Error("synthetic spec: band too narrow for N");
+            uint64_t st = hash3h(seed ^ 0x0FF5E7ULL, (uint64_t)b, 0x51ULL);
+            std::vector<int32_t> tmp;
+            while ((int)tmp.size() < half) {
+                st = mix64h(st);
+                const int64_t d = sym ? (int64_t)(1 + st % range) : (int64_t)(st % range) - Wb;
+                if (std::find(tmp.begin(), tmp.end(), (int32_t)d) == tmp.end()) tmp.push_back((int32_t)d);
+            }
+            offs[b].clear();
+            if (sym) {
+                for (int32_t d : tmp) { offs[b].push_back(d); offs[b].push_back(-d); }
+                offs[b].push_back(0);
+            } else {
+                offs[b] = tmp;
+            }
+            std::sort(offs[b].begin(), offs[b].end());
+        }
+    }
+    bool is_bc(int64_t ip) const { return (hash3h(seed ^ 0x00BC00ULL, (uint64_t)ip, 7ULL) & 15ULL) == 0ULL; }
+};
+
+// ============================================================ Anderson ===
+// Least squares min ||f + F a|| for the Anderson steps (reference lib/AAR.py:
+// 102-105 and lib/AndersonAcceleration.py:62-65 use numpy Householder QR).
+// Here: Cholesky-QR2 of [F | f] from two fused device Gram passes; the top
+// block of the last R column is Q_F^T f, so a = R_FF^{-1} (-Q_F^T f).
+struct AndersonLS {
+    DBuf<const double *> dptr;
+    DBuf<double> dR;     // Rinv column-major
+    DBuf<double> dG;     // packed gram
+    std::vector<double> solve(const std::vector<const double *> &cols, const double *f, int64_t n, Ctx &c) {
+        const int L = (int)cols.size();
+        const int m = L + 1;
+        if (m > 16) throw Error("Anderson order > 15 not supported");
+        if (dptr.n < 16) { dptr.alloc(16); dR.alloc(256); dG.alloc(256); }
+        std::vector<const double *> hp(cols);
+        hp.push_back(f);
+        HIPCHK(hipMemcpyAsync((void *)dptr.p, hp.data(), sizeof(double *) * m, hipMemcpyHostToDevice, c.st));
+        auto gram = [&](const double *rinv_dev) {
+            launch_gram(n, m, dptr.p, rinv_dev, c.partial.p, dG.p, c.st);
+            const int np = m * (m + 1) / 2;
+            HIPCHK(hipMemcpyAsync(c.hscal, dG.p, sizeof(double) * np, hipMemcpyDeviceToHost, c.st));
+            c.sync();
+            std::vector<double> G(m * m, 0.0);
+            int t = 0;
+            for (int r = 0; r < m; ++r)
+                for (int cc = r; cc < m; ++cc, ++t) G[r * m + cc] = G[cc * m + r] = c.hscal[t];
+            return G;
+        };
+        auto chol = [&](const std::vector<double> &G, std::vector<double> &R) {  // G = R^T R, R upper (row-major)
+            R.assign(m * m, 0.0);
+            for (int j = 0; j < m; ++j) {
+                double s = G[j * m + j];
+                for (int k = 0; k < j; ++k) s -= R[k * m + j] * R[k * m + j];
+                if (!(s > 0.0)) s = 0.0;
+                R[j * m + j] = std::sqrt(s);
+                for (int i = j + 1; i < m; ++i) {
+                    double t = G[j * m + i];
+                    for (int k = 0; k < j; ++k) t -= R[k * m + j] * R[k * m + i];
+                    R[j * m + i] = (R[j * m + j] > 0.0) ? t / R[j * m + j] : 0.0;
+                }
+            }
+        };
+        auto inv_upper = [&](const std::vector<double> &R) {  // returns Rinv column-major
+            std::vector<double> X(m * m, 0.0);  // row-major inverse
+            for (int j = 0; j < m; ++j) {
+                X[j * m + j] = (R[j * m + j] != 0.0) ? 1.0 / R[j * m + j] : 0.0;
+                for (int i = j - 1; i >= 0; --i) {
+                    double s = 0.0;
+                    for (int k = i + 1; k <= j; ++k) s += R[i * m + k] * X[k * m + j];
+                    X[i * m + j] = (R[i * m + i] != 0.0) ? -s / R[i * m + i] : 0.0;
+                }
+            }
+            std::vector<double> cm(m * m);
+            for (int r = 0; r < m; ++r)
+                for (int cc = 0; cc < m; ++cc) cm[cc * m + r] = X[r * m + cc];
+            return cm;
+        };
+        std::vector<double> R1, R2;
+        chol(gram(nullptr), R1);
+        std::vector<double> R1inv = inv_upper(R1);
+        HIPCHK(hipMemcpyAsync(dR.p, R1inv.data(), sizeof(double) * m * m, hipMemcpyHostToDevice, c.st));
+        chol(gram(dR.p), R2);
+        // R = R2 R1
+        std::vector<double> R(m * m, 0.0);
+        for (int i = 0; i < m; ++i)
+            for (int j = i; j < m; ++j) {
+                double s = 0.0;
+                for (int k = i; k <= j; ++k) s += R2[i * m + k] * R1[k * m + j];
+                R[i * m + j] = s;
+            }
+        // a = R_FF^{-1} (-r_Ff)
+        std::vector<double> a(L, 0.0);
+        for (int i = L - 1; i >= 0; --i) {
+            double s = -R[i * m + L];
+            for (int k = i + 1; k < L; ++k) s -= R[i * m + k] * a[k];
+            if (R[i * m + i] == 0.0) throw Error("Anderson least squares: singular R (numpy would raise LinAlgError)");
+            a[i] = s / R[i * m + i];
+        }
+        return a;
+    }
+};
+
+// y = y + beta * f + sum_{i<mk} alpha_i (X_i + beta F_i)   (AAR.py:109-111)
+__global__ void k_anderson_update(int64_t n, int mk, const double *const *X, const double *const *F,
+                                  const double *alpha, double beta, const double *f, double *y) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        double v = y[e] + beta * f[e];
+        for (int i = 0; i < mk; ++i) v = v + alpha[i] * (X[i][e] + beta * F[i][e]);
+        y[e] = v;
+    }
+}
+
+struct RingVecs {
+    DBuf<double> store;
+    int cap = 0;
+    int64_t n = 0;
+    std::deque<int> live;
+    std::vector<int> free_;
+    void init(int capacity, int64_t n_) {
+        cap = capacity;
+        n = n_;
+        store.alloc((size_t)std::max(cap, 1) * std::max<int64_t>(n, 1));
+        live.clear();
+        free_.clear();
+        for (int i = cap - 1; i >= 0; --i) free_.push_back(i);
+    }
+    double *slot(int s) const { return store.p + (int64_t)s * n; }
+    // append a copy of v; pop the oldest when more than `keep` remain
+    void append(const double *v, int keep, Ctx &c) {
+        if (free_.empty()) { free_.push_back(live.front()); live.pop_front(); }
+        int s = free_.back();
+        free_.pop_back();
+        launch_copy(n, v, slot(s), c.st);
+        live.push_back(s);
+        while ((int)live.size() > keep) { free_.push_back(live.front()); live.pop_front(); }
+    }
+    int size() const { return (int)live.size(); }
+    const double *at(int i) const { return slot(live[i]); }
+};
+
+struct AndersonMixer {  // lib/AndersonAcceleration.py:19-78
+    int order = 0;
+    int64_t k = 0;
+    int64_t n = 0;
+    DBuf<double> xk, fk, dxk, dfk;
+    RingVecs F, X;
+    AndersonLS ls;
+    DBuf<const double *> pX, pF;
+    DBuf<double> dalpha;
+    void init(int order_, int64_t n_) {
+        order = order_;
+        n = n_;
+        if (order <= 0) return;
+        xk.alloc(n); fk.alloc(n); dxk.alloc(n); dfk.alloc(n);
+        F.init(order + 1, n);
+        X.init(order + 1, n);
+        pX.alloc(16); pF.alloc(16); dalpha.alloc(16);
+    }
+    void next(double *gk, Ctx &c) {
+        if (k == 0) {
+            launch_set(n, 0.0, xk.p, c.st);
+            launch_set(n, 0.0, fk.p, c.st);
+        }
+        launch_copy(n, fk.p, dfk.p, c.st);
+        launch_copy(n, xk.p, dxk.p, c.st);
+        launch_waxpby(n, 1.0, gk, -1.0, xk.p, fk.p, c.st);  // fk = gk - xk
+        const int64_t mk = std::min<int64_t>(k, order);
+        if (mk > 0) {
+            launch_waxpby(n, 1.0, fk.p, -1.0, dfk.p, dfk.p, c.st);  // dfk = fk - dfk
+            if (c.norm2(n, dfk.p) < 1e-12) {
+                k -= 1;
+                launch_copy(n, gk, xk.p, c.st);
+            } else {
+                F.append(dfk.p, order, c);
+                std::vector<const double *> cols;
+                for (int i = 0; i < F.size(); ++i) cols.push_back(F.at(i));
+                std::vector<double> alpha = ls.solve(cols, fk.p, n, c);
+                if ((int64_t)X.size() < mk || (int64_t)F.size() < mk)
+                    throw Error("AndersonAcceleration: history shorter than mk (reference raises IndexError)");
+                std::vector<const double *> hx, hf;
+                for (int64_t i = 0; i < mk; ++i) { hx.push_back(X.at((int)i)); hf.push_back(F.at((int)i)); }
+                HIPCHK(hipMemcpyAsync((void *)pX.p, hx.data(), sizeof(double *) * mk, hipMemcpyHostToDevice, c.st));
+                HIPCHK(hipMemcpyAsync((void *)pF.p, hf.data(), sizeof(double *) * mk, hipMemcpyHostToDevice, c.st));
+                HIPCHK(hipMemcpyAsync(dalpha.p, alpha.data(), sizeof(double) * mk, hipMemcpyHostToDevice, c.st));
+                k_anderson_update<<<2048, 256, 0, c.st>>>(n, (int)mk, pX.p, pF.p, dalpha.p, 1.0, fk.p, xk.p);
+                c.sync();
+            }
+        } else {
+            launch_copy(n, gk, xk.p, c.st);
+        }
+        launch_waxpby(n, 1.0, xk.p, -1.0, dxk.p, dxk.p, c.st);  // dxk = xk - dxk
+        X.append(dxk.p, order, c);
+        k += 1;
+        launch_copy(n, xk.p, gk, c.st);
+    }
+};
+
+// ====================================================== block PC (apply) ===
+struct Handle;
+struct BlockPC : PC {
+    Handle *h = nullptr;
+    void apply(const double *x, double *y, Ctx &c) override;
+};
+
+// ================================================================ handle ===
+static void validate_pc_type(const Options &o) {
+    std::string pt = o.str("pls.pc_type", "diagonal");
+    std::replace(pt.begin(), pt.end(), '_', ' ');
+    static const char *ok[] = {"undrained", "undrained 3-way", "diagonal", "diagonal 3-way", "diagonal 3-way-II", "lu"};
+    for (auto s : ok)
+        if (pt == s) return;
+    throw Error("pc type must be one of lu, undrained, diagonal, diagonal 3-way, diagonal 3-way-II.");
+}
+
+struct Handle {
+    Ctx ctx;
+    Options opt;
+    Timers timers;
+    int64_t n = 0, ns = 0, nf = 0, np = 0;
+    bool three_way = false, setup_done = false, solver_ready = false, keep = true;
+    std::string pc_type, solver_type, inner_ksp, inner_pc;
+    std::vector<int64_t> perm;   // internal -> caller
+    DBuf<int64_t> dperm;
+    DevCSR A, P, Pd;
+    bool have_Pd = false;
+    std::vector<int32_t> bcs;
+    DBuf<int32_t> dbcs;
+    // sub-blocks (field-major)
+    DevCSR Ks, Kf, Kp, Kpd, Kfp, Mfp_s, Ms_fp, Mf_p;
+    std::unique_ptr<KSP> ksp_s, ksp_f, ksp_p, ksp_pd, ksp_fp, outer;
+    BlockPC bpc;
+    AndersonMixer mixer;
+    // AAR state (lib/AAR.py)
+    struct {
+        int order = 10, p = 5;
+        double omega = 1.0, beta = 1.0, atol = 1e-8, rtol = 1e-6;
+        int64_t maxiter = 500;
+        bool monitor = false;
+        RingVecs F, X;
+        AndersonLS ls;
+        DBuf<double> xk, fk, dxk, dfk, tmp;
+        DBuf<const double *> pX, pF;
+        DBuf<double> dalpha;
+        bool init = false;
+    } aar;
+    // work
+    DBuf<double> t_fp, t_s, t_f, xpd, yfpd, ysd, vin, vout;
+    // result
+    pls_result res{};
+    std::vector<double> history;
+    int pc_applies = 0;
+    std::unique_ptr<MatOp> Aop;
+
+    void parse_params() {
+        pc_type = opt.str("pls.pc_type", "diagonal");
+        static const char *ok[] = {"undrained", "undrained 3-way", "diagonal", "diagonal 3-way", "diagonal 3-way-II",
+                                   "lu"};
+        // values with spaces are passed with '_' or as the literal tail
+        std::string pt = pc_type;
+        std::replace(pt.begin(), pt.end(), '_', ' ');
+        pc_type = pt;
+        bool good = false;
+        for (auto s : ok) good = good || (pc_type == s);
+        if (!good) throw Error("pc type must be one of lu, undrained, diagonal, diagonal 3-way, diagonal 3-way-II.");
+        three_way = (pc_type == "diagonal 3-way" || pc_type == "undrained 3-way");
+        solver_type = opt.str("pls.solver_type", "gmres");
+        inner_ksp = opt.str("pls.inner_ksp_type", "gmres");
+        inner_pc = opt.str("pls.inner_pc_type", "hypre");
+        timers.enabled = opt.flag("pls.timers", true);
+    }
+};
+
+void BlockPC::apply(const double *x, double *y, Ctx &c) {
+    Handle &H = *h;
+    Timers &T = H.timers;
+    T.begin(T_PC_TOTAL);
+    const int64_t ns = H.ns, nf = H.nf, np = H.np;
+    if (!H.three_way) {
+        T.begin(T_PC_SOLID);
+        H.ksp_s->solve(x, y, c);
+        T.end(T_PC_SOLID);
+        T.begin(T_PC_FLUID);
+        // t = x_fp - P_fp,s y_s   (Preconditioner.py:232-233, fused)
+        spmv(H.Mfp_s, y, H.t_fp.p, c, -1.0, 1.0, x + ns);
+        H.ksp_fp->solve(H.t_fp.p, y + ns, c);
+        T.end(T_PC_FLUID);
+    } else {
+        const double *xs = x, *xf = x + ns, *xp = x + ns + nf;
+        double *ys = y, *yf = y + ns, *yp = y + ns + nf;
+        double *yfd = H.yfpd.p, *ypd = H.yfpd.p + nf;
+        T.begin(T_PC_PRESS);
+        H.ksp_p->solve(xp, yp, c);                               // :170
+        launch_copy(np, xp, H.xpd.p, c.st);                      // :172-173 BC rows of x_p zeroed
+        launch_zero_entries((int64_t)H.bcs.size(), H.dbcs.p, H.xpd.p, c.st);
+        H.ksp_pd->solve(H.xpd.p, ypd, c);                        // :174
+        T.end(T_PC_PRESS);
+        T.begin(T_PC_FLUID);
+        spmv(H.Mf_p, yp, H.t_f.p, c, -1.0, 1.0, xf);             // :180-181
+        H.ksp_f->solve(H.t_f.p, yf, c);                          // :182
+        spmv(H.Mf_p, ypd, H.t_f.p, c, -1.0, 1.0, xf);            // :184-185
+        H.ksp_f->solve(H.t_f.p, yfd, c);                         // :186
+        T.end(T_PC_FLUID);
+        T.begin(T_PC_SOLID);
+        spmv(H.Ms_fp, yf, H.t_s.p, c, -1.0, 1.0, xs);            // :192-195 (y_f, y_p contiguous)
+        H.ksp_s->solve(H.t_s.p, ys, c);                          // :196
+        spmv(H.Ms_fp, yfd, H.t_s.p, c, -1.0, 1.0, xs);           // :198-201
+        H.ksp_s->solve(H.t_s.p, H.ysd.p, c);                     // :202
+        T.end(T_PC_SOLID);
+        // y = w1 y_FS + w2 y_DIFF (:207-212)
+        launch_axpby(ns, 0.1, H.ysd.p, 1.0, ys, c.st);
+        launch_axpby(nf + np, 0.1, yfd, 1.0, yf, c.st);
+    }
+    if (H.mixer.order > 0) H.mixer.next(y, c);                 // :248-249
+    T.end(T_PC_TOTAL);
+    H.pc_applies++;
+}
+
+// ------------------------------------------------------------ setup path ---
+static void permute_host(const pls_csr *M, const std::vector<int64_t> &perm, const std::vector<int64_t> &inv,
+                         std::vector<int64_t> &rp, std::vector<int32_t> &ci, std::vector<double> &v) {
+    const int64_t n = (int64_t)perm.size();
+    rp.assign(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i) rp[i + 1] = rp[i] + (M->row_ptr[perm[i] + 1] - M->row_ptr[perm[i]]);
+    ci.resize(rp[n]);
+    v.resize(rp[n]);
+    std::vector<std::pair<int32_t, double>> row;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t o = perm[i];
+        row.clear();
+        for (int64_t k = M->row_ptr[o]; k < M->row_ptr[o + 1]; ++k) {
+            const int32_t cc = M->col[k];
+            if (cc < 0 || cc >= n) throw Error("column index out of range");
+            row.emplace_back((int32_t)inv[cc], M->val[k]);
+        }
+        std::sort(row.begin(), row.end(), [](auto &a, auto &b) { return a.first < b.first; });
+        for (size_t t = 0; t < row.size(); ++t) {
+            ci[rp[i] + t] = row[t].first;
+            v[rp[i] + t] = row[t].second;
+        }
+    }
+}
+
+static void upload_permuted(const pls_csr *M, Handle &H, const std::vector<int64_t> &inv, DevCSR &out) {
+    if (M->nrows != H.n || M->ncols != H.n) throw Error("matrix must be n x n with n = ns + nf + np");
+    std::vector<int64_t> rp;
+    std::vector<int32_t> ci;
+    std::vector<double> v;
+    permute_host(M, H.perm, inv, rp, ci, v);
+    upload_csr(out, H.n, H.n, rp.data(), ci.data(), v.data(), H.ctx);
+}
+
+static void alloc_work(Handle &H) {
+    H.t_fp.alloc(std::max<int64_t>(H.nf + H.np, 1));
+    H.t_s.alloc(std::max<int64_t>(H.ns, 1));
+    H.t_f.alloc(std::max<int64_t>(H.nf, 1));
+    H.xpd.alloc(std::max<int64_t>(H.np, 1));
+    H.yfpd.alloc(std::max<int64_t>(H.nf + H.np, 1));
+    H.ysd.alloc(std::max<int64_t>(H.ns, 1));
+    H.vin.alloc(std::max<int64_t>(H.n, 1));
+    H.vout.alloc(std::max<int64_t>(H.n, 1));
+}
+
+static void do_setup(Handle &H) {
+    if (H.setup_done) return;
+    Ctx &c = H.ctx;
+    const int64_t ns = H.ns, nf = H.nf, n = H.n;
+    WindowSpec w{};
+    w.mode = 0;
+    auto ext = [&](const DevCSR &M, int64_t r0, int64_t r1, int64_t c0, int64_t c1, DevCSR &dst) {
+        WindowSpec ww{};
+        ww.mode = 0;
+        ww.c0 = c0;
+        ww.c1 = c1;
+        extract_csr(M, r0, r1, ww, c0, c1 - c0, dst, c);
+    };
+    (void)w;
+    // lib/Preconditioner.py:60-75 allocate_submatrices (field-major: contiguous ranges)
+    ext(H.P, 0, ns, 0, ns, H.Ks);
+    if (!H.three_way) {
+        ext(H.P, ns, n, 0, ns, H.Mfp_s);
+        ext(H.P, ns, n, ns, n, H.Kfp);
+    } else {
+        if (!H.have_Pd) throw Error("3-way preconditioner needs P_diff");
+        ext(H.P, ns, ns + nf, ns, ns + nf, H.Kf);
+        ext(H.P, ns + nf, n, ns + nf, n, H.Kp);
+        ext(H.Pd, ns + nf, n, ns + nf, n, H.Kpd);
+        ext(H.P, 0, ns, ns, n, H.Ms_fp);
+        ext(H.P, ns, ns + nf, ns + nf, n, H.Mf_p);
+    }
+    // inner solvers (setup_elliptic_solver / setup_fieldsplit; options win)
+    const Options &o = H.opt;
+    H.ksp_s = make_ksp("s_", o, &H.Ks, &H.Ks, H.inner_ksp, H.inner_pc, c);
+    if (H.three_way) {
+        H.ksp_f = make_ksp("f_", o, &H.Kf, &H.Kf, H.inner_ksp, H.inner_pc, c);
+        H.ksp_p = make_ksp("p_", o, &H.Kp, &H.Kp, H.inner_ksp, H.inner_pc, c);
+        H.ksp_pd = make_ksp("diff_", o, &H.Kpd, &H.Kpd, H.inner_ksp, H.inner_pc, c);
+    } else {
+        if (H.inner_pc == "lu") {
+            H.ksp_fp = make_ksp("fp_", o, &H.Kfp, &H.Kfp, H.inner_ksp, "lu", c);
+        } else {
+            const std::string pt = o.str("fp_pc_type", "fieldsplit");
+            if (pt == "fieldsplit")
+                throw Error("fp_ fieldsplit (Schur) preconditioner is not available yet; set fp_pc_type");
+            H.ksp_fp = make_ksp("fp_", o, &H.Kfp, &H.Kfp, "gmres", pt, c);
+        }
+    }
+    H.mixer.init((int)o.integer("pls.inner_accel_order", 0), n);
+    H.bpc.h = &H;
+    H.bpc.type = "python";
+    H.bpc.n = n;
+    alloc_work(H);
+    if (!H.keep) {
+        H.P = DevCSR();
+        H.Pd = DevCSR();
+    }
+    c.sync();
+    H.setup_done = true;
+}
+
+
+// lib/Solver.py:64-103 create_solver (after the PC exists, as in Poromechanics.py:62-67)
+static void do_setup_solver(Handle &H) {
+    if (H.solver_ready) return;
+    Ctx &c = H.ctx;
+    const Options &o = H.opt;
+    const int64_t n = H.n;
+    H.solver_type = o.str("pls.solver_type", "gmres");
+    const double atol = o.num("pls.solver_atol", 1e-8), rtol = o.num("pls.solver_rtol", 1e-6);
+    const int64_t maxiter = o.integer("pls.solver_maxiter", 500);
+    H.Aop = std::make_unique<MatOp>(&H.A);
+    H.Aop->timers = &H.timers;
+    if (H.solver_type == "aar") {
+        auto &a = H.aar;
+        a.order = (int)o.integer("pls.aar_order", 10);
+        a.p = (int)o.integer("pls.aar_p", 5);
+        a.omega = o.num("pls.aar_omega", 1.0);
+        a.beta = o.num("pls.aar_beta", 1.0);
+        a.atol = atol;
+        a.rtol = rtol;
+        a.maxiter = maxiter;
+        a.monitor = o.flag("pls.solver_monitor", false);
+        if (a.order > 15) throw Error("AAR order > 15 not supported");
+        a.F.init(a.order + 1, n);
+        a.X.init(a.order + 1, n);
+        a.xk.alloc(n); a.fk.alloc(n); a.dxk.alloc(n); a.dfk.alloc(n); a.tmp.alloc(n);
+        a.pX.alloc(16); a.pF.alloc(16); a.dalpha.alloc(16);
+    } else {
+        const int64_t restart = (H.solver_type == "gmres") ? maxiter : 30;
+        H.outer = make_ksp("global_", o, &H.A, nullptr, H.solver_type, "python", c, rtol, atol, 1e20, maxiter, restart,
+                           &H.bpc);
+        H.outer->owned_op.reset();
+        H.outer->A = H.Aop.get();
+        H.outer->monitor = H.outer->monitor || o.flag("pls.solver_monitor", false);
+        const std::string gpc = o.str("global_pc_type", "python");
+        if (gpc != "python") throw Error("global_pc_type must stay 'python' (the block preconditioner)");
+    }
+    c.sync();
+    H.solver_ready = true;
+}
+
+// ---------------------------------------------------------------- AAR -----
+// lib/AAR.py:46-128 (single process: the rank-0 gathers are the identity).
+static void aar_solve(Handle &H, const double *b, double *x) {
+    Ctx &c = H.ctx;
+    auto &a = H.aar;
+    const int64_t n = H.n;
+    // x0 = 0; fk = b - A x0 = b
+    launch_set(n, 0.0, a.xk.p, c.st);
+    launch_copy(n, b, a.fk.p, c.st);
+    const double error0 = c.norm2(n, a.fk.p);
+    double err_abs = error0, err_rel = 1.0;
+    int64_t it = 0;
+    H.history.assign(1, error0);
+    while (err_abs > a.atol && err_rel > a.rtol && it < a.maxiter) {
+        launch_copy(n, a.fk.p, a.dfk.p, c.st);
+        launch_copy(n, a.xk.p, a.dxk.p, c.st);
+        // update_residual: temp = b - A xk ; fk = PC(temp)
+        H.Aop->apply(a.xk.p, a.tmp.p, c);
+        launch_waxpby(n, 1.0, b, -1.0, a.tmp.p, a.tmp.p, c.st);
+        H.bpc.apply(a.tmp.p, a.fk.p, c);
+        launch_waxpby(n, 1.0, a.fk.p, -1.0, a.dfk.p, a.dfk.p, c.st);  // dfk = fk - dfk
+        a.F.append(a.dfk.p, a.order, c);
+        const double fnorm = c.norm2(n, a.fk.p);
+        const char *kind = "R";
+        if (fnorm < 1e-14) {
+            // no update (AAR.py:91-92)
+        } else if (it == 0 || a.order == 0 || ((it + 1) % a.p) != 0) {
+            launch_axpby(n, a.omega, a.fk.p, 1.0, a.xk.p, c.st);
+        } else {
+            kind = "A";
+            const int64_t mk = std::min<int64_t>(a.order, it);
+            std::vector<const double *> cols;
+            for (int i = 0; i < a.F.size(); ++i) cols.push_back(a.F.at(i));
+            std::vector<double> alpha = a.ls.solve(cols, a.fk.p, n, c);
+            if ((int64_t)a.X.size() < mk) throw Error("AAR: history shorter than mk");
+            std::vector<const double *> hx, hf;
+            for (int64_t i = 0; i < mk; ++i) { hx.push_back(a.X.at((int)i)); hf.push_back(a.F.at((int)i)); }
+            if (mk > 0) {
+                HIPCHK(hipMemcpyAsync((void *)a.pX.p, hx.data(), sizeof(double *) * mk, hipMemcpyHostToDevice, c.st));
+                HIPCHK(hipMemcpyAsync((void *)a.pF.p, hf.data(), sizeof(double *) * mk, hipMemcpyHostToDevice, c.st));
+                HIPCHK(hipMemcpyAsync(a.dalpha.p, alpha.data(), sizeof(double) * mk, hipMemcpyHostToDevice, c.st));
+            }
+            k_anderson_update<<<2048, 256, 0, c.st>>>(n, (int)mk, a.pX.p, a.pF.p, a.dalpha.p, a.beta, a.fk.p, a.xk.p);
+            c.sync();
+        }
+        launch_waxpby(n, 1.0, a.xk.p, -1.0, a.dxk.p, a.dxk.p, c.st);  // dxk = xk - dxk
+        a.X.append(a.dxk.p, a.order, c);
+        err_abs = fnorm;
+        err_rel = err_abs / error0;
+        it += 1;
+        H.history.push_back(err_abs);
+        if (a.monitor) printf("---- Iteration [%s] %3lld\tabs=%1.2e\trel=%1.2e\n", kind, (long long)it, err_abs, err_rel);
+        H.timers.flush();
+    }
+    launch_copy(n, a.xk.p, x, c.st);
+    c.sync();
+    H.res.its = (int)it;
+    H.res.rnorm = err_abs;
+    H.res.reason = (err_abs <= a.atol) ? 3 : (err_rel <= a.rtol) ? 2 : -3;
+}
+
+static void solve_device(Handle &H, const double *b, double *x) {
+    do_setup(H);
+    do_setup_solver(H);
+    Ctx &c = H.ctx;
+    H.pc_applies = 0;
+    H.timers.begin(T_SOLVER);
+    if (H.solver_type == "aar") {
+        aar_solve(H, b, x);
+    } else {
+        H.outer->solve(b, x, c);
+        H.res.its = H.outer->its;
+        H.res.reason = H.outer->reason;
+        H.res.rnorm = H.outer->rnorm;
+        H.history = H.outer->history;
+    }
+    H.timers.end(T_SOLVER);
+    c.sync();
+    H.timers.flush();
+    H.res.pc_applies = H.pc_applies;
+    H.res.history_len = (int32_t)H.history.size();
+}
+
+}  // namespace pls
+
+// ======================================================== extern "C" ABI ===
+using namespace pls;
+
+#define PLS_TRY(...)                                            \
+    try {                                                       \
+        __VA_ARGS__;                                            \
+        return 0;                                               \
+    } catch (const std::exception &e) {                         \
+        g_last_error = e.what();                                \
+        return 1;                                               \
+    } catch (...) {                                             \
+        g_last_error = "unknown error";                         \
+        return 1;                                               \
+    }
+
+extern "C" {
+
+int pls_abi_version(void) { return PLS_ABI_VERSION; }
+const char *pls_last_error(void) { return g_last_error.c_str(); }
+
+int pls_device_count(int *count) {
+    PLS_TRY({
+        int c = 0;
+        hipError_t e = hipGetDeviceCount(&c);
+        if (e != hipSuccess) c = 0;
+        *count = c;
+    })
+}
+int pls_set_device(int device) { PLS_TRY(HIPCHK(hipSetDevice(device))) }
+
+static void check_is(const int32_t *is, int64_t m, int64_t n, std::vector<char> &seen, const char *name) {
+    for (int64_t i = 0; i < m; ++i) {
+        if (is[i] < 0 || is[i] >= n) throw Error(std::string(name) + ": index out of range");
+        if (i && is[i] <= is[i - 1]) throw Error(std::string(name) + ": must be sorted ascending and unique");
+        if (seen[is[i]]) throw Error(std::string(name) + ": overlaps another field");
+        seen[is[i]] = 1;
+    }
+}
+
+int pls_create(const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff, const int32_t *is_s, int64_t ns,
+               const int32_t *is_f, int64_t nf, const int32_t *is_p, int64_t np, const int32_t *bcs_sub_p, int64_t nbc,
+               const char *options, pls_handle **out) {
+    PLS_TRY({
+        if (!A || !P || !out) throw Error("pls_create: A, P and out are required");
+        {
+            Options pre;
+            pre.parse(options);
+            validate_pc_type(pre);
+        }
+        auto H = std::make_unique<Handle>();
+        H->opt.parse(options);
+        H->parse_params();
+        H->timers.st = H->ctx.st;
+        H->ns = ns; H->nf = nf; H->np = np; H->n = ns + nf + np;
+        const int64_t n = H->n;
+        std::vector<char> seen(n, 0);
+        check_is(is_s, ns, n, seen, "is_s");
+        check_is(is_f, nf, n, seen, "is_f");
+        check_is(is_p, np, n, seen, "is_p");
+        // internal order: 2-way [is_s | is_fp = sorted(f U p)], 3-way [is_s | is_f | is_p]
+        H->perm.assign(is_s, is_s + ns);
+        if (H->three_way) {
+            H->perm.insert(H->perm.end(), is_f, is_f + nf);
+            H->perm.insert(H->perm.end(), is_p, is_p + np);
+        } else {
+            std::vector<int64_t> fp(is_f, is_f + nf);
+            fp.insert(fp.end(), is_p, is_p + np);
+            std::sort(fp.begin(), fp.end());
+            H->perm.insert(H->perm.end(), fp.begin(), fp.end());
+        }
+        std::vector<int64_t> inv(n);
+        for (int64_t i = 0; i < n; ++i) inv[H->perm[i]] = i;
+        upload_permuted(A, *H, inv, H->A);
+        upload_permuted(P, *H, inv, H->P);
+        if (Pdiff) {
+            upload_permuted(Pdiff, *H, inv, H->Pd);
+            H->have_Pd = true;
+        }
+        H->dperm.alloc(std::max<int64_t>(n, 1));
+        HIPCHK(hipMemcpy(H->dperm.p, H->perm.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+        H->bcs.assign(bcs_sub_p, bcs_sub_p + nbc);
+        for (int32_t b : H->bcs)
+            if (b < 0 || b >= np) throw Error("bcs_sub_pressure: position out of range of the p sub-vector");
+        H->dbcs.alloc(std::max<int64_t>(nbc, 1));
+        if (nbc) HIPCHK(hipMemcpy(H->dbcs.p, H->bcs.data(), sizeof(int32_t) * nbc, hipMemcpyHostToDevice));
+        H->keep = H->opt.flag("pls.keep_matrices", true);
+        *out = reinterpret_cast<pls_handle *>(H.release());
+    })
+}
+
+int pls_create_synthetic(const pls_synth_spec *spec, const char *options, pls_handle **out) {
+    PLS_TRY({
+        {
+            Options pre;
+            pre.parse(options);
+            validate_pc_type(pre);
+        }
+        auto H = std::make_unique<Handle>();
+        H->opt.parse(options);
+        H->parse_params();
+        H->timers.st = H->ctx.st;
+        SynthHost S;
+        S.init(*spec);
+        H->ns = S.n[0]; H->nf = S.n[1]; H->np = S.n[2];
+        H->n = H->ns + H->nf + H->np;
+        const int64_t n = H->n;
+        Ctx &c = H->ctx;
+        DBuf<int32_t> doffs(6 * 128);
+        SynthDev D{};
+        D.dim = S.dim;
+        D.seed = S.seed;
+        D.delta = S.delta;
+        for (int f = 0; f < 3; ++f) { D.n[f] = S.n[f]; D.off[f] = S.off[f]; }
+        for (int b = 0; b < 6; ++b) {
+            D.cnt[b] = S.cnt[b];
+            HIPCHK(hipMemcpy(doffs.p + b * 128, S.offs[b].data(), sizeof(int32_t) * S.cnt[b], hipMemcpyHostToDevice));
+            D.offs[b] = doffs.p + b * 128;
+        }
+        // pattern (shared by A, P, P_diff)
+        DBuf<int64_t> len(n + 1);
+        launch_synth_count(D, len.p, c.st);
+        H->A.rp.alloc(n + 1);
+        c.ensure_scan(n);
+        exclusive_scan_i64(len.p, H->A.rp.p, n, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
+        int64_t nnz = 0;
+        HIPCHK(hipMemcpyAsync(&nnz, H->A.rp.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
+        c.sync();
+        auto gen = [&](DevCSR &M, int variant) {
+            M.nrows = n; M.ncols = n; M.nnz = nnz;
+            if (!M.rp.p) {
+                M.rp.alloc(n + 1);
+                HIPCHK(hipMemcpyAsync(M.rp.p, H->A.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, c.st));
+            }
+            M.ci.alloc(nnz);
+            M.val.alloc(nnz);
+            launch_synth_fill(D, variant, M.rp.p, M.ci.p, M.val.p, c.st);
+            HIPCHK(hipGetLastError());
+        };
+        gen(H->A, 0);
+        gen(H->P, 1);
+        if (H->three_way) {
+            gen(H->Pd, 2);
+            H->have_Pd = true;
+        }
+        c.sync();
+        H->A.max_row = H->P.max_row = H->Pd.max_row = 0;
+        H->perm.resize(n);
+        std::iota(H->perm.begin(), H->perm.end(), 0);
+        H->dperm.alloc(std::max<int64_t>(n, 1));
+        HIPCHK(hipMemcpy(H->dperm.p, H->perm.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+        for (int64_t i = 0; i < H->np; ++i)
+            if (S.is_bc(i)) H->bcs.push_back((int32_t)i);
+        H->dbcs.alloc(std::max<size_t>(H->bcs.size(), 1));
+        if (!H->bcs.empty())
+            HIPCHK(hipMemcpy(H->dbcs.p, H->bcs.data(), sizeof(int32_t) * H->bcs.size(), hipMemcpyHostToDevice));
+        H->keep = H->opt.flag("pls.keep_matrices", nnz < 50000000);
+        *out = reinterpret_cast<pls_handle *>(H.release());
+    })
+}
+
+int pls_setup(pls_handle *h) { PLS_TRY(do_setup(*reinterpret_cast<Handle *>(h))) }
+int pls_destroy(pls_handle *h) { PLS_TRY(delete reinterpret_cast<Handle *>(h)) }
+int pls_set_option(pls_handle *hh, const char *key, const char *value) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        std::string k(key ? key : "");
+        while (!k.empty() && k[0] == '-') k.erase(0, 1);
+        if (k.empty()) throw Error("pls_set_option: empty key");
+        const bool solver_key = k.rfind("pls.solver", 0) == 0 || k.rfind("pls.aar", 0) == 0 || k.rfind("global_", 0) == 0;
+        if (solver_key && H.solver_ready) throw Error("option " + k + " set after the solver was created");
+        if (!solver_key && H.setup_done) throw Error("option " + k + " set after the preconditioner was set up");
+        H.opt.kv[k] = value ? value : "";
+        if (k == "pls.timers") H.timers.enabled = H.opt.flag(k, true);
+    })
+}
+int pls_create_solver(pls_handle *hh) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        do_setup(H);
+        do_setup_solver(H);
+    })
+}
+
+int pls_get_sizes(pls_handle *hh, int64_t *n, int64_t *ns, int64_t *nf, int64_t *np, int64_t *nnz_A) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        if (n) *n = H.n;
+        if (ns) *ns = H.ns;
+        if (nf) *nf = H.nf;
+        if (np) *np = H.np;
+        if (nnz_A) *nnz_A = H.A.nnz;
+    })
+}
+
+static void to_internal(Handle &H, const double *x_host, double *d_internal) {
+    HIPCHK(hipMemcpyAsync(H.vout.p, x_host, sizeof(double) * H.n, hipMemcpyHostToDevice, H.ctx.st));
+    launch_gather(H.n, H.dperm.p, H.vout.p, d_internal, H.ctx.st);
+}
+static void from_internal(Handle &H, const double *d_internal, double *y_host) {
+    launch_scatter(H.n, H.dperm.p, d_internal, H.vout.p, H.ctx.st);
+    HIPCHK(hipMemcpyAsync(y_host, H.vout.p, sizeof(double) * H.n, hipMemcpyDeviceToHost, H.ctx.st));
+    H.ctx.sync();
+}
+
+int pls_pc_apply(pls_handle *hh, const double *x, double *y) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        do_setup(H);
+        DBuf<double> xi(H.n), yi(H.n);
+        to_internal(H, x, xi.p);
+        H.bpc.apply(xi.p, yi.p, H.ctx);
+        from_internal(H, yi.p, y);
+        H.timers.flush();
+    })
+}
+
+int pls_matmult(pls_handle *hh, const double *x, double *y) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        DBuf<double> xi(H.n), yi(H.n);
+        if (!H.vout.p) H.vout.alloc(H.n);
+        to_internal(H, x, xi.p);
+        spmv(H.A, xi.p, yi.p, H.ctx);
+        from_internal(H, yi.p, y);
+    })
+}
+
+int pls_solve(pls_handle *hh, const double *b, double *x, pls_result *res) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        do_setup(H);
+        DBuf<double> bi(H.n), xi(H.n);
+        to_internal(H, b, bi.p);
+        solve_device(H, bi.p, xi.p);
+        from_internal(H, xi.p, x);
+        if (res) *res = H.res;
+    })
+}
+
+int pls_solve_device(pls_handle *hh, const double *d_b, double *d_x, pls_result *res) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        solve_device(H, d_b, d_x);
+        if (res) *res = H.res;
+    })
+}
+int pls_pc_apply_device(pls_handle *hh, const double *d_x, double *d_y) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        do_setup(H);
+        H.bpc.apply(d_x, d_y, H.ctx);
+        H.ctx.sync();
+        H.timers.flush();
+    })
+}
+int pls_matmult_device(pls_handle *hh, const double *d_x, double *d_y) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        spmv(H.A, d_x, d_y, H.ctx);
+        H.ctx.sync();
+    })
+}
+int pls_synthetic_rhs_device(pls_handle *hh, uint64_t seed, double *d_b) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        launch_synth_rhs(seed, H.n, d_b, H.ctx.st);
+        H.ctx.sync();
+    })
+}
+int pls_device_alloc(int64_t bytes, void **d_ptr) { PLS_TRY(HIPCHK(hipMalloc(d_ptr, (size_t)bytes))) }
+int pls_device_free(void *d_ptr) { PLS_TRY(HIPCHK(hipFree(d_ptr))) }
+int pls_memcpy_h2d(void *d_dst, const void *h_src, int64_t bytes) {
+    PLS_TRY(HIPCHK(hipMemcpy(d_dst, h_src, (size_t)bytes, hipMemcpyHostToDevice)))
+}
+int pls_memcpy_d2h(void *h_dst, const void *d_src, int64_t bytes) {
+    PLS_TRY(HIPCHK(hipMemcpy(h_dst, d_src, (size_t)bytes, hipMemcpyDeviceToHost)))
+}
+
+int pls_get_result(pls_handle *hh, pls_result *res) {
+    PLS_TRY({ *res = reinterpret_cast<Handle *>(hh)->res; })
+}
+int pls_get_history(pls_handle *hh, double *hist, int32_t cap) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        const int32_t m = std::min<int32_t>(cap, (int32_t)H.history.size());
+        std::copy(H.history.begin(), H.history.begin() + m, hist);
+    })
+}
+int pls_get_timings(pls_handle *hh, pls_timings *t) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        H.timers.flush();
+        t->pc_total = H.timers.acc[T_PC_TOTAL];
+        t->pc_solid = H.timers.acc[T_PC_SOLID];
+        t->pc_fluid = H.timers.acc[T_PC_FLUID];
+        t->pc_press = H.three_way ? H.timers.acc[T_PC_PRESS] : H.timers.acc[T_PC_FLUID];
+        t->pc_alloc = H.timers.acc[T_PC_ALLOC];
+        t->solver_total = H.timers.acc[T_SOLVER];
+        t->spmv_total = H.timers.acc[T_SPMV];
+        t->spmv_calls = H.timers.spmv_calls;
+    })
+}
+int pls_reset_timings(pls_handle *hh) { PLS_TRY(reinterpret_cast<Handle *>(hh)->timers.reset()) }
+
+int pls_export_matrix(pls_handle *hh, int which, int64_t *nrows, int64_t *nnz, int64_t *row_ptr, int32_t *col,
+                      double *val) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        const DevCSR &M = which == 0 ? H.A : which == 1 ? H.P : H.Pd;
+        if (!M.rp.p) throw Error("matrix not available (freed after setup, or not generated)");
+        *nrows = M.nrows;
+        *nnz = M.nnz;
+        if (col) {
+            HIPCHK(hipMemcpy(row_ptr, M.rp.p, sizeof(int64_t) * (M.nrows + 1), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(col, M.ci.p, sizeof(int32_t) * M.nnz, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(val, M.val.p, sizeof(double) * M.nnz, hipMemcpyDeviceToHost));
+        }
+    })
+}
+int pls_get_permutation(pls_handle *hh, int64_t *perm) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        std::copy(H.perm.begin(), H.perm.end(), perm);
+    })
+}
+
+int pls_bench_spmv(pls_handle *hh, const double *d_x, double *d_y, int32_t reps, double *sec_per_launch) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        hipEvent_t a, b;
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+        HIPCHK(hipEventRecord(a, H.ctx.st));
+        for (int r = 0; r < reps; ++r) spmv(H.A, d_x, d_y, H.ctx);
+        HIPCHK(hipEventRecord(b, H.ctx.st));
+        HIPCHK(hipEventSynchronize(b));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, a, b));
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        *sec_per_launch = (double)ms * 1e-3 / std::max(1, reps);
+    })
+}
+
+}  // extern "C"

@@ -1,0 +1,750 @@
+// kernels.hip -- HIP kernels for gfx950 (MI355X / CDNA4) behind libpls.so.
+//
+// Everything on the solver path is HBM-bandwidth bound fp64 sparse / BLAS-1
+// work (no MFMA).  Design rules applied (cdna_hip_programming.md):
+//  * 64-lane wavefronts: CSR rows are mapped to groups of LPR lanes
+//    (LPR in {8,16,32,64}) sized from the mean row length, reductions are
+//    __shfl_xor trees inside the group;
+//  * val / col streams use non-temporal loads (read once), the x gathers go
+//    through L2 / the Infinity Cache (banded columns: hot window);
+//  * reductions are deterministic: a fixed grid that depends only on n, one
+//    partial per block, then a single-block final pass in fixed order, so a
+//    solve is bitwise reproducible run to run;
+//  * the ILU(0) factor and sweeps are level scheduled; the triangular factors
+//    are stored in level order so each level streams a contiguous slice.
+#include "kernels.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+#include <cstdio>
+
+namespace pls {
+
+static constexpr int TPB = 256;
+
+static inline unsigned grid_for(int64_t work, int per_block) {
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+// ============================================================ synthetic ====
+// Bit-exact restatement of the synthetic spec; every float
+// expression rounds as written (no FMA contraction) so the device matrices are
+// identical to the CPU definition.
+#pragma clang fp contract(off)
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t hash3(uint64_t s, uint64_t a, uint64_t b) {
+    return mix64(mix64(mix64(s) ^ a) ^ b);
+}
+__device__ __forceinline__ double u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+
+#define SALT_VAL 0x5A1BE5ULL
+#define SALT_DIAGA 0xD1A60AULL
+#define SALT_DIAGP 0xD1A60BULL
+#define SALT_BC 0x00BC00ULL
+#define SALT_RHS 0x00B0B0ULL
+
+__device__ __forceinline__ int blk_id(int a, int b) {
+    // ss sf sp / sf ff fp / sp fp pp
+    const int t = a * 3 + b;
+    return (t == 0) ? 0 : (t == 1 || t == 3) ? 1 : (t == 2 || t == 6) ? 2 : (t == 4) ? 3 : (t == 5 || t == 7) ? 4 : 5;
+}
+
+__device__ __forceinline__ int field_of(const SynthDev &S, int64_t g) {
+    return g < S.off[1] ? 0 : (g < S.off[2] ? 1 : 2);
+}
+
+// Visits the global columns of row i (local in field a) in ascending order.
+template <typename F>
+__device__ __forceinline__ void synth_visit(const SynthDev &S, int a, int64_t i, F &&f) {
+    for (int b = 0; b < 3; ++b) {
+        const int bid = blk_id(a, b);
+        const int32_t *D = S.offs[bid];
+        const int m = S.cnt[bid];
+        const int64_t na = S.n[a], nb = S.n[b];
+        if (a <= b) {
+            const int64_t ctr = (a == b) ? i : (i * nb) / na;
+            for (int k = 0; k < m; ++k) {
+                const int64_t j = ctr + D[k];
+                if (j >= 0 && j < nb) f(b, S.off[b] + j);
+            }
+        } else {
+            for (int k = m - 1; k >= 0; --k) {
+                const int64_t mm = i - D[k];
+                if (mm < 0 || mm >= na) continue;
+                const int64_t lo = (mm * nb + na - 1) / na;
+                int64_t hi = ((mm + 1) * nb + na - 1) / na;
+                if (hi > nb) hi = nb;
+                for (int64_t j = lo; j < hi; ++j) f(b, S.off[b] + j);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(TPB) void k_synth_count(SynthDev S, int64_t *row_len) {
+    const int64_t n = S.n[0] + S.n[1] + S.n[2];
+    const int64_t g = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (g > n) return;
+    if (g == n) { row_len[n] = 0; return; }
+    const int a = field_of(S, g);
+    int64_t c = 0;
+    synth_visit(S, a, g - S.off[a], [&](int, int64_t) { ++c; });
+    row_len[g] = c;
+}
+
+__global__ __launch_bounds__(TPB) void k_synth_fill(SynthDev S, int variant, const int64_t *rp,
+                                                    int32_t *col, double *val) {
+    const int64_t n = S.n[0] + S.n[1] + S.n[2];
+    const int64_t g = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (g >= n) return;
+    const int a = field_of(S, g);
+    const int64_t i = g - S.off[a];
+    const uint64_t sv = S.seed ^ SALT_VAL;
+    const uint64_t sd = S.seed ^ (variant == 0 ? SALT_DIAGA : SALT_DIAGP);
+    const bool bcrow = (variant == 2 && a == 2 &&
+                        ((hash3(S.seed ^ SALT_BC, (uint64_t)i, 7ULL) & 15ULL) == 0ULL));
+    int64_t pos = rp[g];
+    int64_t dpos = -1;
+    double sum = 0.0;
+    synth_visit(S, a, i, [&](int b, int64_t gj) {
+        col[pos] = (int32_t)gj;
+        if (gj == g) {
+            dpos = pos;
+            val[pos] = 0.0;
+        } else {
+            const uint64_t lo = (uint64_t)(g < gj ? g : gj), hi = (uint64_t)(g < gj ? gj : g);
+            const double u = u01(hash3(sv, lo, hi));
+            const double v = (a == b) ? -u : -(0.1 * u);
+            val[pos] = bcrow ? 0.0 : v;
+            sum = sum + fabs(v);
+        }
+        ++pos;
+    });
+    if (dpos >= 0) {
+        if (bcrow) {
+            val[dpos] = 1.0;
+        } else {
+            const double u = u01(hash3(sd, (uint64_t)g, (uint64_t)g));
+            const double sh = S.delta * (1.0 + u);
+            val[dpos] = sum + sh;
+        }
+    }
+}
+
+__global__ __launch_bounds__(TPB) void k_synth_rhs(uint64_t seed, int64_t n, double *b) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const double u = u01(hash3(seed ^ SALT_RHS, (uint64_t)i, 3ULL));
+    b[i] = 2.0 * u - 1.0;
+}
+
+#pragma clang fp contract(on)
+
+void launch_synth_count(const SynthDev &S, int64_t *row_len, hipStream_t st) {
+    const int64_t n = S.n[0] + S.n[1] + S.n[2];
+    k_synth_count<<<grid_for(n + 1, TPB), TPB, 0, st>>>(S, row_len);
+}
+void launch_synth_fill(const SynthDev &S, int variant, const int64_t *row_ptr, int32_t *col,
+                       double *val, hipStream_t st) {
+    const int64_t n = S.n[0] + S.n[1] + S.n[2];
+    k_synth_fill<<<grid_for(n, TPB), TPB, 0, st>>>(S, variant, row_ptr, col, val);
+}
+void launch_synth_rhs(uint64_t seed, int64_t n, double *b, hipStream_t st) {
+    k_synth_rhs<<<grid_for(n, TPB), TPB, 0, st>>>(seed, n, b);
+}
+
+// ================================================================ scans ====
+size_t exclusive_scan_tmp_bytes(int64_t n) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int64_t *)nullptr, (int64_t *)nullptr,
+                                     (int)(n + 1));
+    return bytes;
+}
+void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, void *tmp, size_t tmp_bytes,
+                        hipStream_t st) {
+    (void)hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, in, out, (int)(n + 1), st);
+}
+
+// ========================================================== extraction =====
+__device__ __forceinline__ void window_of(const WindowSpec &w, int64_t lr, int64_t nloc, int64_t r0,
+                                          int64_t &lo, int64_t &hi) {
+    if (w.mode == 0) {
+        lo = w.c0;
+        hi = w.c1;
+        return;
+    }
+    const int64_t nb = w.nblocks;
+    const int64_t q = nloc / nb, r = nloc % nb;
+    int64_t b0, len;
+    if (lr < r * (q + 1)) {
+        const int64_t b = lr / (q + 1);
+        b0 = b * (q + 1);
+        len = q + 1;
+    } else {
+        const int64_t b = r + (lr - r * (q + 1)) / q;
+        b0 = r * (q + 1) + (b - r) * q;
+        len = q;
+    }
+    lo = r0 + b0;
+    hi = r0 + b0 + len;
+}
+
+__device__ __forceinline__ int64_t lower_bound_i32(const int32_t *a, int64_t s, int64_t e, int64_t v) {
+    while (s < e) {
+        const int64_t m = (s + e) >> 1;
+        if ((int64_t)a[m] < v) s = m + 1; else e = m;
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(TPB) void k_extract_count(const int64_t *rp, const int32_t *ci, int64_t r0,
+                                                       int64_t r1, WindowSpec w, int64_t *len) {
+    const int64_t nloc = r1 - r0;
+    const int64_t lr = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (lr > nloc) return;
+    if (lr == nloc) { len[nloc] = 0; return; }
+    const int64_t r = r0 + lr;
+    int64_t lo, hi;
+    window_of(w, lr, nloc, r0, lo, hi);
+    const int64_t a = lower_bound_i32(ci, rp[r], rp[r + 1], lo);
+    const int64_t b = lower_bound_i32(ci, a, rp[r + 1], hi);
+    len[lr] = b - a;
+}
+
+__global__ __launch_bounds__(TPB) void k_extract_fill(const int64_t *rp, const int32_t *ci, const double *val,
+                                                      int64_t r0, int64_t r1, WindowSpec w, int64_t cshift,
+                                                      const int64_t *orp, int32_t *oci, double *oval) {
+    const int64_t nloc = r1 - r0;
+    // one wave per row: contiguous copy
+    const int64_t lr = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (lr >= nloc) return;
+    const int64_t r = r0 + lr;
+    int64_t lo, hi;
+    window_of(w, lr, nloc, r0, lo, hi);
+    const int64_t a = lower_bound_i32(ci, rp[r], rp[r + 1], lo);
+    const int64_t dst = orp[lr];
+    const int64_t cnt = orp[lr + 1] - dst;
+    for (int64_t k = lane; k < cnt; k += 64) {
+        oci[dst + k] = (int32_t)((int64_t)ci[a + k] - cshift);
+        oval[dst + k] = val[a + k];
+    }
+}
+
+void launch_extract_count(const int64_t *rp, const int32_t *ci, int64_t r0, int64_t r1, WindowSpec w,
+                          int64_t *row_len, hipStream_t st) {
+    k_extract_count<<<grid_for(r1 - r0 + 1, TPB), TPB, 0, st>>>(rp, ci, r0, r1, w, row_len);
+}
+void launch_extract_fill(const int64_t *rp, const int32_t *ci, const double *val, int64_t r0, int64_t r1,
+                         WindowSpec w, int64_t cshift, const int64_t *out_rp, int32_t *out_ci,
+                         double *out_val, hipStream_t st) {
+    k_extract_fill<<<grid_for((r1 - r0) * 64, TPB), TPB, 0, st>>>(rp, ci, val, r0, r1, w, cshift, out_rp,
+                                                                  out_ci, out_val);
+}
+
+// ================================================================= SpMV ====
+// y = alpha * (M x) + beta * z.  LPR lanes per row; 256 / LPR rows per block.
+template <int LPR>
+__global__ __launch_bounds__(TPB) void k_spmv(int64_t nrows, const int64_t *__restrict__ rp,
+                                              const int32_t *__restrict__ ci, const double *__restrict__ val,
+                                              const double *__restrict__ x, double *__restrict__ y,
+                                              double alpha, double beta, const double *__restrict__ z) {
+    const int sub = threadIdx.x & (LPR - 1);
+    const int64_t row = ((int64_t)blockIdx.x * TPB + threadIdx.x) / LPR;
+    if (row >= nrows) return;
+    const int64_t s = rp[row], e = rp[row + 1];
+    double a0 = 0.0, a1 = 0.0;
+    int64_t k = s + sub;
+    for (; k + LPR < e; k += 2 * LPR) {
+        const int32_t c0 = __builtin_nontemporal_load(ci + k);
+        const int32_t c1 = __builtin_nontemporal_load(ci + k + LPR);
+        const double v0 = __builtin_nontemporal_load(val + k);
+        const double v1 = __builtin_nontemporal_load(val + k + LPR);
+        a0 += v0 * x[c0];
+        a1 += v1 * x[c1];
+    }
+    if (k < e) a0 += __builtin_nontemporal_load(val + k) * x[__builtin_nontemporal_load(ci + k)];
+    double acc = a0 + a1;
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (sub == 0) {
+        double r = alpha * acc;
+        if (beta != 0.0) r += beta * z[row];
+        y[row] = r;
+    }
+}
+
+void launch_spmv(int64_t nrows, int64_t nnz, const int64_t *rp, const int32_t *ci, const double *val,
+                 const double *x, double *y, double alpha, double beta, const double *z, hipStream_t st) {
+    if (nrows <= 0) return;
+    const double mean = (double)nnz / (double)nrows;
+    if (mean >= 96.0)
+        k_spmv<64><<<grid_for(nrows, TPB / 64), TPB, 0, st>>>(nrows, rp, ci, val, x, y, alpha, beta, z);
+    else if (mean >= 40.0)
+        k_spmv<32><<<grid_for(nrows, TPB / 32), TPB, 0, st>>>(nrows, rp, ci, val, x, y, alpha, beta, z);
+    else if (mean >= 16.0)
+        k_spmv<16><<<grid_for(nrows, TPB / 16), TPB, 0, st>>>(nrows, rp, ci, val, x, y, alpha, beta, z);
+    else
+        k_spmv<8><<<grid_for(nrows, TPB / 8), TPB, 0, st>>>(nrows, rp, ci, val, x, y, alpha, beta, z);
+}
+
+// =============================================================== BLAS-1 ====
+__global__ __launch_bounds__(TPB) void k_copy(int64_t n, const double *x, double *y) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) y[i] = x[i];
+}
+__global__ __launch_bounds__(TPB) void k_set(int64_t n, double a, double *y) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) y[i] = a;
+}
+__global__ __launch_bounds__(TPB) void k_scale(int64_t n, double a, double *y) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) y[i] *= a;
+}
+__global__ __launch_bounds__(TPB) void k_axpby(int64_t n, double a, const double *x, double b, double *y) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
+        y[i] = a * x[i] + b * y[i];
+}
+__global__ __launch_bounds__(TPB) void k_waxpby(int64_t n, double a, const double *x, double b,
+                                                const double *y, double *w) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
+        w[i] = a * x[i] + b * y[i];
+}
+__global__ __launch_bounds__(TPB) void k_pmult(int64_t n, const double *x, const double *d, double *y) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
+        y[i] = x[i] * d[i];
+}
+__global__ __launch_bounds__(TPB) void k_zero_entries(int64_t m, const int32_t *idx, double *y) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i < m) y[idx[i]] = 0.0;
+}
+__global__ __launch_bounds__(TPB) void k_gather(int64_t n, const int64_t *idx, const double *x, double *y) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
+        y[i] = x[idx[i]];
+}
+__global__ __launch_bounds__(TPB) void k_scatter(int64_t n, const int64_t *idx, const double *x, double *y) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
+        y[idx[i]] = x[i];
+}
+
+static inline unsigned stream_grid(int64_t n) {
+    int64_t g = (n + TPB - 1) / TPB;
+    if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+void launch_copy(int64_t n, const double *x, double *y, hipStream_t st) {
+    if (n > 0) k_copy<<<stream_grid(n), TPB, 0, st>>>(n, x, y);
+}
+void launch_set(int64_t n, double a, double *y, hipStream_t st) {
+    if (n > 0) k_set<<<stream_grid(n), TPB, 0, st>>>(n, a, y);
+}
+void launch_scale(int64_t n, double a, double *y, hipStream_t st) {
+    if (n > 0) k_scale<<<stream_grid(n), TPB, 0, st>>>(n, a, y);
+}
+void launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st) {
+    if (n > 0) k_axpby<<<stream_grid(n), TPB, 0, st>>>(n, a, x, b, y);
+}
+void launch_waxpby(int64_t n, double a, const double *x, double b, const double *y, double *w, hipStream_t st) {
+    if (n > 0) k_waxpby<<<stream_grid(n), TPB, 0, st>>>(n, a, x, b, y, w);
+}
+void launch_pointwise_mult(int64_t n, const double *x, const double *d, double *y, hipStream_t st) {
+    if (n > 0) k_pmult<<<stream_grid(n), TPB, 0, st>>>(n, x, d, y);
+}
+void launch_zero_entries(int64_t m, const int32_t *idx, double *y, hipStream_t st) {
+    if (m > 0) k_zero_entries<<<grid_for(m, TPB), TPB, 0, st>>>(m, idx, y);
+}
+void launch_gather(int64_t n, const int64_t *idx, const double *x, double *y, hipStream_t st) {
+    if (n > 0) k_gather<<<stream_grid(n), TPB, 0, st>>>(n, idx, x, y);
+}
+void launch_scatter(int64_t n, const int64_t *idx, const double *x, double *y, hipStream_t st) {
+    if (n > 0) k_scatter<<<stream_grid(n), TPB, 0, st>>>(n, idx, x, y);
+}
+
+// ---------------------------------------------- deterministic reductions --
+static constexpr int NB_MAX = 1024;
+int reduce_blocks(int64_t n) {
+    int64_t nb = (n + 4095) / 4096;
+    if (nb < 1) nb = 1;
+    if (nb > NB_MAX) nb = NB_MAX;
+    return (int)nb;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+// fixed-order block reduction (TPB threads); result valid in thread 0
+__device__ __forceinline__ double block_sum(double v, double *lds) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) lds[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < TPB / 64; ++i) r += lds[i];
+    }
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ void chunk_of(int64_t n, int nb, int b, int64_t &s, int64_t &e) {
+    const int64_t c = (n + nb - 1) / nb;
+    s = (int64_t)b * c;
+    e = s + c;
+    if (e > n) e = n;
+    if (s > n) s = n;
+}
+
+// final pass: out[j] = sum_b partial[j*nb + b]
+__global__ __launch_bounds__(TPB) void k_final(int nb, const double *partial, double *out, int sqrt_it) {
+    __shared__ double lds[TPB / 64];
+    const int j = blockIdx.x;
+    double v = 0.0;
+    for (int b = threadIdx.x; b < nb; b += TPB) v += partial[(int64_t)j * nb + b];
+    v = block_sum(v, lds);
+    if (threadIdx.x == 0) out[j] = sqrt_it ? sqrt(v) : v;
+}
+
+// mdot: blockIdx.x = chunk, blockIdx.y = group of 4 vectors
+__global__ __launch_bounds__(TPB) void k_mdot(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
+                                              const double *__restrict__ w, double *partial) {
+    __shared__ double lds[TPB / 64];
+    const int nb = gridDim.x;
+    int64_t s, e;
+    chunk_of(n, nb, blockIdx.x, s, e);
+    const int j0 = blockIdx.y * 4;
+    const int nj = (k - j0) < 4 ? (k - j0) : 4;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const double *v0 = V + (int64_t)j0 * ldv;
+    for (int64_t i = s + threadIdx.x; i < e; i += TPB) {
+        const double wi = w[i];
+        a0 += v0[i] * wi;
+        if (nj > 1) a1 += v0[ldv + i] * wi;
+        if (nj > 2) a2 += v0[2 * ldv + i] * wi;
+        if (nj > 3) a3 += v0[3 * ldv + i] * wi;
+    }
+    double r;
+    r = block_sum(a0, lds);
+    if (threadIdx.x == 0) partial[(int64_t)(j0 + 0) * nb + blockIdx.x] = r;
+    if (nj > 1) { r = block_sum(a1, lds); if (threadIdx.x == 0) partial[(int64_t)(j0 + 1) * nb + blockIdx.x] = r; }
+    if (nj > 2) { r = block_sum(a2, lds); if (threadIdx.x == 0) partial[(int64_t)(j0 + 2) * nb + blockIdx.x] = r; }
+    if (nj > 3) { r = block_sum(a3, lds); if (threadIdx.x == 0) partial[(int64_t)(j0 + 3) * nb + blockIdx.x] = r; }
+}
+
+void launch_mdot(int64_t n, int k, const double *const *, const double *V, int64_t ldv, const double *w,
+                 double *partial, double *out, hipStream_t st) {
+    if (k <= 0) return;
+    const int nb = reduce_blocks(n);
+    dim3 grid(nb, (k + 3) / 4);
+    k_mdot<<<grid, TPB, 0, st>>>(n, k, V, ldv, w, partial);
+    k_final<<<k, TPB, 0, st>>>(nb, partial, out, 0);
+}
+
+__global__ __launch_bounds__(TPB) void k_dot(int64_t n, const double *__restrict__ x, const double *__restrict__ y,
+                                             double *partial) {
+    __shared__ double lds[TPB / 64];
+    int64_t s, e;
+    chunk_of(n, gridDim.x, blockIdx.x, s, e);
+    double a = 0.0;
+    for (int64_t i = s + threadIdx.x; i < e; i += TPB) a += x[i] * y[i];
+    a = block_sum(a, lds);
+    if (threadIdx.x == 0) partial[blockIdx.x] = a;
+}
+
+void launch_dot(int64_t n, const double *x, const double *y, double *partial, double *out, hipStream_t st) {
+    const int nb = reduce_blocks(n);
+    k_dot<<<nb, TPB, 0, st>>>(n, x, y, partial);
+    k_final<<<1, TPB, 0, st>>>(nb, partial, out, 0);
+}
+void launch_norm2(int64_t n, const double *x, double *partial, double *out, hipStream_t st) {
+    const int nb = reduce_blocks(n);
+    k_dot<<<nb, TPB, 0, st>>>(n, x, x, partial);
+    k_final<<<1, TPB, 0, st>>>(nb, partial, out, 1);
+}
+
+// w -= sum_j h[j] V[:, j]; partial ||w||^2
+__global__ __launch_bounds__(TPB) void k_maxpy_norm(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
+                                                    const double *__restrict__ h, double *__restrict__ w,
+                                                    double *partial) {
+    __shared__ double lds[TPB / 64];
+    __shared__ double hs[512];
+    for (int j = threadIdx.x; j < k && j < 512; j += TPB) hs[j] = h[j];
+    __syncthreads();
+    int64_t s, e;
+    chunk_of(n, gridDim.x, blockIdx.x, s, e);
+    double a = 0.0;
+    for (int64_t i = s + threadIdx.x; i < e; i += TPB) {
+        double t = w[i];
+        for (int j = 0; j < k; ++j) t -= (j < 512 ? hs[j] : h[j]) * V[(int64_t)j * ldv + i];
+        w[i] = t;
+        a += t * t;
+    }
+    if (partial) {
+        a = block_sum(a, lds);
+        if (threadIdx.x == 0) partial[blockIdx.x] = a;
+    }
+}
+
+void launch_maxpy_norm(int64_t n, int k, const double *V, int64_t ldv, const double *h_dev, double,
+                       double *w, double *partial, double *out, hipStream_t st) {
+    const int nb = reduce_blocks(n);
+    k_maxpy_norm<<<nb, TPB, 0, st>>>(n, k, V, ldv, h_dev, w, out ? partial : nullptr);
+    if (out) k_final<<<1, TPB, 0, st>>>(nb, partial, out, 1);
+}
+
+__global__ __launch_bounds__(TPB) void k_lincomb(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
+                                                 const double *__restrict__ c, double *__restrict__ y) {
+    __shared__ double cs[512];
+    for (int j = threadIdx.x; j < k && j < 512; j += TPB) cs[j] = c[j];
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+        double t = 0.0;
+        for (int j = 0; j < k; ++j) t += (j < 512 ? cs[j] : c[j]) * V[(int64_t)j * ldv + i];
+        y[i] = t;
+    }
+}
+void launch_lincomb(int64_t n, int k, const double *V, int64_t ldv, const double *c_dev, double *y,
+                    hipStream_t st) {
+    if (n > 0) k_lincomb<<<stream_grid(n), TPB, 0, st>>>(n, k, V, ldv, c_dev, y);
+}
+
+// Gram matrix of M <= 16 columns: G[a][b] for a <= b (packed upper, row-major),
+// optionally of Q = A * Rinv (Rinv upper triangular M x M, column-major) --
+// the second pass of Cholesky-QR2 for the Anderson least squares.
+template <int M>
+__global__ __launch_bounds__(TPB) void k_gram(int64_t n, const double *const *cols, const double *Rinv,
+                                              double *partial) {
+    __shared__ double lds[TPB / 64];
+    __shared__ double rinv[M * M];
+    if (Rinv)
+        for (int t = threadIdx.x; t < M * M; t += TPB) rinv[t] = Rinv[t];
+    __syncthreads();
+    const double *cp[M];
+#pragma unroll
+    for (int c = 0; c < M; ++c) cp[c] = cols[c];
+    int64_t s, e;
+    chunk_of(n, gridDim.x, blockIdx.x, s, e);
+    constexpr int NP = M * (M + 1) / 2;
+    double acc[NP];
+#pragma unroll
+    for (int t = 0; t < NP; ++t) acc[t] = 0.0;
+    for (int64_t i = s + threadIdx.x; i < e; i += TPB) {
+        double a[M];
+#pragma unroll
+        for (int c = 0; c < M; ++c) a[c] = cp[c][i];
+        if (Rinv) {
+            double q[M];
+#pragma unroll
+            for (int c = 0; c < M; ++c) {
+                double t = 0.0;
+#pragma unroll
+                for (int r = 0; r <= c; ++r) t += a[r] * rinv[c * M + r];
+                q[c] = t;
+            }
+#pragma unroll
+            for (int c = 0; c < M; ++c) a[c] = q[c];
+        }
+        int t = 0;
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+#pragma unroll
+            for (int c = r; c < M; ++c) acc[t++] += a[r] * a[c];
+    }
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+        const double v = block_sum(acc[t], lds);
+        if (threadIdx.x == 0) partial[(int64_t)t * gridDim.x + blockIdx.x] = v;
+    }
+}
+
+template <int M>
+static void gram_m(int nb, int64_t n, const double *const *cols, const double *Rinv, double *partial,
+                   hipStream_t st) {
+    k_gram<M><<<nb, TPB, 0, st>>>(n, cols, Rinv, partial);
+}
+
+void launch_gram(int64_t n, int m, const double *const *cols_dev, const double *Rinv_dev, double *partial,
+                 double *out, hipStream_t st) {
+    const int nb = reduce_blocks(n);
+    switch (m) {
+        case 1: gram_m<1>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 2: gram_m<2>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 3: gram_m<3>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 4: gram_m<4>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 5: gram_m<5>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 6: gram_m<6>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 7: gram_m<7>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 8: gram_m<8>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 9: gram_m<9>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 10: gram_m<10>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 11: gram_m<11>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 12: gram_m<12>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 13: gram_m<13>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 14: gram_m<14>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 15: gram_m<15>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        case 16: gram_m<16>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+        default: return;
+    }
+    k_final<<<m * (m + 1) / 2, TPB, 0, st>>>(nb, partial, out, 0);
+}
+
+// ================================================================ ILU(0) ===
+__global__ __launch_bounds__(TPB) void k_find_diag(int64_t n, const int64_t *rp, const int32_t *ci,
+                                                   int64_t *diag, int32_t *fail) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const int64_t p = lower_bound_i32(ci, rp[i], rp[i + 1], i);
+    if (p < rp[i + 1] && (int64_t)ci[p] == i) {
+        diag[i] = p;
+    } else {
+        diag[i] = -1;
+        atomicMax(fail, 1);
+    }
+}
+void launch_find_diag(int64_t n, const int64_t *rp, const int32_t *ci, int64_t *diag, int32_t *fail,
+                      hipStream_t st) {
+    if (n > 0) k_find_diag<<<grid_for(n, TPB), TPB, 0, st>>>(n, rp, ci, diag, fail);
+}
+
+// One 64-lane wave per row; the row is staged in LDS (cols + values), the
+// IKJ elimination runs over its strict-lower entries in column order, each
+// step updating the row's pattern positions that match row r's upper part
+// (binary search in LDS).  Rounds as the CPU restatement (no contraction).
+#pragma clang fp contract(off)
+__global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ rows, const int64_t *__restrict__ rp,
+                                                   const int32_t *__restrict__ ci, double *__restrict__ lu,
+                                                   const int64_t *__restrict__ diag, double *__restrict__ dinv,
+                                                   int32_t *fail) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x;
+    const int64_t i = rows[blockIdx.x];
+    const int64_t s = rp[i], e = rp[i + 1];
+    const int len = (int)(e - s);
+    double *rv = reinterpret_cast<double *>(smem);
+    int32_t *rc = reinterpret_cast<int32_t *>(smem + sizeof(double) * (size_t)len);
+    for (int t = lane; t < len; t += 64) {
+        rv[t] = lu[s + t];
+        rc[t] = ci[s + t];
+    }
+    __syncthreads();
+    const int dl = (int)(diag[i] - s);
+    for (int t = 0; t < dl; ++t) {
+        const double pc = rv[t];
+        __syncthreads();
+        if (pc != 0.0) {
+            const int64_t r = rc[t];
+            const double mult = pc * dinv[r];
+            if (lane == 0) rv[t] = mult;
+            const int64_t us = diag[r] + 1, ue = rp[r + 1];
+            for (int64_t kk = us + lane; kk < ue; kk += 64) {
+                const int32_t j = ci[kk];
+                // search j in rc[t+1, len)
+                int lo = t + 1, hi = len;
+                while (lo < hi) {
+                    const int m = (lo + hi) >> 1;
+                    if (rc[m] < j) lo = m + 1; else hi = m;
+                }
+                if (lo < len && rc[lo] == j) rv[lo] = rv[lo] - mult * lu[kk];
+            }
+        }
+        __syncthreads();
+    }
+    for (int t = lane; t < len; t += 64) lu[s + t] = rv[t];
+    if (lane == 0) {
+        const double piv = rv[dl];
+        if (piv == 0.0) {
+            atomicMax(fail, 2);
+            dinv[i] = 0.0;
+        } else {
+            dinv[i] = 1.0 / piv;
+        }
+    }
+}
+#pragma clang fp contract(on)
+
+void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
+                       const int64_t *diag, double *dinv, int32_t *fail, hipStream_t st) {
+    // caller guarantees max row length * 12 B <= 64 KiB; dynamic LDS sized per launch by caller contract
+    if (nrows_level <= 0) return;
+    k_ilu0_level<<<(unsigned)nrows_level, 64, 65536, st>>>(rows, rp, ci, lu, diag, dinv, fail);
+}
+
+__global__ __launch_bounds__(TPB) void k_lvl_count(int64_t n, const int32_t *order, const int64_t *rp,
+                                                   const int64_t *diag, int upper, int64_t *len) {
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (r > n) return;
+    if (r == n) { len[n] = 0; return; }
+    const int64_t i = order[r];
+    len[r] = upper ? (rp[i + 1] - diag[i] - 1) : (diag[i] - rp[i]);
+}
+__global__ __launch_bounds__(TPB) void k_lvl_fill(int64_t n, const int32_t *order, const int64_t *rp,
+                                                  const int32_t *ci, const double *lu, const int64_t *diag, int upper,
+                                                  const int64_t *orp, int32_t *oci, double *oval) {
+    const int64_t r = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 4;
+    const int l = threadIdx.x & 15;
+    if (r >= n) return;
+    const int64_t i = order[r];
+    const int64_t src = upper ? diag[i] + 1 : rp[i];
+    const int64_t dst = orp[r], cnt = orp[r + 1] - dst;
+    for (int64_t k = l; k < cnt; k += 16) {
+        oci[dst + k] = ci[src + k];
+        oval[dst + k] = lu[src + k];
+    }
+}
+void launch_lvl_count(int64_t n, const int32_t *order, const int64_t *rp, const int64_t *diag, int upper,
+                      int64_t *len, hipStream_t st) {
+    k_lvl_count<<<grid_for(n + 1, TPB), TPB, 0, st>>>(n, order, rp, diag, upper, len);
+}
+void launch_lvl_fill(int64_t n, const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu,
+                     const int64_t *diag, int upper, const int64_t *out_rp, int32_t *out_ci, double *out_val,
+                     hipStream_t st) {
+    if (n > 0)
+        k_lvl_fill<<<grid_for(n * 16, TPB), TPB, 0, st>>>(n, order, rp, ci, lu, diag, upper, out_rp, out_ci,
+                                                         out_val);
+}
+
+// level of a triangular sweep.  forward (dinv == null): y[i] = b[i] - sum
+// backward: y[i] = (y[i] - sum) * dinv[r]
+template <int LPR>
+__global__ __launch_bounds__(TPB) void k_trsv_level(int64_t r0, int64_t r1, const int32_t *__restrict__ row_of,
+                                                    const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                    const double *__restrict__ val, const double *__restrict__ dinv,
+                                                    const double *b, double *y) {
+    const int sub = threadIdx.x & (LPR - 1);
+    const int64_t r = r0 + ((int64_t)blockIdx.x * TPB + threadIdx.x) / LPR;
+    if (r >= r1) return;
+    const int64_t i = row_of[r];
+    const int64_t s = rp[r], e = rp[r + 1];
+    double acc = 0.0;
+    for (int64_t k = s + sub; k < e; k += LPR) acc += val[k] * y[ci[k]];
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (sub == 0) {
+        if (dinv) y[i] = (y[i] - acc) * dinv[r];
+        else y[i] = b[i] - acc;
+    }
+}
+
+void launch_trsv_level(int64_t r0, int64_t r1, const int32_t *row_of, const int64_t *rp, const int32_t *ci,
+                       const double *val, const double *dinv_lvl, const double *b, double *y, int lpr,
+                       hipStream_t st) {
+    const int64_t rows = r1 - r0;
+    if (rows <= 0) return;
+    switch (lpr) {
+        case 64: k_trsv_level<64><<<grid_for(rows, TPB / 64), TPB, 0, st>>>(r0, r1, row_of, rp, ci, val, dinv_lvl, b, y); break;
+        case 32: k_trsv_level<32><<<grid_for(rows, TPB / 32), TPB, 0, st>>>(r0, r1, row_of, rp, ci, val, dinv_lvl, b, y); break;
+        case 16: k_trsv_level<16><<<grid_for(rows, TPB / 16), TPB, 0, st>>>(r0, r1, row_of, rp, ci, val, dinv_lvl, b, y); break;
+        case 8: k_trsv_level<8><<<grid_for(rows, TPB / 8), TPB, 0, st>>>(r0, r1, row_of, rp, ci, val, dinv_lvl, b, y); break;
+        default: k_trsv_level<4><<<grid_for(rows, TPB / 4), TPB, 0, st>>>(r0, r1, row_of, rp, ci, val, dinv_lvl, b, y); break;
+    }
+}
+
+}  // namespace pls

@@ -1,0 +1,104 @@
+// kernels.hpp -- host launchers of the HIP/CDNA4 kernels (kernels.hip).
+// Every launcher enqueues on `st` and never synchronises.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace pls {
+
+// ----------------------------------------------------------------- synth --
+struct SynthDev {
+    int32_t dim;
+    uint64_t seed;
+    double delta;
+    int64_t n[3];
+    int64_t off[3];
+    int32_t cnt[6];
+    const int32_t *offs[6];  // device pointers, sorted offsets per forward block
+};
+void launch_synth_count(const SynthDev &S, int64_t *row_len, hipStream_t st);
+void launch_synth_fill(const SynthDev &S, int variant, const int64_t *row_ptr, int32_t *col,
+                       double *val, hipStream_t st);
+void launch_synth_rhs(uint64_t seed, int64_t n, double *b, hipStream_t st);
+
+// ---------------------------------------------------------------- CSR ops --
+// Exclusive scan of n+1 entries: in[0..n) lengths -> out[0..n] offsets.
+void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, void *tmp, size_t tmp_bytes,
+                        hipStream_t st);
+size_t exclusive_scan_tmp_bytes(int64_t n);
+
+// Column-window extraction: rows [r0, r1) of (rp, ci, val); keep entries with
+// column in the window of the row; output columns shifted by -cshift.
+//   mode 0: window [c0, c1) for every row
+//   mode 1: block-Jacobi window of the row's block, blocks over [0, r1-r0)
+//           with PETSc sizes (first nb % .. blocks one longer), cshift = r0
+struct WindowSpec {
+    int mode;
+    int64_t c0, c1;
+    int64_t nblocks;  // mode 1
+};
+void launch_extract_count(const int64_t *rp, const int32_t *ci, int64_t r0, int64_t r1,
+                          WindowSpec w, int64_t *row_len, hipStream_t st);
+void launch_extract_fill(const int64_t *rp, const int32_t *ci, const double *val, int64_t r0,
+                         int64_t r1, WindowSpec w, int64_t cshift, const int64_t *out_rp,
+                         int32_t *out_ci, double *out_val, hipStream_t st);
+
+// y = alpha * (M x) + beta * z     (z may be null when beta == 0)
+void launch_spmv(int64_t nrows, int64_t nnz, const int64_t *rp, const int32_t *ci,
+                 const double *val, const double *x, double *y, double alpha, double beta,
+                 const double *z, hipStream_t st);
+
+// ----------------------------------------------------------------- BLAS-1 --
+void launch_copy(int64_t n, const double *x, double *y, hipStream_t st);
+void launch_set(int64_t n, double a, double *y, hipStream_t st);
+void launch_scale(int64_t n, double a, double *y, hipStream_t st);
+// y = a*x + b*y
+void launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
+// w = a*x + b*y  (out of place)
+void launch_waxpby(int64_t n, double a, const double *x, double b, const double *y, double *w,
+                   hipStream_t st);
+void launch_pointwise_mult(int64_t n, const double *x, const double *d, double *y, hipStream_t st);
+void launch_zero_entries(int64_t m, const int32_t *idx, double *y, hipStream_t st);
+void launch_gather(int64_t n, const int64_t *idx, const double *x, double *y, hipStream_t st);
+void launch_scatter(int64_t n, const int64_t *idx, const double *x, double *y, hipStream_t st);
+
+// deterministic reductions: fixed grid (depends only on n)
+int reduce_blocks(int64_t n);
+// partial[j*NB + b] for j < k :  dot(v_j, w) ; then final into out[j]
+void launch_mdot(int64_t n, int k, const double *const *v_dev_ptrs, const double *V, int64_t ldv,
+                 const double *w, double *partial, double *out, hipStream_t st);
+void launch_dot(int64_t n, const double *x, const double *y, double *partial, double *out,
+                hipStream_t st);
+// out = ||x||_2 (sqrt of sum of squares)
+void launch_norm2(int64_t n, const double *x, double *partial, double *out, hipStream_t st);
+// w -= sum_j h[j] * V[:, j] (h on device, j < k); out = ||w||_2 when out != null
+void launch_maxpy_norm(int64_t n, int k, const double *V, int64_t ldv, const double *h_dev,
+                       double hscale, double *w, double *partial, double *out, hipStream_t st);
+// y = sum_j c[j] * V[:, j] (c on device)
+void launch_lincomb(int64_t n, int k, const double *V, int64_t ldv, const double *c_dev, double *y,
+                    hipStream_t st);
+// Gram of m columns (ptr list on device): G (upper, m*(m+1)/2) into out.
+// If Rinv != null, columns are first transformed q_row = a_row * Rinv (m x m upper, column-major).
+void launch_gram(int64_t n, int m, const double *const *cols_dev, const double *Rinv_dev,
+                 double *partial, double *out, hipStream_t st);
+
+// -------------------------------------------------------------------- ILU --
+// Factor the rows of one level in place (original CSR): lu, diag pos, dinv.
+void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp,
+                       const int32_t *ci, double *lu, const int64_t *diag, double *dinv,
+                       int32_t *fail, hipStream_t st);
+void launch_find_diag(int64_t n, const int64_t *rp, const int32_t *ci, int64_t *diag, int32_t *fail,
+                      hipStream_t st);
+// Level-ordered triangular factor storage ("row r of level order"): build
+void launch_lvl_count(int64_t n, const int32_t *order, const int64_t *rp, const int64_t *diag,
+                      int upper, int64_t *len, hipStream_t st);
+void launch_lvl_fill(int64_t n, const int32_t *order, const int64_t *rp, const int32_t *ci,
+                     const double *lu, const int64_t *diag, int upper, const int64_t *out_rp,
+                     int32_t *out_ci, double *out_val, hipStream_t st);
+// One level of the forward (unit lower) sweep: y[i] = b[i] - sum l_ij y[j]
+// One level of the backward sweep:           y[i] = (y[i] - sum u_ij y[j]) * dinv[i]
+void launch_trsv_level(int64_t r0, int64_t r1, const int32_t *row_of, const int64_t *rp,
+                       const int32_t *ci, const double *val, const double *dinv_lvl,
+                       const double *b, double *y, int lanes_per_row, hipStream_t st);
+
+}  // namespace pls

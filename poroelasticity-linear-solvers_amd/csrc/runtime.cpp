@@ -1,0 +1,671 @@
+// runtime.cpp -- device memory, options, timers, operators, preconditioners
+// and PETSc-semantics Krylov solvers of libpls.so.
+//
+// The Krylov algorithms follow PETSc as the reference configures it
+// (reference lib/Solver.py:91-102 for the outer solver, lib/Preconditioner.py:
+// 94-118 for the inner ones): GMRES with classical Gram-Schmidt, Givens
+// rotations, happy-breakdown test and BuildSoln (gmres.c); CG (cg.c);
+// PREONLY; KSPConvergedDefault (iterativ.c).  The scalar recurrences run on the
+// host in double precision without FMA contraction (-ffp-contract=off), exactly
+// as the CPU oracle evaluates them.
+#include "runtime.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+
+namespace pls {
+
+// ============================================================== context ===
+Ctx::Ctx() {
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    partial.alloc(1024 * 136);
+    dscal.alloc(4096);
+    HIPCHK(hipHostMalloc((void **)&hscal, sizeof(double) * 4096, hipHostMallocDefault));
+}
+Ctx::~Ctx() {
+    if (hscal) (void)hipHostFree(hscal);
+    if (st) (void)hipStreamDestroy(st);
+}
+void Ctx::ensure_scan(int64_t n) {
+    size_t need = exclusive_scan_tmp_bytes(n);
+    if (need > scan_tmp_bytes) {
+        scan_tmp.alloc(need);
+        scan_tmp_bytes = need;
+    }
+}
+double Ctx::dot(int64_t n, const double *x, const double *y) {
+    launch_dot(n, x, y, partial.p, dscal.p, st);
+    HIPCHK(hipMemcpyAsync(hscal, dscal.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    sync();
+    return hscal[0];
+}
+double Ctx::norm2(int64_t n, const double *x) {
+    launch_norm2(n, x, partial.p, dscal.p, st);
+    HIPCHK(hipMemcpyAsync(hscal, dscal.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    sync();
+    return hscal[0];
+}
+
+// ================================================================== CSR ===
+void upload_csr(DevCSR &M, int64_t nrows, int64_t ncols, const int64_t *rp, const int32_t *ci, const double *val,
+                Ctx &c) {
+    M.nrows = nrows;
+    M.ncols = ncols;
+    M.nnz = rp[nrows] - rp[0];
+    if (rp[0] != 0) throw Error("CSR row_ptr must start at 0");
+    int64_t mr = 0;
+    for (int64_t i = 0; i < nrows; ++i) {
+        const int64_t l = rp[i + 1] - rp[i];
+        if (l < 0) throw Error("CSR row_ptr not monotone");
+        mr = std::max(mr, l);
+        for (int64_t k = rp[i] + 1; k < rp[i + 1]; ++k)
+            if (ci[k] <= ci[k - 1]) throw Error("CSR columns must be strictly ascending within a row");
+        if (l > 0 && (ci[rp[i]] < 0 || ci[rp[i + 1] - 1] >= ncols)) throw Error("CSR column index out of range");
+    }
+    M.max_row = mr;
+    M.rp.alloc(nrows + 1);
+    M.ci.alloc(std::max<int64_t>(M.nnz, 1));
+    M.val.alloc(std::max<int64_t>(M.nnz, 1));
+    HIPCHK(hipMemcpyAsync(M.rp.p, rp, sizeof(int64_t) * (nrows + 1), hipMemcpyHostToDevice, c.st));
+    if (M.nnz) {
+        HIPCHK(hipMemcpyAsync(M.ci.p, ci, sizeof(int32_t) * M.nnz, hipMemcpyHostToDevice, c.st));
+        HIPCHK(hipMemcpyAsync(M.val.p, val, sizeof(double) * M.nnz, hipMemcpyHostToDevice, c.st));
+    }
+    c.sync();
+}
+
+static int64_t max_row_of(const DBuf<int64_t> &rp, int64_t nrows, Ctx &c) {
+    std::vector<int64_t> h(nrows + 1);
+    HIPCHK(hipMemcpyAsync(h.data(), rp.p, sizeof(int64_t) * (nrows + 1), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    int64_t m = 0;
+    for (int64_t i = 0; i < nrows; ++i) m = std::max(m, h[i + 1] - h[i]);
+    return m;
+}
+
+void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_t cshift, int64_t ncols,
+                 DevCSR &dst, Ctx &c) {
+    const int64_t nl = r1 - r0;
+    DBuf<int64_t> len(nl + 1);
+    launch_extract_count(src.rp.p, src.ci.p, r0, r1, w, len.p, c.st);
+    dst.rp.alloc(nl + 1);
+    c.ensure_scan(nl);
+    exclusive_scan_i64(len.p, dst.rp.p, nl, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
+    int64_t nnz = 0;
+    HIPCHK(hipMemcpyAsync(&nnz, dst.rp.p + nl, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    dst.nrows = nl;
+    dst.ncols = ncols;
+    dst.nnz = nnz;
+    dst.ci.alloc(std::max<int64_t>(nnz, 1));
+    dst.val.alloc(std::max<int64_t>(nnz, 1));
+    launch_extract_fill(src.rp.p, src.ci.p, src.val.p, r0, r1, w, cshift, dst.rp.p, dst.ci.p, dst.val.p, c.st);
+    HIPCHK(hipGetLastError());
+    dst.max_row = max_row_of(dst.rp, nl, c);
+}
+
+void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z) {
+    launch_spmv(M.nrows, M.nnz, M.rp.p, M.ci.p, M.val.p, x, y, alpha, beta, z, c.st);
+}
+
+// ============================================================== options ===
+void Options::parse(const char *text) {
+    if (!text) return;
+    std::istringstream is(text);
+    std::string line;
+    while (std::getline(is, line)) {
+        // trim
+        size_t a = line.find_first_not_of(" \t\r");
+        if (a == std::string::npos) continue;
+        size_t b = line.find_last_not_of(" \t\r");
+        line = line.substr(a, b - a + 1);
+        size_t sp = line.find(' ');
+        std::string k = line.substr(0, sp), v;
+        if (sp != std::string::npos) {
+            size_t vs = line.find_last_of(' ');
+            v = line.substr(vs + 1);
+        }
+        while (!k.empty() && k[0] == '-') k.erase(0, 1);
+        kv[k] = v;
+    }
+}
+std::string Options::str(const std::string &k, const std::string &d) const {
+    auto it = kv.find(k);
+    return it == kv.end() || it->second.empty() ? d : it->second;
+}
+double Options::num(const std::string &k, double d) const {
+    auto it = kv.find(k);
+    if (it == kv.end() || it->second.empty()) return d;
+    try { return std::stod(it->second); } catch (...) { throw Error("option " + k + ": not a number: " + it->second); }
+}
+int64_t Options::integer(const std::string &k, int64_t d) const {
+    auto it = kv.find(k);
+    if (it == kv.end() || it->second.empty()) return d;
+    try { return (int64_t)std::stoll(it->second); } catch (...) { throw Error("option " + k + ": not an integer: " + it->second); }
+}
+bool Options::flag(const std::string &k, bool d) const {
+    auto it = kv.find(k);
+    if (it == kv.end()) return d;
+    const std::string &v = it->second;
+    if (v.empty() || v == "1" || v == "true" || v == "yes" || v == "on" || v == "True" || v == "TRUE") return true;
+    return false;
+}
+
+// =============================================================== timers ===
+Timers::~Timers() {
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+}
+hipEvent_t Timers::ev() {
+    if (next == pool.size()) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        pool.push_back(e);
+    }
+    return pool[next++];
+}
+void Timers::begin(int cat) {
+    if (!enabled) return;
+    hipEvent_t e = ev();
+    HIPCHK(hipEventRecord(e, st));
+    open_stack.push_back(cat);
+    open_ev.push_back(e);
+}
+void Timers::end(int cat) {
+    if (!enabled) return;
+    if (open_stack.empty() || open_stack.back() != cat) throw Error("timer nesting error");
+    hipEvent_t e = ev();
+    HIPCHK(hipEventRecord(e, st));
+    pending.push_back({cat, open_ev.back(), e});
+    open_stack.pop_back();
+    open_ev.pop_back();
+}
+void Timers::flush() {
+    for (auto &p : pending) {
+        float ms = 0.f;
+        HIPCHK(hipEventSynchronize(p.b));
+        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        acc[p.cat] += ms * 1e-3;
+    }
+    pending.clear();
+    if (open_stack.empty()) next = 0;
+}
+
+void MatOp::apply(const double *x, double *y, Ctx &c) {
+    if (timers) timers->begin(T_SPMV);
+    spmv(*M, x, y, c);
+    if (timers) { timers->end(T_SPMV); timers->spmv_calls++; }
+}
+
+// ====================================================== preconditioners ===
+void PCNone::apply(const double *x, double *y, Ctx &c) {
+    if (x != y) launch_copy(n, x, y, c.st);
+}
+
+static void __attribute__((unused)) dummy() {}
+
+PCJacobi::PCJacobi(const DevCSR &M, Ctx &c) {
+    type = "jacobi";
+    n = M.nrows;
+    // diag from host copy of the diagonal (setup only)
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> ci(M.nnz);
+    std::vector<double> v(M.nnz);
+    HIPCHK(hipMemcpyAsync(rp.data(), M.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, c.st));
+    if (M.nnz) {
+        HIPCHK(hipMemcpyAsync(ci.data(), M.ci.p, sizeof(int32_t) * M.nnz, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipMemcpyAsync(v.data(), M.val.p, sizeof(double) * M.nnz, hipMemcpyDeviceToHost, c.st));
+    }
+    c.sync();
+    std::vector<double> d(n, 1.0);
+    for (int64_t i = 0; i < n; ++i) {
+        double di = 0.0;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k)
+            if (ci[k] == i) { di = v[k]; break; }
+        d[i] = (di == 0.0) ? 1.0 : 1.0 / di;
+    }
+    dinv.alloc(std::max<int64_t>(n, 1));
+    HIPCHK(hipMemcpyAsync(dinv.p, d.data(), sizeof(double) * n, hipMemcpyHostToDevice, c.st));
+    c.sync();
+}
+void PCJacobi::apply(const double *x, double *y, Ctx &c) { launch_pointwise_mult(n, x, dinv.p, y, c.st); }
+
+static int choose_lpr(double mean) {
+    if (mean >= 96.0) return 64;
+    if (mean >= 40.0) return 32;
+    if (mean >= 16.0) return 16;
+    if (mean >= 6.0) return 8;
+    return 4;
+}
+
+// levels of the strict lower (upper) dependency graph; counting sort into order
+static int64_t level_order(int64_t n, const std::vector<int64_t> &rp, const std::vector<int32_t> &ci, bool upper,
+                           std::vector<int32_t> &order, std::vector<int64_t> &ptr) {
+    std::vector<int32_t> lvl(n, 0);
+    int64_t nl = 0;
+    if (!upper) {
+        for (int64_t i = 0; i < n; ++i) {
+            int32_t L = 0;
+            for (int64_t k = rp[i]; k < rp[i + 1] && ci[k] < i; ++k) L = std::max(L, lvl[ci[k]] + 1);
+            lvl[i] = L;
+            nl = std::max<int64_t>(nl, L + 1);
+        }
+    } else {
+        for (int64_t i = n - 1; i >= 0; --i) {
+            int32_t L = 0;
+            for (int64_t k = rp[i + 1] - 1; k >= rp[i] && ci[k] > i; --k) L = std::max(L, lvl[ci[k]] + 1);
+            lvl[i] = L;
+            nl = std::max<int64_t>(nl, L + 1);
+        }
+    }
+    ptr.assign(nl + 1, 0);
+    for (int64_t i = 0; i < n; ++i) ptr[lvl[i] + 1]++;
+    for (int64_t l = 0; l < nl; ++l) ptr[l + 1] += ptr[l];
+    order.assign(n, 0);
+    std::vector<int64_t> pos(ptr.begin(), ptr.end() - 1);
+    for (int64_t i = 0; i < n; ++i) order[pos[lvl[i]]++] = (int32_t)i;
+    return nl;
+}
+
+static void build_level_factor(const PCILU &P, const std::vector<int32_t> &order, bool upper, DevCSR &out,
+                               DBuf<int32_t> &rows_dev, Ctx &c) {
+    const int64_t n = P.F.nrows;
+    rows_dev.alloc(std::max<int64_t>(n, 1));
+    HIPCHK(hipMemcpyAsync(rows_dev.p, order.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+    DBuf<int64_t> len(n + 1);
+    launch_lvl_count(n, rows_dev.p, P.F.rp.p, P.diag.p, upper ? 1 : 0, len.p, c.st);
+    out.rp.alloc(n + 1);
+    c.ensure_scan(n);
+    exclusive_scan_i64(len.p, out.rp.p, n, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
+    int64_t nnz = 0;
+    HIPCHK(hipMemcpyAsync(&nnz, out.rp.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    out.nrows = n;
+    out.ncols = n;
+    out.nnz = nnz;
+    out.ci.alloc(std::max<int64_t>(nnz, 1));
+    out.val.alloc(std::max<int64_t>(nnz, 1));
+    launch_lvl_fill(n, rows_dev.p, P.F.rp.p, P.F.ci.p, P.F.val.p, P.diag.p, upper ? 1 : 0, out.rp.p, out.ci.p,
+                    out.val.p, c.st);
+    HIPCHK(hipGetLastError());
+}
+
+PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
+    type = nb > 1 ? "bjacobi" : "ilu";
+    n = M.nrows;
+    nblocks = std::max<int64_t>(1, std::min<int64_t>(nb, n));
+    WindowSpec w{};
+    if (nblocks > 1) {
+        w.mode = 1;
+        w.nblocks = nblocks;
+    } else {
+        w.mode = 0;
+        w.c0 = 0;
+        w.c1 = M.ncols;
+    }
+    extract_csr(M, 0, n, w, 0, n, F, c);
+    if (F.max_row * 12 > 65536) throw Error("ILU(0): row too long for the LDS-staged factorization");
+    diag.alloc(std::max<int64_t>(n, 1));
+    dinv.alloc(std::max<int64_t>(n, 1));
+    DBuf<int32_t> fail(1);
+    HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
+    launch_find_diag(n, F.rp.p, F.ci.p, diag.p, fail.p, c.st);
+    // host copy of the pattern for the level schedule
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> ci(F.nnz);
+    HIPCHK(hipMemcpyAsync(rp.data(), F.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, c.st));
+    if (F.nnz) HIPCHK(hipMemcpyAsync(ci.data(), F.ci.p, sizeof(int32_t) * F.nnz, hipMemcpyDeviceToHost, c.st));
+    int32_t hfail = 0;
+    HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    if (hfail) throw Error("ILU(0): missing diagonal entry (PETSc: MAT_FACTOR_STRUCT_ZEROPIVOT)");
+    std::vector<int32_t> ordL, ordU;
+    nlev_L = level_order(n, rp, ci, false, ordL, Lptr);
+    nlev_U = level_order(n, rp, ci, true, ordU, Uptr);
+    // numeric factorization, level by level (dependencies = forward sweep)
+    DBuf<int32_t> rowsL(std::max<int64_t>(n, 1));
+    HIPCHK(hipMemcpyAsync(rowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+    for (int64_t l = 0; l < nlev_L; ++l)
+        launch_ilu0_level(Lptr[l + 1] - Lptr[l], rowsL.p + Lptr[l], F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p, fail.p,
+                          c.st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    if (hfail) throw Error("ILU(0): zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+    build_level_factor(*this, ordL, false, L, Lrow, c);
+    build_level_factor(*this, ordU, true, U, Urow, c);
+    Udinv.alloc(std::max<int64_t>(n, 1));
+    // Udinv[r] = dinv[Urow[r]]
+    {
+        DBuf<int64_t> idx(std::max<int64_t>(n, 1));
+        std::vector<int64_t> h(ordU.begin(), ordU.end());
+        HIPCHK(hipMemcpyAsync(idx.p, h.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c.st));
+        launch_gather(n, idx.p, dinv.p, Udinv.p, c.st);
+        c.sync();
+    }
+    lpr_L = choose_lpr(n ? (double)L.nnz / n : 0.0);
+    lpr_U = choose_lpr(n ? (double)U.nnz / n : 0.0);
+}
+
+void PCILU::apply(const double *x, double *y, Ctx &c) {
+    for (int64_t l = 0; l < nlev_L; ++l)
+        launch_trsv_level(Lptr[l], Lptr[l + 1], Lrow.p, L.rp.p, L.ci.p, L.val.p, nullptr, x, y, lpr_L, c.st);
+    for (int64_t l = 0; l < nlev_U; ++l)
+        launch_trsv_level(Uptr[l], Uptr[l + 1], Urow.p, U.rp.p, U.ci.p, U.val.p, Udinv.p, y, y, lpr_U, c.st);
+}
+
+std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
+                            Ctx &c) {
+    if (type == "none") return std::make_unique<PCNone>(M.nrows);
+    if (type == "jacobi") return std::make_unique<PCJacobi>(M, c);
+    if (type == "ilu") {
+        if (o.integer(prefix + "pc_factor_levels", 0) != 0)
+            throw Error(prefix + "pc_factor_levels > 0: only ILU(0) is implemented");
+        return std::make_unique<PCILU>(M, 1, c);
+    }
+    if (type == "bjacobi") {
+        const int64_t nb = o.integer(prefix + "pc_bjacobi_blocks", 1);
+        const std::string sub = o.str(prefix + "sub_pc_type", "ilu");
+        if (sub == "ilu") {
+            if (o.integer(prefix + "sub_pc_factor_levels", 0) != 0)
+                throw Error(prefix + "sub_pc_factor_levels > 0: only ILU(0) is implemented");
+            return std::make_unique<PCILU>(M, nb, c);
+        }
+        if (sub == "jacobi") return std::make_unique<PCJacobi>(M, c);
+        if (sub == "none") return std::make_unique<PCNone>(M.nrows);
+        throw Error(prefix + "sub_pc_type " + sub + " is not available on the device");
+    }
+    throw Error("PC type '" + type + "' (prefix " + prefix +
+                ") is not available in this build (supported: none, jacobi, ilu, bjacobi)");
+}
+
+// ================================================================= KSP ===
+void KSP::resolve_side_norm(const std::string &side, const std::string &nt) {
+    // KSPSetUpNorms_Private for the types implemented here
+    if (type == "preonly") {
+        right = false;
+        norm = "none";
+        return;
+    }
+    if (type == "gmres") {
+        std::string s = side;
+        if (s.empty()) s = (nt == "unpreconditioned") ? "right" : "left";
+        std::string nn = nt;
+        if (nn.empty()) nn = (s == "right") ? "unpreconditioned" : "preconditioned";
+        const bool ok = (s == "left" && (nn == "preconditioned" || nn == "none")) ||
+                        (s == "right" && (nn == "unpreconditioned" || nn == "none"));
+        if (!ok) throw Error("KSPGMRES (" + prefix + ") does not support norm " + nn + " with pc side " + s);
+        right = (s == "right");
+        norm = nn;
+        return;
+    }
+    if (type == "cg") {
+        if (!side.empty() && side != "left") throw Error("KSPCG (" + prefix + ") supports only left preconditioning");
+        right = false;
+        norm = nt.empty() ? "preconditioned" : nt;
+        if (norm != "preconditioned" && norm != "unpreconditioned" && norm != "none")
+            throw Error("KSPCG (" + prefix + "): unsupported norm type " + norm);
+        return;
+    }
+    throw Error("KSP type '" + type + "' (prefix " + prefix + ") is not available (supported: gmres, cg, preonly)");
+}
+
+void KSP::ensure_work(Ctx &) {
+    if (type == "gmres") {
+        if (allocated_k != restart) {
+            V.alloc((size_t)(restart + 1) * n);
+            t1.alloc(n);
+            t2.alloc(n);
+            dh.alloc(restart + 4);
+            allocated_k = restart;
+        }
+    } else if (type == "cg") {
+        if (allocated_k != 0) {
+            t1.alloc(n);  // r
+            t2.alloc(n);  // z
+            t3.alloc(n);  // p
+            t4.alloc(n);  // w
+            allocated_k = 0;
+        }
+    }
+}
+
+int KSP::converged(int it, double r) {
+    if (it == 0) {
+        rnorm0 = r;
+        ttol = std::max(rtol * rnorm0, atol);
+    }
+    if (std::isnan(r) || std::isinf(r)) return DIVERGED_NANORINF;
+    if (r <= ttol) return r < atol ? CONVERGED_ATOL : CONVERGED_RTOL;
+    if (r >= dtol * rnorm0) return DIVERGED_DTOL;
+    return CONVERGED_ITERATING;
+}
+
+void KSP::solve(const double *b, double *x, Ctx &c) {
+    history.clear();
+    if (type == "preonly") {
+        pc->apply(b, x, c);
+        its = 1;
+        reason = CONVERGED_ITS;
+        return;
+    }
+    ensure_work(c);
+    if (type == "gmres") return solve_gmres(b, x, c);
+    if (type == "cg") return solve_cg(b, x, c);
+    throw Error("KSP type " + type + " not available");
+}
+
+void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
+    const int64_t mk = restart;
+    const double haptol = 1e-30;
+    std::vector<double> HH((mk + 1) * (mk + 1), 0.0), cc(mk + 1, 0.0), ss(mk + 1, 0.0), grs(mk + 2, 0.0),
+        nrs(mk + 1, 0.0);
+    auto H = [&](int64_t i, int64_t j) -> double & { return HH[(size_t)i * (mk + 1) + j]; };
+    double *t1p = t1.p, *t2p = t2.p;
+    launch_set(n, 0.0, x, c.st);
+    its = 0;
+    reason = 0;
+    bool first = true;
+    while (!reason) {
+        double *v0 = V.p;
+        if (first) {
+            launch_copy(n, b, right ? v0 : t1p, c.st);
+        } else {
+            A->apply(x, t2p, c);
+            launch_waxpby(n, 1.0, b, -1.0, t2p, right ? v0 : t1p, c.st);
+        }
+        if (!right) pc->apply(t1p, v0, c);
+        double res = c.norm2(n, v0);
+        history.push_back(res);
+        if (monitor) printf("  %3d KSP Residual norm %.12e\n", its, res);
+        if (res == 0.0) {
+            reason = CONVERGED_ATOL;
+            rnorm = 0.0;
+            break;
+        }
+        launch_scale(n, 1.0 / res, v0, c.st);
+        reason = converged(its, res);
+        rnorm = res;
+        std::fill(HH.begin(), HH.end(), 0.0);
+        grs.assign(mk + 2, 0.0);
+        grs[0] = res;
+        int64_t loc_it = 0;
+        while (!reason && loc_it < mk && its < maxit) {
+            double *vk = V.p + loc_it * n;
+            double *vn = V.p + (loc_it + 1) * n;
+            if (right) {
+                pc->apply(vk, t1p, c);
+                A->apply(t1p, vn, c);
+            } else {
+                A->apply(vk, t1p, c);
+                pc->apply(t1p, vn, c);
+            }
+            const int k = (int)(loc_it + 1);
+            launch_mdot(n, k, nullptr, V.p, n, vn, c.partial.p, dh.p, c.st);
+            launch_maxpy_norm(n, k, V.p, n, dh.p, -1.0, vn, c.partial.p, dh.p + k, c.st);
+            HIPCHK(hipMemcpyAsync(c.hscal, dh.p, sizeof(double) * (k + 1), hipMemcpyDeviceToHost, c.st));
+            c.sync();
+            for (int j = 0; j < k; ++j) H(j, loc_it) = c.hscal[j];
+            const double tt = c.hscal[k];
+            H(loc_it + 1, loc_it) = tt;
+            double hapbnd = std::fabs(tt / grs[loc_it]);
+            if (hapbnd > haptol) hapbnd = haptol;
+            const bool hapend = tt < hapbnd;
+            if (!hapend) launch_scale(n, 1.0 / tt, vn, c.st);
+            // KSPGMRESUpdateHessenberg
+            const int64_t it = loc_it;
+            for (int64_t j = 0; j < it; ++j) {
+                const double t0 = H(j, it);
+                H(j, it) = cc[j] * t0 + ss[j] * H(j + 1, it);
+                H(j + 1, it) = cc[j] * H(j + 1, it) - ss[j] * t0;
+            }
+            if (!hapend) {
+                const double t0 = std::sqrt(H(it, it) * H(it, it) + H(it + 1, it) * H(it + 1, it));
+                if (t0 == 0.0) {
+                    reason = DIVERGED_NULL;
+                    break;
+                }
+                cc[it] = H(it, it) / t0;
+                ss[it] = H(it + 1, it) / t0;
+                grs[it + 1] = -(ss[it] * grs[it]);
+                grs[it] = cc[it] * grs[it];
+                H(it, it) = cc[it] * H(it, it) + ss[it] * H(it + 1, it);
+                res = std::fabs(grs[it + 1]);
+            } else {
+                res = 0.0;
+            }
+            loc_it++;
+            its++;
+            rnorm = res;
+            history.push_back(res);
+            if (monitor) printf("  %3d KSP Residual norm %.12e\n", its, res);
+            reason = converged(its, res);
+            if (hapend && !reason) {
+                reason = DIVERGED_BREAKDOWN;
+                break;
+            }
+        }
+        // KSPGMRESBuildSoln
+        const int64_t it = loc_it - 1;
+        if (it >= 0) {
+            if (H(it, it) == 0.0) {
+                reason = DIVERGED_BREAKDOWN;
+            } else {
+                nrs[it] = grs[it] / H(it, it);
+                for (int64_t k = it - 1; k >= 0; --k) {
+                    double t0 = grs[k];
+                    for (int64_t j = k + 1; j <= it; ++j) t0 = t0 - H(k, j) * nrs[j];
+                    nrs[k] = t0 / H(k, k);
+                }
+                HIPCHK(hipMemcpyAsync(dh.p, nrs.data(), sizeof(double) * (it + 1), hipMemcpyHostToDevice, c.st));
+                launch_lincomb(n, (int)(it + 1), V.p, n, dh.p, t2p, c.st);
+                if (right) {
+                    pc->apply(t2p, t1p, c);
+                    launch_axpby(n, 1.0, t1p, 1.0, x, c.st);
+                } else {
+                    launch_axpby(n, 1.0, t2p, 1.0, x, c.st);
+                }
+                c.sync();  // nrs host buffer reuse
+            }
+        }
+        if (its >= maxit) {
+            if (!reason) reason = DIVERGED_ITS;
+            break;
+        }
+        first = false;
+    }
+}
+
+void KSP::solve_cg(const double *b, double *x, Ctx &c) {
+    double *r = t1.p, *z = t2.p, *p = t3.p, *w = t4.p;
+    launch_set(n, 0.0, x, c.st);
+    launch_copy(n, b, r, c.st);
+    double dp = 0.0;
+    if (norm == "preconditioned") {
+        pc->apply(r, z, c);
+        dp = c.norm2(n, z);
+    } else if (norm == "unpreconditioned") {
+        dp = c.norm2(n, r);
+    }
+    history.push_back(dp);
+    if (monitor) printf("  %3d KSP Residual norm %.12e\n", 0, dp);
+    rnorm = dp;
+    its = 0;
+    reason = (norm != "none") ? converged(0, dp) : 0;
+    if (reason) return;
+    if (norm != "preconditioned") pc->apply(r, z, c);
+    double beta = c.dot(n, z, r), betaold = 0.0, dpi = 0.0, dpiold = 0.0;
+    int64_t i = 0;
+    while (true) {
+        its = (int)(i + 1);
+        if (beta == 0.0) {
+            reason = CONVERGED_ATOL;
+            break;
+        }
+        if (i == 0) launch_copy(n, z, p, c.st);
+        else launch_axpby(n, 1.0, z, beta / betaold, p, c.st);
+        dpiold = dpi;
+        A->apply(p, w, c);
+        dpi = c.dot(n, p, w);
+        betaold = beta;
+        auto sgn = [](double v) { return (v > 0) - (v < 0); };
+        if (dpi == 0.0 || (i > 0 && sgn(dpi) * sgn(dpiold) < 0)) {
+            reason = DIVERGED_INDEFINITE_MAT;
+            break;
+        }
+        const double a = beta / dpi;
+        launch_axpby(n, a, p, 1.0, x, c.st);
+        launch_axpby(n, -a, w, 1.0, r, c.st);
+        if (norm == "preconditioned") {
+            pc->apply(r, z, c);
+            dp = c.norm2(n, z);
+        } else if (norm == "unpreconditioned") {
+            dp = c.norm2(n, r);
+        } else {
+            dp = 0.0;
+        }
+        rnorm = dp;
+        history.push_back(dp);
+        if (monitor) printf("  %3d KSP Residual norm %.12e\n", (int)(i + 1), dp);
+        if (norm != "none") reason = converged((int)(i + 1), dp);
+        if (reason) break;
+        if (norm != "preconditioned") pc->apply(r, z, c);
+        beta = c.dot(n, z, r);
+        i++;
+        if (i >= maxit) break;
+    }
+    if (i >= maxit && !reason) reason = DIVERGED_ITS;
+}
+
+std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const DevCSR *Amat, const DevCSR *Pmat,
+                              const std::string &default_ksp, const std::string &default_pc, Ctx &c, double rtol,
+                              double atol, double dtol, int64_t maxit, int64_t restart, PC *external_pc) {
+    auto k = std::make_unique<KSP>();
+    k->prefix = prefix;
+    k->type = o.str(prefix + "ksp_type", default_ksp);
+    k->rtol = o.num(prefix + "ksp_rtol", rtol);
+    k->atol = o.num(prefix + "ksp_atol", atol);
+    k->dtol = o.num(prefix + "ksp_divtol", dtol);
+    k->maxit = o.integer(prefix + "ksp_max_it", maxit);
+    k->restart = o.integer(prefix + "ksp_gmres_restart", restart);
+    k->monitor = o.has(prefix + "ksp_monitor");
+    if (o.has(prefix + "ksp_gmres_modifiedgramschmidt") && k->type == "gmres")
+        throw Error(prefix + "ksp_gmres_modifiedgramschmidt: only classical Gram-Schmidt is implemented");
+    k->resolve_side_norm(o.str(prefix + "ksp_pc_side", ""), o.str(prefix + "ksp_norm_type", ""));
+    if (Amat) {
+        k->owned_op = std::make_unique<MatOp>(Amat);
+        k->A = k->owned_op.get();
+        k->n = Amat->nrows;
+    }
+    if (external_pc) {
+        k->pc = external_pc;
+    } else {
+        k->owned_pc = make_pc(o.str(prefix + "pc_type", default_pc), *Pmat, o, prefix, c);
+        k->pc = k->owned_pc.get();
+    }
+    return k;
+}
+
+}  // namespace pls

@@ -1,0 +1,220 @@
+// runtime.hpp -- host runtime of libpls.so: device memory, options database,
+// operators, preconditioners, Krylov solvers, the block preconditioner and
+// AAR.  The Krylov loops run on the host over device-resident vectors; every
+// vector operation is a HIP kernel on one stream, and the only device->host
+// traffic per outer iteration is the handful of scalars the PETSc algorithms
+// branch on (Hessenberg column, norms).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+
+namespace pls {
+
+struct Error : std::runtime_error {
+    explicit Error(const std::string &m) : std::runtime_error(m) {}
+};
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess)                                                                       \
+            throw ::pls::Error(std::string(#x) + " failed: " + hipGetErrorString(e_) + " at " +    \
+                               __FILE__ + ":" + std::to_string(__LINE__));                          \
+    } while (0)
+
+// ------------------------------------------------------------ device buffer --
+template <class T>
+struct DBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DBuf() = default;
+    explicit DBuf(size_t count) { alloc(count); }
+    DBuf(const DBuf &) = delete;
+    DBuf &operator=(const DBuf &) = delete;
+    DBuf(DBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DBuf &operator=(DBuf &&o) noexcept {
+        if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+        return *this;
+    }
+    ~DBuf() { release(); }
+    void alloc(size_t count) {
+        release();
+        n = count;
+        if (count) HIPCHK(hipMalloc((void **)&p, sizeof(T) * count));
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    T *get() const { return p; }
+};
+
+// ------------------------------------------------------------------ context --
+struct Ctx {
+    hipStream_t st = nullptr;
+    DBuf<double> partial;   // reduction partials (NB_MAX * 136)
+    DBuf<double> dscal;     // device scalars
+    double *hscal = nullptr;  // pinned host mirror
+    DBuf<char> scan_tmp;
+    size_t scan_tmp_bytes = 0;
+    Ctx();
+    ~Ctx();
+    void sync() { HIPCHK(hipStreamSynchronize(st)); }
+    void ensure_scan(int64_t n);
+    // deterministic reductions returning host values (synchronising)
+    double dot(int64_t n, const double *x, const double *y);
+    double norm2(int64_t n, const double *x);
+};
+
+// ------------------------------------------------------------------ matrix --
+struct DevCSR {
+    int64_t nrows = 0, ncols = 0, nnz = 0;
+    DBuf<int64_t> rp;
+    DBuf<int32_t> ci;
+    DBuf<double> val;
+    int64_t max_row = 0;
+};
+
+void upload_csr(DevCSR &M, int64_t nrows, int64_t ncols, const int64_t *rp, const int32_t *ci, const double *val,
+                Ctx &c);
+// Extract rows [r0, r1) with a column window (see WindowSpec), columns shifted.
+void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_t cshift, int64_t ncols,
+                 DevCSR &dst, Ctx &c);
+void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha = 1.0, double beta = 0.0,
+          const double *z = nullptr);
+
+// ----------------------------------------------------------------- options --
+struct Options {
+    std::map<std::string, std::string> kv;
+    void parse(const char *text);
+    bool has(const std::string &k) const { return kv.count(k) > 0; }
+    std::string str(const std::string &k, const std::string &d) const;
+    double num(const std::string &k, double d) const;
+    int64_t integer(const std::string &k, int64_t d) const;
+    bool flag(const std::string &k, bool d) const;
+};
+
+// -------------------------------------------------------------- timer pool --
+enum TimerCat { T_PC_TOTAL = 0, T_PC_SOLID, T_PC_FLUID, T_PC_PRESS, T_PC_ALLOC, T_SOLVER, T_SPMV, T_NCAT };
+struct Timers {
+    double acc[T_NCAT] = {0};
+    int64_t spmv_calls = 0;
+    bool enabled = true;
+    std::vector<hipEvent_t> pool;
+    struct Pending { int cat; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<int> open_stack;
+    std::vector<hipEvent_t> open_ev;
+    size_t next = 0;
+    hipStream_t st = nullptr;
+    ~Timers();
+    hipEvent_t ev();
+    void begin(int cat);
+    void end(int cat);
+    void flush();  // call after a stream sync
+    void reset() { for (double &a : acc) a = 0; spmv_calls = 0; }
+};
+
+// --------------------------------------------------------------- operators --
+struct Op {
+    int64_t n = 0;
+    virtual ~Op() = default;
+    virtual void apply(const double *x, double *y, Ctx &c) = 0;
+};
+struct MatOp : Op {
+    const DevCSR *M;
+    Timers *timers = nullptr;
+    explicit MatOp(const DevCSR *m) : M(m) { n = m->nrows; }
+    void apply(const double *x, double *y, Ctx &c) override;
+};
+
+// --------------------------------------------------------- preconditioners --
+struct PC {
+    std::string type;
+    int64_t n = 0;
+    virtual ~PC() = default;
+    virtual void apply(const double *x, double *y, Ctx &c) = 0;
+};
+struct PCNone : PC {
+    explicit PCNone(int64_t n_) { type = "none"; n = n_; }
+    void apply(const double *x, double *y, Ctx &c) override;
+};
+struct PCJacobi : PC {
+    DBuf<double> dinv;
+    PCJacobi(const DevCSR &M, Ctx &c);
+    void apply(const double *x, double *y, Ctx &c) override;
+};
+// ILU(0) of the block-Jacobi truncation of M (nblocks == 1: plain ILU(0)).
+struct PCILU : PC {
+    int64_t nblocks = 1;
+    DevCSR F;                     // truncated matrix, factored in place
+    DBuf<int64_t> diag;
+    DBuf<double> dinv;
+    // level-ordered strict lower / strict upper factors
+    DevCSR L, U;
+    DBuf<int32_t> Lrow, Urow;     // original row of each level-ordered row
+    DBuf<double> Udinv;           // dinv in U level order
+    std::vector<int64_t> Lptr, Uptr;  // level boundaries (rows)
+    int lpr_L = 8, lpr_U = 8;
+    int64_t nlev_L = 0, nlev_U = 0;
+    PCILU(const DevCSR &M, int64_t nblocks, Ctx &c);
+    void apply(const double *x, double *y, Ctx &c) override;
+};
+std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
+                            Ctx &c);
+
+// ---------------------------------------------------------------------- KSP --
+enum Reason {
+    CONVERGED_ITERATING = 0, CONVERGED_RTOL = 2, CONVERGED_ATOL = 3, CONVERGED_ITS = 4,
+    DIVERGED_NULL = -2, DIVERGED_ITS = -3, DIVERGED_DTOL = -4, DIVERGED_BREAKDOWN = -5,
+    DIVERGED_INDEFINITE_MAT = -8, DIVERGED_NANORINF = -9
+};
+
+struct KSP {
+    std::string prefix, type = "gmres";
+    double rtol = 1e-5, atol = 1e-50, dtol = 1e4;
+    int64_t maxit = 10000, restart = 30;
+    bool right = false;
+    std::string norm = "preconditioned";
+    Op *A = nullptr;
+    PC *pc = nullptr;
+    std::unique_ptr<PC> owned_pc;
+    std::unique_ptr<Op> owned_op;
+    int64_t n = 0;
+    // results
+    int its = 0, reason = 0;
+    double rnorm = 0;
+    std::vector<double> history;
+    bool keep_history = true;
+    bool monitor = false;
+    // work
+    DBuf<double> V, w, t1, t2, t3, t4;
+    DBuf<double> dh;  // device Hessenberg column / coefficients
+    int64_t allocated_k = -1;
+    void set_type_defaults();
+    void resolve_side_norm(const std::string &side, const std::string &nt);
+    void solve(const double *b, double *x, Ctx &c);
+  private:
+    void ensure_work(Ctx &c);
+    void solve_gmres(const double *b, double *x, Ctx &c);
+    void solve_cg(const double *b, double *x, Ctx &c);
+    int converged(int it, double r);
+    double rnorm0 = 0, ttol = 0;
+};
+
+// Configure a KSP from programmatic defaults + options (setFromOptions order).
+std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const DevCSR *Amat, const DevCSR *Pmat,
+                              const std::string &default_ksp, const std::string &default_pc, Ctx &c,
+                              double rtol = 1e-5, double atol = 1e-50, double dtol = 1e4, int64_t maxit = 10000,
+                              int64_t restart = 30, PC *external_pc = nullptr);
+
+}  // namespace pls

@@ -1,0 +1,167 @@
+"""Owning wrapper of a ``pls_handle`` (include/pls.h)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+
+def params_to_options(parameters: dict) -> dict:
+    """The reference's parameter dict -> ``pls.*`` option keys."""
+    keymap = {
+        "solver type": "pls.solver_type", "solver atol": "pls.solver_atol", "solver rtol": "pls.solver_rtol",
+        "solver maxiter": "pls.solver_maxiter", "solver monitor": "pls.solver_monitor",
+        "pc type": "pls.pc_type", "inner ksp type": "pls.inner_ksp_type", "inner pc type": "pls.inner_pc_type",
+        "inner rtol": "pls.inner_rtol", "inner atol": "pls.inner_atol", "inner maxiter": "pls.inner_maxiter",
+        "inner monitor": "pls.inner_monitor", "inner accel order": "pls.inner_accel_order",
+        "AAR order": "pls.aar_order", "AAR p": "pls.aar_p", "AAR omega": "pls.aar_omega", "AAR beta": "pls.aar_beta",
+    }
+    out = {}
+    for k, v in parameters.items():
+        if k in keymap:
+            if isinstance(v, bool):
+                v = "1" if v else "0"
+            out[keymap[k]] = str(v).replace(" ", "_")
+    return out
+
+
+def options_text(d: dict) -> bytes:
+    lines = []
+    for k, v in d.items():
+        lines.append(k if v is None else f"{k} {v}")
+    return "\n".join(lines).encode()
+
+
+class Handle:
+    def __init__(self, ptr: C.c_void_p):
+        self.ptr = ptr
+        n, ns, nf, np_, nnz = (C.c_int64() for _ in range(5))
+        N.check(N.lib().pls_get_sizes(ptr, C.byref(n), C.byref(ns), C.byref(nf), C.byref(np_), C.byref(nnz)))
+        self.n, self.ns, self.nf, self.np, self.nnz_A = n.value, ns.value, nf.value, np_.value, nnz.value
+
+    # ----------------------------------------------------------- creation --
+    @classmethod
+    def from_csr(cls, A, P, P_diff, is_s, is_f, is_p, bcs_sub_pressure, options: dict):
+        keep = []
+
+        def mk(M):
+            if M is None:
+                return None
+            ai, aj, av, nr, nc = N.csr_of(M)
+            keep.extend([ai, aj, av])
+            return N.pls_csr(nr, nc, ai.ctypes.data, aj.ctypes.data, av.ctypes.data)
+
+        cA, cP, cD = mk(A), mk(P), mk(P_diff)
+        is_s, is_f, is_p = N.is_array(is_s), N.is_array(is_f), N.is_array(is_p)
+        bcs = np.ascontiguousarray(np.asarray(bcs_sub_pressure if bcs_sub_pressure is not None else [],
+                                              dtype=np.int32))
+        out = C.c_void_p()
+        N.check(N.lib().pls_create(C.byref(cA), C.byref(cP), C.byref(cD) if cD is not None else None,
+                                   N.ptr(is_s), is_s.size, N.ptr(is_f), is_f.size, N.ptr(is_p), is_p.size,
+                                   N.ptr(bcs), bcs.size, options_text(options), C.byref(out)))
+        return cls(out)
+
+    @classmethod
+    def synthetic(cls, dim, Nel, seed, delta, options: dict):
+        spec = N.pls_synth_spec(int(dim), int(Nel), int(seed), float(delta))
+        out = C.c_void_p()
+        N.check(N.lib().pls_create_synthetic(C.byref(spec), options_text(options), C.byref(out)))
+        return cls(out)
+
+    # ------------------------------------------------------------- control --
+    def set_option(self, key, value=None):
+        N.check(N.lib().pls_set_option(self.ptr, str(key).encode(), None if value is None else str(value).encode()))
+
+    def setup(self):
+        N.check(N.lib().pls_setup(self.ptr))
+
+    def create_solver(self):
+        N.check(N.lib().pls_create_solver(self.ptr))
+
+    def destroy(self):
+        if self.ptr:
+            N.lib().pls_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------- host vectors --
+    def pc_apply(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.empty_like(x)
+        N.check(N.lib().pls_pc_apply(self.ptr, N.ptr(x), N.ptr(y)))
+        return y
+
+    def matmult(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.empty_like(x)
+        N.check(N.lib().pls_matmult(self.ptr, N.ptr(x), N.ptr(y)))
+        return y
+
+    def solve(self, b):
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        x = np.empty_like(b)
+        r = N.pls_result()
+        N.check(N.lib().pls_solve(self.ptr, N.ptr(b), N.ptr(x), C.byref(r)))
+        return x, r
+
+    # ------------------------------------------------------- device vectors --
+    def solve_device(self, d_b, d_x):
+        r = N.pls_result()
+        N.check(N.lib().pls_solve_device(self.ptr, d_b, d_x, C.byref(r)))
+        return r
+
+    def pc_apply_device(self, d_x, d_y):
+        N.check(N.lib().pls_pc_apply_device(self.ptr, d_x, d_y))
+
+    def matmult_device(self, d_x, d_y):
+        N.check(N.lib().pls_matmult_device(self.ptr, d_x, d_y))
+
+    def rhs_device(self, seed, d_b):
+        N.check(N.lib().pls_synthetic_rhs_device(self.ptr, int(seed), d_b))
+
+    def bench_spmv(self, d_x, d_y, reps):
+        s = C.c_double()
+        N.check(N.lib().pls_bench_spmv(self.ptr, d_x, d_y, int(reps), C.byref(s)))
+        return s.value
+
+    # -------------------------------------------------------------- queries --
+    def result(self):
+        r = N.pls_result()
+        N.check(N.lib().pls_get_result(self.ptr, C.byref(r)))
+        return r
+
+    def history(self):
+        r = self.result()
+        h = np.zeros(max(r.history_len, 1), dtype=np.float64)
+        N.check(N.lib().pls_get_history(self.ptr, N.ptr(h), r.history_len))
+        return h[:r.history_len]
+
+    def timings(self):
+        t = N.pls_timings()
+        N.check(N.lib().pls_get_timings(self.ptr, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in t._fields_}
+
+    def reset_timings(self):
+        N.check(N.lib().pls_reset_timings(self.ptr))
+
+    def export_matrix(self, which=0):
+        import scipy.sparse as sp
+        nr, nnz = C.c_int64(), C.c_int64()
+        N.check(N.lib().pls_export_matrix(self.ptr, which, C.byref(nr), C.byref(nnz), None, None, None))
+        rp = np.zeros(nr.value + 1, dtype=np.int64)
+        ci = np.zeros(nnz.value, dtype=np.int32)
+        v = np.zeros(nnz.value, dtype=np.float64)
+        N.check(N.lib().pls_export_matrix(self.ptr, which, C.byref(nr), C.byref(nnz), N.ptr(rp), N.ptr(ci), N.ptr(v)))
+        return sp.csr_matrix((v, ci, rp), shape=(nr.value, nr.value))
+
+    def permutation(self):
+        p = np.zeros(self.n, dtype=np.int64)
+        N.check(N.lib().pls_get_permutation(self.ptr, N.ptr(p)))
+        return p

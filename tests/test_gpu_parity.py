@@ -1,0 +1,223 @@
+"""GPU parity: libpls.so (HIP, through the C-ABI) against the CPU oracle.
+
+Tolerances (north star: iteration counts bit-exact, residual norms within
+1e-10 relative):
+  * synthetic matrices / ILU(0) factors: bitwise equal (integer + rounding-
+    controlled fp64 arithmetic on both sides);
+  * SpMV / PC apply: <= 1e-13 relative (different summation order only);
+  * Krylov solves: identical iteration count and convergence reason, every
+    residual-history entry within RTOL_HIST = 1e-10 relative.
+"""
+import numpy as np
+import pytest
+
+from oracle import synthetic as S
+from oracle.solver import OracleSolver
+
+pytestmark = pytest.mark.gpu
+
+RTOL_HIST = 1e-10
+
+BASE = {"solver type": "gmres", "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": 300,
+        "pc type": "diagonal", "inner ksp type": "preonly", "inner pc type": "ilu", "inner rtol": 1e-6,
+        "inner atol": 0, "inner maxiter": 1000, "inner monitor": False, "solver monitor": False,
+        "inner accel order": 0, "AAR order": 10, "AAR p": 5, "AAR omega": 1, "AAR beta": 1}
+ILU_DB = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right",
+          "s_ksp_type": "preonly", "s_pc_type": "ilu", "f_ksp_type": "preonly", "f_pc_type": "ilu",
+          "p_ksp_type": "preonly", "p_pc_type": "ilu", "diff_ksp_type": "preonly", "diff_pc_type": "ilu",
+          "fp_ksp_type": "preonly", "fp_pc_type": "ilu"}
+
+
+def _handle(spec, params, db):
+    from lib.handle import Handle, params_to_options
+    opts = dict(db)
+    opts.update(params_to_options(params))
+    return Handle.synthetic(spec.dim, spec.N, spec.seed, spec.delta, opts)
+
+
+def _oracle(spec, params, db):
+    A, P, Pd = S.matrix(spec, 0), S.matrix(spec, 1), S.matrix(spec, 2)
+    is_s, is_f, is_p = S.field_major_index_sets(spec)
+    return OracleSolver(A, P, Pd, is_s, is_f, is_p, params, db, S.bcs_sub_pressure(spec))
+
+
+def _compare_solve(spec, upd=None, db=None):
+    params = dict(BASE)
+    params.update(upd or {})
+    db = dict(ILU_DB if db is None else db)
+    b = S.rhs(spec)
+    o = _oracle(spec, params, db)
+    xo = o.solve(b)
+    h = _handle(spec, params, db)
+    x, r = h.solve(b)
+    hist = h.history()
+    ho = np.asarray(o.history)
+    assert r.its == o.its, f"its {r.its} vs oracle {o.its}"
+    assert r.reason == o.reason, f"reason {r.reason} vs oracle {o.reason}"
+    assert hist.shape == ho.shape
+    rel = np.max(np.abs(hist - ho) / np.abs(ho))
+    assert rel <= RTOL_HIST, f"residual history rel diff {rel:.3e}"
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+    return r, o
+
+
+@pytest.mark.parametrize("dim,N", [(2, 4), (2, 9), (3, 2), (3, 3)])
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_synthetic_generator_bitwise(gpu, dim, N, variant):
+    spec = S.SynthSpec(dim, N)
+    h = _handle(spec, dict(BASE, **{"pc type": "diagonal 3-way"}), ILU_DB)
+    M = h.export_matrix(variant)
+    R = S.matrix(spec, variant)
+    assert np.array_equal(M.indptr, R.indptr)
+    assert np.array_equal(M.indices, R.indices)
+    assert np.array_equal(M.data, R.data)  # bitwise
+
+
+@pytest.mark.parametrize("dim,N", [(2, 12), (3, 4)])
+def test_spmv_matches_scipy(gpu, dim, N):
+    spec = S.SynthSpec(dim, N)
+    h = _handle(spec, BASE, ILU_DB)
+    A = S.matrix(spec, 0)
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal(A.shape[0])
+    y = h.matmult(x)
+    ref = A @ x
+    scale = abs(A) @ np.abs(x)
+    assert np.max(np.abs(y - ref) / scale) <= 1e-14
+
+
+@pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
+@pytest.mark.parametrize("inner", ["ilu", "jacobi", "bjacobi"])
+def test_pc_apply_matches_oracle(gpu, pc_type, inner):
+    spec = S.SynthSpec(2, 10)
+    params = dict(BASE, **{"pc type": pc_type})
+    db = dict(ILU_DB)
+    for pre in ("s_", "f_", "p_", "diff_", "fp_"):
+        db[pre + "pc_type"] = inner
+        if inner == "bjacobi":
+            db[pre + "pc_bjacobi_blocks"] = "3"
+    h = _handle(spec, params, db)
+    o = _oracle(spec, params, db)
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal(spec.n)
+    y = h.pc_apply(x)
+    yo = o.block_pc.apply(x)
+    assert np.max(np.abs(y - yo)) <= 1e-13 * np.max(np.abs(yo))
+
+
+def test_gmres_right_2way_ilu(gpu):
+    _compare_solve(S.SynthSpec(2, 16))
+
+
+def test_gmres_right_2way_ilu_3d(gpu):
+    _compare_solve(S.SynthSpec(3, 4))
+
+
+def test_gmres_left_default_norm(gpu):
+    db = {k: v for k, v in ILU_DB.items() if not k.startswith("global_")}
+    _compare_solve(S.SynthSpec(2, 12), db=db)
+
+
+def test_gmres_3way_ilu(gpu):
+    _compare_solve(S.SynthSpec(2, 12), {"pc type": "diagonal 3-way"})
+
+
+def test_gmres_bjacobi(gpu):
+    db = dict(ILU_DB)
+    for pre in ("s_", "fp_"):
+        db[pre + "pc_type"] = "bjacobi"
+        db[pre + "pc_bjacobi_blocks"] = "5"
+    _compare_solve(S.SynthSpec(2, 14), db=db)
+
+
+def test_gmres_jacobi(gpu):
+    db = dict(ILU_DB, s_pc_type="jacobi", fp_pc_type="jacobi")
+    _compare_solve(S.SynthSpec(2, 10), db=db)
+
+
+def test_gmres_restarted(gpu):
+    db = dict(ILU_DB, global_ksp_gmres_restart="7")
+    _compare_solve(S.SynthSpec(2, 10), db=db)
+
+
+def test_inner_cg_unpreconditioned(gpu):
+    db = dict(ILU_DB, s_ksp_type="cg", s_ksp_rtol="1e-1", s_ksp_norm_type="unpreconditioned",
+              fp_ksp_type="gmres", fp_ksp_rtol="1e-2", fp_pc_type="jacobi")
+    _compare_solve(S.SynthSpec(2, 10), db=db)
+
+
+def test_outer_maxit_diverged_its(gpu):
+    r, o = _compare_solve(S.SynthSpec(2, 10), {"solver maxiter": 4})
+    assert r.reason == -3 and r.its == 4
+
+
+def test_aar_ilu(gpu):
+    _compare_solve(S.SynthSpec(2, 10), {"solver type": "aar", "solver maxiter": 200})
+
+
+def test_aar_order5(gpu):
+    _compare_solve(S.SynthSpec(2, 8), {"solver type": "aar", "solver maxiter": 200, "AAR order": 5, "AAR p": 3})
+
+
+def test_inner_anderson_order1(gpu):
+    _compare_solve(S.SynthSpec(2, 8), {"inner accel order": 1})
+
+
+def test_interleaved_index_sets_host_path(gpu):
+    """pls_create with dolfin-like interleaved ordering + index sets."""
+    from lib.handle import Handle, params_to_options
+    spec = S.SynthSpec(2, 9)
+    perm = S.interleaving(spec)
+    A = S.permute(S.matrix(spec, 0), perm)
+    P = S.permute(S.matrix(spec, 1), perm)
+    Pd = S.permute(S.matrix(spec, 2), perm)
+    is_s, is_f, is_p = S.index_sets_for(perm, spec)
+    bcs = S.bcs_sub_pressure(spec)
+    b = S.rhs(spec)[perm]
+    for pc_type in ("diagonal", "diagonal 3-way"):
+        params = dict(BASE, **{"pc type": pc_type})
+        o = OracleSolver(A, P, Pd, is_s, is_f, is_p, params, ILU_DB, bcs)
+        xo = o.solve(b)
+        opts = dict(ILU_DB)
+        opts.update(params_to_options(params))
+        h = Handle.from_csr(A, P, Pd, is_s, is_f, is_p, bcs, opts)
+        x, r = h.solve(b)
+        assert r.its == o.its
+        ho = np.asarray(o.history)
+        assert np.max(np.abs(h.history() - ho) / np.abs(ho)) <= RTOL_HIST
+        assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+
+
+def test_facade_end_to_end(gpu):
+    """The reference call sequence (lib/Poromechanics.py:58-68,88-98) on the facades."""
+    from lib import options as popts
+    from lib.IndexSet import IndexSet
+    from lib.Parser import load_options_lines
+    from lib.Preconditioner import Preconditioner
+    from lib.Solver import Solver
+    spec = S.SynthSpec(2, 8)
+    A, P, Pd = S.matrix(spec, 0), S.matrix(spec, 1), S.matrix(spec, 2)
+    dofs = S.field_major_index_sets(spec)
+    popts.DB.clear()
+    load_options_lines([f"-{k} {v}" for k, v in ILU_DB.items()] + ["# comment -s_pc_type lu"])
+    params = dict(BASE)
+    index_map = IndexSet(dofs, two_way=True)
+    pc = Preconditioner(index_map, A, P, Pd, params, S.bcs_sub_pressure(spec)).get_pc()
+    b = S.rhs(spec)
+    solver = Solver(A, b, pc, params, index_map)
+    solver.create_solver(A, b, pc)
+    solver.set_up()
+    x = np.zeros_like(b)
+    solver.solve(b, x)
+    o = _oracle(spec, params, ILU_DB)
+    xo = o.solve(b)
+    assert solver.getIterationNumber() == o.its
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+    popts.DB.clear()
+
+
+def test_unsupported_pc_fails_loudly(gpu):
+    spec = S.SynthSpec(2, 4)
+    h = _handle(spec, BASE, dict(ILU_DB, s_pc_type="hypre"))
+    with pytest.raises(RuntimeError, match="hypre"):
+        h.setup()
