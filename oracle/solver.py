@@ -75,4 +75,14 @@ class OracleSolver:
 
     @property
     def reason(self):
-        return 0 if self.kind == "aar" else self.solver.reason
+        """KSP reason; for AAR the stop test that ended the loop (AAR.py:73):
+        CONVERGED_ATOL (3), CONVERGED_RTOL (2) or DIVERGED_ITS (-3)."""
+        if self.kind != "aar":
+            return self.solver.reason
+        s = self.solver
+        h = s.history
+        if h[-1] <= s.atol:
+            return 3
+        if h[-1] / h[0] <= s.rtol:
+            return 2
+        return -3

@@ -90,22 +90,28 @@ struct SynthHost {
 
 // ============================================================ Anderson ===
 // Least squares min ||f + F a|| for the Anderson steps (reference lib/AAR.py:
-// 102-105 and lib/AndersonAcceleration.py:62-65 use numpy Householder QR).
-// Here: Cholesky-QR2 of [F | f] from two fused device Gram passes; the top
-// block of the last R column is Q_F^T f, so a = R_FF^{-1} (-Q_F^T f).
+// 102-105 and lib/AndersonAcceleration.py:62-65 use numpy Householder QR of F).
+// Here Cholesky-QR2 of F from two fused device Gram passes (no n x m panel is
+// ever gathered to one place):
+//   pass 1: G1 = F^T F = R1^T R1;
+//   pass 2: Gram of [Q1 | f] with Q1 = F R1^{-1} formed on the fly
+//           -> Q1^T Q1 = R2^T R2 and Q1^T f;
+//   R = R2 R1, Q^T f = R2^{-T} Q1^T f, a = R^{-1} (-Q^T f).
+// f never enters a Cholesky factor, so a nearly-consistent f (the regime where
+// Anderson works) does not degrade R.
 struct AndersonLS {
     DBuf<const double *> dptr;
-    DBuf<double> dR;     // Rinv column-major
+    DBuf<double> dR;     // Rinv (extended) column-major
     DBuf<double> dG;     // packed gram
     std::vector<double> solve(const std::vector<const double *> &cols, const double *f, int64_t n, Ctx &c) {
         const int L = (int)cols.size();
-        const int m = L + 1;
-        if (m > 16) throw Error("Anderson order > 15 not supported");
+        if (L < 1) return {};
+        if (L + 1 > 16) throw Error("Anderson order > 15 not supported");
         if (dptr.n < 16) { dptr.alloc(16); dR.alloc(256); dG.alloc(256); }
         std::vector<const double *> hp(cols);
         hp.push_back(f);
-        HIPCHK(hipMemcpyAsync((void *)dptr.p, hp.data(), sizeof(double *) * m, hipMemcpyHostToDevice, c.st));
-        auto gram = [&](const double *rinv_dev) {
+        HIPCHK(hipMemcpyAsync((void *)dptr.p, hp.data(), sizeof(double *) * (L + 1), hipMemcpyHostToDevice, c.st));
+        auto gram = [&](int m, const double *rinv_dev) {
             launch_gram(n, m, dptr.p, rinv_dev, c.partial.p, dG.p, c.st);
             const int np = m * (m + 1) / 2;
             HIPCHK(hipMemcpyAsync(c.hscal, dG.p, sizeof(double) * np, hipMemcpyDeviceToHost, c.st));
@@ -116,55 +122,61 @@ struct AndersonLS {
                 for (int cc = r; cc < m; ++cc, ++t) G[r * m + cc] = G[cc * m + r] = c.hscal[t];
             return G;
         };
-        auto chol = [&](const std::vector<double> &G, std::vector<double> &R) {  // G = R^T R, R upper (row-major)
-            R.assign(m * m, 0.0);
-            for (int j = 0; j < m; ++j) {
+        // Cholesky of the leading L x L block of G (stride m): G = R^T R, R upper row-major L x L
+        auto chol = [&](const std::vector<double> &G, int m, std::vector<double> &R) {
+            R.assign(L * L, 0.0);
+            for (int j = 0; j < L; ++j) {
                 double s = G[j * m + j];
-                for (int k = 0; k < j; ++k) s -= R[k * m + j] * R[k * m + j];
-                if (!(s > 0.0)) s = 0.0;
-                R[j * m + j] = std::sqrt(s);
-                for (int i = j + 1; i < m; ++i) {
+                for (int k = 0; k < j; ++k) s -= R[k * L + j] * R[k * L + j];
+                if (!(s > 0.0)) throw Error("Anderson least squares: rank-deficient history (numpy would raise LinAlgError)");
+                R[j * L + j] = std::sqrt(s);
+                for (int i = j + 1; i < L; ++i) {
                     double t = G[j * m + i];
-                    for (int k = 0; k < j; ++k) t -= R[k * m + j] * R[k * m + i];
-                    R[j * m + i] = (R[j * m + j] > 0.0) ? t / R[j * m + j] : 0.0;
+                    for (int k = 0; k < j; ++k) t -= R[k * L + j] * R[k * L + i];
+                    R[j * L + i] = t / R[j * L + j];
                 }
             }
-        };
-        auto inv_upper = [&](const std::vector<double> &R) {  // returns Rinv column-major
-            std::vector<double> X(m * m, 0.0);  // row-major inverse
-            for (int j = 0; j < m; ++j) {
-                X[j * m + j] = (R[j * m + j] != 0.0) ? 1.0 / R[j * m + j] : 0.0;
-                for (int i = j - 1; i >= 0; --i) {
-                    double s = 0.0;
-                    for (int k = i + 1; k <= j; ++k) s += R[i * m + k] * X[k * m + j];
-                    X[i * m + j] = (R[i * m + i] != 0.0) ? -s / R[i * m + i] : 0.0;
-                }
-            }
-            std::vector<double> cm(m * m);
-            for (int r = 0; r < m; ++r)
-                for (int cc = 0; cc < m; ++cc) cm[cc * m + r] = X[r * m + cc];
-            return cm;
         };
         std::vector<double> R1, R2;
-        chol(gram(nullptr), R1);
-        std::vector<double> R1inv = inv_upper(R1);
-        HIPCHK(hipMemcpyAsync(dR.p, R1inv.data(), sizeof(double) * m * m, hipMemcpyHostToDevice, c.st));
-        chol(gram(dR.p), R2);
-        // R = R2 R1
-        std::vector<double> R(m * m, 0.0);
-        for (int i = 0; i < m; ++i)
-            for (int j = i; j < m; ++j) {
+        chol(gram(L, nullptr), L, R1);
+        // extended inverse diag(R1^{-1}, 1), column-major (L+1) x (L+1)
+        const int m = L + 1;
+        std::vector<double> X(L * L, 0.0);  // row-major R1^{-1}
+        for (int j = 0; j < L; ++j) {
+            X[j * L + j] = 1.0 / R1[j * L + j];
+            for (int i = j - 1; i >= 0; --i) {
                 double s = 0.0;
-                for (int k = i; k <= j; ++k) s += R2[i * m + k] * R1[k * m + j];
-                R[i * m + j] = s;
+                for (int k = i + 1; k <= j; ++k) s += R1[i * L + k] * X[k * L + j];
+                X[i * L + j] = -s / R1[i * L + i];
             }
-        // a = R_FF^{-1} (-r_Ff)
+        }
+        std::vector<double> ext(m * m, 0.0);
+        for (int r = 0; r < L; ++r)
+            for (int cc = 0; cc < L; ++cc) ext[cc * m + r] = X[r * L + cc];
+        ext[L * m + L] = 1.0;
+        HIPCHK(hipMemcpyAsync(dR.p, ext.data(), sizeof(double) * m * m, hipMemcpyHostToDevice, c.st));
+        std::vector<double> G2 = gram(m, dR.p);
+        chol(G2, m, R2);
+        // qtf = R2^{-T} (Q1^T f)
+        std::vector<double> qtf(L, 0.0);
+        for (int i = 0; i < L; ++i) {
+            double s = G2[i * m + L];
+            for (int k = 0; k < i; ++k) s -= R2[k * L + i] * qtf[k];
+            qtf[i] = s / R2[i * L + i];
+        }
+        // R = R2 R1 ; a = R^{-1} (-qtf)
+        std::vector<double> R(L * L, 0.0);
+        for (int i = 0; i < L; ++i)
+            for (int j = i; j < L; ++j) {
+                double s = 0.0;
+                for (int k = i; k <= j; ++k) s += R2[i * L + k] * R1[k * L + j];
+                R[i * L + j] = s;
+            }
         std::vector<double> a(L, 0.0);
         for (int i = L - 1; i >= 0; --i) {
-            double s = -R[i * m + L];
-            for (int k = i + 1; k < L; ++k) s -= R[i * m + k] * a[k];
-            if (R[i * m + i] == 0.0) throw Error("Anderson least squares: singular R (numpy would raise LinAlgError)");
-            a[i] = s / R[i * m + i];
+            double s = -qtf[i];
+            for (int k = i + 1; k < L; ++k) s -= R[i * L + k] * a[k];
+            a[i] = s / R[i * L + i];
         }
         return a;
     }

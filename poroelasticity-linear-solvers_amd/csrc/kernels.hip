@@ -28,6 +28,13 @@ static inline unsigned grid_for(int64_t work, int per_block) {
     return (unsigned)g;
 }
 
+
+__device__ __forceinline__ double wave_reduce(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
 // ============================================================ synthetic ====
 // Bit-exact restatement of the synthetic spec; every float
 // expression rounds as written (no FMA contraction) so the device matrices are
@@ -281,13 +288,72 @@ __global__ __launch_bounds__(TPB) void k_spmv(int64_t nrows, const int64_t *__re
     }
 }
 
+// Long rows (mean >= 96 nnz): one wave walks `rpw` consecutive rows two at a
+// time; for each row pair all U*64 val/col loads per row are issued before the
+// x gathers, so a wave keeps ~4.6 KB of HBM loads in flight (the one-row-per-
+// wave form is latency bound at ~2 TB/s).
+template <int U>
+__global__ __launch_bounds__(TPB) void k_spmv_w64(int64_t nrows, int rpw, const int64_t *__restrict__ rp,
+                                                  const int32_t *__restrict__ ci, const double *__restrict__ val,
+                                                  const double *__restrict__ x, double *__restrict__ y,
+                                                  double alpha, double beta, const double *__restrict__ z) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
+    const int64_t r0 = (int64_t)wave * rpw;
+    if (r0 >= nrows) return;
+    const int64_t r1 = (r0 + rpw < nrows) ? r0 + rpw : nrows;
+    for (int64_t r = r0; r < r1; r += 2) {
+        const bool two = (r + 1 < r1);
+        const int64_t sa = rp[r], ea = rp[r + 1];
+        const int64_t eb = two ? rp[r + 2] : ea;
+        double acc_a = 0.0, acc_b = 0.0;
+        for (int64_t ka = sa, kb = ea; ka < ea || kb < eb; ka += U * 64, kb += U * 64) {
+            int32_t ca[U], cb[U];
+            double va[U], vb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t k = ka + u * 64 + lane;
+                const bool in = k < ea;
+                ca[u] = in ? __builtin_nontemporal_load(ci + k) : 0;
+                va[u] = in ? __builtin_nontemporal_load(val + k) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t k = kb + u * 64 + lane;
+                const bool in = k < eb;
+                cb[u] = in ? __builtin_nontemporal_load(ci + k) : 0;
+                vb[u] = in ? __builtin_nontemporal_load(val + k) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (ka + u * 64 + lane < ea) acc_a += va[u] * x[ca[u]];
+                if (kb + u * 64 + lane < eb) acc_b += vb[u] * x[cb[u]];
+            }
+        }
+        acc_a = wave_reduce(acc_a);
+        acc_b = wave_reduce(acc_b);
+        if (lane == 0) {
+            double ra = alpha * acc_a;
+            if (beta != 0.0) ra += beta * z[r];
+            y[r] = ra;
+            if (two) {
+                double rb = alpha * acc_b;
+                if (beta != 0.0) rb += beta * z[r + 1];
+                y[r + 1] = rb;
+            }
+        }
+    }
+}
+
 void launch_spmv(int64_t nrows, int64_t nnz, const int64_t *rp, const int32_t *ci, const double *val,
                  const double *x, double *y, double alpha, double beta, const double *z, hipStream_t st) {
     if (nrows <= 0) return;
     const double mean = (double)nnz / (double)nrows;
-    if (mean >= 96.0)
-        k_spmv<64><<<grid_for(nrows, TPB / 64), TPB, 0, st>>>(nrows, rp, ci, val, x, y, alpha, beta, z);
-    else if (mean >= 40.0)
+    if (mean >= 96.0) {
+        const int rpw = 8;
+        const int64_t waves = (nrows + rpw - 1) / rpw;
+        k_spmv_w64<3><<<grid_for(waves, TPB / 64), TPB, 0, st>>>(nrows, rpw, rp, ci, val, x, y, alpha, beta, z);
+    } else if (mean >= 40.0)
         k_spmv<32><<<grid_for(nrows, TPB / 32), TPB, 0, st>>>(nrows, rp, ci, val, x, y, alpha, beta, z);
     else if (mean >= 16.0)
         k_spmv<16><<<grid_for(nrows, TPB / 16), TPB, 0, st>>>(nrows, rp, ci, val, x, y, alpha, beta, z);
@@ -744,6 +810,53 @@ void launch_trsv_level(int64_t r0, int64_t r1, const int32_t *row_of, const int6
         case 16: k_trsv_level<16><<<grid_for(rows, TPB / 16), TPB, 0, st>>>(r0, r1, row_of, rp, ci, val, dinv_lvl, b, y); break;
         case 8: k_trsv_level<8><<<grid_for(rows, TPB / 8), TPB, 0, st>>>(r0, r1, row_of, rp, ci, val, dinv_lvl, b, y); break;
         default: k_trsv_level<4><<<grid_for(rows, TPB / 4), TPB, 0, st>>>(r0, r1, row_of, rp, ci, val, dinv_lvl, b, y); break;
+    }
+}
+
+// Block-Jacobi sweep: one workgroup per diagonal block walks that block's
+// levels (rows stored block-major, level-ordered) with only a workgroup
+// barrier between levels -- the blocks are independent, so no grid-wide sync
+// and no per-level launch.  y is read/written through L1 by the workgroup's
+// own waves only (workgroup-scope visibility via __syncthreads()).
+template <int LPR>
+__global__ __launch_bounds__(512) void k_trsv_blocks(const int64_t *__restrict__ blk_off,
+                                                     const int64_t *__restrict__ lvl_ptr,
+                                                     const int32_t *__restrict__ row_of,
+                                                     const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                     const double *__restrict__ val, const double *__restrict__ dinv,
+                                                     const double *b, double *y) {
+    const int sub = threadIdx.x & (LPR - 1);
+    const int grp = threadIdx.x / LPR;
+    constexpr int NG = 512 / LPR;
+    const int64_t l0 = blk_off[blockIdx.x], l1 = blk_off[blockIdx.x + 1];
+    for (int64_t l = l0; l < l1; ++l) {
+        const int64_t rs = lvl_ptr[l], re = lvl_ptr[l + 1];
+        for (int64_t r = rs + grp; r < re; r += NG) {
+            const int64_t i = row_of[r];
+            const int64_t s = rp[r], e = rp[r + 1];
+            double acc = 0.0;
+            for (int64_t k = s + sub; k < e; k += LPR) acc += val[k] * y[ci[k]];
+#pragma unroll
+            for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+            if (sub == 0) {
+                if (dinv) y[i] = (y[i] - acc) * dinv[r];
+                else y[i] = b[i] - acc;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+void launch_trsv_blocks(int64_t nblocks, const int64_t *blk_off, const int64_t *lvl_ptr, const int32_t *row_of,
+                        const int64_t *rp, const int32_t *ci, const double *val, const double *dinv_lvl,
+                        const double *b, double *y, int lpr, hipStream_t st) {
+    if (nblocks <= 0) return;
+    switch (lpr) {
+        case 64: k_trsv_blocks<64><<<(unsigned)nblocks, 512, 0, st>>>(blk_off, lvl_ptr, row_of, rp, ci, val, dinv_lvl, b, y); break;
+        case 32: k_trsv_blocks<32><<<(unsigned)nblocks, 512, 0, st>>>(blk_off, lvl_ptr, row_of, rp, ci, val, dinv_lvl, b, y); break;
+        case 16: k_trsv_blocks<16><<<(unsigned)nblocks, 512, 0, st>>>(blk_off, lvl_ptr, row_of, rp, ci, val, dinv_lvl, b, y); break;
+        case 8: k_trsv_blocks<8><<<(unsigned)nblocks, 512, 0, st>>>(blk_off, lvl_ptr, row_of, rp, ci, val, dinv_lvl, b, y); break;
+        default: k_trsv_blocks<4><<<(unsigned)nblocks, 512, 0, st>>>(blk_off, lvl_ptr, row_of, rp, ci, val, dinv_lvl, b, y); break;
     }
 }
 

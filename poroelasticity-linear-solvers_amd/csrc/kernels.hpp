@@ -101,4 +101,10 @@ void launch_trsv_level(int64_t r0, int64_t r1, const int32_t *row_of, const int6
                        const int32_t *ci, const double *val, const double *dinv_lvl,
                        const double *b, double *y, int lanes_per_row, hipStream_t st);
 
+// Block-Jacobi sweep: blocks independent, one workgroup per block.
+// blk_off[b]..blk_off[b+1] index lvl_ptr (row boundaries of block b's levels).
+void launch_trsv_blocks(int64_t nblocks, const int64_t *blk_off, const int64_t *lvl_ptr, const int32_t *row_of,
+                        const int64_t *rp, const int32_t *ci, const double *val, const double *dinv_lvl,
+                        const double *b, double *y, int lanes_per_row, hipStream_t st);
+
 }  // namespace pls

@@ -269,6 +269,51 @@ static int64_t level_order(int64_t n, const std::vector<int64_t> &rp, const std:
     return nl;
 }
 
+// Block-major level groups: rows sorted by (block, level); grp[g] = first row
+// of group g, off[b] = first group of block b (PETSc bjacobi block sizes).
+static void block_level_groups(int64_t n, int64_t nb, const std::vector<int64_t> &rp, const std::vector<int32_t> &ci,
+                               bool upper, std::vector<int32_t> &order, std::vector<int64_t> &grp,
+                               std::vector<int64_t> &off) {
+    std::vector<int32_t> lvl(n, 0);
+    if (!upper) {
+        for (int64_t i = 0; i < n; ++i) {
+            int32_t L = 0;
+            for (int64_t k = rp[i]; k < rp[i + 1] && ci[k] < i; ++k) L = std::max(L, lvl[ci[k]] + 1);
+            lvl[i] = L;
+        }
+    } else {
+        for (int64_t i = n - 1; i >= 0; --i) {
+            int32_t L = 0;
+            for (int64_t k = rp[i + 1] - 1; k >= rp[i] && ci[k] > i; --k) L = std::max(L, lvl[ci[k]] + 1);
+            lvl[i] = L;
+        }
+    }
+    const int64_t q = n / nb, r = n % nb;
+    order.clear();
+    order.reserve(n);
+    grp.clear();
+    off.assign(nb + 1, 0);
+    int64_t b0 = 0;
+    std::vector<int64_t> cnt;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t len = q + (b < r ? 1 : 0);
+        int32_t nl = 0;
+        for (int64_t i = b0; i < b0 + len; ++i) nl = std::max(nl, lvl[i] + 1);
+        cnt.assign(nl + 1, 0);
+        for (int64_t i = b0; i < b0 + len; ++i) cnt[lvl[i] + 1]++;
+        for (int32_t l = 0; l < nl; ++l) cnt[l + 1] += cnt[l];
+        off[b] = (int64_t)grp.size();
+        const int64_t base = (int64_t)order.size();
+        for (int32_t l = 0; l < nl; ++l) grp.push_back(base + cnt[l]);
+        order.resize(base + len);
+        std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+        for (int64_t i = b0; i < b0 + len; ++i) order[base + pos[lvl[i]]++] = (int32_t)i;
+        b0 += len;
+    }
+    off[nb] = (int64_t)grp.size();
+    grp.push_back(n);
+}
+
 static void build_level_factor(const PCILU &P, const std::vector<int32_t> &order, bool upper, DevCSR &out,
                                DBuf<int32_t> &rows_dev, Ctx &c) {
     const int64_t n = P.F.nrows;
@@ -334,6 +379,18 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
     HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
     c.sync();
     if (hfail) throw Error("ILU(0): zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+    blockwise = nblocks >= 64;
+    if (blockwise) {
+        std::vector<int64_t> gL, gU, oL, oU;
+        block_level_groups(n, nblocks, rp, ci, false, ordL, gL, oL);
+        block_level_groups(n, nblocks, rp, ci, true, ordU, gU, oU);
+        auto up = [&](DBuf<int64_t> &d, const std::vector<int64_t> &v) {
+            d.alloc(v.size());
+            HIPCHK(hipMemcpyAsync(d.p, v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice, c.st));
+        };
+        up(dLgrp, gL); up(dUgrp, gU); up(dLoff, oL); up(dUoff, oU);
+        c.sync();
+    }
     build_level_factor(*this, ordL, false, L, Lrow, c);
     build_level_factor(*this, ordU, true, U, Urow, c);
     Udinv.alloc(std::max<int64_t>(n, 1));
@@ -350,6 +407,11 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
 }
 
 void PCILU::apply(const double *x, double *y, Ctx &c) {
+    if (blockwise) {
+        launch_trsv_blocks(nblocks, dLoff.p, dLgrp.p, Lrow.p, L.rp.p, L.ci.p, L.val.p, nullptr, x, y, lpr_L, c.st);
+        launch_trsv_blocks(nblocks, dUoff.p, dUgrp.p, Urow.p, U.rp.p, U.ci.p, U.val.p, Udinv.p, y, y, lpr_U, c.st);
+        return;
+    }
     for (int64_t l = 0; l < nlev_L; ++l)
         launch_trsv_level(Lptr[l], Lptr[l + 1], Lrow.p, L.rp.p, L.ci.p, L.val.p, nullptr, x, y, lpr_L, c.st);
     for (int64_t l = 0; l < nlev_U; ++l)

@@ -166,6 +166,9 @@ struct PCILU : PC {
     std::vector<int64_t> Lptr, Uptr;  // level boundaries (rows)
     int lpr_L = 8, lpr_U = 8;
     int64_t nlev_L = 0, nlev_U = 0;
+    // block-major level groups (block-Jacobi with many blocks): one workgroup per block
+    bool blockwise = false;
+    DBuf<int64_t> dLgrp, dUgrp, dLoff, dUoff;
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c);
     void apply(const double *x, double *y, Ctx &c) override;
 };

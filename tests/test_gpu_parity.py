@@ -130,6 +130,17 @@ def test_gmres_bjacobi(gpu):
     _compare_solve(S.SynthSpec(2, 14), db=db)
 
 
+@pytest.mark.parametrize("blocks", [64, 200])
+def test_gmres_bjacobi_blockwise(gpu, blocks):
+    """>= 64 blocks: one workgroup per block walks its own levels."""
+    db = dict(ILU_DB)
+    for pre in ("s_", "fp_", "f_", "p_", "diff_"):
+        db[pre + "pc_type"] = "bjacobi"
+        db[pre + "pc_bjacobi_blocks"] = str(blocks)
+    _compare_solve(S.SynthSpec(2, 24), db=db)
+    _compare_solve(S.SynthSpec(3, 4), {"pc type": "diagonal 3-way"}, db=db)
+
+
 def test_gmres_jacobi(gpu):
     db = dict(ILU_DB, s_pc_type="jacobi", fp_pc_type="jacobi")
     _compare_solve(S.SynthSpec(2, 10), db=db)
