@@ -35,6 +35,37 @@ __device__ __forceinline__ double wave_reduce(double v) {
     return v;
 }
 
+
+// Partial dot of a CSR row slice over LPR lanes, U entries per lane in flight:
+// unconditional loads at a clamped index (s is valid inside the loop) and a
+// masked value, so the loads of one pass issue back to back.
+template <int LPR, int U, bool NT>
+__device__ __forceinline__ double row_dot(int64_t s, int64_t e, int sub, const int32_t *__restrict__ ci,
+                                          const double *__restrict__ val, const double *x) {
+    double acc = 0.0;
+    for (int64_t k0 = s; k0 < e; k0 += U * LPR) {
+        int32_t c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = k0 + u * LPR + sub;
+            const int64_t kk = k < e ? k : s;
+            if (NT) {
+                c[u] = __builtin_nontemporal_load(ci + kk);
+                const double t = __builtin_nontemporal_load(val + kk);
+                v[u] = k < e ? t : 0.0;
+            } else {
+                c[u] = ci[kk];
+                const double t = val[kk];
+                v[u] = k < e ? t : 0.0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u] * x[(uint32_t)c[u]];
+    }
+    return acc;
+}
+
 // ============================================================ synthetic ====
 // Bit-exact restatement of the synthetic spec; every float
 // expression rounds as written (no FMA contraction) so the device matrices are
@@ -267,18 +298,7 @@ __global__ __launch_bounds__(TPB) void k_spmv(int64_t nrows, const int64_t *__re
     const int64_t row = ((int64_t)blockIdx.x * TPB + threadIdx.x) / LPR;
     if (row >= nrows) return;
     const int64_t s = rp[row], e = rp[row + 1];
-    double a0 = 0.0, a1 = 0.0;
-    int64_t k = s + sub;
-    for (; k + LPR < e; k += 2 * LPR) {
-        const int32_t c0 = __builtin_nontemporal_load(ci + k);
-        const int32_t c1 = __builtin_nontemporal_load(ci + k + LPR);
-        const double v0 = __builtin_nontemporal_load(val + k);
-        const double v1 = __builtin_nontemporal_load(val + k + LPR);
-        a0 += v0 * x[c0];
-        a1 += v1 * x[c1];
-    }
-    if (k < e) a0 += __builtin_nontemporal_load(val + k) * x[__builtin_nontemporal_load(ci + k)];
-    double acc = a0 + a1;
+    double acc = row_dot<LPR, 4, true>(s, e, sub, ci, val, x);
 #pragma unroll
     for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (sub == 0) {
@@ -310,24 +330,28 @@ __global__ __launch_bounds__(TPB) void k_spmv_w64(int64_t nrows, int rpw, const 
         for (int64_t ka = sa, kb = ea; ka < ea || kb < eb; ka += U * 64, kb += U * 64) {
             int32_t ca[U], cb[U];
             double va[U], vb[U];
+// unconditional loads at a clamped index (entry 0 is always valid), value
+            // masked to 0: no exec-masked branch, so all 4U loads issue back to back
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t k = ka + u * 64 + lane;
-                const bool in = k < ea;
-                ca[u] = in ? __builtin_nontemporal_load(ci + k) : 0;
-                va[u] = in ? __builtin_nontemporal_load(val + k) : 0.0;
+                const int64_t kk = k < ea ? k : 0;
+                ca[u] = __builtin_nontemporal_load(ci + kk);
+                const double v = __builtin_nontemporal_load(val + kk);
+                va[u] = k < ea ? v : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t k = kb + u * 64 + lane;
-                const bool in = k < eb;
-                cb[u] = in ? __builtin_nontemporal_load(ci + k) : 0;
-                vb[u] = in ? __builtin_nontemporal_load(val + k) : 0.0;
+                const int64_t kk = k < eb ? k : 0;
+                cb[u] = __builtin_nontemporal_load(ci + kk);
+                const double v = __builtin_nontemporal_load(val + kk);
+                vb[u] = k < eb ? v : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                if (ka + u * 64 + lane < ea) acc_a += va[u] * x[ca[u]];
-                if (kb + u * 64 + lane < eb) acc_b += vb[u] * x[cb[u]];
+                acc_a += va[u] * x[(uint32_t)ca[u]];
+                acc_b += vb[u] * x[(uint32_t)cb[u]];
             }
         }
         acc_a = wave_reduce(acc_a);
@@ -789,8 +813,7 @@ __global__ __launch_bounds__(TPB) void k_trsv_level(int64_t r0, int64_t r1, cons
     if (r >= r1) return;
     const int64_t i = row_of[r];
     const int64_t s = rp[r], e = rp[r + 1];
-    double acc = 0.0;
-    for (int64_t k = s + sub; k < e; k += LPR) acc += val[k] * y[ci[k]];
+    double acc = row_dot<LPR, 2, false>(s, e, sub, ci, val, y);
 #pragma unroll
     for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (sub == 0) {
@@ -834,8 +857,7 @@ __global__ __launch_bounds__(512) void k_trsv_blocks(const int64_t *__restrict__
         for (int64_t r = rs + grp; r < re; r += NG) {
             const int64_t i = row_of[r];
             const int64_t s = rp[r], e = rp[r + 1];
-            double acc = 0.0;
-            for (int64_t k = s + sub; k < e; k += LPR) acc += val[k] * y[ci[k]];
+            double acc = row_dot<LPR, 2, false>(s, e, sub, ci, val, y);
 #pragma unroll
             for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
             if (sub == 0) {
