@@ -29,6 +29,7 @@ class AAR:
         self.F, self.X, self.F0 = [], [], []
         self.it = 0
         self.history = []
+        self.max_cond = 1.0  # largest cond(F) met in an Anderson least squares
 
     def _update_residual(self, b, xk):
         temp = b - self.A @ xk
@@ -62,6 +63,7 @@ class AAR:
                 F = np.vstack(self.F0).T
                 Q, R = np.linalg.qr(F)
                 alpha = np.linalg.solve(R, -Q.T @ fk)
+                self.max_cond = max(self.max_cond, float(np.linalg.cond(R)))
                 xk = xk + self.beta * fk
                 for i in range(mk):
                     xk = xk + alpha[i] * (self.X[i] + self.beta * self.F[i])
@@ -87,6 +89,7 @@ class AndersonAcceleration:
         self.order = order
         self.k = 0
         self.F, self.X, self.F0 = [], [], []
+        self.max_cond = 1.0
 
     def get_next_vector(self, gk):
         gk = np.asarray(gk, dtype=np.float64)
@@ -112,6 +115,7 @@ class AndersonAcceleration:
                 F = np.vstack(self.F0).T
                 Q, R = np.linalg.qr(F)
                 alpha = np.linalg.solve(R, -Q.T @ self.fk)
+                self.max_cond = max(self.max_cond, float(np.linalg.cond(R)))
                 self.xk = self.xk + 1.0 * self.fk
                 for i in range(mk):
                     self.xk = self.xk + alpha[i] * (self.X[i] + self.F[i])

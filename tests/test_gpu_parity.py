@@ -7,6 +7,13 @@ Tolerances (north star: iteration counts bit-exact, residual norms within
   * SpMV / PC apply: <= 1e-13 relative (different summation order only);
   * Krylov solves: identical iteration count and convergence reason, every
     residual-history entry within RTOL_HIST = 1e-10 relative.
+  * Anderson steps (AAR, inner Anderson mixing): the least squares
+    min ||f + F a|| is solved by numpy Householder QR in the reference and by a
+    device Cholesky-QR2 here; two backward-stable solvers agree only to
+    ~cond(F) * eps in a (measured: numpy QR vs CPU Cholesky-QR2 differ by 9e-9
+    in the AAR history at cond(F) = 6e7).  The history bound there is
+    max(RTOL_HIST, 50 * eps * max cond(F)) with cond(F) measured by the oracle;
+    iteration counts and reasons stay exact.
 """
 import numpy as np
 import pytest
@@ -56,8 +63,12 @@ def _compare_solve(spec, upd=None, db=None):
     assert r.reason == o.reason, f"reason {r.reason} vs oracle {o.reason}"
     assert hist.shape == ho.shape
     rel = np.max(np.abs(hist - ho) / np.abs(ho))
-    assert rel <= RTOL_HIST, f"residual history rel diff {rel:.3e}"
-    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+    tol = RTOL_HIST
+    cond = max(getattr(o.solver, "max_cond", 1.0), getattr(o.block_pc.anderson, "max_cond", 1.0))
+    if cond > 1.0:
+        tol = max(RTOL_HIST, 50 * np.finfo(float).eps * cond)
+    assert rel <= tol, f"residual history rel diff {rel:.3e} (tol {tol:.1e}, cond(F) {cond:.1e})"
+    assert np.linalg.norm(x - xo) <= max(1e-8, tol) * np.linalg.norm(xo)
     return r, o
 
 
