@@ -469,6 +469,13 @@ static void do_setup(Handle &H) {
         ext(H.P, 0, ns, ns, n, H.Ms_fp);
         ext(H.P, ns, ns + nf, ns + nf, n, H.Mf_p);
     }
+    // SELL-64 copies of every matrix the PC multiplies with
+    if (!H.three_way) {
+        build_sell(H.Mfp_s, c);
+    } else {
+        build_sell(H.Ms_fp, c);
+        build_sell(H.Mf_p, c);
+    }
     // inner solvers (setup_elliptic_solver / setup_fieldsplit; options win)
     const Options &o = H.opt;
     H.ksp_s = make_ksp("s_", o, &H.Ks, &H.Ks, H.inner_ksp, H.inner_pc, c);
@@ -509,6 +516,7 @@ static void do_setup_solver(Handle &H) {
     H.solver_type = o.str("pls.solver_type", "gmres");
     const double atol = o.num("pls.solver_atol", 1e-8), rtol = o.num("pls.solver_rtol", 1e-6);
     const int64_t maxiter = o.integer("pls.solver_maxiter", 500);
+    build_sell(H.A, c);
     H.Aop = std::make_unique<MatOp>(&H.A);
     H.Aop->timers = &H.timers;
     if (H.solver_type == "aar") {
@@ -847,6 +855,7 @@ int pls_matmult(pls_handle *hh, const double *x, double *y) {
         DBuf<double> xi(H.n), yi(H.n);
         if (!H.vout.p) H.vout.alloc(H.n);
         to_internal(H, x, xi.p);
+        build_sell(H.A, H.ctx);
         spmv(H.A, xi.p, yi.p, H.ctx);
         from_internal(H, yi.p, y);
     })
@@ -883,6 +892,7 @@ int pls_pc_apply_device(pls_handle *hh, const double *d_x, double *d_y) {
 int pls_matmult_device(pls_handle *hh, const double *d_x, double *d_y) {
     PLS_TRY({
         Handle &H = *reinterpret_cast<Handle *>(hh);
+        build_sell(H.A, H.ctx);
         spmv(H.A, d_x, d_y, H.ctx);
         H.ctx.sync();
     })
@@ -954,6 +964,7 @@ int pls_get_permutation(pls_handle *hh, int64_t *perm) {
 int pls_bench_spmv(pls_handle *hh, const double *d_x, double *d_y, int32_t reps, double *sec_per_launch) {
     PLS_TRY({
         Handle &H = *reinterpret_cast<Handle *>(hh);
+        build_sell(H.A, H.ctx);
         hipEvent_t a, b;
         HIPCHK(hipEventCreate(&a));
         HIPCHK(hipEventCreate(&b));

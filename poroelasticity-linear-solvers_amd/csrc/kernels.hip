@@ -882,4 +882,103 @@ void launch_trsv_blocks(int64_t nblocks, const int64_t *blk_off, const int64_t *
     }
 }
 
+// ============================================================== SELL-64 ====
+// Sliced ELLPACK, slice height = one 64-lane wave: slice s holds rows
+// [64 s, 64 s + 64), entry k of its rows stored contiguously
+// (sptr[s] + 64 k + lane).  Lane = row, so the val / col streams are fully
+// coalesced, no cross-lane reduction is needed, each row sums its entries in
+// column order, and for banded / stencil columns the 64 x gathers of one
+// wave-instruction hit 4-5 consecutive cache lines instead of 64.
+__global__ __launch_bounds__(TPB) void k_sell_slice_len(int64_t nrows, int64_t nslices, const int64_t *rp,
+                                                        int64_t *slen) {
+    const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sl > nslices) return;
+    if (sl == nslices) { if (lane == 0) slen[nslices] = 0; return; }
+    const int64_t row = sl * 64 + lane;
+    int64_t len = row < nrows ? rp[row + 1] - rp[row] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t t = __shfl_xor(len, o);
+        len = t > len ? t : len;
+    }
+    if (lane == 0) slen[sl] = 64 * len;
+}
+
+__global__ __launch_bounds__(TPB) void k_sell_fill(int64_t nrows, int64_t nslices, const int64_t *rp, const int32_t *ci,
+                                                   const double *val, const int64_t *sptr, int32_t *scol, double *sval) {
+    const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sl >= nslices) return;
+    const int64_t row = sl * 64 + lane;
+    const int64_t base = sptr[sl];
+    const int64_t L = (sptr[sl + 1] - base) >> 6;
+    const int64_t s0 = row < nrows ? rp[row] : 0;
+    const int64_t len = row < nrows ? rp[row + 1] - s0 : 0;
+    const int32_t padc = len > 0 ? ci[s0 + len - 1] : 0;
+    for (int64_t k = 0; k < L; ++k) {
+        const int64_t pos = base + k * 64 + lane;
+        if (k < len) {
+            scol[pos] = ci[s0 + k];
+            sval[pos] = val[s0 + k];
+        } else {
+            scol[pos] = padc;
+            sval[pos] = 0.0;
+        }
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(TPB) void k_sell_spmv(int64_t nrows, int64_t nslices, const int64_t *__restrict__ sptr,
+                                                   const int32_t *__restrict__ scol, const double *__restrict__ sval,
+                                                   const double *__restrict__ x, double *__restrict__ y, double alpha,
+                                                   double beta, const double *__restrict__ z) {
+    const int lane = threadIdx.x & 63;
+    const int64_t sl = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
+    if (sl >= nslices) return;
+    const int64_t base = sptr[sl];
+    const int64_t L = (sptr[sl + 1] - base) >> 6;
+    const int32_t *cp = scol + base + lane;
+    const double *vp = sval + base + lane;
+    double acc = 0.0;
+    for (int64_t k0 = 0; k0 < L; k0 += U) {
+        int32_t c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = k0 + u;
+            const int64_t kk = k < L ? k : L - 1;  // wave-uniform clamp, value masked
+            c[u] = __builtin_nontemporal_load(cp + kk * 64);
+            const double t = __builtin_nontemporal_load(vp + kk * 64);
+            v[u] = k < L ? t : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u] * x[(uint32_t)c[u]];
+    }
+    const int64_t row = sl * 64 + lane;
+    if (row < nrows) {
+        double r = alpha * acc;
+        if (beta != 0.0) r += beta * z[row];
+        y[row] = r;
+    }
+}
+
+int64_t sell_nslices(int64_t nrows) { return (nrows + 63) / 64; }
+
+void launch_sell_slice_len(int64_t nrows, const int64_t *rp, int64_t *slen, hipStream_t st) {
+    const int64_t ns = sell_nslices(nrows);
+    k_sell_slice_len<<<grid_for((ns + 1) * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, slen);
+}
+void launch_sell_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const double *val, const int64_t *sptr,
+                      int32_t *scol, double *sval, hipStream_t st) {
+    const int64_t ns = sell_nslices(nrows);
+    if (ns > 0) k_sell_fill<<<grid_for(ns * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, ci, val, sptr, scol, sval);
+}
+void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, const double *sval, const double *x,
+                      double *y, double alpha, double beta, const double *z, hipStream_t st) {
+    const int64_t ns = sell_nslices(nrows);
+    if (ns > 0)
+        k_sell_spmv<8><<<grid_for(ns, TPB / 64), TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z);
+}
+
 }  // namespace pls

@@ -107,4 +107,12 @@ void launch_trsv_blocks(int64_t nblocks, const int64_t *blk_off, const int64_t *
                         const int64_t *rp, const int32_t *ci, const double *val, const double *dinv_lvl,
                         const double *b, double *y, int lanes_per_row, hipStream_t st);
 
+// SELL-64 (sliced ELLPACK, slice = 64 rows = one wave)
+int64_t sell_nslices(int64_t nrows);
+void launch_sell_slice_len(int64_t nrows, const int64_t *rp, int64_t *slen /* nslices+1 */, hipStream_t st);
+void launch_sell_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const double *val, const int64_t *sptr,
+                      int32_t *scol, double *sval, hipStream_t st);
+void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, const double *sval, const double *x,
+                      double *y, double alpha, double beta, const double *z, hipStream_t st);
+
 }  // namespace pls

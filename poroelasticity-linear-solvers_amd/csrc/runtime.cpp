@@ -107,7 +107,30 @@ void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_
     dst.max_row = max_row_of(dst.rp, nl, c);
 }
 
+void build_sell(DevCSR &M, Ctx &c) {
+    if (M.sell || M.nrows == 0) return;
+    auto S = std::make_unique<DevSELL>();
+    S->nslices = sell_nslices(M.nrows);
+    DBuf<int64_t> slen(S->nslices + 1);
+    launch_sell_slice_len(M.nrows, M.rp.p, slen.p, c.st);
+    S->sptr.alloc(S->nslices + 1);
+    c.ensure_scan(S->nslices);
+    exclusive_scan_i64(slen.p, S->sptr.p, S->nslices, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
+    HIPCHK(hipMemcpyAsync(&S->stored, S->sptr.p + S->nslices, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    S->col.alloc(std::max<int64_t>(S->stored, 1));
+    S->val.alloc(std::max<int64_t>(S->stored, 1));
+    launch_sell_fill(M.nrows, M.rp.p, M.ci.p, M.val.p, S->sptr.p, S->col.p, S->val.p, c.st);
+    HIPCHK(hipGetLastError());
+    c.sync();
+    M.sell = std::move(S);
+}
+
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z) {
+    if (M.sell) {
+        launch_sell_spmv(M.nrows, M.sell->sptr.p, M.sell->col.p, M.sell->val.p, x, y, alpha, beta, z, c.st);
+        return;
+    }
     launch_spmv(M.nrows, M.nnz, M.rp.p, M.ci.p, M.val.p, x, y, alpha, beta, z, c.st);
 }
 
@@ -194,6 +217,7 @@ void Timers::flush() {
 }
 
 void MatOp::apply(const double *x, double *y, Ctx &c) {
+    if (!M->sell) build_sell(const_cast<DevCSR &>(*M), c);
     if (timers) timers->begin(T_SPMV);
     spmv(*M, x, y, c);
     if (timers) { timers->end(T_SPMV); timers->spmv_calls++; }

@@ -76,13 +76,23 @@ struct Ctx {
 };
 
 // ------------------------------------------------------------------ matrix --
+struct DevSELL {
+    int64_t nslices = 0, stored = 0;  // stored = padded entries
+    DBuf<int64_t> sptr;
+    DBuf<int32_t> col;
+    DBuf<double> val;
+};
+
 struct DevCSR {
     int64_t nrows = 0, ncols = 0, nnz = 0;
     DBuf<int64_t> rp;
     DBuf<int32_t> ci;
     DBuf<double> val;
     int64_t max_row = 0;
+    std::unique_ptr<DevSELL> sell;  // SpMV layout (built on demand)
 };
+// Build the SELL-64 copy used by every SpMV with this matrix.
+void build_sell(DevCSR &M, Ctx &c);
 
 void upload_csr(DevCSR &M, int64_t nrows, int64_t ncols, const int64_t *rp, const int32_t *ci, const double *val,
                 Ctx &c);
@@ -134,6 +144,7 @@ struct MatOp : Op {
     const DevCSR *M;
     Timers *timers = nullptr;
     explicit MatOp(const DevCSR *m) : M(m) { n = m->nrows; }
+    Ctx *ctx_for_build = nullptr;
     void apply(const double *x, double *y, Ctx &c) override;
 };
 

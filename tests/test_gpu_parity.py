@@ -62,12 +62,19 @@ def _compare_solve(spec, upd=None, db=None):
     assert r.its == o.its, f"its {r.its} vs oracle {o.its}"
     assert r.reason == o.reason, f"reason {r.reason} vs oracle {o.reason}"
     assert hist.shape == ho.shape
-    rel = np.max(np.abs(hist - ho) / np.abs(ho))
     tol = RTOL_HIST
     cond = max(getattr(o.solver, "max_cond", 1.0), getattr(o.block_pc.anderson, "max_cond", 1.0))
     if cond > 1.0:
         tol = max(RTOL_HIST, 50 * np.finfo(float).eps * cond)
-    assert rel <= tol, f"residual history rel diff {rel:.3e} (tol {tol:.1e}, cond(F) {cond:.1e})"
+    if params["solver type"] == "aar":
+        # AAR's history is a recomputed residual ||M^-1 (b - A x_k)||: its attainable
+        # absolute accuracy is ~eps * ||b|| = eps * h_0, not relative to h_k
+        bound = tol * np.abs(ho) + 100 * np.finfo(float).eps * ho[0]
+        worst = np.max(np.abs(hist - ho) / bound)
+        assert worst <= 1.0, f"AAR history off by {worst:.2f}x the bound (cond(F) {cond:.1e})"
+    else:
+        rel = np.max(np.abs(hist - ho) / np.abs(ho))
+        assert rel <= tol, f"residual history rel diff {rel:.3e} (tol {tol:.1e}, cond(F) {cond:.1e})"
     assert np.linalg.norm(x - xo) <= max(1e-8, tol) * np.linalg.norm(xo)
     return r, o
 
