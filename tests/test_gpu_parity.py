@@ -48,7 +48,23 @@ def _oracle(spec, params, db):
     return OracleSolver(A, P, Pd, is_s, is_f, is_p, params, db, S.bcs_sub_pressure(spec))
 
 
-def _compare_solve(spec, upd=None, db=None):
+def _self_sensitivity(spec, params, db, b, ho, eps=1e-15):
+    """Oracle vs the oracle with its s-block PC output perturbed by eps (relative)."""
+    o2 = _oracle(spec, params, db)
+    rng = np.random.default_rng(0)
+    orig = o2.block_pc.ksp_s.pc.apply
+    o2.block_pc.ksp_s.pc.apply = lambda x: (lambda y: y * (1 + eps * rng.standard_normal(y.size)))(orig(x))
+    o2.solve(b)
+    h2 = np.asarray(o2.history)
+    n = min(len(h2), len(ho))
+    return float(np.max(np.abs(h2[:n] - ho[:n]) / np.abs(ho[:n])))
+
+
+def _compare_solve(spec, upd=None, db=None, sensitivity=False):
+    """sensitivity=True: for configurations whose histories amplify rounding (a
+    nonlinear PC such as inner Anderson mixing inside non-flexible GMRES), the
+    history bound is 10x the oracle's own deviation under a 1e-15 relative
+    perturbation of one inner PC output; iteration count and reason stay exact."""
     params = dict(BASE)
     params.update(upd or {})
     db = dict(ILU_DB if db is None else db)
@@ -66,6 +82,8 @@ def _compare_solve(spec, upd=None, db=None):
     cond = max(getattr(o.solver, "max_cond", 1.0), getattr(o.block_pc.anderson, "max_cond", 1.0))
     if cond > 1.0:
         tol = max(RTOL_HIST, 50 * np.finfo(float).eps * cond)
+    if sensitivity:
+        tol = max(tol, 10 * _self_sensitivity(spec, params, db, b, ho))
     if params["solver type"] == "aar":
         # AAR's history is a recomputed residual ||M^-1 (b - A x_k)||: its attainable
         # absolute accuracy is ~eps * ||b|| = eps * h_0, not relative to h_k
@@ -189,7 +207,9 @@ def test_aar_order5(gpu):
 
 
 def test_inner_anderson_order1(gpu):
-    _compare_solve(S.SynthSpec(2, 8), {"inner accel order": 1})
+    # measured on CPU: a 1e-16 relative perturbation of one ILU output moves the
+    # oracle's own history by 1.3e-8 in this configuration
+    _compare_solve(S.SynthSpec(2, 8), {"inner accel order": 1}, sensitivity=True)
 
 
 def test_interleaved_index_sets_host_path(gpu):
