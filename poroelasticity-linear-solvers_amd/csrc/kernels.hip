@@ -981,4 +981,123 @@ void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, c
         k_sell_spmv<8><<<grid_for(ns, TPB / 64), TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z);
 }
 
+// ================================================= level-aligned SELL-64 ====
+// Triangular factors for the sweeps: rows grouped by (block, level), every
+// group padded to whole 64-row slices, entry k of a slice's rows contiguous
+// (sptr[s] + 64 k + lane).  Lane = row: coalesced val/col loads, no lane
+// reduction, and the U entries a lane keeps in flight are independent of the
+// level barrier.  Padding entries are discarded by a select (never multiplied
+// into the sum), so uninitialised y entries cannot leak NaNs.
+__global__ __launch_bounds__(TPB) void k_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *slot_len,
+                                                  const int64_t *rp, const int32_t *ci, const double *lu,
+                                                  const int64_t *diag, const double *dinv, int upper,
+                                                  const int64_t *sptr, int32_t *ocol, double *oval, double *odinv) {
+    const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sl >= nslices) return;
+    const int64_t slot = sl * 64 + lane;
+    const int32_t i = slot_row[slot];
+    const int32_t len = slot_len[slot];
+    const int64_t base = sptr[sl];
+    const int64_t L = (sptr[sl + 1] - base) >> 6;
+    const int64_t src = (i < 0) ? 0 : (upper ? diag[i] + 1 : rp[i]);
+    for (int64_t k = 0; k < L; ++k) {
+        const int64_t pos = base + k * 64 + lane;
+        if (k < len) {
+            ocol[pos] = ci[src + k];
+            oval[pos] = lu[src + k];
+        } else {
+            ocol[pos] = 0;
+            oval[pos] = 0.0;
+        }
+    }
+    if (odinv) odinv[slot] = (i < 0) ? 1.0 : dinv[i];
+}
+
+template <int U>
+__device__ __forceinline__ void tri_slice(int64_t sl, int lane, const int64_t *__restrict__ sptr,
+                                          const int32_t *__restrict__ slot_row, const int32_t *__restrict__ slot_len,
+                                          const int32_t *__restrict__ col, const double *__restrict__ val,
+                                          const double *__restrict__ sdinv, const double *b, double *y) {
+    const int64_t slot = sl * 64 + lane;
+    const int32_t i = slot_row[slot];
+    const int32_t len = slot_len[slot];
+    const int64_t base = sptr[sl];
+    const int64_t L = (sptr[sl + 1] - base) >> 6;
+    const int32_t *cp = col + base + lane;
+    const double *vp = val + base + lane;
+    double acc = 0.0;
+    for (int64_t k0 = 0; k0 < L; k0 += U) {
+        int32_t c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t kk = (k0 + u < L) ? k0 + u : L - 1;
+            c[u] = cp[kk * 64];
+            v[u] = vp[kk * 64];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const double t = v[u] * y[(uint32_t)c[u]];
+            acc += (k0 + u < len) ? t : 0.0;
+        }
+    }
+    if (i >= 0) {
+        if (sdinv) y[i] = (y[i] - acc) * sdinv[slot];
+        else y[i] = b[i] - acc;
+    }
+}
+
+// one workgroup per block: goff[blk]..goff[blk+1] groups, gslice[g] slices
+__global__ __launch_bounds__(1024) void k_tri_blocks(const int64_t *__restrict__ goff,
+                                                     const int64_t *__restrict__ gslice,
+                                                     const int64_t *__restrict__ sptr, const int32_t *__restrict__ slot_row,
+                                                     const int32_t *__restrict__ slot_len, const int32_t *__restrict__ col,
+                                                     const double *__restrict__ val, const double *__restrict__ sdinv,
+                                                     const double *b, double *y) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int nw = blockDim.x >> 6;
+    const int64_t g0 = goff[blockIdx.x], g1 = goff[blockIdx.x + 1];
+    for (int64_t g = g0; g < g1; ++g) {
+        const int64_t s1 = gslice[g + 1];
+        for (int64_t sl = gslice[g] + wave; sl < s1; sl += nw)
+            tri_slice<4>(sl, lane, sptr, slot_row, slot_len, col, val, sdinv, b, y);
+        __syncthreads();
+    }
+}
+
+// one launch per group (global levels): slices [s0, s1)
+__global__ __launch_bounds__(TPB) void k_tri_group(int64_t s0, int64_t s1, const int64_t *__restrict__ sptr,
+                                                   const int32_t *__restrict__ slot_row,
+                                                   const int32_t *__restrict__ slot_len, const int32_t *__restrict__ col,
+                                                   const double *__restrict__ val, const double *__restrict__ sdinv,
+                                                   const double *b, double *y) {
+    const int lane = threadIdx.x & 63;
+    const int64_t sl = s0 + (((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6);
+    if (sl >= s1) return;
+    tri_slice<4>(sl, lane, sptr, slot_row, slot_len, col, val, sdinv, b, y);
+}
+
+void launch_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *slot_len, const int64_t *rp,
+                     const int32_t *ci, const double *lu, const int64_t *diag, const double *dinv, int upper,
+                     const int64_t *sptr, int32_t *ocol, double *oval, double *odinv, hipStream_t st) {
+    if (nslices > 0)
+        k_tri_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, slot_row, slot_len, rp, ci, lu, diag, dinv,
+                                                                upper, sptr, ocol, oval, odinv);
+}
+void launch_tri_blocks(int64_t nblocks, const int64_t *goff, const int64_t *gslice, const int64_t *sptr,
+                       const int32_t *slot_row, const int32_t *slot_len, const int32_t *col, const double *val,
+                       const double *sdinv, const double *b, double *y, hipStream_t st) {
+    if (nblocks > 0)
+        k_tri_blocks<<<(unsigned)nblocks, 1024, 0, st>>>(goff, gslice, sptr, slot_row, slot_len, col, val, sdinv, b, y);
+}
+void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t *slot_row, const int32_t *slot_len,
+                      const int32_t *col, const double *val, const double *sdinv, const double *b, double *y,
+                      hipStream_t st) {
+    if (s1 > s0)
+        k_tri_group<<<grid_for((s1 - s0) * 64, TPB), TPB, 0, st>>>(s0, s1, sptr, slot_row, slot_len, col, val, sdinv,
+                                                                   b, y);
+}
+
 }  // namespace pls

@@ -115,4 +115,15 @@ void launch_sell_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const
 void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, const double *sval, const double *x,
                       double *y, double alpha, double beta, const double *z, hipStream_t st);
 
+// Level-aligned SELL-64 triangular factors (see kernels.hip)
+void launch_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *slot_len, const int64_t *rp,
+                     const int32_t *ci, const double *lu, const int64_t *diag, const double *dinv, int upper,
+                     const int64_t *sptr, int32_t *ocol, double *oval, double *odinv, hipStream_t st);
+void launch_tri_blocks(int64_t nblocks, const int64_t *goff, const int64_t *gslice, const int64_t *sptr,
+                       const int32_t *slot_row, const int32_t *slot_len, const int32_t *col, const double *val,
+                       const double *sdinv, const double *b, double *y, hipStream_t st);
+void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t *slot_row, const int32_t *slot_len,
+                      const int32_t *col, const double *val, const double *sdinv, const double *b, double *y,
+                      hipStream_t st);
+
 }  // namespace pls

@@ -256,13 +256,6 @@ PCJacobi::PCJacobi(const DevCSR &M, Ctx &c) {
 }
 void PCJacobi::apply(const double *x, double *y, Ctx &c) { launch_pointwise_mult(n, x, dinv.p, y, c.st); }
 
-static int choose_lpr(double mean) {
-    if (mean >= 96.0) return 64;
-    if (mean >= 40.0) return 32;
-    if (mean >= 16.0) return 16;
-    if (mean >= 6.0) return 8;
-    return 4;
-}
 
 // levels of the strict lower (upper) dependency graph; counting sort into order
 static int64_t level_order(int64_t n, const std::vector<int64_t> &rp, const std::vector<int32_t> &ci, bool upper,
@@ -338,27 +331,75 @@ static void block_level_groups(int64_t n, int64_t nb, const std::vector<int64_t>
     grp.push_back(n);
 }
 
-static void build_level_factor(const PCILU &P, const std::vector<int32_t> &order, bool upper, DevCSR &out,
-                               DBuf<int32_t> &rows_dev, Ctx &c) {
-    const int64_t n = P.F.nrows;
-    rows_dev.alloc(std::max<int64_t>(n, 1));
-    HIPCHK(hipMemcpyAsync(rows_dev.p, order.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
-    DBuf<int64_t> len(n + 1);
-    launch_lvl_count(n, rows_dev.p, P.F.rp.p, P.diag.p, upper ? 1 : 0, len.p, c.st);
-    out.rp.alloc(n + 1);
-    c.ensure_scan(n);
-    exclusive_scan_i64(len.p, out.rp.p, n, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
-    int64_t nnz = 0;
-    HIPCHK(hipMemcpyAsync(&nnz, out.rp.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
-    c.sync();
-    out.nrows = n;
-    out.ncols = n;
-    out.nnz = nnz;
-    out.ci.alloc(std::max<int64_t>(nnz, 1));
-    out.val.alloc(std::max<int64_t>(nnz, 1));
-    launch_lvl_fill(n, rows_dev.p, P.F.rp.p, P.F.ci.p, P.F.val.p, P.diag.p, upper ? 1 : 0, out.rp.p, out.ci.p,
-                    out.val.p, c.st);
+// Build a level-aligned SELL-64 factor from the factored F: rows in `order`,
+// groups = row ranges [grp[g], grp[g+1]) of `order`, goff = first group of
+// each block (blockwise) -- padded to whole slices per group.
+static void build_tri_sell(const PCILU &P, const std::vector<int64_t> &rp, const std::vector<int64_t> &dg,
+                           const std::vector<int32_t> &order, const std::vector<int64_t> &grp,
+                           const std::vector<int64_t> *goff, bool upper, TriSELL &T, Ctx &c) {
+    const int64_t ng = (int64_t)grp.size() - 1;
+    std::vector<int32_t> srow, slen;
+    std::vector<int64_t> sl_len;  // 64 * L per slice
+    T.gslice_h.assign(ng + 1, 0);
+    for (int64_t g = 0; g < ng; ++g) {
+        T.gslice_h[g] = (int64_t)sl_len.size();
+        for (int64_t r = grp[g]; r < grp[g + 1]; r += 64) {
+            int32_t L = 0;
+            for (int l = 0; l < 64; ++l) {
+                const int64_t rr = r + l;
+                if (rr < grp[g + 1]) {
+                    const int64_t i = order[rr];
+                    const int32_t len = (int32_t)(upper ? rp[i + 1] - dg[i] - 1 : dg[i] - rp[i]);
+                    srow.push_back((int32_t)i);
+                    slen.push_back(len);
+                    L = std::max(L, len);
+                } else {
+                    srow.push_back(-1);
+                    slen.push_back(0);
+                }
+            }
+            sl_len.push_back(64 * (int64_t)L);
+        }
+    }
+    T.gslice_h[ng] = (int64_t)sl_len.size();
+    T.ngroups = ng;
+    T.nslices = (int64_t)sl_len.size();
+    std::vector<int64_t> sptr(T.nslices + 1, 0);
+    for (int64_t s = 0; s < T.nslices; ++s) sptr[s + 1] = sptr[s] + sl_len[s];
+    auto up64 = [&](DBuf<int64_t> &d, const std::vector<int64_t> &v) {
+        d.alloc(std::max<size_t>(v.size(), 1));
+        if (!v.empty()) HIPCHK(hipMemcpyAsync(d.p, v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice, c.st));
+    };
+    auto up32 = [&](DBuf<int32_t> &d, const std::vector<int32_t> &v) {
+        d.alloc(std::max<size_t>(v.size(), 1));
+        if (!v.empty()) HIPCHK(hipMemcpyAsync(d.p, v.data(), sizeof(int32_t) * v.size(), hipMemcpyHostToDevice, c.st));
+    };
+    up64(T.sptr, sptr);
+    up64(T.gslice, T.gslice_h);
+    up32(T.slot_row, srow);
+    up32(T.slot_len, slen);
+    T.blockwise = goff != nullptr;
+    if (goff) {
+        up64(T.goff, *goff);
+        T.nblocks = (int64_t)goff->size() - 1;
+    }
+    T.col.alloc(std::max<int64_t>(sptr.back(), 1));
+    T.val.alloc(std::max<int64_t>(sptr.back(), 1));
+    if (upper) T.sdinv.alloc(std::max<int64_t>(T.nslices * 64, 1));
+    launch_tri_fill(T.nslices, T.slot_row.p, T.slot_len.p, P.F.rp.p, P.F.ci.p, P.F.val.p, P.diag.p, P.dinv.p,
+                    upper ? 1 : 0, T.sptr.p, T.col.p, T.val.p, upper ? T.sdinv.p : nullptr, c.st);
     HIPCHK(hipGetLastError());
+    c.sync();
+}
+
+void TriSELL::apply(const double *b, double *y, Ctx &c) const {
+    const double *dv = sdinv.p;
+    if (blockwise) {
+        launch_tri_blocks(nblocks, goff.p, gslice.p, sptr.p, slot_row.p, slot_len.p, col.p, val.p, dv, b, y, c.st);
+        return;
+    }
+    for (int64_t g = 0; g < ngroups; ++g)
+        launch_tri_group(gslice_h[g], gslice_h[g + 1], sptr.p, slot_row.p, slot_len.p, col.p, val.p, dv, b, y, c.st);
 }
 
 PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
@@ -381,8 +422,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
     DBuf<int32_t> fail(1);
     HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
     launch_find_diag(n, F.rp.p, F.ci.p, diag.p, fail.p, c.st);
-    // host copy of the pattern for the level schedule
-    std::vector<int64_t> rp(n + 1);
+    std::vector<int64_t> rp(n + 1), dg(n);
     std::vector<int32_t> ci(F.nnz);
     HIPCHK(hipMemcpyAsync(rp.data(), F.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, c.st));
     if (F.nnz) HIPCHK(hipMemcpyAsync(ci.data(), F.ci.p, sizeof(int32_t) * F.nnz, hipMemcpyDeviceToHost, c.st));
@@ -390,56 +430,43 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
     HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
     c.sync();
     if (hfail) throw Error("ILU(0): missing diagonal entry (PETSc: MAT_FACTOR_STRUCT_ZEROPIVOT)");
-    std::vector<int32_t> ordL, ordU;
-    nlev_L = level_order(n, rp, ci, false, ordL, Lptr);
-    nlev_U = level_order(n, rp, ci, true, ordU, Uptr);
-    // numeric factorization, level by level (dependencies = forward sweep)
-    DBuf<int32_t> rowsL(std::max<int64_t>(n, 1));
-    HIPCHK(hipMemcpyAsync(rowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
-    for (int64_t l = 0; l < nlev_L; ++l)
-        launch_ilu0_level(Lptr[l + 1] - Lptr[l], rowsL.p + Lptr[l], F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p, fail.p,
-                          c.st);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipMemcpyAsync(dg.data(), diag.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c.st));
     c.sync();
-    if (hfail) throw Error("ILU(0): zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
-    blockwise = nblocks >= 64;
-    if (blockwise) {
-        std::vector<int64_t> gL, gU, oL, oU;
-        block_level_groups(n, nblocks, rp, ci, false, ordL, gL, oL);
-        block_level_groups(n, nblocks, rp, ci, true, ordU, gU, oU);
-        auto up = [&](DBuf<int64_t> &d, const std::vector<int64_t> &v) {
-            d.alloc(v.size());
-            HIPCHK(hipMemcpyAsync(d.p, v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice, c.st));
-        };
-        up(dLgrp, gL); up(dUgrp, gU); up(dLoff, oL); up(dUoff, oU);
-        c.sync();
-    }
-    build_level_factor(*this, ordL, false, L, Lrow, c);
-    build_level_factor(*this, ordU, true, U, Urow, c);
-    Udinv.alloc(std::max<int64_t>(n, 1));
-    // Udinv[r] = dinv[Urow[r]]
+    // numeric factorization, level by level (global levels of the forward sweep)
+    std::vector<int32_t> ordL;
+    std::vector<int64_t> Lptr;
+    nlev_L = level_order(n, rp, ci, false, ordL, Lptr);
     {
-        DBuf<int64_t> idx(std::max<int64_t>(n, 1));
-        std::vector<int64_t> h(ordU.begin(), ordU.end());
-        HIPCHK(hipMemcpyAsync(idx.p, h.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, c.st));
-        launch_gather(n, idx.p, dinv.p, Udinv.p, c.st);
+        DBuf<int32_t> rowsL(std::max<int64_t>(n, 1));
+        HIPCHK(hipMemcpyAsync(rowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+        for (int64_t l = 0; l < nlev_L; ++l)
+            launch_ilu0_level(Lptr[l + 1] - Lptr[l], rowsL.p + Lptr[l], F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p,
+                              fail.p, c.st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
         c.sync();
     }
-    lpr_L = choose_lpr(n ? (double)L.nnz / n : 0.0);
-    lpr_U = choose_lpr(n ? (double)U.nnz / n : 0.0);
+    if (hfail) throw Error("ILU(0): zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+    if (nblocks >= 64) {
+        std::vector<int32_t> oL, oU;
+        std::vector<int64_t> gL, gU, fL, fU;
+        block_level_groups(n, nblocks, rp, ci, false, oL, gL, fL);
+        block_level_groups(n, nblocks, rp, ci, true, oU, gU, fU);
+        build_tri_sell(*this, rp, dg, oL, gL, &fL, false, Lf, c);
+        build_tri_sell(*this, rp, dg, oU, gU, &fU, true, Uf, c);
+        nlev_U = (int64_t)gU.size() - 1;
+    } else {
+        std::vector<int32_t> ordU;
+        std::vector<int64_t> Uptr;
+        nlev_U = level_order(n, rp, ci, true, ordU, Uptr);
+        build_tri_sell(*this, rp, dg, ordL, Lptr, nullptr, false, Lf, c);
+        build_tri_sell(*this, rp, dg, ordU, Uptr, nullptr, true, Uf, c);
+    }
 }
 
 void PCILU::apply(const double *x, double *y, Ctx &c) {
-    if (blockwise) {
-        launch_trsv_blocks(nblocks, dLoff.p, dLgrp.p, Lrow.p, L.rp.p, L.ci.p, L.val.p, nullptr, x, y, lpr_L, c.st);
-        launch_trsv_blocks(nblocks, dUoff.p, dUgrp.p, Urow.p, U.rp.p, U.ci.p, U.val.p, Udinv.p, y, y, lpr_U, c.st);
-        return;
-    }
-    for (int64_t l = 0; l < nlev_L; ++l)
-        launch_trsv_level(Lptr[l], Lptr[l + 1], Lrow.p, L.rp.p, L.ci.p, L.val.p, nullptr, x, y, lpr_L, c.st);
-    for (int64_t l = 0; l < nlev_U; ++l)
-        launch_trsv_level(Uptr[l], Uptr[l + 1], Urow.p, U.rp.p, U.ci.p, U.val.p, Udinv.p, y, y, lpr_U, c.st);
+    Lf.apply(x, y, c);
+    Uf.apply(y, y, c);
 }
 
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,

@@ -164,22 +164,28 @@ struct PCJacobi : PC {
     PCJacobi(const DevCSR &M, Ctx &c);
     void apply(const double *x, double *y, Ctx &c) override;
 };
+// Level-aligned SELL-64 strict triangular factor (see kernels.hip).
+struct TriSELL {
+    int64_t nslices = 0, ngroups = 0, nblocks = 0;
+    bool blockwise = false;
+    DBuf<int64_t> sptr, gslice, goff;
+    DBuf<int32_t> slot_row, slot_len, col;
+    DBuf<double> val, sdinv;
+    std::vector<int64_t> gslice_h;
+    void apply(const double *b, double *y, Ctx &c) const;
+};
+
 // ILU(0) of the block-Jacobi truncation of M (nblocks == 1: plain ILU(0)).
+// Factorization: level scheduled, one wave per row.  Sweeps: level-aligned
+// SELL-64; with >= 64 blocks one workgroup per block walks its own levels,
+// otherwise one launch per global level.
 struct PCILU : PC {
     int64_t nblocks = 1;
     DevCSR F;                     // truncated matrix, factored in place
     DBuf<int64_t> diag;
     DBuf<double> dinv;
-    // level-ordered strict lower / strict upper factors
-    DevCSR L, U;
-    DBuf<int32_t> Lrow, Urow;     // original row of each level-ordered row
-    DBuf<double> Udinv;           // dinv in U level order
-    std::vector<int64_t> Lptr, Uptr;  // level boundaries (rows)
-    int lpr_L = 8, lpr_U = 8;
+    TriSELL Lf, Uf;
     int64_t nlev_L = 0, nlev_U = 0;
-    // block-major level groups (block-Jacobi with many blocks): one workgroup per block
-    bool blockwise = false;
-    DBuf<int64_t> dLgrp, dUgrp, dLoff, dUoff;
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c);
     void apply(const double *x, double *y, Ctx &c) override;
 };
