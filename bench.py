@@ -87,7 +87,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--N", type=int, default=59)
     ap.add_argument("--inner", default="bjacobi", choices=["bjacobi", "ilu", "jacobi"])
-    ap.add_argument("--blocks", type=int, default=256)
+    ap.add_argument("--blocks", type=int, default=264)
     ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-N", type=int, default=20)

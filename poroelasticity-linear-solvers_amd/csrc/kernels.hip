@@ -1100,4 +1100,108 @@ void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t
                                                                    b, y);
 }
 
+// Block-Jacobi ILU(0) apply with the block's solution resident in LDS: the
+// truncated factors only reference rows of their own block, so one workgroup
+// loads x[b0, b0+len) into LDS, runs every forward level then every backward
+// level against LDS (gathers and updates never leave the CU), and writes the
+// block of y once.  Blocks are launched heaviest-last-index first (the
+// pressure blocks at the end of the fp ordering carry the most levels).
+template <int U>
+__device__ __forceinline__ void tri_slice_lds(int64_t sl, int lane, int64_t b0, const int64_t *__restrict__ sptr,
+                                              const int32_t *__restrict__ slot_row,
+                                              const int32_t *__restrict__ slot_len, const int32_t *__restrict__ col,
+                                              const double *__restrict__ val, const double *__restrict__ sdinv,
+                                              double *ys) {
+    const int64_t slot = sl * 64 + lane;
+    const int32_t i = slot_row[slot];
+    const int32_t len = slot_len[slot];
+    const int64_t base = sptr[sl];
+    const int64_t L = (sptr[sl + 1] - base) >> 6;
+    const int32_t *cp = col + base + lane;
+    const double *vp = val + base + lane;
+    double acc = 0.0;
+    for (int64_t k0 = 0; k0 < L; k0 += U) {
+        int32_t c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t kk = (k0 + u < L) ? k0 + u : L - 1;
+            c[u] = __builtin_nontemporal_load(cp + kk * 64);
+            v[u] = __builtin_nontemporal_load(vp + kk * 64);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t lc = (k0 + u < len) ? c[u] - (int32_t)b0 : 0;
+            const double t = v[u] * ys[lc];
+            acc += (k0 + u < len) ? t : 0.0;
+        }
+    }
+    if (i >= 0) {
+        const int32_t li = i - (int32_t)b0;
+        if (sdinv) ys[li] = (ys[li] - acc) * sdinv[slot];
+        else ys[li] = ys[li] - acc;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *__restrict__ Lgoff,
+                                                         const int64_t *__restrict__ Lgslice,
+                                                         const int64_t *__restrict__ Lsptr,
+                                                         const int32_t *__restrict__ Lrow,
+                                                         const int32_t *__restrict__ Llen,
+                                                         const int32_t *__restrict__ Lcol,
+                                                         const double *__restrict__ Lval,
+                                                         const int64_t *__restrict__ Ugoff,
+                                                         const int64_t *__restrict__ Ugslice,
+                                                         const int64_t *__restrict__ Usptr,
+                                                         const int32_t *__restrict__ Urow,
+                                                         const int32_t *__restrict__ Ulen,
+                                                         const int32_t *__restrict__ Ucol,
+                                                         const double *__restrict__ Uval,
+                                                         const double *__restrict__ Udinv, const double *__restrict__ x,
+                                                         double *__restrict__ y) {
+    extern __shared__ __attribute__((aligned(16))) double ys[];
+    const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
+    const int64_t q = n / nblocks, r = n % nblocks;
+    const int64_t b0 = blk * q + (blk < r ? blk : r);
+    const int64_t len = q + (blk < r ? 1 : 0);
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int nw = blockDim.x >> 6;
+    for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
+    __syncthreads();
+    for (int64_t g = Lgoff[blk]; g < Lgoff[blk + 1]; ++g) {
+        const int64_t s1 = Lgslice[g + 1];
+        for (int64_t sl = Lgslice[g] + wave; sl < s1; sl += nw)
+            tri_slice_lds<8>(sl, lane, b0, Lsptr, Lrow, Llen, Lcol, Lval, nullptr, ys);
+        __syncthreads();
+    }
+    for (int64_t g = Ugoff[blk]; g < Ugoff[blk + 1]; ++g) {
+        const int64_t s1 = Ugslice[g + 1];
+        for (int64_t sl = Ugslice[g] + wave; sl < s1; sl += nw)
+            tri_slice_lds<8>(sl, lane, b0, Usptr, Urow, Ulen, Ucol, Uval, Udinv, ys);
+        __syncthreads();
+    }
+    for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
+}
+
+int ilu_lds_max_rows() { return 163840 / 8; }
+
+void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,
+                           const int64_t *Lsptr, const int32_t *Lrow, const int32_t *Llen, const int32_t *Lcol,
+                           const double *Lval, const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr,
+                           const int32_t *Urow, const int32_t *Ulen, const int32_t *Ucol, const double *Uval,
+                           const double *Udinv, const double *x, double *y, hipStream_t st) {
+    const int64_t maxlen = n / nblocks + 1;
+    const size_t bytes = (size_t)maxlen * 8;
+    static size_t configured = 0;
+    if (bytes > configured) {
+        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)163840);
+        configured = 163840;
+    }
+    k_ilu_blocks_lds<<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lrow, Llen, Lcol, Lval,
+                                                              Ugoff, Ugslice, Usptr, Urow, Ulen, Ucol, Uval, Udinv, x,
+                                                              y);
+}
+
 }  // namespace pls

@@ -126,4 +126,13 @@ void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t
                       const int32_t *col, const double *val, const double *sdinv, const double *b, double *y,
                       hipStream_t st);
 
+// Block-Jacobi ILU(0) apply, block solution resident in LDS (forward + backward
+// in one launch).  Valid when every block has <= ilu_lds_max_rows() rows.
+int ilu_lds_max_rows();
+void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,
+                           const int64_t *Lsptr, const int32_t *Lrow, const int32_t *Llen, const int32_t *Lcol,
+                           const double *Lval, const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr,
+                           const int32_t *Urow, const int32_t *Ulen, const int32_t *Ucol, const double *Uval,
+                           const double *Udinv, const double *x, double *y, hipStream_t st);
+
 }  // namespace pls

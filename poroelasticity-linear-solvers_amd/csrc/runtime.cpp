@@ -465,6 +465,12 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
 }
 
 void PCILU::apply(const double *x, double *y, Ctx &c) {
+    if (allow_lds && Lf.blockwise && (n / nblocks + 1) <= ilu_lds_max_rows()) {
+        launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Lf.gslice.p, Lf.sptr.p, Lf.slot_row.p, Lf.slot_len.p, Lf.col.p,
+                              Lf.val.p, Uf.goff.p, Uf.gslice.p, Uf.sptr.p, Uf.slot_row.p, Uf.slot_len.p, Uf.col.p,
+                              Uf.val.p, Uf.sdinv.p, x, y, c.st);
+        return;
+    }
     Lf.apply(x, y, c);
     Uf.apply(y, y, c);
 }
@@ -484,7 +490,9 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         if (sub == "ilu") {
             if (o.integer(prefix + "sub_pc_factor_levels", 0) != 0)
                 throw Error(prefix + "sub_pc_factor_levels > 0: only ILU(0) is implemented");
-            return std::make_unique<PCILU>(M, nb, c);
+            auto p = std::make_unique<PCILU>(M, nb, c);
+            p->allow_lds = o.flag("pls.ilu_lds", true);
+            return p;
         }
         if (sub == "jacobi") return std::make_unique<PCJacobi>(M, c);
         if (sub == "none") return std::make_unique<PCNone>(M.nrows);

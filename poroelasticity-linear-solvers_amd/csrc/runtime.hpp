@@ -186,6 +186,7 @@ struct PCILU : PC {
     DBuf<double> dinv;
     TriSELL Lf, Uf;
     int64_t nlev_L = 0, nlev_U = 0;
+    bool allow_lds = true;  // block solution resident in LDS when it fits
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c);
     void apply(const double *x, double *y, Ctx &c) override;
 };

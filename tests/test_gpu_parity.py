@@ -166,10 +166,12 @@ def test_gmres_bjacobi(gpu):
     _compare_solve(S.SynthSpec(2, 14), db=db)
 
 
+@pytest.mark.parametrize("lds", ["1", "0"])
 @pytest.mark.parametrize("blocks", [64, 200])
-def test_gmres_bjacobi_blockwise(gpu, blocks):
-    """>= 64 blocks: one workgroup per block walks its own levels."""
-    db = dict(ILU_DB)
+def test_gmres_bjacobi_blockwise(gpu, blocks, lds):
+    """>= 64 blocks: one workgroup per block walks its own levels (LDS-resident
+    block solution, or the global-memory variant used for blocks > 20480 rows)."""
+    db = dict(ILU_DB, **{"pls.ilu_lds": lds})
     for pre in ("s_", "fp_", "f_", "p_", "diff_"):
         db[pre + "pc_type"] = "bjacobi"
         db[pre + "pc_bjacobi_blocks"] = str(blocks)
