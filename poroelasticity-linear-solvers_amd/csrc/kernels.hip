@@ -1143,6 +1143,96 @@ __device__ __forceinline__ void tri_slice_lds(int64_t sl, int lane, int64_t b0, 
     }
 }
 
+// One sweep over a block's groups (levels) with a software pipeline: the
+// slice metadata of level g+2 and the first P entries of level g+1 are loaded
+// while level g computes against LDS, so the per-level critical path is the
+// LDS work plus the barrier instead of two dependent global round trips.
+// Plain global loads stay in flight across __syncthreads() (no LDS-DMA here).
+template <int P>
+struct SliceMeta {
+    int32_t i, len;
+    int64_t base, L, sl;
+};
+
+template <int P>
+__device__ __forceinline__ SliceMeta<P> load_meta(int64_t g, int64_t g1, int wave, const int64_t *gslice,
+                                                  const int64_t *sptr, const int32_t *slot_row,
+                                                  const int32_t *slot_len, int lane) {
+    SliceMeta<P> m;
+    m.sl = -1; m.i = -1; m.len = 0; m.base = 0; m.L = 0;
+    if (g < g1) {
+        const int64_t sl = gslice[g] + wave;
+        if (sl < gslice[g + 1]) {
+            m.sl = sl;
+            m.i = slot_row[sl * 64 + lane];
+            m.len = slot_len[sl * 64 + lane];
+            m.base = sptr[sl];
+            m.L = (sptr[sl + 1] - m.base) >> 6;
+        }
+    }
+    return m;
+}
+
+template <int P>
+__device__ __forceinline__ void load_data(const SliceMeta<P> &m, int lane, const int32_t *col, const double *val,
+                                          int32_t (&c)[P], double (&v)[P]) {
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+        const int64_t kk = (m.sl >= 0 && u < m.L) ? u : 0;
+        const int64_t pos = (m.sl >= 0) ? m.base + kk * 64 + lane : 0;
+        c[u] = __builtin_nontemporal_load(col + pos);
+        v[u] = __builtin_nontemporal_load(val + pos);
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void sweep_lds(int64_t g0, int64_t g1, int64_t b0, int lane, int wave, int nw,
+                                          const int64_t *__restrict__ gslice, const int64_t *__restrict__ sptr,
+                                          const int32_t *__restrict__ slot_row, const int32_t *__restrict__ slot_len,
+                                          const int32_t *__restrict__ col, const double *__restrict__ val,
+                                          const double *__restrict__ sdinv, double *ys) {
+    SliceMeta<P> m0 = load_meta<P>(g0, g1, wave, gslice, sptr, slot_row, slot_len, lane);
+    SliceMeta<P> m1 = load_meta<P>(g0 + 1, g1, wave, gslice, sptr, slot_row, slot_len, lane);
+    int32_t c0[P], c1[P];
+    double v0[P], v1[P];
+    load_data<P>(m0, lane, col, val, c0, v0);
+    for (int64_t g = g0; g < g1; ++g) {
+        // prefetch: data of g+1 (meta known), meta of g+2
+        load_data<P>(m1, lane, col, val, c1, v1);
+        const SliceMeta<P> m2 = load_meta<P>(g + 2, g1, wave, gslice, sptr, slot_row, slot_len, lane);
+        double dv = 1.0;
+        if (sdinv && m0.sl >= 0) dv = sdinv[m0.sl * 64 + lane];
+        // level g: first slice of this wave from registers, the rest inline
+        if (m0.sl >= 0) {
+            double acc = 0.0;
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const int32_t lc = (u < m0.len) ? c0[u] - (int32_t)b0 : 0;
+                const double t = v0[u] * ys[lc];
+                acc += (u < m0.len) ? t : 0.0;
+            }
+            for (int64_t k = P; k < m0.L; ++k) {
+                const int64_t pos = m0.base + k * 64 + lane;
+                const int32_t cc = col[pos];
+                const double vv = val[pos];
+                if (k < m0.len) acc += vv * ys[cc - (int32_t)b0];
+            }
+            if (m0.i >= 0) {
+                const int32_t li = m0.i - (int32_t)b0;
+                ys[li] = sdinv ? (ys[li] - acc) * dv : ys[li] - acc;
+            }
+            const int64_t s1 = gslice[g + 1];
+            for (int64_t sl = m0.sl + nw; sl < s1; sl += nw)
+                tri_slice_lds<8>(sl, lane, b0, sptr, slot_row, slot_len, col, val, sdinv, ys);
+        }
+        __syncthreads();
+        m0 = m1;
+        m1 = m2;
+#pragma unroll
+        for (int u = 0; u < P; ++u) { c0[u] = c1[u]; v0[u] = v1[u]; }
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *__restrict__ Lgoff,
                                                          const int64_t *__restrict__ Lgslice,
                                                          const int64_t *__restrict__ Lsptr,
@@ -1169,18 +1259,8 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
     const int nw = blockDim.x >> 6;
     for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
     __syncthreads();
-    for (int64_t g = Lgoff[blk]; g < Lgoff[blk + 1]; ++g) {
-        const int64_t s1 = Lgslice[g + 1];
-        for (int64_t sl = Lgslice[g] + wave; sl < s1; sl += nw)
-            tri_slice_lds<8>(sl, lane, b0, Lsptr, Lrow, Llen, Lcol, Lval, nullptr, ys);
-        __syncthreads();
-    }
-    for (int64_t g = Ugoff[blk]; g < Ugoff[blk + 1]; ++g) {
-        const int64_t s1 = Ugslice[g + 1];
-        for (int64_t sl = Ugslice[g] + wave; sl < s1; sl += nw)
-            tri_slice_lds<8>(sl, lane, b0, Usptr, Urow, Ulen, Ucol, Uval, Udinv, ys);
-        __syncthreads();
-    }
+    sweep_lds<8>(Lgoff[blk], Lgoff[blk + 1], b0, lane, wave, nw, Lgslice, Lsptr, Lrow, Llen, Lcol, Lval, nullptr, ys);
+    sweep_lds<8>(Ugoff[blk], Ugoff[blk + 1], b0, lane, wave, nw, Ugslice, Usptr, Urow, Ulen, Ucol, Uval, Udinv, ys);
     for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
 }
 
