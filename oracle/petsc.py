@@ -280,7 +280,10 @@ def _gmres(ksp: KSP, b):
                 hapbnd = GMRES_HAPTOL
             hapend = tt < hapbnd
             if not hapend:
-                w = w * (1.0 / tt)
+                with np.errstate(divide="ignore"):
+                    inv = np.float64(1.0) / np.float64(tt)  # C semantics: 1/0 = inf (never reused)
+                with np.errstate(invalid="ignore", over="ignore"):
+                    w = w * inv
             V.append(w)
             # KSPGMRESUpdateHessenberg
             it = loc_it

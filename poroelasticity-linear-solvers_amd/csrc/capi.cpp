@@ -516,6 +516,7 @@ static void do_setup_solver(Handle &H) {
     H.solver_type = o.str("pls.solver_type", "gmres");
     const double atol = o.num("pls.solver_atol", 1e-8), rtol = o.num("pls.solver_rtol", 1e-6);
     const int64_t maxiter = o.integer("pls.solver_maxiter", 500);
+    H.A.tag = 1;
     build_sell(H.A, c);
     H.Aop = std::make_unique<MatOp>(&H.A);
     H.Aop->timers = &H.timers;
@@ -964,6 +965,7 @@ int pls_get_permutation(pls_handle *hh, int64_t *perm) {
 int pls_bench_spmv(pls_handle *hh, const double *d_x, double *d_y, int32_t reps, double *sec_per_launch) {
     PLS_TRY({
         Handle &H = *reinterpret_cast<Handle *>(hh);
+        H.A.tag = 1;
         build_sell(H.A, H.ctx);
         hipEvent_t a, b;
         HIPCHK(hipEventCreate(&a));

@@ -928,7 +928,9 @@ __global__ __launch_bounds__(TPB) void k_sell_fill(int64_t nrows, int64_t nslice
     }
 }
 
-template <int U>
+// TAG only separates the outer-operator instantiation (TAG 1: y = A x of the
+// Krylov loop) from the preconditioner's block products in profiles.
+template <int U, int TAG>
 __global__ __launch_bounds__(TPB) void k_sell_spmv(int64_t nrows, int64_t nslices, const int64_t *__restrict__ sptr,
                                                    const int32_t *__restrict__ scol, const double *__restrict__ sval,
                                                    const double *__restrict__ x, double *__restrict__ y, double alpha,
@@ -975,10 +977,13 @@ void launch_sell_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const
     if (ns > 0) k_sell_fill<<<grid_for(ns * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, ci, val, sptr, scol, sval);
 }
 void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, const double *sval, const double *x,
-                      double *y, double alpha, double beta, const double *z, hipStream_t st) {
+                      double *y, double alpha, double beta, const double *z, int tag, hipStream_t st) {
     const int64_t ns = sell_nslices(nrows);
-    if (ns > 0)
-        k_sell_spmv<8><<<grid_for(ns, TPB / 64), TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z);
+    if (ns <= 0) return;
+    if (tag)
+        k_sell_spmv<8, 1><<<grid_for(ns, TPB / 64), TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z);
+    else
+        k_sell_spmv<8, 0><<<grid_for(ns, TPB / 64), TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z);
 }
 
 // ================================================= level-aligned SELL-64 ====

@@ -112,8 +112,9 @@ int64_t sell_nslices(int64_t nrows);
 void launch_sell_slice_len(int64_t nrows, const int64_t *rp, int64_t *slen /* nslices+1 */, hipStream_t st);
 void launch_sell_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const double *val, const int64_t *sptr,
                       int32_t *scol, double *sval, hipStream_t st);
+// tag 1 = the outer operator A (separate kernel symbol in profiles)
 void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, const double *sval, const double *x,
-                      double *y, double alpha, double beta, const double *z, hipStream_t st);
+                      double *y, double alpha, double beta, const double *z, int tag, hipStream_t st);
 
 // Level-aligned SELL-64 triangular factors (see kernels.hip)
 void launch_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *slot_len, const int64_t *rp,

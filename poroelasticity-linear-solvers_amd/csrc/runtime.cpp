@@ -128,7 +128,7 @@ void build_sell(DevCSR &M, Ctx &c) {
 
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z) {
     if (M.sell) {
-        launch_sell_spmv(M.nrows, M.sell->sptr.p, M.sell->col.p, M.sell->val.p, x, y, alpha, beta, z, c.st);
+        launch_sell_spmv(M.nrows, M.sell->sptr.p, M.sell->col.p, M.sell->val.p, x, y, alpha, beta, z, M.tag, c.st);
         return;
     }
     launch_spmv(M.nrows, M.nnz, M.rp.p, M.ci.p, M.val.p, x, y, alpha, beta, z, c.st);
@@ -402,10 +402,48 @@ void TriSELL::apply(const double *b, double *y, Ctx &c) const {
         launch_tri_group(gslice_h[g], gslice_h[g + 1], sptr.p, slot_row.p, slot_len.p, col.p, val.p, dv, b, y, c.st);
 }
 
-PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
-    type = nb > 1 ? "bjacobi" : "ilu";
+// Profile (envelope) pattern of M with M's values and explicit zeros.
+static void envelope_csr(const DevCSR &M, DevCSR &E, Ctx &c) {
+    const int64_t n = M.nrows;
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> ci(M.nnz);
+    std::vector<double> v(M.nnz);
+    HIPCHK(hipMemcpyAsync(rp.data(), M.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, c.st));
+    if (M.nnz) {
+        HIPCHK(hipMemcpyAsync(ci.data(), M.ci.p, sizeof(int32_t) * M.nnz, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipMemcpyAsync(v.data(), M.val.p, sizeof(double) * M.nnz, hipMemcpyDeviceToHost, c.st));
+    }
+    c.sync();
+    std::vector<int64_t> erp(n + 1, 0), lo(n), hi(n);
+    int64_t hmax = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t a = i, b = i;
+        if (rp[i + 1] > rp[i]) {
+            a = std::min<int64_t>(a, ci[rp[i]]);
+            b = std::max<int64_t>(b, ci[rp[i + 1] - 1]);
+        }
+        hmax = std::max(hmax, b);
+        lo[i] = a;
+        hi[i] = std::max<int64_t>(hmax, i);
+        erp[i + 1] = erp[i] + (hi[i] - lo[i] + 1);
+        if (hi[i] - lo[i] + 1 > 5461) throw Error("lu: profile row longer than 5461 entries; use ilu/bjacobi");
+    }
+    if (erp[n] > 400000000LL) throw Error("lu: profile fill exceeds 4e8 entries; use ilu/bjacobi on the device");
+    std::vector<int32_t> eci(erp[n]);
+    std::vector<double> ev(erp[n], 0.0);
+    for (int64_t i = 0; i < n; ++i) {
+        for (int64_t j = lo[i]; j <= hi[i]; ++j) eci[erp[i] + (j - lo[i])] = (int32_t)j;
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) ev[erp[i] + (ci[k] - lo[i])] = v[k];
+    }
+    upload_csr(E, n, n, erp.data(), eci.data(), ev.data(), c);
+}
+
+PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds) {
+    exact = exact_lu;
+    allow_lds = lds;
+    type = exact ? "lu" : (nb > 1 ? "bjacobi" : "ilu");
     n = M.nrows;
-    nblocks = std::max<int64_t>(1, std::min<int64_t>(nb, n));
+    nblocks = exact ? 1 : std::max<int64_t>(1, std::min<int64_t>(nb, n));
     WindowSpec w{};
     if (nblocks > 1) {
         w.mode = 1;
@@ -415,7 +453,8 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
         w.c0 = 0;
         w.c1 = M.ncols;
     }
-    extract_csr(M, 0, n, w, 0, n, F, c);
+    if (exact) envelope_csr(M, F, c);
+    else extract_csr(M, 0, n, w, 0, n, F, c);
     if (F.max_row * 12 > 65536) throw Error("ILU(0): row too long for the LDS-staged factorization");
     diag.alloc(std::max<int64_t>(n, 1));
     dinv.alloc(std::max<int64_t>(n, 1));
@@ -447,7 +486,8 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c) {
         c.sync();
     }
     if (hfail) throw Error("ILU(0): zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
-    if (nblocks >= 64) {
+    const bool fits_lds = (n / nblocks + 1) <= ilu_lds_max_rows();
+    if (nblocks >= 64 || (fits_lds && allow_lds)) {
         std::vector<int32_t> oL, oU;
         std::vector<int64_t> gL, gU, fL, fU;
         block_level_groups(n, nblocks, rp, ci, false, oL, gL, fL);
@@ -482,7 +522,10 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
     if (type == "ilu") {
         if (o.integer(prefix + "pc_factor_levels", 0) != 0)
             throw Error(prefix + "pc_factor_levels > 0: only ILU(0) is implemented");
-        return std::make_unique<PCILU>(M, 1, c);
+        return std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true));
+    }
+    if (type == "lu" || type == "cholesky") {
+        return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true));
     }
     if (type == "bjacobi") {
         const int64_t nb = o.integer(prefix + "pc_bjacobi_blocks", 1);
@@ -490,16 +533,14 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         if (sub == "ilu") {
             if (o.integer(prefix + "sub_pc_factor_levels", 0) != 0)
                 throw Error(prefix + "sub_pc_factor_levels > 0: only ILU(0) is implemented");
-            auto p = std::make_unique<PCILU>(M, nb, c);
-            p->allow_lds = o.flag("pls.ilu_lds", true);
-            return p;
+            return std::make_unique<PCILU>(M, nb, c, false, o.flag("pls.ilu_lds", true));
         }
         if (sub == "jacobi") return std::make_unique<PCJacobi>(M, c);
         if (sub == "none") return std::make_unique<PCNone>(M.nrows);
         throw Error(prefix + "sub_pc_type " + sub + " is not available on the device");
     }
     throw Error("PC type '" + type + "' (prefix " + prefix +
-                ") is not available in this build (supported: none, jacobi, ilu, bjacobi)");
+                ") is not available in this build (supported: none, jacobi, ilu, bjacobi, lu)");
 }
 
 // ================================================================= KSP ===

@@ -90,6 +90,7 @@ struct DevCSR {
     DBuf<double> val;
     int64_t max_row = 0;
     std::unique_ptr<DevSELL> sell;  // SpMV layout (built on demand)
+    int tag = 0;                    // 1: outer operator A
 };
 // Build the SELL-64 copy used by every SpMV with this matrix.
 void build_sell(DevCSR &M, Ctx &c);
@@ -176,6 +177,10 @@ struct TriSELL {
 };
 
 // ILU(0) of the block-Jacobi truncation of M (nblocks == 1: plain ILU(0)).
+// exact_lu: the same pipeline on the profile (envelope) pattern of M -- row i
+// spans the contiguous columns [first nonzero of row i, max column of rows
+// <= i], which contains every fill entry of LU without pivoting, so the
+// "ILU" of that pattern is the exact LU factorization (PCLU).
 // Factorization: level scheduled, one wave per row.  Sweeps: level-aligned
 // SELL-64; with >= 64 blocks one workgroup per block walks its own levels,
 // otherwise one launch per global level.
@@ -187,7 +192,8 @@ struct PCILU : PC {
     TriSELL Lf, Uf;
     int64_t nlev_L = 0, nlev_U = 0;
     bool allow_lds = true;  // block solution resident in LDS when it fits
-    PCILU(const DevCSR &M, int64_t nblocks, Ctx &c);
+    bool exact = false;     // envelope pattern: exact LU (PCLU)
+    PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true);
     void apply(const double *x, double *y, Ctx &c) override;
 };
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,

@@ -267,6 +267,69 @@ def test_facade_end_to_end(gpu):
     popts.DB.clear()
 
 
+@pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
+def test_exact_lu_inner_blocks(gpu, pc_type):
+    """The reference's exact configuration: every block PREONLY + LU."""
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right"}
+    for pre in ("s_", "f_", "p_", "diff_", "fp_"):
+        db[pre + "ksp_type"] = "preonly"
+        db[pre + "pc_type"] = "lu"
+    _compare_solve(S.SynthSpec(2, 10), {"pc type": pc_type, "inner pc type": "lu"}, db=db)
+
+
+def test_exact_lu_pc_apply_is_exact(gpu):
+    spec = S.SynthSpec(3, 2)
+    db = {p + k: v for p in ("s_", "fp_") for k, v in (("ksp_type", "preonly"), ("pc_type", "lu"))}
+    h = _handle(spec, dict(BASE, **{"inner pc type": "lu"}), db)
+    P = S.matrix(spec, 1).toarray()
+    ns = spec.sizes()[0]
+    M = P.copy()
+    M[:ns, ns:] = 0.0
+    x = np.random.default_rng(3).standard_normal(spec.n)
+    y = h.pc_apply(x)
+    assert np.linalg.norm(M @ y - x) <= 1e-12 * np.linalg.norm(x)
+
+
+@pytest.mark.parametrize("inner", ["ilu", "lu"])
+def test_global_level_launch_path(gpu, inner):
+    """pls.ilu_lds 0 with one block: one launch per global level."""
+    db = dict(ILU_DB, **{"pls.ilu_lds": "0"})
+    for pre in ("s_", "fp_", "f_", "p_", "diff_"):
+        db[pre + "pc_type"] = inner
+    _compare_solve(S.SynthSpec(2, 6), {"inner pc type": inner}, db=db)
+
+
+def test_facade_with_repo_option_files(gpu):
+    """Parser(--petsc-options options/exact) + the facade, exact inner solves."""
+    import os
+    from lib import options as popts
+    from lib.IndexSet import IndexSet
+    from lib.Parser import Parser
+    from lib.Preconditioner import Preconditioner
+    from lib.Solver import Solver
+    from oracle.options import parse_options_file
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    popts.DB.clear()
+    parser = Parser(["--petsc-options", os.path.join(root, "options", "exact"), "--pc-type", "diagonal 3-way"])
+    params = dict(BASE, **{"inner pc type": "lu"})
+    params.update(parser.options_dict)
+    spec = S.SynthSpec(2, 8)
+    A, P, Pd = S.matrix(spec, 0), S.matrix(spec, 1), S.matrix(spec, 2)
+    index_map = IndexSet(S.field_major_index_sets(spec), two_way=False)
+    pc = Preconditioner(index_map, A, P, Pd, params, S.bcs_sub_pressure(spec)).get_pc()
+    b = S.rhs(spec)
+    solver = Solver(A, b, pc, params, index_map)
+    solver.create_solver(A, b, pc)
+    x = np.zeros_like(b)
+    solver.solve(b, x)
+    db = parse_options_file(os.path.join(root, "options", "exact"))
+    o = _oracle(spec, params, db)
+    xo = o.solve(b)
+    assert solver.getIterationNumber() == o.its
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+    popts.DB.clear()
+
+
 def test_unsupported_pc_fails_loudly(gpu):
     spec = S.SynthSpec(2, 4)
     h = _handle(spec, BASE, dict(ILU_DB, s_pc_type="hypre"))
