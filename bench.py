@@ -8,9 +8,15 @@ one full outer solve from a zero guess exactly as the reference runs it
 maxit = 100, swelling-3d.py:64-66) with the 2-way block preconditioner
 (lib/Preconditioner.py:219-246) and inner PREONLY + BJACOBI(ILU(0)) blocks.
 
-value = whole-job Krylov iterations per second (sum over ranks of the outer
-iterations done in the timed steps / max-over-ranks wall time).  At N GPUs
-every rank solves its own N=59 system (weak scaling, "replicas" for round 1).
+value = whole-job Krylov iterations per second on the 10.33M-DoF system.  At
+G GPUs the solve is sharded the way the reference runs under MPI (one process
+per GPU, PETSc row slabs of every field, halo exchange before each SpMV,
+rank-ordered global sums, BJACOBI blocks inside each rank; RCCL over xGMI, see
+DESIGN.md §6) on a global system G times as large (3-D N = round(59 G^(1/3)),
+weak scaling: ~10.3M DoF per GPU, 256/264 s/fp blocks per GPU); one outer
+iteration there is worth n_global / 10,326,954 iterations of the metric's
+system, so value = outer iterations x n_global / 10,326,954 / max-over-ranks
+time.  ``--replicas`` instead runs G independent N=59 solves.
 
 roofline: the dominant kernel is the CSR SpMV with A (one per outer
 iteration).  achieved = algorithmic bytes per launch
@@ -95,6 +101,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-N", type=int, default=20)
     ap.add_argument("--cpu-maxit", type=int, default=100)
+    ap.add_argument("--replicas", action="store_true", help="G independent N=59 solves instead of one sharded solve")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -103,17 +110,29 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo")  # bootstrap + timing reductions; the solve talks RCCL
 
     import lib._native as Nat
     from lib.handle import Handle, params_to_options
     Nat.check(Nat.lib().pls_set_device(local))
 
+    sharded = world > 1 and not args.replicas
+    N_glob = args.N
+    if sharded:
+        N_glob = int(round(args.N * world ** (1.0 / 3.0)))
+        args.blocks_s *= world
+        args.blocks_fp *= world
     params, db = solver_options(args)
     opts = dict(db)
     opts.update(params_to_options(params))
     t0 = time.perf_counter()
-    h = Handle.synthetic(3, args.N, SEED + rank, DELTA, opts)
+    comm = None
+    if sharded:
+        from lib.dist import Communicator
+        comm = Communicator.rccl()
+        h = Handle.synthetic_dist(3, N_glob, SEED, DELTA, opts, comm)
+    else:
+        h = Handle.synthetic(3, args.N, SEED + rank, DELTA, opts)
     h.setup()
     h.create_solver()
     t_setup = time.perf_counter() - t0
@@ -151,6 +170,16 @@ def main():
         its_all = float(it_t.item())
     else:
         its_all = float(its)
+    n_metric = 10326954  # DoF of the N=59 system the metric is quoted on
+    n_global = n
+    if sharded:
+        import torch
+        nt = torch.tensor([float(n)], dtype=torch.float64)
+        dist.all_reduce(nt, op=dist.ReduceOp.SUM)
+        n_global = int(nt.item())
+        its_all = float(its) * n_global / n_metric  # every rank did the same its
+    elif world == 1:
+        n_metric = n
 
     spmv_avg = tm["spmv_total"] / max(1, tm["spmv_calls"])
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 8.0 * n + 8.0 * n
@@ -162,7 +191,8 @@ def main():
         out = {
             "metric": METRIC,
             "value": its_all / dt,
-            "unit": "Krylov iters/s (outer GMRES iterations on the 10.33M-DoF system, summed over ranks)",
+            "unit": ("Krylov iters/s (outer GMRES iterations on the 10.33M-DoF system; sharded runs: "
+                     "iterations x n_global/10.33M)"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -173,11 +203,12 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded SPD 3-field block system, SURVEY.md 8(d); generated in HBM)",
             "config": {
-                "workload": (f"swelling-3d-shaped 3-D N={args.N} ({n} DoF, nnz(A)={nnz}): outer GMRES right-PC "
+                "workload": (f"swelling-3d-shaped 3-D N={N_glob} ({n_global} DoF): outer GMRES right-PC "
                              f"rtol 1e-6 atol 1e-8 restart=maxit={args.maxit}, 2-way block PC, inner preonly+"
                              f"{args.inner}" + (f"(ILU(0), {args.blocks_s}/{args.blocks_fp} blocks s/fp)" if args.inner == "bjacobi" else "")),
-                "dim": 3, "N": args.N, "dofs": n, "nnz_A": nnz,
-                "parallelism": f"replicas x{world}" if world > 1 else "single GPU",
+                "dim": 3, "N": N_glob, "dofs": n_global, "dofs_rank0": n, "nnz_A_rank0": nnz,
+                "parallelism": (f"row slabs x{world} (RCCL)" if sharded else
+                                f"replicas x{world}" if world > 1 else "single GPU"),
             },
             "its_per_solve": its / args.steps,
             "reasons": sorted(set(reasons)),
@@ -189,9 +220,14 @@ def main():
                          "isolated_spmv_gbs": alg_bytes / iso / 1e9},
             "timings_s": {k: v for k, v in tm.items()},
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(args, params, db)
         print(json.dumps(out))
+    d_b.free()
+    d_x.free()
+    h.destroy()
+    if comm is not None:
+        comm.destroy()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -51,6 +51,11 @@ typedef struct pls_csr {
 } pls_csr;
 
 typedef struct pls_handle pls_handle;
+typedef struct pls_comm pls_comm;
+
+/* Host allgather callback: every rank passes `bytes` bytes, receives
+ * size * bytes (rank order) into recv.  Returns 0 on success.               */
+typedef int (*pls_allgather_fn)(const void *send, int64_t bytes, void *recv, void *user);
 
 /* Result of the last solve (KSPGetIterationNumber / KSPGetConvergedReason /
  * residual history as KSPSetResidualHistory records it).                      */
@@ -107,6 +112,21 @@ int pls_create(const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff,
 /* Build a solver whose A, P, P_diff, index sets and pressure BCs come from the
  * seeded synthetic generator, directly on the device, field-major order.     */
 int pls_create_synthetic(const pls_synth_spec *spec, const char *options, pls_handle **out);
+
+/* ---- distributed solve (one process per GPU) ----------
+ * Row slabs per field (PETSc ownership split), halo exchange before each
+ * SpMV, deterministic global sums (allgather + rank-ordered sum), block-Jacobi
+ * inner blocks per rank.  Replaces the reference's MPI data parallelism
+ * (mpirun -np 8, paper-scripts/robustness_2d.sh:29; PETSc MPIAIJ + VecScatter,
+ * lib/Solver.py:151, lib/Preconditioner.py:170-234).                        */
+int pls_rccl_unique_id(char out[128]);
+int pls_comm_create_rccl(const char id[128], int rank, int size, pls_comm **out);
+int pls_comm_create_callback(int rank, int size, pls_allgather_fn fn, void *user, pls_comm **out);
+int pls_comm_destroy(pls_comm *comm);
+/* Each rank generates and owns its slabs of the synthetic system; the handle
+ * must be destroyed before its communicator.  Vectors of the device entry
+ * points are rank-local ([s_r | f_r | p_r]).                                 */
+int pls_create_synthetic_dist(const pls_synth_spec *spec, const char *options, pls_comm *comm, pls_handle **out);
 
 int pls_setup(pls_handle *h);
 /* Set / override one option ("key", "value" or NULL for a flag).  Options of

@@ -36,15 +36,32 @@ def submatrix(M, isrow, iscol):
 class BlockPC:
     def __init__(self, P, P_diff, index_sets, dims, flag_3_way, db,
                  inner_ksp_type="gmres", inner_pc_type="lu", w1=1.0, w2=0.1,
-                 accel_order=0, bcs_sub_pressure=()):
+                 accel_order=0, bcs_sub_pressure=(), dist_size=1):
         self.flag_3_way = flag_3_way
         self.w1, self.w2 = w1, w2
         self.ns, self.nf, self.np = dims
         self.is_s, self.is_f, self.is_p, self.is_fp = [np.asarray(i, dtype=np.int64) for i in index_sets]
         self.bcs = np.asarray(bcs_sub_pressure, dtype=np.int64)
         self.anderson = AndersonAcceleration(accel_order)
+        sizes = (self.ns, self.nf, self.np)
+
+        def inner(prefix, M, ksp_type, pc_type, fields):
+            # G ranks: BJACOBI blocks live inside each rank's [field slabs] rows
+            # (oracle/dist.py); other PC types are the same at any G
+            pc = None
+            if dist_size > 1:
+                ptype = opt(db, prefix, "pc_type", pc_type)
+                if ptype in ("ilu", "lu", "cholesky"):
+                    raise ValueError(f"{prefix}pc_type {ptype} is not distributable; use bjacobi")
+                if ptype == "bjacobi":
+                    from .dist import PCBJacobiIndexed, bjacobi_blocks
+                    nbt = opt(db, prefix, "pc_bjacobi_blocks", dist_size, int)
+                    pc = PCBJacobiIndexed(M, bjacobi_blocks(sizes, fields, dist_size, nbt),
+                                          opt(db, prefix + "sub_", "pc_type", "ilu"))
+            return petsc.ksp_from_options(prefix, db, M, M, ksp_type, pc_type, pc=pc)
+
         Ms_s = submatrix(P, self.is_s, self.is_s)
-        self.ksp_s = petsc.ksp_from_options("s_", db, Ms_s, Ms_s, inner_ksp_type, inner_pc_type)
+        self.ksp_s = inner("s_", Ms_s, inner_ksp_type, inner_pc_type, (0,))
         if flag_3_way:
             self.Ms_f = submatrix(P, self.is_s, self.is_f)
             self.Ms_p = submatrix(P, self.is_s, self.is_p)
@@ -52,21 +69,20 @@ class BlockPC:
             Mf_f = submatrix(P, self.is_f, self.is_f)
             Mp_p = submatrix(P, self.is_p, self.is_p)
             Mp_diff = submatrix(P_diff, self.is_p, self.is_p)
-            self.ksp_f = petsc.ksp_from_options("f_", db, Mf_f, Mf_f, inner_ksp_type, inner_pc_type)
-            self.ksp_p = petsc.ksp_from_options("p_", db, Mp_p, Mp_p, inner_ksp_type, inner_pc_type)
-            self.ksp_p_diff = petsc.ksp_from_options("diff_", db, Mp_diff, Mp_diff,
-                                                     inner_ksp_type, inner_pc_type)
+            self.ksp_f = inner("f_", Mf_f, inner_ksp_type, inner_pc_type, (1,))
+            self.ksp_p = inner("p_", Mp_p, inner_ksp_type, inner_pc_type, (2,))
+            self.ksp_p_diff = inner("diff_", Mp_diff, inner_ksp_type, inner_pc_type, (2,))
         else:
             self.Mfp_s = submatrix(P, self.is_fp, self.is_s)
             Mfp_fp = submatrix(P, self.is_fp, self.is_fp)
             if inner_pc_type == "lu":
-                self.ksp_fp = petsc.ksp_from_options("fp_", db, Mfp_fp, Mfp_fp, inner_ksp_type, "lu")
+                self.ksp_fp = inner("fp_", Mfp_fp, inner_ksp_type, "lu", (1, 2))
             else:
                 # setup_fieldsplit: GMRES + fieldsplit unless the options override the pc type
                 ptype = opt(db, "fp_", "pc_type", "fieldsplit")
                 if ptype == "fieldsplit":
                     raise NotImplementedError("fp_ fieldsplit (Schur) is not restated yet (SURVEY 8f rank 1)")
-                self.ksp_fp = petsc.ksp_from_options("fp_", db, Mfp_fp, Mfp_fp, "gmres", ptype)
+                self.ksp_fp = inner("fp_", Mfp_fp, "gmres", ptype, (1, 2))
 
     def apply(self, x):
         x = np.asarray(x, dtype=np.float64)
@@ -101,7 +117,7 @@ class BlockPC:
         return y
 
 
-def make_block_pc(P, P_diff, index_sets, dims, parameters, db, bcs_sub_pressure):
+def make_block_pc(P, P_diff, index_sets, dims, parameters, db, bcs_sub_pressure, dist_size=1):
     """Preconditioner(...).get_pc() restated (lib/Preconditioner.py:263-291)."""
     pc_type = parameters["pc type"]
     if pc_type not in PC_TYPES:
@@ -109,4 +125,4 @@ def make_block_pc(P, P_diff, index_sets, dims, parameters, db, bcs_sub_pressure)
     flag_3_way = pc_type in ("diagonal 3-way", "undrained 3-way")
     return BlockPC(P, P_diff, index_sets, dims, flag_3_way, db,
                    parameters["inner ksp type"], parameters["inner pc type"], 1.0, 0.1,
-                   parameters["inner accel order"], bcs_sub_pressure)
+                   parameters["inner accel order"], bcs_sub_pressure, dist_size)

@@ -190,6 +190,13 @@ class KSP:
     def matvec(self, x):
         return self.A @ x
 
+    # inner products (oracle/dist.py overrides them with rank-ordered global sums)
+    def dot(self, a, b):
+        return float(np.dot(a, b))
+
+    def norm(self, a):
+        return float(np.linalg.norm(a))
+
     def solve(self, b):
         b = np.asarray(b, dtype=np.float64)
         if self.type == "preonly":
@@ -247,7 +254,7 @@ def _gmres(ksp: KSP, b):
         if not right:
             r = ksp.pc.apply(r)
         # --- cycle
-        res = float(np.linalg.norm(r))
+        res = ksp.norm(r)
         V = [r * (1.0 / res) if res != 0.0 else r]
         hist.append(res)
         if ksp.monitor:
@@ -269,11 +276,11 @@ def _gmres(ksp: KSP, b):
             else:
                 w = ksp.pc.apply(ksp.matvec(v))
             # classical Gram-Schmidt: h = V^T w ; w -= V h
-            h = np.array([float(np.dot(V[j], w)) for j in range(loc_it + 1)])
+            h = np.array([ksp.dot(V[j], w) for j in range(loc_it + 1)])
             for j in range(loc_it + 1):
                 w = w - h[j] * V[j]
             HH[:loc_it + 1, loc_it] = h
-            tt = float(np.linalg.norm(w))
+            tt = ksp.norm(w)
             HH[loc_it + 1, loc_it] = tt
             hapbnd = abs(tt / grs[loc_it])
             if hapbnd > GMRES_HAPTOL:
@@ -351,9 +358,9 @@ def _cg(ksp: KSP, b):
     z = None
     if ksp.norm_type == "preconditioned":
         z = ksp.pc.apply(r)
-        dp = float(np.linalg.norm(z))
+        dp = ksp.norm(z)
     elif ksp.norm_type == "unpreconditioned":
-        dp = float(np.linalg.norm(r))
+        dp = ksp.norm(r)
     else:
         dp = 0.0
     hist.append(dp)
@@ -366,7 +373,7 @@ def _cg(ksp: KSP, b):
         return x
     if ksp.norm_type != "preconditioned":
         z = ksp.pc.apply(r)
-    beta = float(np.dot(z, r))
+    beta = ksp.dot(z, r)
     i = 0
     p = None
     dpi = 0.0
@@ -383,7 +390,7 @@ def _cg(ksp: KSP, b):
             p = bb * p + z
         dpiold = dpi
         w = ksp.matvec(p)
-        dpi = float(np.dot(p, w))
+        dpi = ksp.dot(p, w)
         betaold = beta
         if dpi == 0.0 or (i > 0 and np.sign(dpi) * np.sign(dpiold) < 0.0):
             reason = DIVERGED_INDEFINITE_MAT
@@ -393,9 +400,9 @@ def _cg(ksp: KSP, b):
         r = r + (-a) * w
         if ksp.norm_type == "preconditioned":
             z = ksp.pc.apply(r)
-            dp = float(np.linalg.norm(z))
+            dp = ksp.norm(z)
         elif ksp.norm_type == "unpreconditioned":
-            dp = float(np.linalg.norm(r))
+            dp = ksp.norm(r)
         else:
             dp = 0.0
         hist.append(dp)
@@ -407,7 +414,7 @@ def _cg(ksp: KSP, b):
             break
         if ksp.norm_type != "preconditioned":
             z = ksp.pc.apply(r)
-        beta = float(np.dot(z, r))
+        beta = ksp.dot(z, r)
         i += 1
         if i >= ksp.maxit:
             break

@@ -114,6 +114,7 @@ struct AndersonLS {
         auto gram = [&](int m, const double *rinv_dev) {
             launch_gram(n, m, dptr.p, rinv_dev, c.partial.p, dG.p, c.st);
             const int np = m * (m + 1) / 2;
+            c.comm->global_sum_dev(dG.p, np, c.st);
             HIPCHK(hipMemcpyAsync(c.hscal, dG.p, sizeof(double) * np, hipMemcpyDeviceToHost, c.st));
             c.sync();
             std::vector<double> G(m * m, 0.0);
@@ -284,6 +285,112 @@ struct BlockPC : PC {
     void apply(const double *x, double *y, Ctx &c) override;
 };
 
+// ========================================================== distribution ===
+// Row slabs per field (the analogue of PETSc MPIAIJ ownership ranges): rank r
+// owns rows [lo_f, lo_f + len_f) of every field f (PETSc split: the first
+// n % size ranks one row more); local layout [s_r | f_r | p_r].
+struct Dist {
+    int rank = 0, size = 1;
+    int64_t n[3] = {0, 0, 0}, off[3] = {0, 0, 0}, lo[3] = {0, 0, 0}, len[3] = {0, 0, 0}, loff[3] = {0, 0, 0};
+    int64_t nloc = 0;
+    static void slab(int64_t N, int size, int r, int64_t &lo, int64_t &len) {
+        const int64_t q = N / size, rem = N % size;
+        lo = r * q + std::min<int64_t>(r, rem);
+        len = q + (r < rem ? 1 : 0);
+    }
+    void init(const int64_t nf[3], int r, int s) {
+        rank = r;
+        size = s;
+        int64_t o = 0, lo_ = 0;
+        for (int f = 0; f < 3; ++f) {
+            n[f] = nf[f];
+            off[f] = o;
+            o += nf[f];
+            slab(nf[f], s, r, lo[f], len[f]);
+            loff[f] = lo_;
+            lo_ += len[f];
+        }
+        nloc = lo_;
+    }
+};
+
+// Turn a local-row matrix whose columns are indices into the column space of
+// fields [f0, f1] (0 = first column of field f0) into a distributed matrix:
+// owned columns -> local index (my slabs of those fields, field order), other
+// referenced columns -> ghosts nlocal + position (owner-major, then global),
+// plus the halo plan.  Builds the SELL-64 copy.
+static void make_dist(DevCSR &M, const Dist &D, int f0, int f1, Comm *comm, Ctx &c) {
+    int64_t gsize = 0, nlocal = 0;
+    int64_t cs_off[3] = {0, 0, 0}, l_off[3] = {0, 0, 0};
+    for (int f = f0; f <= f1; ++f) {
+        cs_off[f] = gsize;
+        l_off[f] = nlocal;
+        gsize += D.n[f];
+        nlocal += D.len[f];
+    }
+    std::vector<int32_t> own(gsize, -1);
+    for (int f = f0; f <= f1; ++f)
+        for (int64_t i = 0; i < D.len[f]; ++i) own[cs_off[f] + D.lo[f] + i] = (int32_t)(l_off[f] + i);
+    DBuf<int32_t> down(std::max<int64_t>(gsize, 1));
+    DBuf<uint8_t> dflag(std::max<int64_t>(gsize, 1));
+    HIPCHK(hipMemcpyAsync(down.p, own.data(), sizeof(int32_t) * gsize, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemsetAsync(dflag.p, 0, gsize, c.st));
+    launch_flag_ghosts(M.nnz, M.ci.p, down.p, dflag.p, c.st);
+    std::vector<uint8_t> flag(gsize);
+    HIPCHK(hipMemcpyAsync(flag.data(), dflag.p, gsize, hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    std::vector<std::vector<int64_t>> need(D.size);
+    std::vector<int32_t> gmap(own);
+    int64_t pos = 0;
+    auto H = std::make_shared<Halo>();
+    H->rcnt.assign(D.size, 0);
+    H->roff.assign(D.size, 0);
+    for (int q = 0; q < D.size; ++q) {
+        H->roff[q] = pos;
+        if (q == D.rank) continue;
+        for (int f = f0; f <= f1; ++f) {
+            int64_t lo, len;
+            Dist::slab(D.n[f], D.size, q, lo, len);
+            for (int64_t i = 0; i < len; ++i) {
+                const int64_t g = cs_off[f] + lo + i;
+                if (flag[g]) {
+                    gmap[g] = (int32_t)(nlocal + pos++);
+                    need[q].push_back(g);
+                }
+            }
+        }
+        H->rcnt[q] = (int64_t)need[q].size();
+    }
+    H->nlocal = nlocal;
+    H->nghost = pos;
+    std::vector<std::vector<int64_t>> asked;
+    comm->alltoallv_i64(need, asked);
+    std::vector<int32_t> sidx;
+    H->scnt.assign(D.size, 0);
+    H->soff.assign(D.size, 0);
+    for (int q = 0; q < D.size; ++q) {
+        H->soff[q] = (int64_t)sidx.size();
+        for (int64_t g : asked[q]) {
+            if (g < 0 || g >= gsize || own[g] < 0) throw Error("halo plan: peer asked for a column this rank does not own");
+            sidx.push_back(own[g]);
+        }
+        H->scnt[q] = (int64_t)asked[q].size();
+    }
+    H->nsend = (int64_t)sidx.size();
+    H->send_idx.alloc(std::max<int64_t>(H->nsend, 1));
+    if (H->nsend) HIPCHK(hipMemcpyAsync(H->send_idx.p, sidx.data(), sizeof(int32_t) * H->nsend, hipMemcpyHostToDevice, c.st));
+    H->sendbuf.alloc(std::max<int64_t>(H->nsend, 1));
+    H->ghost.alloc(std::max<int64_t>(H->nghost, 1));
+    DBuf<int32_t> dgmap(std::max<int64_t>(gsize, 1));
+    HIPCHK(hipMemcpyAsync(dgmap.p, gmap.data(), sizeof(int32_t) * gsize, hipMemcpyHostToDevice, c.st));
+    launch_remap_cols(M.nnz, M.ci.p, dgmap.p, c.st);
+    c.sync();
+    M.ncols = nlocal + H->nghost;
+    M.halo = H;
+    M.sell.reset();
+    build_sell(M, c);
+}
+
 // ================================================================ handle ===
 static void validate_pc_type(const Options &o) {
     std::string pt = o.str("pls.pc_type", "diagonal");
@@ -300,6 +407,10 @@ struct Handle {
     Timers timers;
     int64_t n = 0, ns = 0, nf = 0, np = 0;
     bool three_way = false, setup_done = false, solver_ready = false, keep = true;
+    Dist dist;                          // row slabs (size 1: everything local)
+    bool distributed = false;
+    std::unique_ptr<SynthDev> synth_rows;  // synthetic handles: row map for the rhs
+    DBuf<int32_t> synth_offs;
     std::string pc_type, solver_type, inner_ksp, inner_pc;
     std::vector<int64_t> perm;   // internal -> caller
     DBuf<int64_t> dperm;
@@ -457,6 +568,32 @@ static void do_setup(Handle &H) {
     };
     (void)w;
     // lib/Preconditioner.py:60-75 allocate_submatrices (field-major: contiguous ranges)
+    if (H.distributed) {
+        // local rows, global columns of the fields [f0, f1] -> distributed block
+        const Dist &D = H.dist;
+        auto dext = [&](const DevCSR &M, int64_t r0, int64_t r1, int f0, int f1, DevCSR &dst) {
+            const int64_t g0 = D.off[f0], g1 = D.off[f1] + D.n[f1];
+            WindowSpec ww{};
+            ww.mode = 0;
+            ww.c0 = g0;
+            ww.c1 = g1;
+            extract_csr(M, r0, r1, ww, g0, g1 - g0, dst, c);
+            make_dist(dst, D, f0, f1, c.comm, c);
+        };
+        const int64_t nfl = H.nf;
+        dext(H.P, 0, ns, 0, 0, H.Ks);
+        if (!H.three_way) {
+            dext(H.P, ns, n, 0, 0, H.Mfp_s);
+            dext(H.P, ns, n, 1, 2, H.Kfp);
+        } else {
+            if (!H.have_Pd) throw Error("3-way preconditioner needs P_diff");
+            dext(H.P, ns, ns + nfl, 1, 1, H.Kf);
+            dext(H.P, ns + nfl, n, 2, 2, H.Kp);
+            dext(H.Pd, ns + nfl, n, 2, 2, H.Kpd);
+            dext(H.P, 0, ns, 1, 2, H.Ms_fp);
+            dext(H.P, ns, ns + nfl, 2, 2, H.Mf_p);
+        }
+    } else {
     ext(H.P, 0, ns, 0, ns, H.Ks);
     if (!H.three_way) {
         ext(H.P, ns, n, 0, ns, H.Mfp_s);
@@ -468,6 +605,7 @@ static void do_setup(Handle &H) {
         ext(H.Pd, ns + nf, n, ns + nf, n, H.Kpd);
         ext(H.P, 0, ns, ns, n, H.Ms_fp);
         ext(H.P, ns, ns + nf, ns + nf, n, H.Mf_p);
+    }
     }
     // SELL-64 copies of every matrix the PC multiplies with
     if (!H.three_way) {
@@ -724,75 +862,120 @@ int pls_create(const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff, const i
     })
 }
 
+// Synthetic system generated directly in HBM.  With a communicator of size G
+// every rank generates only its row slabs (global columns), then the
+// matrices become distributed (make_dist): the same global system, sharded.
+static Handle *create_synthetic(const pls_synth_spec *spec, const char *options, Comm *comm) {
+    {
+        Options pre;
+        pre.parse(options);
+        validate_pc_type(pre);
+    }
+    auto H = std::make_unique<Handle>();
+    H->opt.parse(options);
+    H->parse_params();
+    H->timers.st = H->ctx.st;
+    if (comm) H->ctx.comm = comm;
+    Comm *cm = H->ctx.comm;
+    SynthHost S;
+    S.init(*spec);
+    H->dist.init(S.n, cm->rank, cm->size);
+    H->distributed = cm->size > 1;
+    const Dist &Dd = H->dist;
+    H->ns = Dd.len[0]; H->nf = Dd.len[1]; H->np = Dd.len[2];
+    H->n = Dd.nloc;
+    const int64_t n = H->n;
+    const int64_t nglob = S.n[0] + S.n[1] + S.n[2];
+    Ctx &c = H->ctx;
+    H->synth_offs.alloc(6 * 128);
+    auto D = std::make_unique<SynthDev>();
+    *D = SynthDev{};
+    D->dim = S.dim;
+    D->seed = S.seed;
+    D->delta = S.delta;
+    for (int f = 0; f < 3; ++f) {
+        D->n[f] = S.n[f];
+        D->off[f] = S.off[f];
+        D->rlo[f] = Dd.lo[f];
+        D->rlen[f] = Dd.len[f];
+        D->rloff[f] = Dd.loff[f];
+    }
+    D->nrows = n;
+    for (int b = 0; b < 6; ++b) {
+        D->cnt[b] = S.cnt[b];
+        HIPCHK(hipMemcpy(H->synth_offs.p + b * 128, S.offs[b].data(), sizeof(int32_t) * S.cnt[b],
+                         hipMemcpyHostToDevice));
+        D->offs[b] = H->synth_offs.p + b * 128;
+    }
+    // pattern (shared by A, P, P_diff)
+    DBuf<int64_t> len(n + 1);
+    launch_synth_count(*D, len.p, c.st);
+    H->A.rp.alloc(n + 1);
+    c.ensure_scan(n);
+    exclusive_scan_i64(len.p, H->A.rp.p, n, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
+    int64_t nnz = 0;
+    HIPCHK(hipMemcpyAsync(&nnz, H->A.rp.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    auto gen = [&](DevCSR &M, int variant) {
+        M.nrows = n; M.ncols = nglob; M.nnz = nnz;
+        if (!M.rp.p) {
+            M.rp.alloc(n + 1);
+            HIPCHK(hipMemcpyAsync(M.rp.p, H->A.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, c.st));
+        }
+        M.ci.alloc(std::max<int64_t>(nnz, 1));
+        M.val.alloc(std::max<int64_t>(nnz, 1));
+        launch_synth_fill(*D, variant, M.rp.p, M.ci.p, M.val.p, c.st);
+        HIPCHK(hipGetLastError());
+    };
+    gen(H->A, 0);
+    gen(H->P, 1);
+    if (H->three_way) {
+        gen(H->Pd, 2);
+        H->have_Pd = true;
+    }
+    c.sync();
+    if (H->distributed) make_dist(H->A, Dd, 0, 2, cm, c);
+    H->perm.resize(n);
+    std::iota(H->perm.begin(), H->perm.end(), 0);
+    H->dperm.alloc(std::max<int64_t>(n, 1));
+    HIPCHK(hipMemcpy(H->dperm.p, H->perm.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+    for (int64_t i = Dd.lo[2]; i < Dd.lo[2] + Dd.len[2]; ++i)
+        if (S.is_bc(i)) H->bcs.push_back((int32_t)(i - Dd.lo[2]));
+    H->dbcs.alloc(std::max<size_t>(H->bcs.size(), 1));
+    if (!H->bcs.empty())
+        HIPCHK(hipMemcpy(H->dbcs.p, H->bcs.data(), sizeof(int32_t) * H->bcs.size(), hipMemcpyHostToDevice));
+    H->keep = H->opt.flag("pls.keep_matrices", nnz < 50000000);
+    H->synth_rows = std::move(D);
+    return H.release();
+}
+
 int pls_create_synthetic(const pls_synth_spec *spec, const char *options, pls_handle **out) {
+    PLS_TRY(*out = reinterpret_cast<pls_handle *>(create_synthetic(spec, options, nullptr)))
+}
+
+int pls_create_synthetic_dist(const pls_synth_spec *spec, const char *options, pls_comm *comm, pls_handle **out) {
     PLS_TRY({
-        {
-            Options pre;
-            pre.parse(options);
-            validate_pc_type(pre);
-        }
-        auto H = std::make_unique<Handle>();
-        H->opt.parse(options);
-        H->parse_params();
-        H->timers.st = H->ctx.st;
-        SynthHost S;
-        S.init(*spec);
-        H->ns = S.n[0]; H->nf = S.n[1]; H->np = S.n[2];
-        H->n = H->ns + H->nf + H->np;
-        const int64_t n = H->n;
-        Ctx &c = H->ctx;
-        DBuf<int32_t> doffs(6 * 128);
-        SynthDev D{};
-        D.dim = S.dim;
-        D.seed = S.seed;
-        D.delta = S.delta;
-        for (int f = 0; f < 3; ++f) { D.n[f] = S.n[f]; D.off[f] = S.off[f]; }
-        for (int b = 0; b < 6; ++b) {
-            D.cnt[b] = S.cnt[b];
-            HIPCHK(hipMemcpy(doffs.p + b * 128, S.offs[b].data(), sizeof(int32_t) * S.cnt[b], hipMemcpyHostToDevice));
-            D.offs[b] = doffs.p + b * 128;
-        }
-        // pattern (shared by A, P, P_diff)
-        DBuf<int64_t> len(n + 1);
-        launch_synth_count(D, len.p, c.st);
-        H->A.rp.alloc(n + 1);
-        c.ensure_scan(n);
-        exclusive_scan_i64(len.p, H->A.rp.p, n, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
-        int64_t nnz = 0;
-        HIPCHK(hipMemcpyAsync(&nnz, H->A.rp.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
-        c.sync();
-        auto gen = [&](DevCSR &M, int variant) {
-            M.nrows = n; M.ncols = n; M.nnz = nnz;
-            if (!M.rp.p) {
-                M.rp.alloc(n + 1);
-                HIPCHK(hipMemcpyAsync(M.rp.p, H->A.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, c.st));
-            }
-            M.ci.alloc(nnz);
-            M.val.alloc(nnz);
-            launch_synth_fill(D, variant, M.rp.p, M.ci.p, M.val.p, c.st);
-            HIPCHK(hipGetLastError());
-        };
-        gen(H->A, 0);
-        gen(H->P, 1);
-        if (H->three_way) {
-            gen(H->Pd, 2);
-            H->have_Pd = true;
-        }
-        c.sync();
-        H->A.max_row = H->P.max_row = H->Pd.max_row = 0;
-        H->perm.resize(n);
-        std::iota(H->perm.begin(), H->perm.end(), 0);
-        H->dperm.alloc(std::max<int64_t>(n, 1));
-        HIPCHK(hipMemcpy(H->dperm.p, H->perm.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
-        for (int64_t i = 0; i < H->np; ++i)
-            if (S.is_bc(i)) H->bcs.push_back((int32_t)i);
-        H->dbcs.alloc(std::max<size_t>(H->bcs.size(), 1));
-        if (!H->bcs.empty())
-            HIPCHK(hipMemcpy(H->dbcs.p, H->bcs.data(), sizeof(int32_t) * H->bcs.size(), hipMemcpyHostToDevice));
-        H->keep = H->opt.flag("pls.keep_matrices", nnz < 50000000);
-        *out = reinterpret_cast<pls_handle *>(H.release());
+        if (!comm) throw Error("pls_create_synthetic_dist: communicator required");
+        *out = reinterpret_cast<pls_handle *>(create_synthetic(spec, options, reinterpret_cast<Comm *>(comm)));
     })
 }
+
+int pls_rccl_unique_id(char out[128]) { PLS_TRY(rccl_unique_id(out)) }
+int pls_comm_create_rccl(const char id[128], int rank, int size, pls_comm **out) {
+    PLS_TRY(*out = reinterpret_cast<pls_comm *>(static_cast<Comm *>(rccl_init(id, rank, size))))
+}
+int pls_comm_create_callback(int rank, int size, pls_allgather_fn fn, void *user, pls_comm **out) {
+    PLS_TRY({
+        if (!fn || rank < 0 || rank >= size) throw Error("pls_comm_create_callback: bad arguments");
+        auto *cb = new CommCallback();
+        cb->rank = rank;
+        cb->size = size;
+        cb->fn = fn;
+        cb->user = user;
+        *out = reinterpret_cast<pls_comm *>(static_cast<Comm *>(cb));
+    })
+}
+int pls_comm_destroy(pls_comm *comm) { PLS_TRY(delete reinterpret_cast<Comm *>(comm)) }
 
 int pls_setup(pls_handle *h) { PLS_TRY(do_setup(*reinterpret_cast<Handle *>(h))) }
 int pls_destroy(pls_handle *h) { PLS_TRY(delete reinterpret_cast<Handle *>(h)) }
@@ -901,7 +1084,8 @@ int pls_matmult_device(pls_handle *hh, const double *d_x, double *d_y) {
 int pls_synthetic_rhs_device(pls_handle *hh, uint64_t seed, double *d_b) {
     PLS_TRY({
         Handle &H = *reinterpret_cast<Handle *>(hh);
-        launch_synth_rhs(seed, H.n, d_b, H.ctx.st);
+        if (!H.synth_rows) throw Error("pls_synthetic_rhs_device: not a synthetic handle");
+        launch_synth_rhs(*H.synth_rows, seed, d_b, H.ctx.st);
         H.ctx.sync();
     })
 }

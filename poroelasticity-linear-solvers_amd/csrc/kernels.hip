@@ -126,29 +126,35 @@ __device__ __forceinline__ void synth_visit(const SynthDev &S, int a, int64_t i,
     }
 }
 
+__device__ __forceinline__ int64_t synth_global_row(const SynthDev &S, int64_t l) {
+    const int f = l < S.rloff[1] ? 0 : (l < S.rloff[2] ? 1 : 2);
+    return S.off[f] + S.rlo[f] + (l - S.rloff[f]);
+}
+
 __global__ __launch_bounds__(TPB) void k_synth_count(SynthDev S, int64_t *row_len) {
-    const int64_t n = S.n[0] + S.n[1] + S.n[2];
-    const int64_t g = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (g > n) return;
-    if (g == n) { row_len[n] = 0; return; }
+    const int64_t n = S.nrows;
+    const int64_t l = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (l > n) return;
+    if (l == n) { row_len[n] = 0; return; }
+    const int64_t g = synth_global_row(S, l);
     const int a = field_of(S, g);
     int64_t c = 0;
     synth_visit(S, a, g - S.off[a], [&](int, int64_t) { ++c; });
-    row_len[g] = c;
+    row_len[l] = c;
 }
 
 __global__ __launch_bounds__(TPB) void k_synth_fill(SynthDev S, int variant, const int64_t *rp,
                                                     int32_t *col, double *val) {
-    const int64_t n = S.n[0] + S.n[1] + S.n[2];
-    const int64_t g = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (g >= n) return;
+    const int64_t l = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (l >= S.nrows) return;
+    const int64_t g = synth_global_row(S, l);
     const int a = field_of(S, g);
     const int64_t i = g - S.off[a];
     const uint64_t sv = S.seed ^ SALT_VAL;
     const uint64_t sd = S.seed ^ (variant == 0 ? SALT_DIAGA : SALT_DIAGP);
     const bool bcrow = (variant == 2 && a == 2 &&
                         ((hash3(S.seed ^ SALT_BC, (uint64_t)i, 7ULL) & 15ULL) == 0ULL));
-    int64_t pos = rp[g];
+    int64_t pos = rp[l];
     int64_t dpos = -1;
     double sum = 0.0;
     synth_visit(S, a, i, [&](int b, int64_t gj) {
@@ -176,26 +182,25 @@ __global__ __launch_bounds__(TPB) void k_synth_fill(SynthDev S, int variant, con
     }
 }
 
-__global__ __launch_bounds__(TPB) void k_synth_rhs(uint64_t seed, int64_t n, double *b) {
-    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (i >= n) return;
+__global__ __launch_bounds__(TPB) void k_synth_rhs(SynthDev S, uint64_t seed, double *b) {
+    const int64_t l = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (l >= S.nrows) return;
+    const int64_t i = synth_global_row(S, l);
     const double u = u01(hash3(seed ^ SALT_RHS, (uint64_t)i, 3ULL));
-    b[i] = 2.0 * u - 1.0;
+    b[l] = 2.0 * u - 1.0;
 }
 
 #pragma clang fp contract(on)
 
 void launch_synth_count(const SynthDev &S, int64_t *row_len, hipStream_t st) {
-    const int64_t n = S.n[0] + S.n[1] + S.n[2];
-    k_synth_count<<<grid_for(n + 1, TPB), TPB, 0, st>>>(S, row_len);
+    k_synth_count<<<grid_for(S.nrows + 1, TPB), TPB, 0, st>>>(S, row_len);
 }
 void launch_synth_fill(const SynthDev &S, int variant, const int64_t *row_ptr, int32_t *col,
                        double *val, hipStream_t st) {
-    const int64_t n = S.n[0] + S.n[1] + S.n[2];
-    k_synth_fill<<<grid_for(n, TPB), TPB, 0, st>>>(S, variant, row_ptr, col, val);
+    if (S.nrows > 0) k_synth_fill<<<grid_for(S.nrows, TPB), TPB, 0, st>>>(S, variant, row_ptr, col, val);
 }
-void launch_synth_rhs(uint64_t seed, int64_t n, double *b, hipStream_t st) {
-    k_synth_rhs<<<grid_for(n, TPB), TPB, 0, st>>>(seed, n, b);
+void launch_synth_rhs(const SynthDev &S, uint64_t seed, double *b, hipStream_t st) {
+    if (S.nrows > 0) k_synth_rhs<<<grid_for(S.nrows, TPB), TPB, 0, st>>>(S, seed, b);
 }
 
 // ================================================================ scans ====
@@ -587,7 +592,7 @@ void launch_maxpy_norm(int64_t n, int k, const double *V, int64_t ldv, const dou
                        double *w, double *partial, double *out, hipStream_t st) {
     const int nb = reduce_blocks(n);
     k_maxpy_norm<<<nb, TPB, 0, st>>>(n, k, V, ldv, h_dev, w, out ? partial : nullptr);
-    if (out) k_final<<<1, TPB, 0, st>>>(nb, partial, out, 1);
+    if (out) k_final<<<1, TPB, 0, st>>>(nb, partial, out, 0);  // ||w||^2 (rank-local)
 }
 
 __global__ __launch_bounds__(TPB) void k_lincomb(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
@@ -930,11 +935,12 @@ __global__ __launch_bounds__(TPB) void k_sell_fill(int64_t nrows, int64_t nslice
 
 // TAG only separates the outer-operator instantiation (TAG 1: y = A x of the
 // Krylov loop) from the preconditioner's block products in profiles.
-template <int U, int TAG>
+template <int U, int TAG, bool HALO>
 __global__ __launch_bounds__(TPB) void k_sell_spmv(int64_t nrows, int64_t nslices, const int64_t *__restrict__ sptr,
                                                    const int32_t *__restrict__ scol, const double *__restrict__ sval,
                                                    const double *__restrict__ x, double *__restrict__ y, double alpha,
-                                                   double beta, const double *__restrict__ z) {
+                                                   double beta, const double *__restrict__ z,
+                                                   const double *__restrict__ ghost, int32_t nlocal) {
     const int lane = threadIdx.x & 63;
     const int64_t sl = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
     if (sl >= nslices) return;
@@ -955,7 +961,15 @@ __global__ __launch_bounds__(TPB) void k_sell_spmv(int64_t nrows, int64_t nslice
             v[u] = k < L ? t : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc += v[u] * x[(uint32_t)c[u]];
+        for (int u = 0; u < U; ++u) {
+            if (HALO) {
+                const bool loc = c[u] < nlocal;
+                const double xv = loc ? x[(uint32_t)c[u]] : ghost[(uint32_t)(c[u] - nlocal)];
+                acc += v[u] * xv;
+            } else {
+                acc += v[u] * x[(uint32_t)c[u]];
+            }
+        }
     }
     const int64_t row = sl * 64 + lane;
     if (row < nrows) {
@@ -977,13 +991,19 @@ void launch_sell_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const
     if (ns > 0) k_sell_fill<<<grid_for(ns * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, ci, val, sptr, scol, sval);
 }
 void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, const double *sval, const double *x,
-                      double *y, double alpha, double beta, const double *z, int tag, hipStream_t st) {
+                      double *y, double alpha, double beta, const double *z, int tag, const double *ghost,
+                      int64_t nlocal, hipStream_t st) {
     const int64_t ns = sell_nslices(nrows);
     if (ns <= 0) return;
-    if (tag)
-        k_sell_spmv<8, 1><<<grid_for(ns, TPB / 64), TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z);
-    else
-        k_sell_spmv<8, 0><<<grid_for(ns, TPB / 64), TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z);
+    const unsigned g = grid_for(ns, TPB / 64);
+    const int32_t nl = (int32_t)nlocal;
+    if (ghost) {
+        if (tag) k_sell_spmv<8, 1, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z, ghost, nl);
+        else k_sell_spmv<8, 0, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z, ghost, nl);
+    } else {
+        if (tag) k_sell_spmv<8, 1, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z, ghost, nl);
+        else k_sell_spmv<8, 0, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, scol, sval, x, y, alpha, beta, z, ghost, nl);
+    }
 }
 
 // ================================================= level-aligned SELL-64 ====
@@ -1287,6 +1307,33 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
     k_ilu_blocks_lds<<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lrow, Llen, Lcol, Lval,
                                                               Ugoff, Ugslice, Usptr, Urow, Ulen, Ucol, Uval, Udinv, x,
                                                               y);
+}
+
+// =========================================================== distribution ====
+// flag[c] = 1 for every column c (relative to the column space) of the matrix
+// that this rank does not own (own[c] < 0)
+__global__ __launch_bounds__(TPB) void k_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint8_t *flag) {
+    for (int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * TPB) {
+        const int32_t c = ci[k];
+        if (own[c] < 0) flag[c] = 1;
+    }
+}
+__global__ __launch_bounds__(TPB) void k_remap_cols(int64_t nnz, int32_t *ci, const int32_t *gmap) {
+    for (int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * TPB)
+        ci[k] = gmap[ci[k]];
+}
+__global__ __launch_bounds__(TPB) void k_pack(int64_t m, const int32_t *idx, const double *x, double *buf) {
+    const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (k < m) buf[k] = x[idx[k]];
+}
+void launch_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint8_t *flag, hipStream_t st) {
+    if (nnz > 0) k_flag_ghosts<<<stream_grid(nnz), TPB, 0, st>>>(nnz, ci, own, flag);
+}
+void launch_remap_cols(int64_t nnz, int32_t *ci, const int32_t *gmap, hipStream_t st) {
+    if (nnz > 0) k_remap_cols<<<stream_grid(nnz), TPB, 0, st>>>(nnz, ci, gmap);
+}
+void launch_pack(int64_t m, const int32_t *idx, const double *x, double *buf, hipStream_t st) {
+    if (m > 0) k_pack<<<grid_for(m, TPB), TPB, 0, st>>>(m, idx, x, buf);
 }
 
 }  // namespace pls

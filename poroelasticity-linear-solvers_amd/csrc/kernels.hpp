@@ -15,11 +15,14 @@ struct SynthDev {
     int64_t off[3];
     int32_t cnt[6];
     const int32_t *offs[6];  // device pointers, sorted offsets per forward block
+    // rows generated: local row l in [rloff[f], rloff[f] + rlen[f]) is global
+    // row off[f] + rlo[f] + (l - rloff[f]) (identity for a single rank)
+    int64_t rlo[3], rlen[3], rloff[3], nrows;
 };
 void launch_synth_count(const SynthDev &S, int64_t *row_len, hipStream_t st);
 void launch_synth_fill(const SynthDev &S, int variant, const int64_t *row_ptr, int32_t *col,
                        double *val, hipStream_t st);
-void launch_synth_rhs(uint64_t seed, int64_t n, double *b, hipStream_t st);
+void launch_synth_rhs(const SynthDev &S, uint64_t seed, double *b, hipStream_t st);
 
 // ---------------------------------------------------------------- CSR ops --
 // Exclusive scan of n+1 entries: in[0..n) lengths -> out[0..n] offsets.
@@ -71,7 +74,7 @@ void launch_dot(int64_t n, const double *x, const double *y, double *partial, do
                 hipStream_t st);
 // out = ||x||_2 (sqrt of sum of squares)
 void launch_norm2(int64_t n, const double *x, double *partial, double *out, hipStream_t st);
-// w -= sum_j h[j] * V[:, j] (h on device, j < k); out = ||w||_2 when out != null
+// w -= sum_j h[j] * V[:, j] (h on device, j < k); out = ||w||_2^2 (local) when out != null
 void launch_maxpy_norm(int64_t n, int k, const double *V, int64_t ldv, const double *h_dev,
                        double hscale, double *w, double *partial, double *out, hipStream_t st);
 // y = sum_j c[j] * V[:, j] (c on device)
@@ -112,9 +115,11 @@ int64_t sell_nslices(int64_t nrows);
 void launch_sell_slice_len(int64_t nrows, const int64_t *rp, int64_t *slen /* nslices+1 */, hipStream_t st);
 void launch_sell_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const double *val, const int64_t *sptr,
                       int32_t *scol, double *sval, hipStream_t st);
-// tag 1 = the outer operator A (separate kernel symbol in profiles)
+// tag 1 = the outer operator A (separate kernel symbol in profiles);
+// ghost != null: columns >= nlocal read ghost[c - nlocal] (halo entries)
 void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, const double *sval, const double *x,
-                      double *y, double alpha, double beta, const double *z, int tag, hipStream_t st);
+                      double *y, double alpha, double beta, const double *z, int tag, const double *ghost,
+                      int64_t nlocal, hipStream_t st);
 
 // Level-aligned SELL-64 triangular factors (see kernels.hip)
 void launch_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *slot_len, const int64_t *rp,
@@ -135,5 +140,10 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const double *Lval, const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr,
                            const int32_t *Urow, const int32_t *Ulen, const int32_t *Ucol, const double *Uval,
                            const double *Udinv, const double *x, double *y, hipStream_t st);
+
+// distribution helpers
+void launch_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint8_t *flag, hipStream_t st);
+void launch_remap_cols(int64_t nnz, int32_t *ci, const int32_t *gmap, hipStream_t st);
+void launch_pack(int64_t m, const int32_t *idx, const double *x, double *buf, hipStream_t st);
 
 }  // namespace pls

@@ -19,7 +19,10 @@
 namespace pls {
 
 // ============================================================== context ===
+static CommSelf g_self_comm;
+
 Ctx::Ctx() {
+    comm = &g_self_comm;
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     partial.alloc(1024 * 136);
     dscal.alloc(4096);
@@ -38,15 +41,17 @@ void Ctx::ensure_scan(int64_t n) {
 }
 double Ctx::dot(int64_t n, const double *x, const double *y) {
     launch_dot(n, x, y, partial.p, dscal.p, st);
+    comm->global_sum_dev(dscal.p, 1, st);
     HIPCHK(hipMemcpyAsync(hscal, dscal.p, sizeof(double), hipMemcpyDeviceToHost, st));
     sync();
     return hscal[0];
 }
 double Ctx::norm2(int64_t n, const double *x) {
-    launch_norm2(n, x, partial.p, dscal.p, st);
+    launch_dot(n, x, x, partial.p, dscal.p, st);
+    comm->global_sum_dev(dscal.p, 1, st);
     HIPCHK(hipMemcpyAsync(hscal, dscal.p, sizeof(double), hipMemcpyDeviceToHost, st));
     sync();
-    return hscal[0];
+    return std::sqrt(hscal[0]);
 }
 
 // ================================================================== CSR ===
@@ -127,8 +132,19 @@ void build_sell(DevCSR &M, Ctx &c) {
 }
 
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z) {
+    const double *ghost = nullptr;
+    int64_t nlocal = M.ncols;
+    if (M.halo) {
+        Halo &H = *M.halo;
+        launch_pack(H.nsend, H.send_idx.p, x, H.sendbuf.p, c.st);
+        c.comm->exchange_dev(H.sendbuf.p, H.scnt, H.soff, H.ghost.p, H.rcnt, H.roff, c.st);
+        ghost = H.ghost.p;
+        nlocal = H.nlocal;
+        if (!M.sell) throw Error("distributed matrix without SELL layout");
+    }
     if (M.sell) {
-        launch_sell_spmv(M.nrows, M.sell->sptr.p, M.sell->col.p, M.sell->val.p, x, y, alpha, beta, z, M.tag, c.st);
+        launch_sell_spmv(M.nrows, M.sell->sptr.p, M.sell->col.p, M.sell->val.p, x, y, alpha, beta, z, M.tag, ghost,
+                         nlocal, c.st);
         return;
     }
     launch_spmv(M.nrows, M.nnz, M.rp.p, M.ci.p, M.val.p, x, y, alpha, beta, z, c.st);
@@ -451,7 +467,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds) {
     } else {
         w.mode = 0;
         w.c0 = 0;
-        w.c1 = M.ncols;
+        w.c1 = M.halo ? n : M.ncols;  // distributed: drop ghost columns (rank block only)
     }
     if (exact) envelope_csr(M, F, c);
     else extract_csr(M, 0, n, w, 0, n, F, c);
@@ -519,6 +535,10 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
                             Ctx &c) {
     if (type == "none") return std::make_unique<PCNone>(M.nrows);
     if (type == "jacobi") return std::make_unique<PCJacobi>(M, c);
+    const bool dist = c.comm && c.comm->size > 1;
+    if (dist && (type == "ilu" || type == "lu" || type == "cholesky"))
+        throw Error("PC type '" + type + "' (prefix " + prefix +
+                    ") acts on the whole parallel matrix; with several ranks use bjacobi (ILU(0) per rank block)");
     if (type == "ilu") {
         if (o.integer(prefix + "pc_factor_levels", 0) != 0)
             throw Error(prefix + "pc_factor_levels > 0: only ILU(0) is implemented");
@@ -528,7 +548,11 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true));
     }
     if (type == "bjacobi") {
-        const int64_t nb = o.integer(prefix + "pc_bjacobi_blocks", 1);
+        // total blocks over all ranks (PCBJacobiSetTotalBlocks): rank r gets
+        // B / size (+1 for the first B % size ranks); at least one per rank
+        const int64_t nbt = o.integer(prefix + "pc_bjacobi_blocks", dist ? c.comm->size : 1);
+        int64_t nb = nbt;
+        if (dist) nb = std::max<int64_t>(1, nbt / c.comm->size + (c.comm->rank < nbt % c.comm->size ? 1 : 0));
         const std::string sub = o.str(prefix + "sub_pc_type", "ilu");
         if (sub == "ilu") {
             if (o.integer(prefix + "sub_pc_factor_levels", 0) != 0)
@@ -666,11 +690,13 @@ void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
             }
             const int k = (int)(loc_it + 1);
             launch_mdot(n, k, nullptr, V.p, n, vn, c.partial.p, dh.p, c.st);
+            c.comm->global_sum_dev(dh.p, k, c.st);
             launch_maxpy_norm(n, k, V.p, n, dh.p, -1.0, vn, c.partial.p, dh.p + k, c.st);
+            c.comm->global_sum_dev(dh.p + k, 1, c.st);
             HIPCHK(hipMemcpyAsync(c.hscal, dh.p, sizeof(double) * (k + 1), hipMemcpyDeviceToHost, c.st));
             c.sync();
             for (int j = 0; j < k; ++j) H(j, loc_it) = c.hscal[j];
-            const double tt = c.hscal[k];
+            const double tt = std::sqrt(c.hscal[k]);
             H(loc_it + 1, loc_it) = tt;
             double hapbnd = std::fabs(tt / grs[loc_it]);
             if (hapbnd > haptol) hapbnd = haptol;

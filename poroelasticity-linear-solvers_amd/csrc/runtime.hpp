@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "comm.hpp"
 #include "kernels.hpp"
 
 namespace pls {
@@ -61,6 +62,7 @@ struct DBuf {
 // ------------------------------------------------------------------ context --
 struct Ctx {
     hipStream_t st = nullptr;
+    Comm *comm = nullptr;   // global reductions (CommSelf unless distributed)
     DBuf<double> partial;   // reduction partials (NB_MAX * 136)
     DBuf<double> dscal;     // device scalars
     double *hscal = nullptr;  // pinned host mirror
@@ -83,8 +85,19 @@ struct DevSELL {
     DBuf<double> val;
 };
 
+// Halo of a distributed matrix: columns >= nlocal are ghosts (entries owned by
+// other ranks, ordered owner-major); before each product the owned entries
+// other ranks need are packed and exchanged into `ghost`.
+struct Halo {
+    int64_t nlocal = 0, nghost = 0, nsend = 0;
+    DBuf<int32_t> send_idx;
+    DBuf<double> sendbuf, ghost;
+    std::vector<int64_t> scnt, soff, rcnt, roff;
+};
+
 struct DevCSR {
     int64_t nrows = 0, ncols = 0, nnz = 0;
+    std::shared_ptr<Halo> halo;     // distributed matrices only
     DBuf<int64_t> rp;
     DBuf<int32_t> ci;
     DBuf<double> val;

@@ -43,8 +43,11 @@ EXPORTS = [
     "pls_pc_apply_device", "pls_matmult_device", "pls_synthetic_rhs_device", "pls_device_alloc",
     "pls_device_free", "pls_memcpy_h2d", "pls_memcpy_d2h", "pls_get_result", "pls_get_history",
     "pls_get_timings", "pls_reset_timings", "pls_export_matrix", "pls_get_permutation",
-    "pls_bench_spmv",
+    "pls_bench_spmv", "pls_rccl_unique_id", "pls_comm_create_rccl", "pls_comm_create_callback",
+    "pls_comm_destroy", "pls_create_synthetic_dist",
 ]
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
 
 
 def lib():
@@ -84,6 +87,11 @@ def lib():
     L.pls_export_matrix.argtypes = [vp, C.c_int, C.POINTER(i64), C.POINTER(i64), vp, vp, vp]
     L.pls_get_permutation.argtypes = [vp, vp]
     L.pls_bench_spmv.argtypes = [vp, vp, vp, i32, C.POINTER(C.c_double)]
+    L.pls_rccl_unique_id.argtypes = [C.c_char_p]
+    L.pls_comm_create_rccl.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(vp)]
+    L.pls_comm_create_callback.argtypes = [C.c_int, C.c_int, ALLGATHER_FN, vp, C.POINTER(vp)]
+    L.pls_comm_destroy.argtypes = [vp]
+    L.pls_create_synthetic_dist.argtypes = [C.POINTER(pls_synth_spec), C.c_char_p, vp, C.POINTER(vp)]
     _lib = L
     return L
 

@@ -70,6 +70,18 @@ class Handle:
         N.check(N.lib().pls_create_synthetic(C.byref(spec), options_text(options), C.byref(out)))
         return cls(out)
 
+    @classmethod
+    def synthetic_dist(cls, dim, Nel, seed, delta, options: dict, comm):
+        """This rank's share of the synthetic system on ``comm`` (lib/dist.py).
+
+        Sizes and vectors are rank-local: [s_r | f_r | p_r] (PETSc row slabs)."""
+        spec = N.pls_synth_spec(int(dim), int(Nel), int(seed), float(delta))
+        out = C.c_void_p()
+        N.check(N.lib().pls_create_synthetic_dist(C.byref(spec), options_text(options), comm.ptr, C.byref(out)))
+        h = cls(out)
+        h._comm = comm  # destroyed after the handle
+        return h
+
     # ------------------------------------------------------------- control --
     def set_option(self, key, value=None):
         N.check(N.lib().pls_set_option(self.ptr, str(key).encode(), None if value is None else str(value).encode()))
