@@ -102,6 +102,8 @@ def main():
     ap.add_argument("--cpu-N", type=int, default=20)
     ap.add_argument("--cpu-maxit", type=int, default=100)
     ap.add_argument("--replicas", action="store_true", help="G independent N=59 solves instead of one sharded solve")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="host: host-staged gloo communicator (ranks may share a GPU; rehearsal only)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -114,7 +116,7 @@ def main():
 
     import lib._native as Nat
     from lib.handle import Handle, params_to_options
-    Nat.check(Nat.lib().pls_set_device(local))
+    Nat.check(Nat.lib().pls_set_device(local if args.comm == "rccl" else 0))
 
     sharded = world > 1 and not args.replicas
     N_glob = args.N
@@ -129,7 +131,7 @@ def main():
     comm = None
     if sharded:
         from lib.dist import Communicator
-        comm = Communicator.rccl()
+        comm = Communicator.rccl() if args.comm == "rccl" else Communicator.gloo()
         h = Handle.synthetic_dist(3, N_glob, SEED, DELTA, opts, comm)
     else:
         h = Handle.synthetic(3, args.N, SEED + rank, DELTA, opts)
@@ -207,7 +209,7 @@ def main():
                              f"rtol 1e-6 atol 1e-8 restart=maxit={args.maxit}, 2-way block PC, inner preonly+"
                              f"{args.inner}" + (f"(ILU(0), {args.blocks_s}/{args.blocks_fp} blocks s/fp)" if args.inner == "bjacobi" else "")),
                 "dim": 3, "N": N_glob, "dofs": n_global, "dofs_rank0": n, "nnz_A_rank0": nnz,
-                "parallelism": (f"row slabs x{world} (RCCL)" if sharded else
+                "parallelism": (f"row slabs x{world} ({args.comm})" if sharded else
                                 f"replicas x{world}" if world > 1 else "single GPU"),
             },
             "its_per_solve": its / args.steps,

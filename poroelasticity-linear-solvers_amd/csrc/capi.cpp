@@ -384,6 +384,8 @@ static void make_dist(DevCSR &M, const Dist &D, int f0, int f1, Comm *comm, Ctx 
     DBuf<int32_t> dgmap(std::max<int64_t>(gsize, 1));
     HIPCHK(hipMemcpyAsync(dgmap.p, gmap.data(), sizeof(int32_t) * gsize, hipMemcpyHostToDevice, c.st));
     launch_remap_cols(M.nnz, M.ci.p, dgmap.p, c.st);
+    launch_sort_rows(M.nrows, M.rp.p, M.ci.p, M.val.p, c.st);
+    HIPCHK(hipGetLastError());
     c.sync();
     M.ncols = nlocal + H->nghost;
     M.halo = H;

@@ -1332,6 +1332,30 @@ void launch_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint
 void launch_remap_cols(int64_t nnz, int32_t *ci, const int32_t *gmap, hipStream_t st) {
     if (nnz > 0) k_remap_cols<<<stream_grid(nnz), TPB, 0, st>>>(nnz, ci, gmap);
 }
+// Remapped rows are sorted runs (owned columns in order, ghosts per owner and
+// field in order) -> restore ascending columns; one thread per row, insertion
+// sort (setup only; every consumer -- window extraction, diagonal search, ILU
+// pattern matching -- binary-searches sorted rows).
+__global__ __launch_bounds__(TPB) void k_sort_rows(int64_t n, const int64_t *rp, int32_t *ci, double *val) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const int64_t s = rp[i], e = rp[i + 1];
+    for (int64_t k = s + 1; k < e; ++k) {
+        const int32_t c = ci[k];
+        const double v = val[k];
+        int64_t j = k - 1;
+        while (j >= s && ci[j] > c) {
+            ci[j + 1] = ci[j];
+            val[j + 1] = val[j];
+            --j;
+        }
+        ci[j + 1] = c;
+        val[j + 1] = v;
+    }
+}
+void launch_sort_rows(int64_t n, const int64_t *rp, int32_t *ci, double *val, hipStream_t st) {
+    if (n > 0) k_sort_rows<<<grid_for(n, TPB), TPB, 0, st>>>(n, rp, ci, val);
+}
 void launch_pack(int64_t m, const int32_t *idx, const double *x, double *buf, hipStream_t st) {
     if (m > 0) k_pack<<<grid_for(m, TPB), TPB, 0, st>>>(m, idx, x, buf);
 }

@@ -144,6 +144,7 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
 // distribution helpers
 void launch_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint8_t *flag, hipStream_t st);
 void launch_remap_cols(int64_t nnz, int32_t *ci, const int32_t *gmap, hipStream_t st);
+void launch_sort_rows(int64_t n, const int64_t *rp, int32_t *ci, double *val, hipStream_t st);
 void launch_pack(int64_t m, const int32_t *idx, const double *x, double *buf, hipStream_t st);
 
 }  // namespace pls
