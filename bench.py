@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-N", type=int, default=20)
     ap.add_argument("--cpu-maxit", type=int, default=100)
+    ap.add_argument("--sell-d16", type=int, default=1, help="1: SELL-64/D16 SpMV layout (16-bit column deltas)")
     ap.add_argument("--replicas", action="store_true", help="G independent N=59 solves instead of one sharded solve")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="host: host-staged gloo communicator (ranks may share a GPU; rehearsal only)")
@@ -127,6 +128,7 @@ def main():
     params, db = solver_options(args)
     opts = dict(db)
     opts.update(params_to_options(params))
+    opts["pls.sell_d16"] = str(args.sell_d16)
     t0 = time.perf_counter()
     comm = None
     if sharded:
@@ -187,6 +189,8 @@ def main():
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 8.0 * n + 8.0 * n
     achieved = alg_bytes / spmv_avg / 1e9 if spmv_avg > 0 else 0.0
     iso = h.bench_spmv(d_x.p, d_b.p, 10)
+    d16, mat_bytes = h.spmv_layout()
+    fmt_bytes = mat_bytes + 8.0 * n + 8.0 * n  # + x once + y once
     h.rhs_device(7, d_b.p)
 
     if rank == 0:
@@ -217,9 +221,12 @@ def main():
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_spmv<64> (y = A x, outer MatMult)",
+                         "kernel": ("k_d16_spmv<2,1,false>" if d16 else "k_sell_spmv<8,1,false>") + " (y = A x, outer MatMult)",
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_s": spmv_avg,
-                         "isolated_spmv_gbs": alg_bytes / iso / 1e9},
+                         "isolated_spmv_gbs": alg_bytes / iso / 1e9,
+                         "layout": "SELL-64/D16 (16-bit column deltas)" if d16 else "SELL-64 (int32 columns)",
+                         "layout_bytes_per_launch": fmt_bytes,
+                         "layout_gbs": fmt_bytes / spmv_avg / 1e9 if spmv_avg > 0 else 0.0},
             "timings_s": {k: v for k, v in tm.items()},
         }
         if not args.no_cpu and world == 1:

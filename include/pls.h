@@ -175,6 +175,11 @@ int pls_get_permutation(pls_handle *h, int64_t *perm);
  * y = A x on the handle's A, repeated `reps` times; returns the mean device
  * time per launch in seconds measured with HIP events on the solver stream. */
 int pls_bench_spmv(pls_handle *h, const double *d_x, double *d_y, int32_t reps, double *sec_per_launch);
+/* Layout of A's SpMV copy: d16 = 1 for SELL-64/D16 (16-bit column deltas),
+ * 0 for SELL-64 (int32 columns); matrix_bytes = bytes one product streams
+ * from the matrix arrays (padding included).  Option "pls.sell_d16 0"
+ * forces the int32 layout.                                                   */
+int pls_spmv_layout(pls_handle *h, int32_t *d16, int64_t *matrix_bytes);
 
 #ifdef __cplusplus
 }

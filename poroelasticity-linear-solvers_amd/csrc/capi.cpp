@@ -462,6 +462,7 @@ struct Handle {
         inner_ksp = opt.str("pls.inner_ksp_type", "gmres");
         inner_pc = opt.str("pls.inner_pc_type", "hypre");
         timers.enabled = opt.flag("pls.timers", true);
+        ctx.sell_d16 = opt.flag("pls.sell_d16", true);
     }
 };
 
@@ -1165,6 +1166,15 @@ int pls_bench_spmv(pls_handle *hh, const double *d_x, double *d_y, int32_t reps,
         (void)hipEventDestroy(a);
         (void)hipEventDestroy(b);
         *sec_per_launch = (double)ms * 1e-3 / std::max(1, reps);
+    })
+}
+
+int pls_spmv_layout(pls_handle *hh, int32_t *d16, int64_t *matrix_bytes) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        build_sell(H.A, H.ctx);
+        if (d16) *d16 = H.A.sell && H.A.sell->d16 ? 1 : 0;
+        if (matrix_bytes) *matrix_bytes = H.A.sell ? H.A.sell->bytes() : 0;
     })
 }
 

@@ -1006,6 +1006,171 @@ void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, c
     }
 }
 
+// ====================================================== SELL-64 / D16 =====
+// Compressed SELL-64: entry k of a lane's row stores a 16-bit column delta
+// (col_k - col_{k-1}, 1..65535) instead of an int32 column, 10 B per entry
+// instead of 12.  A delta of 0 means "start the next segment": the column is
+// the next of the row's D16_SEG absolute segment bases (the first entry, and
+// every jump > 65535 -- field-block changes, ghost columns).  Padding entries
+// are segment starts with value 0.0 (the base index clamps to the last one).
+// Layout for 16-B-per-lane loads (1 KiB per wave instruction):
+//   deltas  dl[base + (k / 8) * 512 + lane * 8 + k % 8]   (one uint4 = 8 deltas)
+//   values  dv[base + (k / 2) * 128 + lane * 2 + k % 2]   (one double2 = 2 values)
+//   bases   seg[row * D16_SEG + j]                        (one int4 per lane)
+// Summation order per row is the CSR order: results equal SELL-64 bitwise.
+__global__ __launch_bounds__(TPB) void k_d16_slice_len(int64_t nrows, int64_t nslices, const int64_t *rp,
+                                                       int64_t *slen) {
+    const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sl > nslices) return;
+    if (sl == nslices) { if (lane == 0) slen[nslices] = 0; return; }
+    const int64_t row = sl * 64 + lane;
+    int64_t len = row < nrows ? rp[row + 1] - rp[row] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t t = __shfl_xor(len, o);
+        len = t > len ? t : len;
+    }
+    if (lane == 0) slen[sl] = 64 * ((len + 7) & ~(int64_t)7);
+}
+
+// segments each row needs; *maxseg = max over rows
+__global__ __launch_bounds__(TPB) void k_d16_count(int64_t nrows, const int64_t *rp, const int32_t *ci,
+                                                   int32_t *maxseg) {
+    const int64_t row = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (row >= nrows) return;
+    const int64_t s = rp[row], e = rp[row + 1];
+    int nseg = 0;
+    for (int64_t k = s; k < e; ++k)
+        if (k == s || (int64_t)ci[k] - (int64_t)ci[k - 1] > 65535 || ci[k] <= ci[k - 1]) ++nseg;
+    if (nseg > 0) atomicMax(maxseg, nseg);
+}
+
+__global__ __launch_bounds__(TPB) void k_d16_fill(int64_t nrows, int64_t nslices, const int64_t *rp,
+                                                  const int32_t *ci, const double *val, const int64_t *sptr,
+                                                  uint16_t *dl, double *dv, int32_t *seg) {
+    const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sl >= nslices) return;
+    const int64_t row = sl * 64 + lane;
+    const int64_t base = sptr[sl];
+    const int64_t L = (sptr[sl + 1] - base) >> 6;
+    const int64_t s0 = row < nrows ? rp[row] : 0;
+    const int64_t len = row < nrows ? rp[row + 1] - s0 : 0;
+    int nseg = 0;
+    int32_t last = 0;
+    for (int64_t k = 0; k < L; ++k) {
+        uint16_t d = 0;
+        double v = 0.0;
+        if (k < len) {
+            const int32_t c = ci[s0 + k];
+            v = val[s0 + k];
+            const int64_t gap = (int64_t)c - (int64_t)last;
+            if (k == 0 || gap > 65535 || gap <= 0) {
+                seg[row * D16_SEG + nseg++] = c;
+            } else {
+                d = (uint16_t)gap;
+            }
+            last = c;
+        }
+        dl[base + (k >> 3) * 512 + lane * 8 + (k & 7)] = d;
+        dv[base + (k >> 1) * 128 + lane * 2 + (k & 1)] = v;
+    }
+    if (nseg == 0) seg[row * D16_SEG + nseg++] = 0;
+    for (int j = nseg; j < D16_SEG; ++j) seg[row * D16_SEG + j] = seg[row * D16_SEG + nseg - 1];
+}
+
+typedef int32_t d16_i4 __attribute__((ext_vector_type(4)));
+typedef uint32_t d16_u4 __attribute__((ext_vector_type(4)));
+typedef double d16_d2 __attribute__((ext_vector_type(2)));
+
+template <int G2, int TAG, bool HALO>
+__global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *__restrict__ sptr,
+                                                  const uint16_t *__restrict__ dl, const double *__restrict__ dv,
+                                                  const int32_t *__restrict__ seg, const double *__restrict__ x,
+                                                  double *__restrict__ y, double alpha, double beta,
+                                                  const double *__restrict__ z, const double *__restrict__ ghost,
+                                                  int32_t nlocal) {
+    static_assert(D16_SEG == 4, "segment bases are one int4 per lane");
+    const int lane = threadIdx.x & 63;
+    const int64_t sl = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
+    if (sl >= nslices) return;
+    const int64_t base = sptr[sl];
+    const int64_t L = (sptr[sl + 1] - base) >> 6;  // multiple of 8
+    const int64_t row = sl * 64 + lane;
+    const d16_i4 sb = __builtin_nontemporal_load(reinterpret_cast<const d16_i4 *>(seg) + row);
+    const d16_u4 *dp = reinterpret_cast<const d16_u4 *>(dl + base) + lane;
+    const d16_d2 *vp = reinterpret_cast<const d16_d2 *>(dv + base) + lane;
+    int32_t col = 0;
+    int si = 0;
+    double acc = 0.0;
+    const int64_t ng = L >> 3;
+    for (int64_t g0 = 0; g0 < ng; g0 += G2) {
+        d16_u4 d[G2];
+        d16_d2 v[G2][4];
+#pragma unroll
+        for (int u = 0; u < G2; ++u) {
+            const int64_t g = g0 + u < ng ? g0 + u : ng - 1;  // wave-uniform clamp, values masked
+            d[u] = __builtin_nontemporal_load(dp + g * 64);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[u][q] = __builtin_nontemporal_load(vp + (g * 4 + q) * 64);
+        }
+#pragma unroll
+        for (int u = 0; u < G2; ++u) {
+            if (g0 + u >= ng) break;
+            const uint32_t w[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int32_t dd = (int32_t)((w[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
+                const int32_t b = si == 0 ? sb.x : si == 1 ? sb.y : si == 2 ? sb.z : sb.w;
+                col = dd == 0 ? b : col + dd;
+                si += dd == 0 ? 1 : 0;
+                const double a = (e & 1) ? v[u][e >> 1].y : v[u][e >> 1].x;
+                if (HALO) {
+                    const bool loc = col < nlocal;
+                    const double xv = loc ? x[(uint32_t)col] : ghost[(uint32_t)(col - nlocal)];
+                    acc += a * xv;
+                } else {
+                    acc += a * x[(uint32_t)col];
+                }
+            }
+        }
+    }
+    if (row < nrows) {
+        double r = alpha * acc;
+        if (beta != 0.0) r += beta * z[row];
+        y[row] = r;
+    }
+}
+
+void launch_d16_slice_len(int64_t nrows, const int64_t *rp, int64_t *slen, hipStream_t st) {
+    const int64_t ns = sell_nslices(nrows);
+    k_d16_slice_len<<<grid_for((ns + 1) * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, slen);
+}
+void launch_d16_count(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *maxseg, hipStream_t st) {
+    if (nrows > 0) k_d16_count<<<grid_for(nrows, TPB), TPB, 0, st>>>(nrows, rp, ci, maxseg);
+}
+void launch_d16_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const double *val, const int64_t *sptr,
+                     uint16_t *dl, double *dv, int32_t *seg, hipStream_t st) {
+    const int64_t ns = sell_nslices(nrows);
+    if (ns > 0) k_d16_fill<<<grid_for(ns * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, ci, val, sptr, dl, dv, seg);
+}
+void launch_d16_spmv(int64_t nrows, const int64_t *sptr, const uint16_t *dl, const double *dv, const int32_t *seg,
+                     const double *x, double *y, double alpha, double beta, const double *z, int tag,
+                     const double *ghost, int64_t nlocal, hipStream_t st) {
+    const int64_t ns = sell_nslices(nrows);
+    if (ns <= 0) return;
+    const unsigned g = grid_for(ns, TPB / 64);
+    const int32_t nl = (int32_t)nlocal;
+    if (ghost) {
+        if (tag) k_d16_spmv<2, 1, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        else k_d16_spmv<2, 0, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+    } else {
+        if (tag) k_d16_spmv<2, 1, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        else k_d16_spmv<2, 0, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+    }
+}
+
 // ================================================= level-aligned SELL-64 ====
 // Triangular factors for the sweeps: rows grouped by (block, level), every
 // group padded to whole 64-row slices, entry k of a slice's rows contiguous

@@ -116,16 +116,32 @@ void build_sell(DevCSR &M, Ctx &c) {
     if (M.sell || M.nrows == 0) return;
     auto S = std::make_unique<DevSELL>();
     S->nslices = sell_nslices(M.nrows);
+    if (c.sell_d16 && M.nnz > 0) {
+        DBuf<int32_t> mx(1);
+        HIPCHK(hipMemsetAsync(mx.p, 0, sizeof(int32_t), c.st));
+        launch_d16_count(M.nrows, M.rp.p, M.ci.p, mx.p, c.st);
+        int32_t h = 0;
+        HIPCHK(hipMemcpyAsync(&h, mx.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+        c.sync();
+        S->d16 = h <= D16_SEG;
+    }
     DBuf<int64_t> slen(S->nslices + 1);
-    launch_sell_slice_len(M.nrows, M.rp.p, slen.p, c.st);
+    if (S->d16) launch_d16_slice_len(M.nrows, M.rp.p, slen.p, c.st);
+    else launch_sell_slice_len(M.nrows, M.rp.p, slen.p, c.st);
     S->sptr.alloc(S->nslices + 1);
     c.ensure_scan(S->nslices);
     exclusive_scan_i64(slen.p, S->sptr.p, S->nslices, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
     HIPCHK(hipMemcpyAsync(&S->stored, S->sptr.p + S->nslices, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
     c.sync();
-    S->col.alloc(std::max<int64_t>(S->stored, 1));
-    S->val.alloc(std::max<int64_t>(S->stored, 1));
-    launch_sell_fill(M.nrows, M.rp.p, M.ci.p, M.val.p, S->sptr.p, S->col.p, S->val.p, c.st);
+    S->val.alloc(std::max<int64_t>(S->stored, 2));
+    if (S->d16) {
+        S->dl.alloc(std::max<int64_t>(S->stored, 8));
+        S->seg.alloc(S->nslices * 64 * D16_SEG);
+        launch_d16_fill(M.nrows, M.rp.p, M.ci.p, M.val.p, S->sptr.p, S->dl.p, S->val.p, S->seg.p, c.st);
+    } else {
+        S->col.alloc(std::max<int64_t>(S->stored, 1));
+        launch_sell_fill(M.nrows, M.rp.p, M.ci.p, M.val.p, S->sptr.p, S->col.p, S->val.p, c.st);
+    }
     HIPCHK(hipGetLastError());
     c.sync();
     M.sell = std::move(S);
@@ -141,6 +157,11 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
         ghost = H.ghost.p;
         nlocal = H.nlocal;
         if (!M.sell) throw Error("distributed matrix without SELL layout");
+    }
+    if (M.sell && M.sell->d16) {
+        launch_d16_spmv(M.nrows, M.sell->sptr.p, M.sell->dl.p, M.sell->val.p, M.sell->seg.p, x, y, alpha, beta, z,
+                        M.tag, ghost, nlocal, c.st);
+        return;
     }
     if (M.sell) {
         launch_sell_spmv(M.nrows, M.sell->sptr.p, M.sell->col.p, M.sell->val.p, x, y, alpha, beta, z, M.tag, ghost,

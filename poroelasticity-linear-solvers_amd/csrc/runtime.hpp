@@ -66,6 +66,7 @@ struct Ctx {
     DBuf<double> partial;   // reduction partials (NB_MAX * 136)
     DBuf<double> dscal;     // device scalars
     double *hscal = nullptr;  // pinned host mirror
+    bool sell_d16 = true;     // build SpMV layouts as SELL-64/D16 where every row fits
     DBuf<char> scan_tmp;
     size_t scan_tmp_bytes = 0;
     Ctx();
@@ -80,9 +81,15 @@ struct Ctx {
 // ------------------------------------------------------------------ matrix --
 struct DevSELL {
     int64_t nslices = 0, stored = 0;  // stored = padded entries
+    bool d16 = false;                 // SELL-64/D16: 16-bit column deltas (dl, seg) instead of col
     DBuf<int64_t> sptr;
     DBuf<int32_t> col;
     DBuf<double> val;
+    DBuf<uint16_t> dl;
+    DBuf<int32_t> seg;
+    int64_t bytes() const {  // bytes one product streams from the matrix
+        return d16 ? stored * 10 + nslices * 64 * 16 + (nslices + 1) * 8 : stored * 12 + (nslices + 1) * 8;
+    }
 };
 
 // Halo of a distributed matrix: columns >= nlocal are ghosts (entries owned by

@@ -143,6 +143,12 @@ class Handle:
         N.check(N.lib().pls_bench_spmv(self.ptr, d_x, d_y, int(reps), C.byref(s)))
         return s.value
 
+    def spmv_layout(self):
+        """(is SELL-64/D16, matrix bytes streamed per product of A)."""
+        d, b = C.c_int32(), C.c_int64()
+        N.check(N.lib().pls_spmv_layout(self.ptr, C.byref(d), C.byref(b)))
+        return bool(d.value), b.value
+
     # -------------------------------------------------------------- queries --
     def result(self):
         r = N.pls_result()
