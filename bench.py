@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--cpu-N", type=int, default=20)
     ap.add_argument("--cpu-maxit", type=int, default=100)
     ap.add_argument("--sell-d16", type=int, default=1, help="1: SELL-64/D16 SpMV layout (16-bit column deltas)")
+    ap.add_argument("--d16-unroll", type=int, default=0, help="D16 SpMV: 8-entry groups per lane in flight (tuning)")
     ap.add_argument("--replicas", action="store_true", help="G independent N=59 solves instead of one sharded solve")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="host: host-staged gloo communicator (ranks may share a GPU; rehearsal only)")
@@ -129,6 +130,8 @@ def main():
     opts = dict(db)
     opts.update(params_to_options(params))
     opts["pls.sell_d16"] = str(args.sell_d16)
+    if args.d16_unroll:
+        opts["pls.d16_unroll"] = str(args.d16_unroll)
     t0 = time.perf_counter()
     comm = None
     if sharded:
@@ -221,7 +224,7 @@ def main():
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": ("k_d16_spmv<2,1,false>" if d16 else "k_sell_spmv<8,1,false>") + " (y = A x, outer MatMult)",
+                         "kernel": ("k_d16_spmv<4,1,false>" if d16 else "k_sell_spmv<8,1,false>") + " (y = A x, outer MatMult)",
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_s": spmv_avg,
                          "isolated_spmv_gbs": alg_bytes / iso / 1e9,
                          "layout": "SELL-64/D16 (16-bit column deltas)" if d16 else "SELL-64 (int32 columns)",

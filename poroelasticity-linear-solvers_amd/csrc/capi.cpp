@@ -463,6 +463,7 @@ struct Handle {
         inner_pc = opt.str("pls.inner_pc_type", "hypre");
         timers.enabled = opt.flag("pls.timers", true);
         ctx.sell_d16 = opt.flag("pls.sell_d16", true);
+        g_d16_unroll = (int)opt.integer("pls.d16_unroll", 4);
     }
 };
 

@@ -1155,6 +1155,19 @@ void launch_d16_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const 
     const int64_t ns = sell_nslices(nrows);
     if (ns > 0) k_d16_fill<<<grid_for(ns * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, ci, val, sptr, dl, dv, seg);
 }
+template <int G2>
+static void d16_dispatch(unsigned g, hipStream_t st, int64_t nrows, int64_t ns, const int64_t *sptr, const uint16_t *dl,
+                         const double *dv, const int32_t *seg, const double *x, double *y, double alpha, double beta,
+                         const double *z, int tag, const double *ghost, int32_t nl) {
+    if (ghost) {
+        if (tag) k_d16_spmv<G2, 1, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        else k_d16_spmv<G2, 0, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+    } else {
+        if (tag) k_d16_spmv<G2, 1, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        else k_d16_spmv<G2, 0, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+    }
+}
+int g_d16_unroll = 4;
 void launch_d16_spmv(int64_t nrows, const int64_t *sptr, const uint16_t *dl, const double *dv, const int32_t *seg,
                      const double *x, double *y, double alpha, double beta, const double *z, int tag,
                      const double *ghost, int64_t nlocal, hipStream_t st) {
@@ -1162,12 +1175,13 @@ void launch_d16_spmv(int64_t nrows, const int64_t *sptr, const uint16_t *dl, con
     if (ns <= 0) return;
     const unsigned g = grid_for(ns, TPB / 64);
     const int32_t nl = (int32_t)nlocal;
-    if (ghost) {
-        if (tag) k_d16_spmv<2, 1, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-        else k_d16_spmv<2, 0, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-    } else {
-        if (tag) k_d16_spmv<2, 1, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-        else k_d16_spmv<2, 0, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+    switch (g_d16_unroll) {
+        case 1: d16_dispatch<1>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        case 3: d16_dispatch<3>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        case 4: d16_dispatch<4>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        case 6: d16_dispatch<6>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        case 8: d16_dispatch<8>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        default: d16_dispatch<2>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
     }
 }
 

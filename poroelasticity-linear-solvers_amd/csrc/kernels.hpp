@@ -122,6 +122,7 @@ void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, c
                       int64_t nlocal, hipStream_t st);
 // SELL-64 / D16 (16-bit column deltas, D16_SEG segment bases per row)
 constexpr int D16_SEG = 4;
+extern int g_d16_unroll;  // entries per lane in flight / 8 (tuning knob, option pls.d16_unroll)
 void launch_d16_slice_len(int64_t nrows, const int64_t *rp, int64_t *slen /* nslices+1 */, hipStream_t st);
 void launch_d16_count(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *maxseg, hipStream_t st);
 void launch_d16_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const double *val, const int64_t *sptr,
