@@ -196,6 +196,16 @@ def main():
     fmt_bytes = mat_bytes + 8.0 * n + 8.0 * n  # + x once + y once
     h.rhs_device(7, d_b.p)
 
+    # HBM traffic of the same kernel from the committed PMC passes (tools/pmc.sh)
+    traffic, traffic_src = None, None
+    kname = ("void pls::k_d16_spmv<4, 1, false>" if d16 else "void pls::k_sell_spmv<8, 1, false>")
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc_N59_summary.json")
+    if os.path.exists(pmc) and n_global == 10326954 and world == 1:
+        for k, v in json.load(open(pmc)).items():
+            if k.startswith(kname) and v.get("read_bytes"):
+                traffic = v["read_bytes"] + (v.get("write_bytes") or 0.0)
+                traffic_src = os.path.relpath(pmc, ROOT)
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -223,7 +233,7 @@ def main():
             "reasons": sorted(set(reasons)),
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": ("k_d16_spmv<4,1,false>" if d16 else "k_sell_spmv<8,1,false>") + " (y = A x, outer MatMult)",
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_s": spmv_avg,
                          "isolated_spmv_gbs": alg_bytes / iso / 1e9,
