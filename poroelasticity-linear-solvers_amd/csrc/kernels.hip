@@ -509,36 +509,62 @@ __global__ __launch_bounds__(TPB) void k_final(int nb, const double *partial, do
 }
 
 // mdot: blockIdx.x = chunk, blockIdx.y = group of 4 vectors
+// CGS dot block h_j = V_j . w, j in [0, k): blocks of MDOT_NJ columns per
+// grid row, 16-B loads (pairs of rows; chunks start on even rows, V columns
+// are 512-B aligned), one partial per (column, block) -> k_final in fixed order.
+typedef double cgs_d2 __attribute__((ext_vector_type(2)));
+static constexpr int MDOT_NJ = 8;
+__device__ __forceinline__ void chunk_even(int64_t n, int nb, int b, int64_t &s, int64_t &e) {
+    int64_t c = (n + nb - 1) / nb;
+    c = (c + 1) & ~(int64_t)1;
+    s = (int64_t)b * c;
+    e = s + c;
+    if (e > n) e = n;
+    if (s > n) s = n;
+}
 __global__ __launch_bounds__(TPB) void k_mdot(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
                                               const double *__restrict__ w, double *partial) {
     __shared__ double lds[TPB / 64];
     const int nb = gridDim.x;
     int64_t s, e;
-    chunk_of(n, nb, blockIdx.x, s, e);
-    const int j0 = blockIdx.y * 4;
-    const int nj = (k - j0) < 4 ? (k - j0) : 4;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    chunk_even(n, nb, blockIdx.x, s, e);
+    const int j0 = blockIdx.y * MDOT_NJ;
+    const int nj = (k - j0) < MDOT_NJ ? (k - j0) : MDOT_NJ;
+    double a[MDOT_NJ];
+#pragma unroll
+    for (int u = 0; u < MDOT_NJ; ++u) a[u] = 0.0;
     const double *v0 = V + (int64_t)j0 * ldv;
-    for (int64_t i = s + threadIdx.x; i < e; i += TPB) {
-        const double wi = w[i];
-        a0 += v0[i] * wi;
-        if (nj > 1) a1 += v0[ldv + i] * wi;
-        if (nj > 2) a2 += v0[2 * ldv + i] * wi;
-        if (nj > 3) a3 += v0[3 * ldv + i] * wi;
+    for (int64_t i = s + 2 * threadIdx.x; i + 1 < e; i += 2 * TPB) {
+        const cgs_d2 wi = *reinterpret_cast<const cgs_d2 *>(w + i);
+#pragma unroll
+        for (int u = 0; u < MDOT_NJ; ++u) {
+            if (u < nj) {
+                const cgs_d2 v = *reinterpret_cast<const cgs_d2 *>(v0 + (int64_t)u * ldv + i);
+                a[u] += v.x * wi.x;
+                a[u] += v.y * wi.y;
+            }
+        }
     }
-    double r;
-    r = block_sum(a0, lds);
-    if (threadIdx.x == 0) partial[(int64_t)(j0 + 0) * nb + blockIdx.x] = r;
-    if (nj > 1) { r = block_sum(a1, lds); if (threadIdx.x == 0) partial[(int64_t)(j0 + 1) * nb + blockIdx.x] = r; }
-    if (nj > 2) { r = block_sum(a2, lds); if (threadIdx.x == 0) partial[(int64_t)(j0 + 2) * nb + blockIdx.x] = r; }
-    if (nj > 3) { r = block_sum(a3, lds); if (threadIdx.x == 0) partial[(int64_t)(j0 + 3) * nb + blockIdx.x] = r; }
+    if (((e - s) & 1) && threadIdx.x == 0) {
+        const int64_t i = e - 1;
+#pragma unroll
+        for (int u = 0; u < MDOT_NJ; ++u)
+            if (u < nj) a[u] += v0[(int64_t)u * ldv + i] * w[i];
+    }
+#pragma unroll
+    for (int u = 0; u < MDOT_NJ; ++u) {
+        if (u < nj) {
+            const double r = block_sum(a[u], lds);
+            if (threadIdx.x == 0) partial[(int64_t)(j0 + u) * nb + blockIdx.x] = r;
+        }
+    }
 }
 
 void launch_mdot(int64_t n, int k, const double *const *, const double *V, int64_t ldv, const double *w,
                  double *partial, double *out, hipStream_t st) {
     if (k <= 0) return;
     const int nb = reduce_blocks(n);
-    dim3 grid(nb, (k + 3) / 4);
+    dim3 grid(nb, (k + MDOT_NJ - 1) / MDOT_NJ);
     k_mdot<<<grid, TPB, 0, st>>>(n, k, V, ldv, w, partial);
     k_final<<<k, TPB, 0, st>>>(nb, partial, out, 0);
 }
@@ -565,7 +591,9 @@ void launch_norm2(int64_t n, const double *x, double *partial, double *out, hipS
     k_final<<<1, TPB, 0, st>>>(nb, partial, out, 1);
 }
 
-// w -= sum_j h[j] V[:, j]; partial ||w||^2
+// w -= sum_j h[j] V[:, j] (j ascending, as VecMAXPY); partial ||w||^2.
+// Pairs of rows per thread (16-B loads), four basis columns loaded ahead of
+// their FMAs so every lane keeps 4-5 loads in flight.
 __global__ __launch_bounds__(TPB) void k_maxpy_norm(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
                                                     const double *__restrict__ h, double *__restrict__ w,
                                                     double *partial) {
@@ -574,9 +602,34 @@ __global__ __launch_bounds__(TPB) void k_maxpy_norm(int64_t n, int k, const doub
     for (int j = threadIdx.x; j < k && j < 512; j += TPB) hs[j] = h[j];
     __syncthreads();
     int64_t s, e;
-    chunk_of(n, gridDim.x, blockIdx.x, s, e);
+    chunk_even(n, gridDim.x, blockIdx.x, s, e);
     double a = 0.0;
-    for (int64_t i = s + threadIdx.x; i < e; i += TPB) {
+    for (int64_t i = s + 2 * threadIdx.x; i + 1 < e; i += 2 * TPB) {
+        cgs_d2 t = *reinterpret_cast<const cgs_d2 *>(w + i);
+        int j = 0;
+        for (; j + 4 <= k; j += 4) {
+            cgs_d2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const cgs_d2 *>(V + (int64_t)(j + u) * ldv + i);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double hj = (j + u) < 512 ? hs[j + u] : h[j + u];
+                t.x -= hj * v[u].x;
+                t.y -= hj * v[u].y;
+            }
+        }
+        for (; j < k; ++j) {
+            const cgs_d2 v = *reinterpret_cast<const cgs_d2 *>(V + (int64_t)j * ldv + i);
+            const double hj = j < 512 ? hs[j] : h[j];
+            t.x -= hj * v.x;
+            t.y -= hj * v.y;
+        }
+        *reinterpret_cast<cgs_d2 *>(w + i) = t;
+        a += t.x * t.x;
+        a += t.y * t.y;
+    }
+    if (((e - s) & 1) && threadIdx.x == 0) {
+        const int64_t i = e - 1;
         double t = w[i];
         for (int j = 0; j < k; ++j) t -= (j < 512 ? hs[j] : h[j]) * V[(int64_t)j * ldv + i];
         w[i] = t;

@@ -622,7 +622,8 @@ void KSP::resolve_side_norm(const std::string &side, const std::string &nt) {
 void KSP::ensure_work(Ctx &) {
     if (type == "gmres") {
         if (allocated_k != restart) {
-            V.alloc((size_t)(restart + 1) * n);
+            ldv = (n + 63) & ~(int64_t)63;  // 512-B aligned columns (16-B loads)
+            V.alloc((size_t)(restart + 1) * ldv);
             t1.alloc(n);
             t2.alloc(n);
             dh.alloc(restart + 4);
@@ -700,8 +701,8 @@ void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
         grs[0] = res;
         int64_t loc_it = 0;
         while (!reason && loc_it < mk && its < maxit) {
-            double *vk = V.p + loc_it * n;
-            double *vn = V.p + (loc_it + 1) * n;
+            double *vk = V.p + loc_it * ldv;
+            double *vn = V.p + (loc_it + 1) * ldv;
             if (right) {
                 pc->apply(vk, t1p, c);
                 A->apply(t1p, vn, c);
@@ -710,9 +711,9 @@ void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
                 pc->apply(t1p, vn, c);
             }
             const int k = (int)(loc_it + 1);
-            launch_mdot(n, k, nullptr, V.p, n, vn, c.partial.p, dh.p, c.st);
+            launch_mdot(n, k, nullptr, V.p, ldv, vn, c.partial.p, dh.p, c.st);
             c.comm->global_sum_dev(dh.p, k, c.st);
-            launch_maxpy_norm(n, k, V.p, n, dh.p, -1.0, vn, c.partial.p, dh.p + k, c.st);
+            launch_maxpy_norm(n, k, V.p, ldv, dh.p, -1.0, vn, c.partial.p, dh.p + k, c.st);
             c.comm->global_sum_dev(dh.p + k, 1, c.st);
             HIPCHK(hipMemcpyAsync(c.hscal, dh.p, sizeof(double) * (k + 1), hipMemcpyDeviceToHost, c.st));
             c.sync();
@@ -769,7 +770,7 @@ void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
                     nrs[k] = t0 / H(k, k);
                 }
                 HIPCHK(hipMemcpyAsync(dh.p, nrs.data(), sizeof(double) * (it + 1), hipMemcpyHostToDevice, c.st));
-                launch_lincomb(n, (int)(it + 1), V.p, n, dh.p, t2p, c.st);
+                launch_lincomb(n, (int)(it + 1), V.p, ldv, dh.p, t2p, c.st);
                 if (right) {
                     pc->apply(t2p, t1p, c);
                     launch_axpby(n, 1.0, t1p, 1.0, x, c.st);

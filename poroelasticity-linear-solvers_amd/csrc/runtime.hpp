@@ -245,6 +245,7 @@ struct KSP {
     bool monitor = false;
     // work
     DBuf<double> V, w, t1, t2, t3, t4;
+    int64_t ldv = 0;  // column stride of the Krylov basis V
     DBuf<double> dh;  // device Hessenberg column / coefficients
     int64_t allocated_k = -1;
     void set_type_defaults();

@@ -48,23 +48,34 @@ def _oracle(spec, params, db):
     return OracleSolver(A, P, Pd, is_s, is_f, is_p, params, db, S.bcs_sub_pressure(spec))
 
 
-def _self_sensitivity(spec, params, db, b, ho, eps=1e-15):
-    """Oracle vs the oracle with its s-block PC output perturbed by eps (relative)."""
-    o2 = _oracle(spec, params, db)
-    rng = np.random.default_rng(0)
-    orig = o2.block_pc.ksp_s.pc.apply
-    o2.block_pc.ksp_s.pc.apply = lambda x: (lambda y: y * (1 + eps * rng.standard_normal(y.size)))(orig(x))
-    o2.solve(b)
-    h2 = np.asarray(o2.history)
-    n = min(len(h2), len(ho))
-    return float(np.max(np.abs(h2[:n] - ho[:n]) / np.abs(ho[:n])))
+def _self_sensitivity(spec, params, db, b, ho, eps=1e-15, seeds=4):
+    """Max over a few seeds of the oracle's own history deviation when every
+    inner PC output is perturbed by eps (relative) -- the rounding noise floor
+    of configurations that amplify it (the deviation itself varies ~100x
+    between seeds, hence the max)."""
+    worst = 0.0
+    for seed in range(seeds):
+        o2 = _oracle(spec, params, db)
+        rng = np.random.default_rng(seed)
+        for name in ("ksp_s", "ksp_fp", "ksp_f", "ksp_p"):
+            ksp = getattr(o2.block_pc, name, None)
+            if ksp is None:
+                continue
+            orig = ksp.pc.apply
+            ksp.pc.apply = (lambda f: (lambda x: (lambda y: y * (1 + eps * rng.standard_normal(y.size)))(f(x))))(orig)
+        o2.solve(b)
+        h2 = np.asarray(o2.history)
+        n = min(len(h2), len(ho))
+        worst = max(worst, float(np.max(np.abs(h2[:n] - ho[:n]) / np.abs(ho[:n]))))
+    return worst
 
 
 def _compare_solve(spec, upd=None, db=None, sensitivity=False):
     """sensitivity=True: for configurations whose histories amplify rounding (a
     nonlinear PC such as inner Anderson mixing inside non-flexible GMRES), the
-    history bound is 10x the oracle's own deviation under a 1e-15 relative
-    perturbation of one inner PC output; iteration count and reason stay exact."""
+    history bound is 10x the oracle's own deviation under 1e-15 relative
+    perturbations of the inner PC outputs (max over 4 seeds); iteration count
+    and reason stay exact."""
     params = dict(BASE)
     params.update(upd or {})
     db = dict(ILU_DB if db is None else db)
@@ -209,8 +220,8 @@ def test_aar_order5(gpu):
 
 
 def test_inner_anderson_order1(gpu):
-    # measured on CPU: a 1e-16 relative perturbation of one ILU output moves the
-    # oracle's own history by 1.3e-8 in this configuration
+    # measured on CPU: 1e-15 relative perturbations of the inner PC outputs move
+    # the oracle's own history by 8e-10 .. 3.4e-7 depending on the seed
     _compare_solve(S.SynthSpec(2, 8), {"inner accel order": 1}, sensitivity=True)
 
 
