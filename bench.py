@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--cpu-maxit", type=int, default=100)
     ap.add_argument("--sell-d16", type=int, default=1, help="1: SELL-64/D16 SpMV layout (16-bit column deltas)")
     ap.add_argument("--d16-unroll", type=int, default=0, help="D16 SpMV: 8-entry groups per lane in flight (tuning)")
+    ap.add_argument("--opt", action="append", default=[], help="extra library option key=value (diagnostics)")
     ap.add_argument("--replicas", action="store_true", help="G independent N=59 solves instead of one sharded solve")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="host: host-staged gloo communicator (ranks may share a GPU; rehearsal only)")
@@ -130,6 +131,9 @@ def main():
     opts = dict(db)
     opts.update(params_to_options(params))
     opts["pls.sell_d16"] = str(args.sell_d16)
+    for kv in args.opt:
+        k, _, v = kv.partition("=")
+        opts[k] = v
     if args.d16_unroll:
         opts["pls.d16_unroll"] = str(args.d16_unroll)
     t0 = time.perf_counter()

@@ -1363,149 +1363,220 @@ void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t
 // level against LDS (gathers and updates never leave the CU), and writes the
 // block of y once.  Blocks are launched heaviest-last-index first (the
 // pressure blocks at the end of the fp ordering carry the most levels).
-template <int U>
-__device__ __forceinline__ void tri_slice_lds(int64_t sl, int lane, int64_t b0, const int64_t *__restrict__ sptr,
-                                              const int32_t *__restrict__ slot_row,
-                                              const int32_t *__restrict__ slot_len, const int32_t *__restrict__ col,
-                                              const double *__restrict__ val, const double *__restrict__ sdinv,
-                                              double *ys) {
-    const int64_t slot = sl * 64 + lane;
-    const int32_t i = slot_row[slot];
-    const int32_t len = slot_len[slot];
-    const int64_t base = sptr[sl];
-    const int64_t L = (sptr[sl + 1] - base) >> 6;
-    const int32_t *cp = col + base + lane;
-    const double *vp = val + base + lane;
-    double acc = 0.0;
-    for (int64_t k0 = 0; k0 < L; k0 += U) {
-        int32_t c[U];
-        double v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t kk = (k0 + u < L) ? k0 + u : L - 1;
-            c[u] = __builtin_nontemporal_load(cp + kk * 64);
-            v[u] = __builtin_nontemporal_load(vp + kk * 64);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t lc = (k0 + u < len) ? c[u] - (int32_t)b0 : 0;
-            const double t = v[u] * ys[lc];
-            acc += (k0 + u < len) ? t : 0.0;
-        }
-    }
+// ------------------------------------------------ LDS sweep stream layout --
+// The block-Jacobi LDS kernel reads each level's slices as streams.  A block
+// whose rows are long gives each row LPR = 2 or 4 lanes (entries dealt round
+// robin, partial sums combined with two lane shuffles), so every lane's share
+// fits the P entries the pipeline keeps in registers; short-row blocks keep
+// LPR = 1.  Slice = 64 / LPR rows of one level.  Entry 0 of every lane is a
+// header -- col = (row - b0) | (entries of this lane << 16) (row 0xFFFF:
+// padding), val = 1/U_ii (upper factor) -- entries 1..L the lane's factor
+// entries with block-local columns.  The only metadata a level needs is where
+// its slice starts, known 64 levels ahead (see sweep2), so loads are issued D
+// levels before use without a dependent metadata hop.
+__global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n,
+                                                  const int32_t *s_lpr, const int32_t *order, const int64_t *rp,
+                                                  const int32_t *ci, const double *lu, const int64_t *diag,
+                                                  const double *dinv, int upper, int64_t n, int64_t nb,
+                                                  const int64_t *sptr2, int32_t *ocol, double *oval) {
+    const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sl >= nslices) return;
+    const int lpr = s_lpr[sl];
+    const int r = lane / lpr, sub = lane % lpr;
+    const int64_t i = r < s_n[sl] ? order[s_start[sl] + r] : -1;
+    const int64_t base = sptr2[sl], L = (sptr2[sl + 1] - base) >> 6;
+    int64_t b0 = 0, src = 0, len = 0;
     if (i >= 0) {
-        const int32_t li = i - (int32_t)b0;
-        if (sdinv) ys[li] = (ys[li] - acc) * sdinv[slot];
-        else ys[li] = ys[li] - acc;
+        const int64_t q = n / nb, rr = n % nb;
+        const int64_t blk = i < rr * (q + 1) ? i / (q + 1) : rr + (i - rr * (q + 1)) / q;
+        b0 = blk * q + (blk < rr ? blk : rr);
+        src = upper ? diag[i] + 1 : rp[i];
+        len = upper ? rp[i + 1] - diag[i] - 1 : diag[i] - rp[i];
+    }
+    const int64_t mine = len > sub ? (len - sub + lpr - 1) / lpr : 0;
+    ocol[base + lane] = (i >= 0 ? (int32_t)(i - b0) : 0xFFFF) | (int32_t)(mine << 16);
+    oval[base + lane] = (upper && i >= 0) ? dinv[i] : 0.0;
+    for (int64_t k = 1; k < L; ++k) {
+        const int64_t j = (k - 1) * lpr + sub, pos = base + k * 64 + lane;
+        ocol[pos] = j < len ? (int32_t)(ci[src + j] - b0) : 0;
+        oval[pos] = j < len ? lu[src + j] : 0.0;
     }
 }
+void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,
+                     const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu, const int64_t *diag,
+                     const double *dinv, int upper, int64_t n, int64_t nb, const int64_t *sptr2, int32_t *ocol,
+                     double *oval, hipStream_t st) {
+    if (nslices > 0)
+        k_lds_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, s_start, s_n, s_lpr, order, rp, ci, lu, diag,
+                                                                dinv, upper, n, nb, sptr2, ocol, oval);
+}
 
-// One sweep over a block's groups (levels) with a software pipeline: the
-// slice metadata of level g+2 and the first P entries of level g+1 are loaded
-// while level g computes against LDS, so the per-level critical path is the
-// LDS work plus the barrier instead of two dependent global round trips.
-// Plain global loads stay in flight across __syncthreads() (no LDS-DMA here).
+// One sweep over a block's levels.  Pipeline: the loads of level g+2 are
+// issued while level g computes; slots live in a ring of 3 register sets
+// indexed by compile-time constants (a register copy with a load in flight
+// would make the compiler drain vmcnt to 0 every level).  Slice starts for 64
+// levels come from vector registers (lane l: level gbase + l) filled by one
+// gather per 62 levels and read with v_readlane -- no scalar loads in the
+// loop, whose lgkmcnt waits would be paid at every LDS access.
 template <int P>
-struct SliceMeta {
-    int32_t i, len;
-    int64_t base, L, sl;
+struct Sw2Slot {
+    int32_t c[P + 1];
+    double v[P + 1];
+    int64_t base, L;  // L: entries incl. header; base < 0: this wave has no slice
+};
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+    const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)(uint64_t)v, l);
+    const int32_t hi = __builtin_amdgcn_readlane((int32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+struct Sw2Ctx {
+    const int64_t *gslice, *sptr;
+    const int32_t *col;
+    const double *val;
+    double *ys;
+    int64_t g1, gbase;
+    int64_t gv, sb, se;  // lane l: gslice[gbase+l], sptr[gslice+wave], sptr[gslice+wave+1] (-1: none)
+    int lane, wave, nw;
+    bool upper;
+    __device__ __forceinline__ void refill(int64_t g) {
+        gbase = g;
+        const int64_t k = g + lane;
+        const int64_t kc = k < g1 ? k : g1;
+        gv = gslice[kc];
+        const int64_t gn = gslice[kc + 1 <= g1 ? kc + 1 : g1];
+        const int64_t sl = gv + wave;
+        const bool ok = k < g1 && sl < gn;
+        sb = ok ? sptr[sl] : -1;
+        se = ok ? sptr[sl + 1] : -1;
+        // consume the loads here: otherwise every level's v_readlane of these
+        // registers inherits the refill path's "load pending" state and the
+        // compiler drains vmcnt to 0 at each level, exposing all prefetches
+        asm volatile("" : "+v"(gv), "+v"(sb), "+v"(se));
+    }
 };
 
 template <int P>
-__device__ __forceinline__ SliceMeta<P> load_meta(int64_t g, int64_t g1, int wave, const int64_t *gslice,
-                                                  const int64_t *sptr, const int32_t *slot_row,
-                                                  const int32_t *slot_len, int lane) {
-    SliceMeta<P> m;
-    m.sl = -1; m.i = -1; m.len = 0; m.base = 0; m.L = 0;
-    if (g < g1) {
-        const int64_t sl = gslice[g] + wave;
-        if (sl < gslice[g + 1]) {
-            m.sl = sl;
-            m.i = slot_row[sl * 64 + lane];
-            m.len = slot_len[sl * 64 + lane];
-            m.base = sptr[sl];
-            m.L = (sptr[sl + 1] - m.base) >> 6;
-        }
-    }
-    return m;
-}
-
-template <int P>
-__device__ __forceinline__ void load_data(const SliceMeta<P> &m, int lane, const int32_t *col, const double *val,
-                                          int32_t (&c)[P], double (&v)[P]) {
+__device__ __forceinline__ void sw2_issue(Sw2Ctx &x, int64_t g, Sw2Slot<P> &s) {
+    const int l = (int)(g - x.gbase);
+    const int64_t base = g < x.g1 ? readlane64(x.sb, l) : -1;
+    const int64_t L = base >= 0 ? (readlane64(x.se, l) - base) >> 6 : 0;
+    s.base = base;
+    s.L = L;
 #pragma unroll
-    for (int u = 0; u < P; ++u) {
-        const int64_t kk = (m.sl >= 0 && u < m.L) ? u : 0;
-        const int64_t pos = (m.sl >= 0) ? m.base + kk * 64 + lane : 0;
-        c[u] = __builtin_nontemporal_load(col + pos);
-        v[u] = __builtin_nontemporal_load(val + pos);
+    for (int u = 0; u <= P; ++u) {
+        const int64_t pos = base >= 0 ? base + (u < L ? u : 0) * 64 + x.lane : 0;
+        s.c[u] = __builtin_nontemporal_load(x.col + pos);
+        s.v[u] = __builtin_nontemporal_load(x.val + pos);
     }
 }
 
-template <int P>
-__device__ __forceinline__ void sweep_lds(int64_t g0, int64_t g1, int64_t b0, int lane, int wave, int nw,
-                                          const int64_t *__restrict__ gslice, const int64_t *__restrict__ sptr,
-                                          const int32_t *__restrict__ slot_row, const int32_t *__restrict__ slot_len,
-                                          const int32_t *__restrict__ col, const double *__restrict__ val,
-                                          const double *__restrict__ sdinv, double *ys) {
-    SliceMeta<P> m0 = load_meta<P>(g0, g1, wave, gslice, sptr, slot_row, slot_len, lane);
-    SliceMeta<P> m1 = load_meta<P>(g0 + 1, g1, wave, gslice, sptr, slot_row, slot_len, lane);
-    int32_t c0[P], c1[P];
-    double v0[P], v1[P];
-    load_data<P>(m0, lane, col, val, c0, v0);
-    for (int64_t g = g0; g < g1; ++g) {
-        // prefetch: data of g+1 (meta known), meta of g+2
-        load_data<P>(m1, lane, col, val, c1, v1);
-        const SliceMeta<P> m2 = load_meta<P>(g + 2, g1, wave, gslice, sptr, slot_row, slot_len, lane);
-        double dv = 1.0;
-        if (sdinv && m0.sl >= 0) dv = sdinv[m0.sl * 64 + lane];
-        // level g: first slice of this wave from registers, the rest inline
-        if (m0.sl >= 0) {
-            double acc = 0.0;
+template <int LPR>
+__device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv, double acc) {
+    if (LPR >= 2) acc += __shfl_xor(acc, 1);
+    if (LPR >= 4) acc += __shfl_xor(acc, 2);
+    const int32_t li = h & 0xFFFF;
+    if ((x.lane % LPR) == 0 && li != 0xFFFF) x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
+}
+
+template <int LPR>
+__device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
+    const int64_t base = x.sptr[sl], L = (x.sptr[sl + 1] - base) >> 6;
+    const int32_t h = x.col[base + x.lane];
+    const double dv = x.val[base + x.lane];
+    const int32_t len = (int32_t)((uint32_t)h >> 16);
+    double acc = 0.0;
+    for (int64_t k = 1; k < L; ++k) {
+        const int64_t pos = base + k * 64 + x.lane;
+        const int32_t cc = x.col[pos];
+        const double vv = x.val[pos];
+        if (k <= len) acc += vv * x.ys[cc];
+    }
+    sw2_finish<LPR>(x, h, dv, acc);
+}
+
+template <int P, int LPR>
+__device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P> &cur, Sw2Slot<P> &ahead) {
+    if (g + 2 >= x.gbase + 64) x.refill(g);
+    sw2_issue<P>(x, g + 2, ahead);
+    if (cur.base >= 0) {
+        const int32_t h = cur.c[0];
+        const int32_t len = (int32_t)((uint32_t)h >> 16);
+        double acc = 0.0;
 #pragma unroll
-            for (int u = 0; u < P; ++u) {
-                const int32_t lc = (u < m0.len) ? c0[u] - (int32_t)b0 : 0;
-                const double t = v0[u] * ys[lc];
-                acc += (u < m0.len) ? t : 0.0;
-            }
-            for (int64_t k = P; k < m0.L; ++k) {
-                const int64_t pos = m0.base + k * 64 + lane;
-                const int32_t cc = col[pos];
-                const double vv = val[pos];
-                if (k < m0.len) acc += vv * ys[cc - (int32_t)b0];
-            }
-            if (m0.i >= 0) {
-                const int32_t li = m0.i - (int32_t)b0;
-                ys[li] = sdinv ? (ys[li] - acc) * dv : ys[li] - acc;
-            }
-            const int64_t s1 = gslice[g + 1];
-            for (int64_t sl = m0.sl + nw; sl < s1; sl += nw)
-                tri_slice_lds<8>(sl, lane, b0, sptr, slot_row, slot_len, col, val, sdinv, ys);
+        for (int u = 1; u <= P; ++u) {
+            const double t = cur.v[u] * x.ys[u <= len ? cur.c[u] : 0];
+            acc += (u <= len) ? t : 0.0;
         }
-        __syncthreads();
-        m0 = m1;
-        m1 = m2;
+        for (int64_t k0 = P + 1; k0 < cur.L; k0 += 8) {  // lanes with more than P entries: chunks of 8
+            int32_t cc[8];
+            double vv[8];
 #pragma unroll
-        for (int u = 0; u < P; ++u) { c0[u] = c1[u]; v0[u] = v1[u]; }
+            for (int u = 0; u < 8; ++u) {
+                const int64_t k = k0 + u < cur.L ? k0 + u : cur.L - 1;
+                cc[u] = __builtin_nontemporal_load(x.col + cur.base + k * 64 + x.lane);
+                vv[u] = __builtin_nontemporal_load(x.val + cur.base + k * 64 + x.lane);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const double t = vv[u] * x.ys[k0 + u <= len ? cc[u] : 0];
+                acc += (k0 + u <= len) ? t : 0.0;
+            }
+        }
+        sw2_finish<LPR>(x, h, cur.v[0], acc);
+        // levels with more slices than waves: the rest inline
+        const int l = (int)(g - x.gbase);
+        const int64_t s0 = readlane64(x.gv, l), s1 = readlane64(x.gv, l + 1);
+        for (int64_t sl = s0 + x.wave + x.nw; sl < s1; sl += x.nw) sw2_slice_inline<LPR>(x, sl);
+    }
+    __syncthreads();
+}
+
+template <int P, int LPR>
+__device__ __forceinline__ void sweep2(Sw2Ctx &x, int64_t g0) {
+    x.refill(g0);
+    Sw2Slot<P> s0, s1, s2;
+    sw2_issue<P>(x, g0, s0);
+    sw2_issue<P>(x, g0 + 1, s1);
+    for (int64_t g = g0;;) {
+        sw2_level<P, LPR>(x, g, s0, s2);
+        if (++g >= x.g1) break;
+        sw2_level<P, LPR>(x, g, s1, s0);
+        if (++g >= x.g1) break;
+        sw2_level<P, LPR>(x, g, s2, s1);
+        if (++g >= x.g1) break;
     }
 }
+
+template <int P>
+__device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int lane, int wave, int nw, bool upper,
+                                            const int64_t *__restrict__ gslice, const int64_t *__restrict__ sptr,
+                                            const int32_t *__restrict__ col, const double *__restrict__ val,
+                                            double *ys) {
+    if (g0 >= g1) return;
+    Sw2Ctx x{gslice, sptr, col, val, ys, g1, 0, 0, 0, 0, lane, wave, nw, upper};
+    if (lpr == 4) sweep2<P, 4>(x, g0);
+    else if (lpr == 2) sweep2<P, 2>(x, g0);
+    else sweep2<P, 1>(x, g0);
+}
+
+static constexpr int SW_P = 7;  // factor entries per lane kept in registers per pipeline slot
 
 __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *__restrict__ Lgoff,
                                                          const int64_t *__restrict__ Lgslice,
                                                          const int64_t *__restrict__ Lsptr,
-                                                         const int32_t *__restrict__ Lrow,
-                                                         const int32_t *__restrict__ Llen,
                                                          const int32_t *__restrict__ Lcol,
                                                          const double *__restrict__ Lval,
+                                                         const int32_t *__restrict__ Llpr,
                                                          const int64_t *__restrict__ Ugoff,
                                                          const int64_t *__restrict__ Ugslice,
                                                          const int64_t *__restrict__ Usptr,
-                                                         const int32_t *__restrict__ Urow,
-                                                         const int32_t *__restrict__ Ulen,
                                                          const int32_t *__restrict__ Ucol,
                                                          const double *__restrict__ Uval,
-                                                         const double *__restrict__ Udinv, const double *__restrict__ x,
-                                                         double *__restrict__ y) {
+                                                         const int32_t *__restrict__ Ulpr, const double *__restrict__ x,
+                                                         double *__restrict__ y, int64_t *__restrict__ prof) {
     extern __shared__ __attribute__((aligned(16))) double ys[];
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
     const int64_t q = n / nblocks, r = n % nblocks;
@@ -1514,31 +1585,44 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int nw = blockDim.x >> 6;
+    int64_t t0 = 0, t1 = 0;
+    if (prof) t0 = wall_clock64();
     for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
     __syncthreads();
-    sweep_lds<8>(Lgoff[blk], Lgoff[blk + 1], b0, lane, wave, nw, Lgslice, Lsptr, Lrow, Llen, Lcol, Lval, nullptr, ys);
-    sweep_lds<8>(Ugoff[blk], Ugoff[blk + 1], b0, lane, wave, nw, Ugslice, Usptr, Urow, Ulen, Ucol, Uval, Udinv, ys);
+    sweep_block<SW_P>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol, Lval, ys);
+    if (prof) t1 = wall_clock64();
+    sweep_block<SW_P>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol, Uval, ys);
     for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
+    if (prof && threadIdx.x == 0) {  // diagnostics (option pls.sweep_profile): 100 MHz wall clock
+        int64_t *p = prof + blk * 8;
+        p[0] = t0;
+        p[1] = t1;
+        p[2] = wall_clock64();
+        p[3] = Lgoff[blk + 1] - Lgoff[blk];
+        p[4] = Ugoff[blk + 1] - Ugoff[blk];
+        p[5] = len;
+        p[6] = Lgslice[Lgoff[blk + 1]] - Lgslice[Lgoff[blk]];
+        p[7] = Llpr[blk] * 10 + Ulpr[blk];
+    }
 }
 
 int ilu_lds_max_rows() { return 163840 / 8; }
+int ilu_lds_lane_entries() { return SW_P; }
 
 void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,
-                           const int64_t *Lsptr, const int32_t *Lrow, const int32_t *Llen, const int32_t *Lcol,
-                           const double *Lval, const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr,
-                           const int32_t *Urow, const int32_t *Ulen, const int32_t *Ucol, const double *Uval,
-                           const double *Udinv, const double *x, double *y, hipStream_t st) {
-    const int64_t maxlen = n / nblocks + 1;
-    const size_t bytes = (size_t)maxlen * 8;
-    static size_t configured = 0;
-    if (bytes > configured) {
+                           const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
+                           const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
+                           const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
+                           int64_t *prof) {
+    static bool configured = false;
+    if (!configured) {
         (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)163840);
-        configured = 163840;
+        configured = true;
     }
-    k_ilu_blocks_lds<<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lrow, Llen, Lcol, Lval,
-                                                              Ugoff, Ugslice, Usptr, Urow, Ulen, Ucol, Uval, Udinv, x,
-                                                              y);
+    const size_t bytes = (size_t)(n / nblocks + 1) * 8;
+    k_ilu_blocks_lds<<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr, Ugoff,
+                                                              Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof);
 }
 
 // =========================================================== distribution ====

@@ -146,10 +146,16 @@ void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t
 // in one launch).  Valid when every block has <= ilu_lds_max_rows() rows.
 int ilu_lds_max_rows();
 void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,
-                           const int64_t *Lsptr, const int32_t *Lrow, const int32_t *Llen, const int32_t *Lcol,
-                           const double *Lval, const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr,
-                           const int32_t *Urow, const int32_t *Ulen, const int32_t *Ucol, const double *Uval,
-                           const double *Udinv, const double *x, double *y, hipStream_t st);
+                           const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
+                           const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
+                           const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
+                           int64_t *prof = nullptr);
+int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in registers
+// LDS-kernel stream layout (header entry per lane, lanes-per-row slices, block-local columns)
+void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,
+                     const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu, const int64_t *diag,
+                     const double *dinv, int upper, int64_t n, int64_t nb, const int64_t *sptr2, int32_t *ocol,
+                     double *oval, hipStream_t st);
 
 // distribution helpers
 void launch_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint8_t *flag, hipStream_t st);

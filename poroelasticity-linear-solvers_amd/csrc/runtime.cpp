@@ -10,6 +10,8 @@
 // as the CPU oracle evaluates them.
 #include "runtime.hpp"
 
+#include <climits>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -429,6 +431,62 @@ static void build_tri_sell(const PCILU &P, const std::vector<int64_t> &rp, const
     c.sync();
 }
 
+// LDS-kernel stream layout (kernels.hip, "LDS sweep stream layout"): per block
+// the lanes per row (1, 2 or 4) that fit every lane's share of the block's
+// longest row into the kernel's register window; slices of 64 / LPR rows of
+// one level; one header entry per lane.
+static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, const std::vector<int64_t> &rp,
+                          const std::vector<int64_t> &dg, const std::vector<int32_t> &order,
+                          const std::vector<int64_t> &grp, const std::vector<int64_t> &goff, bool upper, LdsTri &D,
+                          Ctx &c) {
+    const int64_t ng = (int64_t)grp.size() - 1, nblk = (int64_t)goff.size() - 1;
+    const int W = ilu_lds_lane_entries();
+    auto rlen = [&](int64_t i) { return upper ? rp[i + 1] - dg[i] - 1 : dg[i] - rp[i]; };
+    std::vector<int32_t> lpr(nblk, 1), s_start, s_n, s_lpr;
+    std::vector<int64_t> gsl(ng + 1, 0), sptr(1, 0);
+    for (int64_t b = 0; b < nblk; ++b) {
+        int64_t mx = 0;
+        for (int64_t r = grp[goff[b]]; r < grp[goff[b + 1]]; ++r) mx = std::max(mx, rlen(order[r]));
+        int l = 1;
+        while (l < 4 && (mx + l - 1) / l > W) l *= 2;
+        lpr[b] = l;
+        const int64_t per = 64 / l;
+        for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {
+            gsl[g] = (int64_t)s_start.size();
+            for (int64_t r0 = grp[g]; r0 < grp[g + 1]; r0 += per) {
+                const int64_t r1 = std::min(grp[g + 1], r0 + per);
+                int64_t L = 0;
+                for (int64_t r = r0; r < r1; ++r) L = std::max(L, (rlen(order[r]) + l - 1) / l);
+                s_start.push_back((int32_t)r0);
+                s_n.push_back((int32_t)(r1 - r0));
+                s_lpr.push_back(l);
+                sptr.push_back(sptr.back() + 64 * (L + 1));
+            }
+        }
+    }
+    gsl[ng] = (int64_t)s_start.size();
+    const int64_t ns = (int64_t)s_start.size();
+    auto up = [&](auto &d, const auto &v) {
+        d.alloc(std::max<size_t>(v.size(), 1));
+        if (!v.empty())
+            HIPCHK(hipMemcpyAsync(d.p, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, c.st));
+    };
+    DBuf<int32_t> d_start, d_n, d_lpr, d_order;
+    up(D.sptr, sptr);
+    up(D.gslice, gsl);
+    up(D.lpr, lpr);
+    up(d_start, s_start);
+    up(d_n, s_n);
+    up(d_lpr, s_lpr);
+    up(d_order, order);
+    D.col.alloc(std::max<int64_t>(sptr.back(), 1));
+    D.val.alloc(std::max<int64_t>(sptr.back(), 1));
+    launch_lds_fill(ns, d_start.p, d_n.p, d_lpr.p, d_order.p, P.F.rp.p, P.F.ci.p, P.F.val.p, P.diag.p, P.dinv.p,
+                    upper ? 1 : 0, n, nb, D.sptr.p, D.col.p, D.val.p, c.st);
+    HIPCHK(hipGetLastError());
+    c.sync();
+}
+
 void TriSELL::apply(const double *b, double *y, Ctx &c) const {
     const double *dv = sdinv.p;
     if (blockwise) {
@@ -532,6 +590,11 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds) {
         build_tri_sell(*this, rp, dg, oL, gL, &fL, false, Lf, c);
         build_tri_sell(*this, rp, dg, oU, gU, &fU, true, Uf, c);
         nlev_U = (int64_t)gU.size() - 1;
+        use_lds = allow_lds && fits_lds;
+        if (use_lds) {
+            build_lds_tri(*this, n, nblocks, rp, dg, oL, gL, fL, false, Ls, c);
+            build_lds_tri(*this, n, nblocks, rp, dg, oU, gU, fU, true, Us, c);
+        }
     } else {
         std::vector<int32_t> ordU;
         std::vector<int64_t> Uptr;
@@ -542,10 +605,38 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds) {
 }
 
 void PCILU::apply(const double *x, double *y, Ctx &c) {
-    if (allow_lds && Lf.blockwise && (n / nblocks + 1) <= ilu_lds_max_rows()) {
-        launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Lf.gslice.p, Lf.sptr.p, Lf.slot_row.p, Lf.slot_len.p, Lf.col.p,
-                              Lf.val.p, Uf.goff.p, Uf.gslice.p, Uf.sptr.p, Uf.slot_row.p, Uf.slot_len.p, Uf.col.p,
-                              Uf.val.p, Uf.sdinv.p, x, y, c.st);
+    if (use_lds) {
+        DBuf<int64_t> prof;
+        if (!profile_tag.empty()) prof.alloc(nblocks * 8);
+        launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
+                              Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof.p);
+        if (!profile_tag.empty()) {
+            // diagnostics: per-block sweep times (100 MHz wall clock), slowest first
+            std::vector<int64_t> h(nblocks * 8);
+            HIPCHK(hipMemcpyAsync(h.data(), prof.p, sizeof(int64_t) * h.size(), hipMemcpyDeviceToHost, c.st));
+            c.sync();
+            int64_t tmin = INT64_MAX, tmax = 0;
+            std::vector<int64_t> order(nblocks);
+            for (int64_t b = 0; b < nblocks; ++b) {
+                order[b] = b;
+                tmin = std::min(tmin, h[b * 8]);
+                tmax = std::max(tmax, h[b * 8 + 2]);
+            }
+            std::sort(order.begin(), order.end(),
+                      [&](int64_t a, int64_t b) { return h[a * 8 + 2] - h[a * 8] > h[b * 8 + 2] - h[b * 8]; });
+            fprintf(stderr, "[sweep %s] %lld blocks, kernel span %.1f us\n", profile_tag.c_str(), (long long)nblocks,
+                    (tmax - tmin) * 0.01);
+            for (int64_t r = 0; r < std::min<int64_t>(nblocks, 12); ++r) {
+                const int64_t b = order[r], *p = &h[b * 8];
+                fprintf(stderr,
+                        "  blk %4lld rows %6lld start %+8.1f us  L %7.1f us (%4lld lv, %5lld sl)  U %7.1f us (%4lld lv)"
+                        "  lanes/row L,U %lld,%lld\n",
+                        (long long)b, (long long)p[5], (p[0] - tmin) * 0.01, (p[1] - p[0]) * 0.01, (long long)p[3],
+                        (long long)p[6], (p[2] - p[1]) * 0.01, (long long)p[4], (long long)(p[7] / 10),
+                        (long long)(p[7] % 10));
+            }
+            profile_tag.clear();
+        }
         return;
     }
     Lf.apply(x, y, c);
@@ -578,7 +669,9 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         if (sub == "ilu") {
             if (o.integer(prefix + "sub_pc_factor_levels", 0) != 0)
                 throw Error(prefix + "sub_pc_factor_levels > 0: only ILU(0) is implemented");
-            return std::make_unique<PCILU>(M, nb, c, false, o.flag("pls.ilu_lds", true));
+            auto pc = std::make_unique<PCILU>(M, nb, c, false, o.flag("pls.ilu_lds", true));
+            if (o.flag("pls.sweep_profile", false)) pc->profile_tag = prefix;
+            return pc;
         }
         if (sub == "jacobi") return std::make_unique<PCJacobi>(M, c);
         if (sub == "none") return std::make_unique<PCNone>(M.nrows);

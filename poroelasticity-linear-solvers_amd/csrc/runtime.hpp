@@ -204,15 +204,25 @@ struct TriSELL {
 // Factorization: level scheduled, one wave per row.  Sweeps: level-aligned
 // SELL-64; with >= 64 blocks one workgroup per block walks its own levels,
 // otherwise one launch per global level.
+// LDS-kernel stream layout of a blockwise TriSELL (header entry per lane,
+// block-local columns; levels/groups shared with the TriSELL).
+struct LdsTri {
+    DBuf<int64_t> sptr, gslice;  // slices differ from the TriSELL's (lanes per row); groups/goff are shared
+    DBuf<int32_t> col, lpr;      // lpr: lanes per row, per block
+    DBuf<double> val;
+};
 struct PCILU : PC {
     int64_t nblocks = 1;
     DevCSR F;                     // truncated matrix, factored in place
     DBuf<int64_t> diag;
     DBuf<double> dinv;
     TriSELL Lf, Uf;
+    LdsTri Ls, Us;            // built when the LDS kernel serves apply()
+    bool use_lds = false;
     int64_t nlev_L = 0, nlev_U = 0;
     bool allow_lds = true;  // block solution resident in LDS when it fits
     bool exact = false;     // envelope pattern: exact LU (PCLU)
+    std::string profile_tag;  // non-empty: dump per-block sweep timings once (option pls.sweep_profile)
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true);
     void apply(const double *x, double *y, Ctx &c) override;
 };
