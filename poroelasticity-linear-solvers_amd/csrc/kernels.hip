@@ -1465,9 +1465,17 @@ __device__ __forceinline__ void sw2_issue(Sw2Ctx &x, int64_t g, Sw2Slot<P> &s) {
     const int64_t L = base >= 0 ? (readlane64(x.se, l) - base) >> 6 : 0;
     s.base = base;
     s.L = L;
+    if (base < 0) {  // wave idle at this level: no loads (they would only queue in the CU's memory pipe)
+#pragma unroll
+        for (int u = 0; u <= P; ++u) {
+            s.c[u] = 0;
+            s.v[u] = 0.0;
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u <= P; ++u) {
-        const int64_t pos = base >= 0 ? base + (u < L ? u : 0) * 64 + x.lane : 0;
+        const int64_t pos = base + (u < L ? u : 0) * 64 + x.lane;
         s.c[u] = __builtin_nontemporal_load(x.col + pos);
         s.v[u] = __builtin_nontemporal_load(x.val + pos);
     }

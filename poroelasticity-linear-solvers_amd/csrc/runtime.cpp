@@ -435,7 +435,7 @@ static void build_tri_sell(const PCILU &P, const std::vector<int64_t> &rp, const
 // the lanes per row (1, 2 or 4) that fit every lane's share of the block's
 // longest row into the kernel's register window; slices of 64 / LPR rows of
 // one level; one header entry per lane.
-static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, const std::vector<int64_t> &rp,
+static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, const std::vector<int64_t> &rp,
                           const std::vector<int64_t> &dg, const std::vector<int32_t> &order,
                           const std::vector<int64_t> &grp, const std::vector<int64_t> &goff, bool upper, LdsTri &D,
                           Ctx &c) {
@@ -445,10 +445,14 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, const std::vect
     std::vector<int32_t> lpr(nblk, 1), s_start, s_n, s_lpr;
     std::vector<int64_t> gsl(ng + 1, 0), sptr(1, 0);
     for (int64_t b = 0; b < nblk; ++b) {
+        // lanes per row: the fewest that fit the longest row's per-lane share
+        // into the kernel's register window (measured at N=59: 2 or 4 lanes
+        // on short rows cost more in extra slices and headers than they gain)
         int64_t mx = 0;
         for (int64_t r = grp[goff[b]]; r < grp[goff[b + 1]]; ++r) mx = std::max(mx, rlen(order[r]));
         int l = 1;
         while (l < 4 && (mx + l - 1) / l > W) l *= 2;
+        if (force_lpr) l = force_lpr;
         lpr[b] = l;
         const int64_t per = 64 / l;
         for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {
@@ -533,7 +537,7 @@ static void envelope_csr(const DevCSR &M, DevCSR &E, Ctx &c) {
     upload_csr(E, n, n, erp.data(), eci.data(), ev.data(), c);
 }
 
-PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds) {
+PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr) {
     exact = exact_lu;
     allow_lds = lds;
     type = exact ? "lu" : (nb > 1 ? "bjacobi" : "ilu");
@@ -592,8 +596,8 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds) {
         nlev_U = (int64_t)gU.size() - 1;
         use_lds = allow_lds && fits_lds;
         if (use_lds) {
-            build_lds_tri(*this, n, nblocks, rp, dg, oL, gL, fL, false, Ls, c);
-            build_lds_tri(*this, n, nblocks, rp, dg, oU, gU, fU, true, Us, c);
+            build_lds_tri(*this, n, nblocks, force_lpr, rp, dg, oL, gL, fL, false, Ls, c);
+            build_lds_tri(*this, n, nblocks, force_lpr, rp, dg, oU, gU, fU, true, Us, c);
         }
     } else {
         std::vector<int32_t> ordU;
@@ -669,7 +673,8 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         if (sub == "ilu") {
             if (o.integer(prefix + "sub_pc_factor_levels", 0) != 0)
                 throw Error(prefix + "sub_pc_factor_levels > 0: only ILU(0) is implemented");
-            auto pc = std::make_unique<PCILU>(M, nb, c, false, o.flag("pls.ilu_lds", true));
+            auto pc = std::make_unique<PCILU>(M, nb, c, false, o.flag("pls.ilu_lds", true),
+                                              (int)o.integer("pls.sweep_lpr", 0));
             if (o.flag("pls.sweep_profile", false)) pc->profile_tag = prefix;
             return pc;
         }

@@ -223,7 +223,7 @@ struct PCILU : PC {
     bool allow_lds = true;  // block solution resident in LDS when it fits
     bool exact = false;     // envelope pattern: exact LU (PCLU)
     std::string profile_tag;  // non-empty: dump per-block sweep timings once (option pls.sweep_profile)
-    PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true);
+    PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0);
     void apply(const double *x, double *y, Ctx &c) override;
 };
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
