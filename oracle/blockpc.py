@@ -9,7 +9,7 @@ Follows the reference ``lib/Preconditioner.py``:
   tolerances left at PETSc defaults (the stored inner rtol/atol/maxiter are
   never applied: ``__init__`` 22-27 vs ``setup_elliptic_solver`` 94-100);
   ``fp_`` is an elliptic solver when inner pc type is ``lu``, otherwise GMRES +
-  fieldsplit (``setUp`` 134-138, ``setup_fieldsplit`` 102-118);
+  fieldsplit (``setUp`` 134-138, ``setup_fieldsplit`` 102-118; oracle/fieldsplit.py);
 * ``apply`` 141-250:
   - 2-way: y_s = K_s^-1 x_s ; y_fp = K_fp^-1 (x_fp - P_fp,s y_s)       (221-234)
   - 3-way: FS sweep p -> f -> s and DIFF sweep (pressure-BC rows of x_p zeroed,
@@ -81,8 +81,14 @@ class BlockPC:
                 # setup_fieldsplit: GMRES + fieldsplit unless the options override the pc type
                 ptype = opt(db, "fp_", "pc_type", "fieldsplit")
                 if ptype == "fieldsplit":
-                    raise NotImplementedError("fp_ fieldsplit (Schur) is not restated yet (SURVEY 8f rank 1)")
-                self.ksp_fp = inner("fp_", Mfp_fp, "gmres", ptype, (1, 2))
+                    # setFieldSplitIS((None, is_p)) then ((None, is_f)): split 0 = pressure
+                    from .fieldsplit import PCFieldSplit
+                    if dist_size > 1:
+                        raise ValueError("fieldsplit is restated for one rank only")
+                    fs = PCFieldSplit(Mfp_fp, self.is_p, self.is_f, db, "fp_")
+                    self.ksp_fp = petsc.ksp_from_options("fp_", db, Mfp_fp, Mfp_fp, "gmres", "fieldsplit", pc=fs)
+                else:
+                    self.ksp_fp = inner("fp_", Mfp_fp, "gmres", ptype, (1, 2))
 
     def apply(self, x):
         x = np.asarray(x, dtype=np.float64)

@@ -415,6 +415,8 @@ struct Handle {
     DBuf<int32_t> synth_offs;
     std::string pc_type, solver_type, inner_ksp, inner_pc;
     std::vector<int64_t> perm;   // internal -> caller
+    std::vector<int32_t> fp_is_f, fp_is_p;  // 2-way: f / p positions inside the sorted fp set (IndexSet.py:10-26)
+    std::unique_ptr<PCFieldSplit> fs_fp;     // fp_ fieldsplit PC (2-way, inexact inner PC)
     DBuf<int64_t> dperm;
     DevCSR A, P, Pd;
     bool have_Pd = false;
@@ -630,9 +632,21 @@ static void do_setup(Handle &H) {
             H.ksp_fp = make_ksp("fp_", o, &H.Kfp, &H.Kfp, H.inner_ksp, "lu", c);
         } else {
             const std::string pt = o.str("fp_pc_type", "fieldsplit");
-            if (pt == "fieldsplit")
-                throw Error("fp_ fieldsplit (Schur) preconditioner is not available yet; set fp_pc_type");
-            H.ksp_fp = make_ksp("fp_", o, &H.Kfp, &H.Kfp, "gmres", pt, c);
+            if (pt == "fieldsplit") {
+                // setup_fieldsplit (Preconditioner.py:102-118): setFieldSplitIS((None, is_p)) then
+                // ((None, is_f)) -- split 0 = pressure, split 1 = fluid, fp-local positions
+                if (H.distributed) throw Error("fp_pc_type fieldsplit is not available with several ranks");
+                std::vector<int32_t> fpf = H.fp_is_f, fpp = H.fp_is_p;
+                if (fpf.empty() && fpp.empty()) {  // field-major fp block: [f | p]
+                    for (int64_t i = 0; i < H.nf; ++i) fpf.push_back((int32_t)i);
+                    for (int64_t i = 0; i < H.np; ++i) fpp.push_back((int32_t)(H.nf + i));
+                }
+                H.fs_fp = std::make_unique<PCFieldSplit>(H.Kfp, fpp, fpf, o, "fp_", c);
+                H.ksp_fp = make_ksp("fp_", o, &H.Kfp, &H.Kfp, "gmres", "fieldsplit", c, 1e-5, 1e-50, 1e4, 10000, 30,
+                                    H.fs_fp.get());
+            } else {
+                H.ksp_fp = make_ksp("fp_", o, &H.Kfp, &H.Kfp, "gmres", pt, c);
+            }
         }
     }
     H.mixer.init((int)o.integer("pls.inner_accel_order", 0), n);
@@ -845,6 +859,9 @@ int pls_create(const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff, const i
             fp.insert(fp.end(), is_p, is_p + np);
             std::sort(fp.begin(), fp.end());
             H->perm.insert(H->perm.end(), fp.begin(), fp.end());
+            std::vector<char> isf(n, 0);
+            for (int64_t i = 0; i < nf; ++i) isf[is_f[i]] = 1;
+            for (size_t t = 0; t < fp.size(); ++t) (isf[fp[t]] ? H->fp_is_f : H->fp_is_p).push_back((int32_t)t);
         }
         std::vector<int64_t> inv(n);
         for (int64_t i = 0; i < n; ++i) inv[H->perm[i]] = i;

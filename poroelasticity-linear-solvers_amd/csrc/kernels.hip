@@ -1680,6 +1680,13 @@ __global__ __launch_bounds__(TPB) void k_sort_rows(int64_t n, const int64_t *rp,
 void launch_sort_rows(int64_t n, const int64_t *rp, int32_t *ci, double *val, hipStream_t st) {
     if (n > 0) k_sort_rows<<<grid_for(n, TPB), TPB, 0, st>>>(n, rp, ci, val);
 }
+__global__ __launch_bounds__(TPB) void k_unpack(int64_t m, const int32_t *idx, const double *buf, double *x) {
+    const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (k < m) x[idx[k]] = buf[k];
+}
+void launch_unpack(int64_t m, const int32_t *idx, const double *buf, double *x, hipStream_t st) {
+    if (m > 0) k_unpack<<<grid_for(m, TPB), TPB, 0, st>>>(m, idx, buf, x);
+}
 void launch_pack(int64_t m, const int32_t *idx, const double *x, double *buf, hipStream_t st) {
     if (m > 0) k_pack<<<grid_for(m, TPB), TPB, 0, st>>>(m, idx, x, buf);
 }

@@ -161,6 +161,7 @@ void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n
 void launch_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint8_t *flag, hipStream_t st);
 void launch_remap_cols(int64_t nnz, int32_t *ci, const int32_t *gmap, hipStream_t st);
 void launch_sort_rows(int64_t n, const int64_t *rp, int32_t *ci, double *val, hipStream_t st);
-void launch_pack(int64_t m, const int32_t *idx, const double *x, double *buf, hipStream_t st);
+void launch_pack(int64_t m, const int32_t *idx, const double *x, double *buf, hipStream_t st);   // buf[k] = x[idx[k]]
+void launch_unpack(int64_t m, const int32_t *idx, const double *buf, double *x, hipStream_t st); // x[idx[k]] = buf[k]
 
 }  // namespace pls

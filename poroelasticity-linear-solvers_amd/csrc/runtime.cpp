@@ -977,3 +977,220 @@ std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const
 }
 
 }  // namespace pls
+
+namespace pls {
+
+// =========================================================== fieldsplit ===
+namespace {
+struct HostCSR {
+    int64_t nrows = 0, ncols = 0;
+    std::vector<int64_t> rp{0};
+    std::vector<int32_t> ci;
+    std::vector<double> v;
+};
+
+HostCSR download(const DevCSR &M, Ctx &c) {
+    HostCSR H;
+    H.nrows = M.nrows;
+    H.ncols = M.ncols;
+    H.rp.resize(M.nrows + 1);
+    H.ci.resize(M.nnz);
+    H.v.resize(M.nnz);
+    HIPCHK(hipMemcpyAsync(H.rp.data(), M.rp.p, sizeof(int64_t) * (M.nrows + 1), hipMemcpyDeviceToHost, c.st));
+    if (M.nnz) {
+        HIPCHK(hipMemcpyAsync(H.ci.data(), M.ci.p, sizeof(int32_t) * M.nnz, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipMemcpyAsync(H.v.data(), M.val.p, sizeof(double) * M.nnz, hipMemcpyDeviceToHost, c.st));
+    }
+    c.sync();
+    return H;
+}
+
+// rows `rows`, columns mapped by cmap (-1: dropped); cmap is monotone on the
+// kept columns, so rows stay sorted (MatCreateSubMatrix with sorted ISs)
+HostCSR submatrix(const HostCSR &M, const std::vector<int32_t> &rows, const std::vector<int32_t> &cmap,
+                  int64_t ncols) {
+    HostCSR S;
+    S.nrows = (int64_t)rows.size();
+    S.ncols = ncols;
+    S.rp.assign(1, 0);
+    for (int32_t r : rows) {
+        for (int64_t k = M.rp[r]; k < M.rp[r + 1]; ++k) {
+            const int32_t m = cmap[M.ci[k]];
+            if (m >= 0) {
+                S.ci.push_back(m);
+                S.v.push_back(M.v[k]);
+            }
+        }
+        S.rp.push_back((int64_t)S.ci.size());
+    }
+    return S;
+}
+
+// MatSchurComplementGetPmat, AINV_DIAG: D - C diag(A)^-1 B.  diag reciprocal
+// keeps zeros (VecReciprocal); AinvB = row-scaled B; the product row i sums
+// over k ascending (MatMatMult, sorted algorithm); then MatAYPX(S, -1, D).
+HostCSR selfp(const HostCSR &A, const HostCSR &B, const HostCSR &C, const HostCSR &D) {
+    std::vector<double> dinv(A.nrows, 0.0);
+    for (int64_t i = 0; i < A.nrows; ++i)
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
+            if (A.ci[k] == i) dinv[i] = A.v[k] != 0.0 ? 1.0 / A.v[k] : 0.0;
+    std::vector<double> bs(B.v.size());
+    for (int64_t i = 0; i < B.nrows; ++i)
+        for (int64_t k = B.rp[i]; k < B.rp[i + 1]; ++k) bs[k] = dinv[i] * B.v[k];
+    HostCSR S;
+    S.nrows = D.nrows;
+    S.ncols = D.ncols;
+    std::vector<double> acc(D.ncols, 0.0);
+    std::vector<char> mark(D.ncols, 0);
+    std::vector<int32_t> cols;
+    for (int64_t i = 0; i < C.nrows; ++i) {
+        cols.clear();
+        for (int64_t kk = C.rp[i]; kk < C.rp[i + 1]; ++kk) {
+            const int32_t k = C.ci[kk];
+            const double a = C.v[kk];
+            for (int64_t jj = B.rp[k]; jj < B.rp[k + 1]; ++jj) {
+                const int32_t j = B.ci[jj];
+                if (!mark[j]) {
+                    mark[j] = 1;
+                    acc[j] = 0.0;
+                    cols.push_back(j);
+                }
+                acc[j] += a * bs[jj];
+            }
+        }
+        for (int64_t kk = D.rp[i]; kk < D.rp[i + 1]; ++kk)
+            if (!mark[D.ci[kk]]) {
+                mark[D.ci[kk]] = 2;  // D only
+                cols.push_back(D.ci[kk]);
+            }
+        std::sort(cols.begin(), cols.end());
+        int64_t dk = D.rp[i];
+        for (int32_t j : cols) {
+            double dv = 0.0;
+            bool hasd = false;
+            while (dk < D.rp[i + 1] && D.ci[dk] < j) ++dk;
+            if (dk < D.rp[i + 1] && D.ci[dk] == j) {
+                dv = D.v[dk];
+                hasd = true;
+            }
+            double out;
+            if (mark[j] == 2) out = dv;
+            else out = hasd ? dv - acc[j] : -acc[j];
+            S.ci.push_back(j);
+            S.v.push_back(out);
+            mark[j] = 0;
+        }
+        S.rp.push_back((int64_t)S.ci.size());
+    }
+    return S;
+}
+
+void upload(const HostCSR &H, DevCSR &M, Ctx &c) {
+    upload_csr(M, H.nrows, H.ncols, H.rp.data(), H.ci.data(), H.v.data(), c);
+}
+
+// S x = A11 x - A10 A00^-1 A01 x (MatMult_SchurComplement; inner solve = the split-0 KSP)
+struct SchurOp : Op {
+    const DevCSR *A01, *A10, *A11;
+    KSP *k0;
+    DBuf<double> w1, w2, w3;
+    SchurOp(const DevCSR *a01, const DevCSR *a10, const DevCSR *a11, KSP *k) : A01(a01), A10(a10), A11(a11), k0(k) {
+        n = a11->nrows;
+        w1.alloc(std::max<int64_t>(a01->nrows, 1));
+        w2.alloc(std::max<int64_t>(a01->nrows, 1));
+        w3.alloc(std::max<int64_t>(n, 1));
+    }
+    void apply(const double *x, double *y, Ctx &c) override {
+        spmv(*A01, x, w1.p, c);
+        k0->solve(w1.p, w2.p, c);
+        spmv(*A10, w2.p, w3.p, c);
+        spmv(*A11, x, y, c, 1.0, -1.0, w3.p);
+    }
+};
+}  // namespace
+
+PCFieldSplit::PCFieldSplit(const DevCSR &M, const std::vector<int32_t> &s0, const std::vector<int32_t> &s1,
+                           const Options &o, const std::string &prefix, Ctx &c) {
+    type = "fieldsplit";
+    n = M.nrows;
+    if (M.halo) throw Error(prefix + "pc_type fieldsplit: not available with several ranks");
+    n0 = (int64_t)s0.size();
+    n1 = (int64_t)s1.size();
+    ftype = o.str(prefix + "pc_fieldsplit_type", "multiplicative");
+    if (ftype != "additive" && ftype != "multiplicative" && ftype != "schur")
+        throw Error(prefix + "pc_fieldsplit_type " + ftype + " is not available (additive, multiplicative, schur)");
+    const HostCSR Mh = download(M, c);
+    std::vector<int32_t> m0(n, -1), m1(n, -1);
+    for (int64_t i = 0; i < n0; ++i) m0[s0[i]] = (int32_t)i;
+    for (int64_t i = 0; i < n1; ++i) m1[s1[i]] = (int32_t)i;
+    const HostCSR h00 = submatrix(Mh, s0, m0, n0), h01 = submatrix(Mh, s0, m1, n1);
+    const HostCSR h10 = submatrix(Mh, s1, m0, n0), h11 = submatrix(Mh, s1, m1, n1);
+    upload(h00, A00, c);
+    upload(h01, A01, c);
+    upload(h10, A10, c);
+    upload(h11, A11, c);
+    for (DevCSR *B : {&A01, &A10, &A11}) build_sell(*B, c);
+    const std::string p0 = prefix + "fieldsplit_0_", p1 = prefix + "fieldsplit_1_";
+    k0 = make_ksp(p0, o, &A00, &A00, "preonly", "ilu", c);
+    if (ftype == "schur") {
+        fact = o.str(prefix + "pc_fieldsplit_schur_fact_type", "full");
+        if (fact != "diag" && fact != "lower" && fact != "upper" && fact != "full")
+            throw Error(prefix + "pc_fieldsplit_schur_fact_type " + fact + " is not available");
+        scale = o.num(prefix + "pc_fieldsplit_schur_scale", -1.0);
+        const std::string pre = o.str(prefix + "pc_fieldsplit_schur_precondition", "a11");
+        const DevCSR *pmat = &A11;
+        if (pre == "selfp") {
+            upload(selfp(h00, h01, h10, h11), Sp, c);
+            pmat = &Sp;
+        } else if (pre != "a11") {
+            throw Error(prefix + "pc_fieldsplit_schur_precondition " + pre + " is not available (selfp, a11)");
+        }
+        k1 = make_ksp(p1, o, nullptr, pmat, "gmres", "ilu", c);
+        k1->owned_op = std::make_unique<SchurOp>(&A01, &A10, &A11, k0.get());
+        k1->A = k1->owned_op.get();
+        k1->n = n1;
+    } else {
+        k1 = make_ksp(p1, o, &A11, &A11, "preonly", "ilu", c);
+    }
+    for (auto *b : {&x0, &y0, &t0}) b->alloc(std::max<int64_t>(n0, 1));
+    for (auto *b : {&x1, &y1, &t1}) b->alloc(std::max<int64_t>(n1, 1));
+    is0.alloc(std::max<int64_t>(n0, 1));
+    is1.alloc(std::max<int64_t>(n1, 1));
+    if (n0) HIPCHK(hipMemcpyAsync(is0.p, s0.data(), sizeof(int32_t) * n0, hipMemcpyHostToDevice, c.st));
+    if (n1) HIPCHK(hipMemcpyAsync(is1.p, s1.data(), sizeof(int32_t) * n1, hipMemcpyHostToDevice, c.st));
+    c.sync();
+}
+
+// PCApply_FieldSplit / PCApply_FieldSplit_Schur
+void PCFieldSplit::apply(const double *x, double *y, Ctx &c) {
+    launch_pack(n0, is0.p, x, x0.p, c.st);
+    launch_pack(n1, is1.p, x, x1.p, c.st);
+    auto x1_minus_A10 = [&](const double *v) { spmv(A10, v, t1.p, c, -1.0, 1.0, x1.p); };   // t1 = x1 - A10 v
+    auto x0_minus_A01 = [&](const double *v) { spmv(A01, v, t0.p, c, -1.0, 1.0, x0.p); };   // t0 = x0 - A01 v
+    if (ftype == "additive") {
+        k0->solve(x0.p, y0.p, c);
+        k1->solve(x1.p, y1.p, c);
+    } else if (ftype == "multiplicative" || fact == "lower") {
+        k0->solve(x0.p, y0.p, c);
+        x1_minus_A10(y0.p);
+        k1->solve(t1.p, y1.p, c);
+    } else if (fact == "diag") {
+        k0->solve(x0.p, y0.p, c);
+        k1->solve(x1.p, y1.p, c);
+        launch_scale(n1, scale, y1.p, c.st);
+    } else if (fact == "upper") {
+        k1->solve(x1.p, y1.p, c);
+        x0_minus_A01(y1.p);
+        k0->solve(t0.p, y0.p, c);
+    } else {  // full
+        k0->solve(x0.p, y0.p, c);
+        x1_minus_A10(y0.p);
+        k1->solve(t1.p, y1.p, c);
+        x0_minus_A01(y1.p);
+        k0->solve(t0.p, y0.p, c);
+    }
+    launch_unpack(n0, is0.p, y0.p, y, c.st);
+    launch_unpack(n1, is1.p, y1.p, y, c.st);
+}
+
+}  // namespace pls

@@ -269,6 +269,24 @@ struct KSP {
     double rnorm0 = 0, ttol = 0;
 };
 
+// PCFIELDSPLIT with two splits given as index sets of the matrix rows
+// (reference lib/Preconditioner.py:102-118: split 0 = is_p, split 1 = is_f in
+// fp-local numbering).  Types additive, multiplicative, schur (fact diag /
+// lower / upper / full; Schur preconditioning matrix selfp or a11; Schur KSP
+// operator S = A11 - A10 A00^-1 A01 applied implicitly with the split-0 KSP).
+struct PCFieldSplit : PC {
+    std::string ftype, fact;
+    double scale = -1.0;
+    int64_t n0 = 0, n1 = 0;
+    DBuf<int32_t> is0, is1;
+    DevCSR A00, A01, A10, A11, Sp;
+    std::unique_ptr<KSP> k0, k1;
+    DBuf<double> x0, x1, y0, y1, t0, t1;
+    PCFieldSplit(const DevCSR &M, const std::vector<int32_t> &is0, const std::vector<int32_t> &is1, const Options &o,
+                 const std::string &prefix, Ctx &c);
+    void apply(const double *x, double *y, Ctx &c) override;
+};
+
 // Configure a KSP from programmatic defaults + options (setFromOptions order).
 std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const DevCSR *Amat, const DevCSR *Pmat,
                               const std::string &default_ksp, const std::string &default_pc, Ctx &c,

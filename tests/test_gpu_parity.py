@@ -346,3 +346,66 @@ def test_unsupported_pc_fails_loudly(gpu):
     h = _handle(spec, BASE, dict(ILU_DB, s_pc_type="hypre"))
     with pytest.raises(RuntimeError, match="hypre"):
         h.setup()
+
+
+# ------------------------------------------------ fp fieldsplit (2-way) ----
+FS_INEXACT = {  # petsc-options-inexact:73-114 with BoomerAMG -> Jacobi / ILU(0) (hypre is not in this build)
+    "global_ksp_type": "gmres", "global_ksp_norm_type": "unpreconditioned",
+    "s_ksp_type": "preonly", "s_pc_type": "ilu",
+    "fp_ksp_type": "preonly", "fp_ksp_rtol": "1e-2", "fp_ksp_atol": "0.0",
+    "fp_ksp_gmres_modifiedgramschmidt": None,
+    "fp_pc_fieldsplit_type": "schur", "fp_pc_fieldsplit_schur_fact_type": "lower",
+    "fp_pc_fieldsplit_schur_precondition": "selfp",
+    "fp_fieldsplit_0_ksp_type": "cg", "fp_fieldsplit_0_ksp_rtol": "1e-4", "fp_fieldsplit_0_ksp_atol": "0.0",
+    "fp_fieldsplit_0_ksp_max_it": "10", "fp_fieldsplit_0_pc_type": "jacobi",
+    "fp_fieldsplit_1_ksp_type": "preonly", "fp_fieldsplit_1_pc_type": "lu",
+}
+FS_PARAMS = {"inner ksp type": "cg", "inner pc type": "hypre"}
+
+
+@pytest.mark.parametrize("variant", ["inexact", "lower_ilu", "full_implicit", "upper", "diag", "multiplicative",
+                                     "additive", "default"])
+def test_fieldsplit_fp(gpu, variant):
+    db = dict(FS_INEXACT)
+    if variant == "lower_ilu":
+        db.update({"fp_fieldsplit_0_ksp_type": "preonly", "fp_fieldsplit_0_pc_type": "ilu",
+                   "fp_fieldsplit_1_pc_type": "ilu"})
+    elif variant == "full_implicit":  # Schur KSP on the implicit S, preconditioned by ILU(selfp)
+        db.update({"fp_pc_fieldsplit_schur_fact_type": "full", "fp_fieldsplit_0_ksp_type": "preonly",
+                   "fp_fieldsplit_0_pc_type": "ilu", "fp_fieldsplit_1_ksp_type": "gmres",
+                   "fp_fieldsplit_1_ksp_rtol": "1e-3", "fp_fieldsplit_1_pc_type": "ilu"})
+    elif variant in ("upper", "diag"):
+        db.update({"fp_pc_fieldsplit_schur_fact_type": variant, "fp_pc_fieldsplit_schur_precondition": "a11",
+                   "fp_fieldsplit_0_ksp_type": "preonly", "fp_fieldsplit_0_pc_type": "ilu",
+                   "fp_fieldsplit_1_pc_type": "ilu"})
+    elif variant in ("multiplicative", "additive"):
+        db["fp_pc_fieldsplit_type"] = variant
+        db["fp_fieldsplit_1_pc_type"] = "ilu"
+    elif variant == "default":  # no fp_ options at all: GMRES + PETSc's fieldsplit defaults
+        db = {k: v for k, v in db.items() if not k.startswith("fp_")}
+    upd = dict(FS_PARAMS, **{"solver maxiter": 200})
+    nonlinear = db.get("fp_fieldsplit_0_ksp_type") == "cg" or variant in ("full_implicit", "default")
+    _compare_solve(S.SynthSpec(2, 8), upd, db=db, sensitivity=nonlinear)
+
+
+def test_fieldsplit_interleaved_index_sets(gpu):
+    """fieldsplit IS built from interleaved (dolfin-like) f/p dofs inside the sorted fp set."""
+    from lib.handle import Handle, params_to_options
+    spec = S.SynthSpec(2, 7)
+    perm = S.interleaving(spec)
+    A = S.permute(S.matrix(spec, 0), perm)
+    P = S.permute(S.matrix(spec, 1), perm)
+    is_s, is_f, is_p = S.index_sets_for(perm, spec)
+    b = S.rhs(spec)[perm]
+    db = dict(FS_INEXACT, **{"fp_fieldsplit_0_ksp_type": "preonly", "fp_fieldsplit_0_pc_type": "ilu"})
+    params = dict(BASE, **FS_PARAMS)
+    o = OracleSolver(A, P, None, is_s, is_f, is_p, params, db, [])
+    xo = o.solve(b)
+    opts = dict(db)
+    opts.update(params_to_options(params))
+    h = Handle.from_csr(A, P, None, is_s, is_f, is_p, [], opts)
+    x, r = h.solve(b)
+    assert r.its == o.its and r.reason == o.reason
+    ho = np.asarray(o.history)
+    assert np.max(np.abs(h.history() - ho) / np.abs(ho)) <= RTOL_HIST
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)

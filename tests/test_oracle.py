@@ -316,13 +316,20 @@ def test_block_pc_rejects_bad_type():
         BP.make_block_pc(None, None, None, None, {"pc type": "bogus"}, {}, [])
 
 
-def test_fieldsplit_not_restated_yet():
+def test_fieldsplit_default_is_gmres_multiplicative():
+    """Inexact inner PC without fp_ options: fp_ is GMRES + PCFIELDSPLIT with
+    PETSc's defaults (MULTIPLICATIVE, split KSPs PREONLY + ILU), split 0 = p
+    (Preconditioner.py:102-118)."""
     spec, A, P, Pd = _small_system()
     is_s, is_f, is_p = S.field_major_index_sets(spec)
     params = {"pc type": "diagonal", "inner ksp type": "cg", "inner pc type": "ilu", "inner accel order": 0,
-              "solver type": "gmres", "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": 10}
-    with pytest.raises(NotImplementedError, match="fieldsplit"):
-        OracleSolver(A, P, Pd, is_s, is_f, is_p, params, {}, [])
+              "solver type": "gmres", "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": 50}
+    o = OracleSolver(A, P, Pd, is_s, is_f, is_p, params, {}, [])
+    fs = o.block_pc.ksp_fp.pc
+    assert o.block_pc.ksp_fp.type == "gmres" and fs.type == "fieldsplit" and fs.ftype == "multiplicative"
+    assert np.array_equal(fs.is0, np.asarray(o.block_pc.is_p)) and fs.k0.type == "preonly"
+    o.solve(S.rhs(spec))
+    assert o.reason > 0
 
 
 # ----------------------------------------------------------------- AAR -------
@@ -453,3 +460,76 @@ def test_synthetic_c_matches_numpy_enumeration(dim, N):
     off = M.copy()
     off.setdiag(0.0)
     assert np.array_equal(off.toarray(), R.toarray())
+
+
+# ---------------------------------------------------------- fieldsplit ----
+def _fp_block(N=6):
+    from oracle import synthetic as S
+    spec = S.SynthSpec(2, N)
+    P = S.matrix(spec, 1)
+    ns, nf, np_ = spec.sizes()
+    K = P[ns:, ns:].tocsr()
+    return K, np.arange(nf, nf + np_), np.arange(nf)
+
+
+def test_fieldsplit_schur_full_exact_inverts_block():
+    """Schur FULL with exact split-0 solves and a converged Schur KSP (implicit
+    S = A11 - A10 A00^-1 A01, preconditioned by LU(selfp)) is K^-1."""
+    from oracle.fieldsplit import PCFieldSplit
+    K, is_p, is_f = _fp_block()
+    db = {"fp_pc_fieldsplit_type": "schur", "fp_pc_fieldsplit_schur_fact_type": "full",
+          "fp_pc_fieldsplit_schur_precondition": "selfp",
+          "fp_fieldsplit_0_ksp_type": "preonly", "fp_fieldsplit_0_pc_type": "lu",
+          "fp_fieldsplit_1_ksp_type": "gmres", "fp_fieldsplit_1_ksp_rtol": "1e-13",
+          "fp_fieldsplit_1_pc_type": "lu"}
+    pc = PCFieldSplit(K, is_p, is_f, db, "fp_")
+    x = np.random.default_rng(3).standard_normal(K.shape[0])
+    y = pc.apply(x)
+    assert np.linalg.norm(K @ y - x) <= 1e-10 * np.linalg.norm(x)
+
+
+def test_fieldsplit_selfp_definition():
+    """SELFP = A11 - A10 diag(A00)^-1 A01 (dense check)."""
+    from oracle.fieldsplit import PCFieldSplit
+    K, is_p, is_f = _fp_block(4)
+    pc = PCFieldSplit(K, is_p, is_f, {"fp_pc_fieldsplit_type": "schur",
+                                      "fp_pc_fieldsplit_schur_precondition": "selfp"}, "fp_")
+    Kd = K.toarray()
+    A00, A01 = Kd[np.ix_(is_p, is_p)], Kd[np.ix_(is_p, is_f)]
+    A10, A11 = Kd[np.ix_(is_f, is_p)], Kd[np.ix_(is_f, is_f)]
+    ref = A11 - A10 @ np.diag(1.0 / np.diag(A00)) @ A01
+    assert np.allclose(pc.Sp.toarray(), ref, rtol=1e-14, atol=1e-14)
+
+
+@pytest.mark.parametrize("ftype,fact", [("additive", None), ("multiplicative", None), ("schur", "diag"),
+                                        ("schur", "lower"), ("schur", "upper")])
+def test_fieldsplit_block_factorizations(ftype, fact):
+    """With exact sub-solves (LU on A00, LU on A11 or on S via selfp when S is
+    replaced by its LU), each variant is the stated block-triangular solve."""
+    from oracle.fieldsplit import PCFieldSplit
+    K, is_p, is_f = _fp_block(4)
+    db = {"fp_pc_fieldsplit_type": ftype, "fp_fieldsplit_0_pc_type": "lu", "fp_fieldsplit_1_pc_type": "lu",
+          "fp_fieldsplit_1_ksp_type": "preonly"}
+    if fact:
+        db["fp_pc_fieldsplit_schur_fact_type"] = fact
+        db["fp_pc_fieldsplit_schur_precondition"] = "a11"
+    pc = PCFieldSplit(K, is_p, is_f, db, "fp_")
+    Kd = K.toarray()
+    A00, A01 = Kd[np.ix_(is_p, is_p)], Kd[np.ix_(is_p, is_f)]
+    A10, A11 = Kd[np.ix_(is_f, is_p)], Kd[np.ix_(is_f, is_f)]
+    x = np.random.default_rng(4).standard_normal(K.shape[0])
+    x0, x1 = x[is_p], x[is_f]
+    inv = np.linalg.solve
+    if ftype == "additive":
+        y0, y1 = inv(A00, x0), inv(A11, x1)
+    elif ftype == "multiplicative" or fact == "lower":
+        y0 = inv(A00, x0)
+        y1 = inv(A11, x1 - A10 @ y0)
+    elif fact == "diag":
+        y0, y1 = inv(A00, x0), -inv(A11, x1)
+    else:  # upper
+        y1 = inv(A11, x1)
+        y0 = inv(A00, x0 - A01 @ y1)
+    y = pc.apply(x)
+    assert np.allclose(y[is_p], y0, rtol=1e-10, atol=1e-12)
+    assert np.allclose(y[is_f], y1, rtol=1e-10, atol=1e-12)
