@@ -99,7 +99,7 @@ def main():
     ap.add_argument("--blocks-fp", type=int, default=264)
     ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-N", type=int, default=20)
+    ap.add_argument("--cpu-N", type=int, default=30)  # ~10-15 s of single-thread oracle work
     ap.add_argument("--cpu-maxit", type=int, default=100)
     ap.add_argument("--sell-d16", type=int, default=1, help="1: SELL-64/D16 SpMV layout (16-bit column deltas)")
     ap.add_argument("--d16-unroll", type=int, default=0, help="D16 SpMV: 8-entry groups per lane in flight (tuning)")
