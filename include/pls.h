@@ -129,6 +129,13 @@ int pls_comm_destroy(pls_comm *comm);
 int pls_create_synthetic_dist(const pls_synth_spec *spec, const char *options, pls_comm *comm, pls_handle **out);
 
 int pls_setup(pls_handle *h);
+/* New values (or patterns) of A / P / P_diff (NULL: unchanged), caller's
+ * ordering as in pls_create.  The block PC is set up again before the next
+ * solve -- PETSc's PCSetUp on an operator state change, which the reference
+ * triggers every time step by re-applying BCs to A and P
+ * (lib/Poromechanics.py:70-86, lib/Solver.py:105 set_up).  Outer solver,
+ * AAR and inner Anderson histories persist, as the reference's objects do. */
+int pls_update_matrices(pls_handle *h, const pls_csr *A, const pls_csr *P, const pls_csr *P_diff);
 /* Set / override one option ("key", "value" or NULL for a flag).  Options of
  * the outer solver ("pls.solver_*", "pls.aar_*", "global_*") may change until
  * pls_create_solver (or the first solve); PC options until pls_setup.        */

@@ -417,6 +417,7 @@ struct Handle {
     std::vector<int64_t> perm;   // internal -> caller
     std::vector<int32_t> fp_is_f, fp_is_p;  // 2-way: f / p positions inside the sorted fp set (IndexSet.py:10-26)
     std::unique_ptr<PCFieldSplit> fs_fp;     // fp_ fieldsplit PC (2-way, inexact inner PC)
+    bool mixer_ready = false;
     DBuf<int64_t> dperm;
     DevCSR A, P, Pd;
     bool have_Pd = false;
@@ -649,7 +650,12 @@ static void do_setup(Handle &H) {
             }
         }
     }
-    H.mixer.init((int)o.integer("pls.inner_accel_order", 0), n);
+    // the inner Anderson history lives as long as the preconditioner object
+    // (lib/Preconditioner.py: created in __init__, not in setUp)
+    if (!H.mixer_ready) {
+        H.mixer.init((int)o.integer("pls.inner_accel_order", 0), n);
+        H.mixer_ready = true;
+    }
     H.bpc.h = &H;
     H.bpc.type = "python";
     H.bpc.n = n;
@@ -1184,6 +1190,37 @@ int pls_bench_spmv(pls_handle *hh, const double *d_x, double *d_y, int32_t reps,
         (void)hipEventDestroy(a);
         (void)hipEventDestroy(b);
         *sec_per_launch = (double)ms * 1e-3 / std::max(1, reps);
+    })
+}
+
+// New values (or patterns) of A, P, P_diff for the next solves, in the
+// caller's ordering as for pls_create.  The block preconditioner is set up
+// again before the next solve (PETSc re-runs PCSetUp when the operator state
+// changes, as after the reference's bc.apply in every time step,
+// lib/Poromechanics.py:70-86); the outer solver and AAR / inner Anderson
+// histories persist, as the reference's objects do.
+int pls_update_matrices(pls_handle *hh, const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        if (H.synth_rows) throw Error("pls_update_matrices: synthetic handles generate their matrices");
+        if (H.distributed) throw Error("pls_update_matrices: not available for distributed handles");
+        if (!P && !H.keep && H.setup_done)
+            throw Error("pls_update_matrices: P was released after setup (pls.keep_matrices 0); pass P");
+        const int64_t n = H.n;
+        std::vector<int64_t> inv(n);
+        for (int64_t i = 0; i < n; ++i) inv[H.perm[i]] = i;
+        if (A) {
+            upload_permuted(A, H, inv, H.A);
+            H.A.sell.reset();
+            H.A.tag = 1;
+            if (H.solver_ready) build_sell(H.A, H.ctx);
+        }
+        if (P) upload_permuted(P, H, inv, H.P);
+        if (Pdiff) {
+            upload_permuted(Pdiff, H, inv, H.Pd);
+            H.have_Pd = true;
+        }
+        H.setup_done = false;
     })
 }
 

@@ -96,6 +96,8 @@ static int64_t max_row_of(const DBuf<int64_t> &rp, int64_t nrows, Ctx &c) {
 void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_t cshift, int64_t ncols,
                  DevCSR &dst, Ctx &c) {
     const int64_t nl = r1 - r0;
+    dst.sell.reset();  // re-extraction (matrix update): the SpMV layout is rebuilt on demand
+    dst.halo.reset();
     DBuf<int64_t> len(nl + 1);
     launch_extract_count(src.rp.p, src.ci.p, r0, r1, w, len.p, c.st);
     dst.rp.alloc(nl + 1);

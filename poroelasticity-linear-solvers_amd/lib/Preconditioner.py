@@ -10,17 +10,29 @@ win), and every ``apply`` (2-way 219-246, 3-way 150-218, inner Anderson
 from time import perf_counter as time
 
 from . import options as _opts
+from ._native import csr_of, vec_array
 from .handle import Handle, params_to_options
 from .Printing import parprint
 
 PC_TYPES = ("undrained", "undrained 3-way", "diagonal", "diagonal 3-way", "diagonal 3-way-II", "lu")
 
 
+def _fingerprint(M):
+    """Cheap value/pattern fingerprint of a matrix-like (scipy / petsc4py / dolfin)."""
+    import numpy as np
+    if M is None:
+        return None
+    ai, aj, av, nr, nc = csr_of(M)
+    return (nr, nc, av.size, float(np.sum(av)), float(np.dot(av, av)), int(np.sum(aj, dtype=np.int64)))
+
+
 class PreconditionerCC(object):
     """The python-PC context: ``setUp(pc)`` / ``apply(pc, x, y)`` / ``print_timings``."""
 
-    def __init__(self, handle: Handle, flag_3_way: bool):
+    def __init__(self, handle: Handle, flag_3_way: bool, mats=(None, None, None)):
         self.handle = handle
+        self.mats = mats
+        self._prints = None
         self.flag_3_way = flag_3_way
 
     def setUp(self, pc=None):
@@ -28,9 +40,22 @@ class PreconditionerCC(object):
         self.handle.setup()
         parprint("---- [Preconditioner] Set up in {}s".format(time() - t0))
 
+    def refresh(self):
+        """Re-set-up after A / P / P_diff changed in place (the reference's
+        bc.apply + PCSetUp every time step, lib/Poromechanics.py:70-86)."""
+        prints = tuple(_fingerprint(M) for M in self.mats)
+        if self._prints is None:
+            self._prints = prints
+            return False
+        changed = [m if p != q else None for m, p, q in zip(self.mats, prints, self._prints)]
+        self._prints = prints
+        if any(c is not None for c in changed):
+            self.handle.update_matrices(*changed)
+            return True
+        return False
+
     def apply(self, pc, x, y):
         """y = M^{-1} x (host vectors in the caller's ordering)."""
-        from ._native import vec_array
         yy = self.handle.pc_apply(vec_array(x))
         ya = vec_array(y)
         ya[...] = yy
@@ -96,7 +121,7 @@ class Preconditioner:
         opts.update(params_to_options(self.parameters))
         handle = Handle.from_csr(self.A, self.P, self.P_diff if flag_3_way else None, is_s, is_f, is_p,
                                  self.bcs_sub_pressure, opts)
-        ctx = PreconditionerCC(handle, flag_3_way)
+        ctx = PreconditionerCC(handle, flag_3_way, (self.A, self.P, self.P_diff if flag_3_way else None))
         self.pc = PC(ctx)
         self.pc.setUp()
         return self.pc

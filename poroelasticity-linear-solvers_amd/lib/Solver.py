@@ -43,7 +43,12 @@ class Solver:
         parprint("---- [Solver] Solver created in {}s".format(time() - t0_create))
 
     def set_up(self):
+        """KSPSetUp (lib/Solver.py:105-143): the PC is set up again when A / P /
+        P_diff changed since the last set_up (PETSc's operator-state check)."""
         t0_setup = time()
+        ctx = getattr(self.PC, "getPythonContext", lambda: None)()
+        if ctx is not None and hasattr(ctx, "refresh"):
+            ctx.refresh()
         parprint("---- [Solver] Solver set up in {}s".format(time() - t0_setup))
 
     def getIterationNumber(self):

@@ -82,6 +82,20 @@ class Handle:
         h._comm = comm  # destroyed after the handle
         return h
 
+    def update_matrices(self, A=None, P=None, P_diff=None):
+        """New values / patterns for the next solves (pls_update_matrices); the
+        block PC is set up again before the next solve."""
+        keep = []
+
+        def mk(M):
+            if M is None:
+                return None
+            ai, aj, av, nr, nc = N.csr_of(M)
+            keep.extend([ai, aj, av])
+            return C.byref(N.pls_csr(nr, nc, ai.ctypes.data, aj.ctypes.data, av.ctypes.data))
+
+        N.check(N.lib().pls_update_matrices(self.ptr, mk(A), mk(P), mk(P_diff)))
+
     # ------------------------------------------------------------- control --
     def set_option(self, key, value=None):
         N.check(N.lib().pls_set_option(self.ptr, str(key).encode(), None if value is None else str(value).encode()))

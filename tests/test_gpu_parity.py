@@ -409,3 +409,64 @@ def test_fieldsplit_interleaved_index_sets(gpu):
     ho = np.asarray(o.history)
     assert np.max(np.abs(h.history() - ho) / np.abs(ho)) <= RTOL_HIST
     assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+
+
+# -------------------------------------------- matrix updates (time loop) ----
+@pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
+def test_update_matrices_equals_fresh_handle(gpu, pc_type):
+    """pls_update_matrices with new values == a handle created with them."""
+    from lib.handle import Handle, params_to_options
+    s1, s2 = S.SynthSpec(2, 9), S.SynthSpec(2, 9, delta=0.2)
+    is_s, is_f, is_p = S.field_major_index_sets(s1)
+    bcs = S.bcs_sub_pressure(s1)
+    params = dict(BASE, **{"pc type": pc_type})
+    opts = dict(ILU_DB)
+    opts.update(params_to_options(params))
+    m1 = [S.matrix(s1, v) for v in (0, 1, 2)]
+    m2 = [S.matrix(s2, v) for v in (0, 1, 2)]
+    b = S.rhs(s1)
+    h = Handle.from_csr(*m1, is_s, is_f, is_p, bcs, opts)
+    h.solve(b)
+    h.update_matrices(*m2)
+    x, r = h.solve(b)
+    hf = Handle.from_csr(*m2, is_s, is_f, is_p, bcs, opts)
+    xf, rf = hf.solve(b)
+    assert r.its == rf.its and np.array_equal(h.history(), hf.history()) and np.array_equal(x, xf)
+    o = _oracle(s2, params, ILU_DB)
+    o.solve(b)
+    assert r.its == o.its
+
+
+def test_facade_set_up_detects_in_place_changes(gpu):
+    """Solver.set_up after the matrices change in place (the reference's bc.apply
+    each time step): the next solve uses the new values."""
+    from lib import options as popts
+    from lib.IndexSet import IndexSet
+    from lib.Preconditioner import Preconditioner
+    from lib.Solver import Solver
+    spec = S.SynthSpec(2, 8)
+    A, P, Pd = (S.matrix(spec, v) for v in (0, 1, 2))
+    is_s, is_f, is_p = S.field_major_index_sets(spec)
+    popts.DB.clear()
+    popts.DB.update(ILU_DB)
+    params = dict(BASE)
+    pc = Preconditioner(IndexSet((is_s, is_f, is_p), True), A, P, Pd, params, S.bcs_sub_pressure(spec)).get_pc()
+    b = S.rhs(spec)
+    solver = Solver(A, b, pc, params, None)
+    solver.create_solver(A, b, pc)
+    x = np.zeros_like(b)
+    solver.set_up()
+    solver.solve(b, x)
+    its1 = solver.getIterationNumber()
+    A.data *= 2.0
+    P.data *= 2.0
+    solver.set_up()
+    solver.solve(b, x)
+    A2, P2, Pd2 = (S.matrix(spec, v) for v in (0, 1, 2))
+    A2.data *= 2.0
+    P2.data *= 2.0
+    o2 = OracleSolver(A2, P2, Pd2, is_s, is_f, is_p, params, ILU_DB, S.bcs_sub_pressure(spec))
+    xo = o2.solve(b)
+    assert its1 > 0 and solver.getIterationNumber() == o2.its
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+    popts.DB.clear()
