@@ -1060,67 +1060,100 @@ void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, c
 }
 
 // ====================================================== SELL-64 / D16 =====
-// Compressed SELL-64: entry k of a lane's row stores a 16-bit column delta
+// Compressed SELL-64: entry k of a lane's stream stores a 16-bit column delta
 // (col_k - col_{k-1}, 1..65535) instead of an int32 column, 10 B per entry
 // instead of 12.  A delta of 0 means "start the next segment": the column is
-// the next of the row's D16_SEG absolute segment bases (the first entry, and
+// the next of the lane's D16_SEG absolute segment bases (the first entry, and
 // every jump > 65535 -- field-block changes, ghost columns).  Padding entries
 // are segment starts with value 0.0 (the base index clamps to the last one).
+// Lanes per row: a slice is 64 lanes; LPR = 1 (64 rows, lane = row) for rows
+// whose neighbours use neighbouring columns, LPR = 8 (8 rows, entry j of a row
+// on lane j % 8) for "wide" rows whose neighbours' columns lie far apart (a
+// pressure row couples to runs of ~(n_u / n_p) displacement columns): there a
+// lane-per-row gather touches 64 cache lines per instruction, 8 lanes per row
+// read 8 consecutive columns.  The LPR partial sums are combined by lane
+// shuffles (LPR = 1 rows sum in CSR order: bitwise equal to SELL-64).
 // Layout for 16-B-per-lane loads (1 KiB per wave instruction):
 //   deltas  dl[base + (k / 8) * 512 + lane * 8 + k % 8]   (one uint4 = 8 deltas)
 //   values  dv[base + (k / 2) * 128 + lane * 2 + k % 2]   (one double2 = 2 values)
-//   bases   seg[row * D16_SEG + j]                        (one int4 per lane)
-// Summation order per row is the CSR order: results equal SELL-64 bitwise.
-__global__ __launch_bounds__(TPB) void k_d16_slice_len(int64_t nrows, int64_t nslices, const int64_t *rp,
-                                                       int64_t *slen) {
+//   bases   seg[(slice * 64 + lane) * D16_SEG + j]        (one int4 per lane)
+//   slices  sfirst[slice] (first row), slpr[slice] (lanes per row)
+__device__ __forceinline__ void d16_lane(int64_t sl, int lane, const int64_t *sfirst, const int32_t *slpr,
+                                         int64_t nrows, int64_t &row, int &lpr, int &sub) {
+    lpr = slpr[sl];
+    row = sfirst[sl] + lane / lpr;
+    sub = lane % lpr;
+    if (row >= sfirst[sl + 1] || row >= nrows) row = -1;
+}
+
+__global__ __launch_bounds__(TPB) void k_d16_slice_len(int64_t nslices, const int64_t *sfirst, const int32_t *slpr,
+                                                       const int64_t *rp, int64_t nrows, int64_t *slen) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl > nslices) return;
     if (sl == nslices) { if (lane == 0) slen[nslices] = 0; return; }
-    const int64_t row = sl * 64 + lane;
-    int64_t len = row < nrows ? rp[row + 1] - rp[row] : 0;
+    int64_t row;
+    int lpr, sub;
+    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub);
+    const int64_t len = row >= 0 ? rp[row + 1] - rp[row] : 0;
+    int64_t mine = len > sub ? (len - sub + lpr - 1) / lpr : 0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const int64_t t = __shfl_xor(len, o);
-        len = t > len ? t : len;
+        const int64_t t = __shfl_xor(mine, o);
+        mine = t > mine ? t : mine;
     }
-    if (lane == 0) slen[sl] = 64 * ((len + 7) & ~(int64_t)7);
+    if (lane == 0) slen[sl] = 64 * ((mine + 7) & ~(int64_t)7);
 }
 
-// segments each row needs; *maxseg = max over rows
-__global__ __launch_bounds__(TPB) void k_d16_count(int64_t nrows, const int64_t *rp, const int32_t *ci,
+// segments each lane's entry stream needs; *maxseg = max over lanes
+__global__ __launch_bounds__(TPB) void k_d16_count(int64_t nslices, const int64_t *sfirst, const int32_t *slpr,
+                                                   const int64_t *rp, const int32_t *ci, int64_t nrows,
                                                    int32_t *maxseg) {
-    const int64_t row = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (row >= nrows) return;
-    const int64_t s = rp[row], e = rp[row + 1];
-    int nseg = 0;
-    for (int64_t k = s; k < e; ++k)
-        if (k == s || (int64_t)ci[k] - (int64_t)ci[k - 1] > 65535 || ci[k] <= ci[k - 1]) ++nseg;
-    if (nseg > 0) atomicMax(maxseg, nseg);
-}
-
-__global__ __launch_bounds__(TPB) void k_d16_fill(int64_t nrows, int64_t nslices, const int64_t *rp,
-                                                  const int32_t *ci, const double *val, const int64_t *sptr,
-                                                  uint16_t *dl, double *dv, int32_t *seg) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl >= nslices) return;
-    const int64_t row = sl * 64 + lane;
+    int64_t row;
+    int lpr, sub;
+    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub);
+    if (row < 0) return;
+    const int64_t s = rp[row], e = rp[row + 1];
+    int nseg = 0;
+    int64_t last = -1;
+    for (int64_t k = s + sub; k < e; k += lpr) {
+        const int64_t c = ci[k];
+        if (last < 0 || c - last > 65535 || c <= last) ++nseg;
+        last = c;
+    }
+    if (nseg > 0) atomicMax(maxseg, nseg);
+}
+
+__global__ __launch_bounds__(TPB) void k_d16_fill(int64_t nslices, const int64_t *sfirst, const int32_t *slpr,
+                                                  const int64_t *rp, const int32_t *ci, const double *val,
+                                                  int64_t nrows, const int64_t *sptr, uint16_t *dl, double *dv,
+                                                  int32_t *seg) {
+    const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (sl >= nslices) return;
+    int64_t row;
+    int lpr, sub;
+    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub);
     const int64_t base = sptr[sl];
     const int64_t L = (sptr[sl + 1] - base) >> 6;
-    const int64_t s0 = row < nrows ? rp[row] : 0;
-    const int64_t len = row < nrows ? rp[row + 1] - s0 : 0;
+    const int64_t s0 = row >= 0 ? rp[row] : 0;
+    const int64_t len = row >= 0 ? rp[row + 1] - s0 : 0;
+    const int64_t slot = sl * 64 + lane;
     int nseg = 0;
     int32_t last = 0;
     for (int64_t k = 0; k < L; ++k) {
+        const int64_t j = k * lpr + sub;  // this lane's k-th entry of the row
         uint16_t d = 0;
         double v = 0.0;
-        if (k < len) {
-            const int32_t c = ci[s0 + k];
-            v = val[s0 + k];
+        if (j < len) {
+            const int32_t c = ci[s0 + j];
+            v = val[s0 + j];
             const int64_t gap = (int64_t)c - (int64_t)last;
             if (k == 0 || gap > 65535 || gap <= 0) {
-                seg[row * D16_SEG + nseg++] = c;
+                seg[slot * D16_SEG + nseg++] = c;
             } else {
                 d = (uint16_t)gap;
             }
@@ -1129,8 +1162,14 @@ __global__ __launch_bounds__(TPB) void k_d16_fill(int64_t nrows, int64_t nslices
         dl[base + (k >> 3) * 512 + lane * 8 + (k & 7)] = d;
         dv[base + (k >> 1) * 128 + lane * 2 + (k & 1)] = v;
     }
-    if (nseg == 0) seg[row * D16_SEG + nseg++] = 0;
-    for (int j = nseg; j < D16_SEG; ++j) seg[row * D16_SEG + j] = seg[row * D16_SEG + nseg - 1];
+    if (nseg == 0) seg[slot * D16_SEG + nseg++] = 0;
+    for (int j = nseg; j < D16_SEG; ++j) seg[slot * D16_SEG + j] = seg[slot * D16_SEG + nseg - 1];
+}
+
+// first column of every row (-1: empty row) -- input of the host slice plan
+__global__ __launch_bounds__(TPB) void k_first_col(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *c0) {
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (r < nrows) c0[r] = rp[r + 1] > rp[r] ? ci[rp[r]] : -1;
 }
 
 typedef int32_t d16_i4 __attribute__((ext_vector_type(4)));
@@ -1139,6 +1178,8 @@ typedef double d16_d2 __attribute__((ext_vector_type(2)));
 
 template <int G2, int TAG, bool HALO>
 __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *__restrict__ sptr,
+                                                  const int64_t *__restrict__ sfirst,
+                                                  const int32_t *__restrict__ slpr,
                                                   const uint16_t *__restrict__ dl, const double *__restrict__ dv,
                                                   const int32_t *__restrict__ seg, const double *__restrict__ x,
                                                   double *__restrict__ y, double alpha, double beta,
@@ -1150,8 +1191,10 @@ __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices
     if (sl >= nslices) return;
     const int64_t base = sptr[sl];
     const int64_t L = (sptr[sl + 1] - base) >> 6;  // multiple of 8
-    const int64_t row = sl * 64 + lane;
-    const d16_i4 sb = __builtin_nontemporal_load(reinterpret_cast<const d16_i4 *>(seg) + row);
+    const int lpr = slpr[sl];
+    const int64_t r0 = sfirst[sl], r1 = sfirst[sl + 1];
+    const int64_t row = r0 + lane / lpr;
+    const d16_i4 sb = __builtin_nontemporal_load(reinterpret_cast<const d16_i4 *>(seg) + sl * 64 + lane);
     const d16_u4 *dp = reinterpret_cast<const d16_u4 *>(dl + base) + lane;
     const d16_d2 *vp = reinterpret_cast<const d16_d2 *>(dv + base) + lane;
     int32_t col = 0;
@@ -1189,52 +1232,61 @@ __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices
             }
         }
     }
-    if (row < nrows) {
+    if (lpr > 1) {  // wave-uniform: combine the LPR partial sums of a row
+        for (int o = 1; o < lpr; o <<= 1) acc += __shfl_xor(acc, o);
+        if (lane % lpr) return;
+    }
+    if (row < r1) {
         double r = alpha * acc;
         if (beta != 0.0) r += beta * z[row];
         y[row] = r;
     }
 }
 
-void launch_d16_slice_len(int64_t nrows, const int64_t *rp, int64_t *slen, hipStream_t st) {
-    const int64_t ns = sell_nslices(nrows);
-    k_d16_slice_len<<<grid_for((ns + 1) * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, slen);
+void launch_d16_slice_len(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
+                          int64_t nrows, int64_t *slen, hipStream_t st) {
+    k_d16_slice_len<<<grid_for((nslices + 1) * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, nrows, slen);
 }
-void launch_d16_count(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *maxseg, hipStream_t st) {
-    if (nrows > 0) k_d16_count<<<grid_for(nrows, TPB), TPB, 0, st>>>(nrows, rp, ci, maxseg);
+void launch_d16_count(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
+                      const int32_t *ci, int64_t nrows, int32_t *maxseg, hipStream_t st) {
+    if (nslices > 0)
+        k_d16_count<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, ci, nrows, maxseg);
 }
-void launch_d16_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const double *val, const int64_t *sptr,
-                     uint16_t *dl, double *dv, int32_t *seg, hipStream_t st) {
-    const int64_t ns = sell_nslices(nrows);
-    if (ns > 0) k_d16_fill<<<grid_for(ns * 64, TPB), TPB, 0, st>>>(nrows, ns, rp, ci, val, sptr, dl, dv, seg);
+void launch_d16_fill(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
+                     const int32_t *ci, const double *val, int64_t nrows, const int64_t *sptr, uint16_t *dl,
+                     double *dv, int32_t *seg, hipStream_t st) {
+    if (nslices > 0)
+        k_d16_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, ci, val, nrows, sptr, dl,
+                                                                dv, seg);
+}
+void launch_first_col(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *c0, hipStream_t st) {
+    if (nrows > 0) k_first_col<<<grid_for(nrows, TPB), TPB, 0, st>>>(nrows, rp, ci, c0);
 }
 template <int G2>
-static void d16_dispatch(unsigned g, hipStream_t st, int64_t nrows, int64_t ns, const int64_t *sptr, const uint16_t *dl,
-                         const double *dv, const int32_t *seg, const double *x, double *y, double alpha, double beta,
-                         const double *z, int tag, const double *ghost, int32_t nl) {
+static void d16_dispatch(unsigned g, hipStream_t st, int64_t nrows, int64_t ns, const int64_t *sptr,
+                         const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
+                         const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
+                         int tag, const double *ghost, int32_t nl) {
     if (ghost) {
-        if (tag) k_d16_spmv<G2, 1, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-        else k_d16_spmv<G2, 0, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        if (tag) k_d16_spmv<G2, 1, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        else k_d16_spmv<G2, 0, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
     } else {
-        if (tag) k_d16_spmv<G2, 1, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-        else k_d16_spmv<G2, 0, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        if (tag) k_d16_spmv<G2, 1, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        else k_d16_spmv<G2, 0, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
     }
 }
 int g_d16_unroll = 4;
-void launch_d16_spmv(int64_t nrows, const int64_t *sptr, const uint16_t *dl, const double *dv, const int32_t *seg,
-                     const double *x, double *y, double alpha, double beta, const double *z, int tag,
-                     const double *ghost, int64_t nlocal, hipStream_t st) {
-    const int64_t ns = sell_nslices(nrows);
-    if (ns <= 0) return;
-    const unsigned g = grid_for(ns, TPB / 64);
+void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
+                     const uint16_t *dl, const double *dv, const int32_t *seg, const double *x, double *y,
+                     double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
+                     hipStream_t st) {
+    if (nslices <= 0) return;
+    const unsigned g = grid_for(nslices, TPB / 64);
     const int32_t nl = (int32_t)nlocal;
     switch (g_d16_unroll) {
-        case 1: d16_dispatch<1>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        case 3: d16_dispatch<3>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        case 4: d16_dispatch<4>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        case 6: d16_dispatch<6>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        case 8: d16_dispatch<8>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        default: d16_dispatch<2>(g, st, nrows, ns, sptr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        case 1: d16_dispatch<1>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        case 2: d16_dispatch<2>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        default: d16_dispatch<4>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
     }
 }
 

@@ -120,16 +120,21 @@ void launch_sell_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const
 void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, const double *sval, const double *x,
                       double *y, double alpha, double beta, const double *z, int tag, const double *ghost,
                       int64_t nlocal, hipStream_t st);
-// SELL-64 / D16 (16-bit column deltas, D16_SEG segment bases per row)
+// SELL-64 / D16 (16-bit column deltas, D16_SEG segment bases per lane, 1 or 8 lanes per row)
 constexpr int D16_SEG = 4;
 extern int g_d16_unroll;  // entries per lane in flight / 8 (tuning knob, option pls.d16_unroll)
-void launch_d16_slice_len(int64_t nrows, const int64_t *rp, int64_t *slen /* nslices+1 */, hipStream_t st);
-void launch_d16_count(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *maxseg, hipStream_t st);
-void launch_d16_fill(int64_t nrows, const int64_t *rp, const int32_t *ci, const double *val, const int64_t *sptr,
-                     uint16_t *dl, double *dv, int32_t *seg, hipStream_t st);
-void launch_d16_spmv(int64_t nrows, const int64_t *sptr, const uint16_t *dl, const double *dv, const int32_t *seg,
-                     const double *x, double *y, double alpha, double beta, const double *z, int tag,
-                     const double *ghost, int64_t nlocal, hipStream_t st);
+void launch_d16_slice_len(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
+                          int64_t nrows, int64_t *slen /* nslices+1 */, hipStream_t st);
+void launch_d16_count(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
+                      const int32_t *ci, int64_t nrows, int32_t *maxseg, hipStream_t st);
+void launch_d16_fill(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
+                     const int32_t *ci, const double *val, int64_t nrows, const int64_t *sptr, uint16_t *dl,
+                     double *dv, int32_t *seg, hipStream_t st);
+void launch_first_col(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *c0, hipStream_t st);
+void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
+                     const uint16_t *dl, const double *dv, const int32_t *seg, const double *x, double *y,
+                     double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
+                     hipStream_t st);
 
 // Level-aligned SELL-64 triangular factors (see kernels.hip)
 void launch_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *slot_len, const int64_t *rp,

@@ -116,36 +116,93 @@ void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_
     dst.max_row = max_row_of(dst.rp, nl, c);
 }
 
+// Slice plan of the D16 layout: per 64-row group, 8 lanes per row when the
+// group's rows are "wide" (first columns of neighbouring rows more than 4
+// apart on average, rows of 16+ entries: a lane-per-row gather would touch a
+// cache line per lane), else lane = row.
+static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<int32_t> &slpr, Ctx &c) {
+    const int64_t n = M.nrows;
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> c0(n);
+    DBuf<int32_t> dc0(std::max<int64_t>(n, 1));
+    launch_first_col(n, M.rp.p, M.ci.p, dc0.p, c.st);
+    HIPCHK(hipMemcpyAsync(rp.data(), M.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipMemcpyAsync(c0.data(), dc0.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    sfirst.clear();
+    slpr.clear();
+    for (int64_t r = 0; r < n; r += 64) {
+        bool wide = false;
+        if (r + 64 <= n && c0[r] >= 0 && c0[r + 63] >= 0) {
+            const int64_t spread = (int64_t)c0[r + 63] - (int64_t)c0[r];
+            const int64_t avg = (rp[r + 64] - rp[r]) / 64;
+            wide = spread > 4 * 63 && avg >= 16;
+        }
+        if (wide) {
+            for (int q = 0; q < 8; ++q) {
+                sfirst.push_back(r + 8 * q);
+                slpr.push_back(8);
+            }
+        } else {
+            sfirst.push_back(r);
+            slpr.push_back(1);
+        }
+    }
+    sfirst.push_back(n);
+}
+
 void build_sell(DevCSR &M, Ctx &c) {
     if (M.sell || M.nrows == 0) return;
     auto S = std::make_unique<DevSELL>();
-    S->nslices = sell_nslices(M.nrows);
     if (c.sell_d16 && M.nnz > 0) {
+        std::vector<int64_t> sf;
+        std::vector<int32_t> lp;
+        d16_plan(M, sf, lp, c);
+        const int64_t ns = (int64_t)lp.size();
+        S->sfirst.alloc(ns + 1);
+        S->slpr.alloc(std::max<int64_t>(ns, 1));
+        HIPCHK(hipMemcpyAsync(S->sfirst.p, sf.data(), sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, c.st));
+        HIPCHK(hipMemcpyAsync(S->slpr.p, lp.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, c.st));
         DBuf<int32_t> mx(1);
         HIPCHK(hipMemsetAsync(mx.p, 0, sizeof(int32_t), c.st));
-        launch_d16_count(M.nrows, M.rp.p, M.ci.p, mx.p, c.st);
+        launch_d16_count(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.ci.p, M.nrows, mx.p, c.st);
         int32_t h = 0;
         HIPCHK(hipMemcpyAsync(&h, mx.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
         c.sync();
         S->d16 = h <= D16_SEG;
+        if (S->d16) {
+            S->nslices = ns;
+            for (int32_t l : lp) S->wide_slices += (l > 1);
+            DBuf<int64_t> slen(ns + 1);
+            launch_d16_slice_len(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.nrows, slen.p, c.st);
+            S->sptr.alloc(ns + 1);
+            c.ensure_scan(ns);
+            exclusive_scan_i64(slen.p, S->sptr.p, ns, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
+            HIPCHK(hipMemcpyAsync(&S->stored, S->sptr.p + ns, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
+            c.sync();
+            S->val.alloc(std::max<int64_t>(S->stored, 2));
+            S->dl.alloc(std::max<int64_t>(S->stored, 8));
+            S->seg.alloc(ns * 64 * D16_SEG);
+            launch_d16_fill(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.ci.p, M.val.p, M.nrows, S->sptr.p, S->dl.p,
+                            S->val.p, S->seg.p, c.st);
+            HIPCHK(hipGetLastError());
+            c.sync();
+            M.sell = std::move(S);
+            return;
+        }
+        S = std::make_unique<DevSELL>();
     }
+    S->nslices = sell_nslices(M.nrows);
     DBuf<int64_t> slen(S->nslices + 1);
-    if (S->d16) launch_d16_slice_len(M.nrows, M.rp.p, slen.p, c.st);
-    else launch_sell_slice_len(M.nrows, M.rp.p, slen.p, c.st);
+    launch_sell_slice_len(M.nrows, M.rp.p, slen.p, c.st);
     S->sptr.alloc(S->nslices + 1);
     c.ensure_scan(S->nslices);
     exclusive_scan_i64(slen.p, S->sptr.p, S->nslices, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
     HIPCHK(hipMemcpyAsync(&S->stored, S->sptr.p + S->nslices, sizeof(int64_t), hipMemcpyDeviceToHost, c.st));
     c.sync();
     S->val.alloc(std::max<int64_t>(S->stored, 2));
-    if (S->d16) {
-        S->dl.alloc(std::max<int64_t>(S->stored, 8));
-        S->seg.alloc(S->nslices * 64 * D16_SEG);
-        launch_d16_fill(M.nrows, M.rp.p, M.ci.p, M.val.p, S->sptr.p, S->dl.p, S->val.p, S->seg.p, c.st);
-    } else {
-        S->col.alloc(std::max<int64_t>(S->stored, 1));
-        launch_sell_fill(M.nrows, M.rp.p, M.ci.p, M.val.p, S->sptr.p, S->col.p, S->val.p, c.st);
-    }
+    S->col.alloc(std::max<int64_t>(S->stored, 1));
+    launch_sell_fill(M.nrows, M.rp.p, M.ci.p, M.val.p, S->sptr.p, S->col.p, S->val.p, c.st);
     HIPCHK(hipGetLastError());
     c.sync();
     M.sell = std::move(S);
@@ -163,8 +220,9 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
         if (!M.sell) throw Error("distributed matrix without SELL layout");
     }
     if (M.sell && M.sell->d16) {
-        launch_d16_spmv(M.nrows, M.sell->sptr.p, M.sell->dl.p, M.sell->val.p, M.sell->seg.p, x, y, alpha, beta, z,
-                        M.tag, ghost, nlocal, c.st);
+        const DevSELL &S = *M.sell;
+        launch_d16_spmv(M.nrows, S.nslices, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, x, y, alpha,
+                        beta, z, M.tag, ghost, nlocal, c.st);
         return;
     }
     if (M.sell) {

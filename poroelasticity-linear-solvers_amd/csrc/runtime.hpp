@@ -86,9 +86,11 @@ struct DevSELL {
     DBuf<int32_t> col;
     DBuf<double> val;
     DBuf<uint16_t> dl;
-    DBuf<int32_t> seg;
+    DBuf<int32_t> seg, slpr;  // D16: segment bases per lane, lanes per row per slice
+    DBuf<int64_t> sfirst;     // D16: first row of each slice (nslices + 1)
+    int64_t wide_slices = 0;  // D16 slices with 8 lanes per row
     int64_t bytes() const {  // bytes one product streams from the matrix
-        return d16 ? stored * 10 + nslices * 64 * 16 + (nslices + 1) * 8 : stored * 12 + (nslices + 1) * 8;
+        return d16 ? stored * 10 + nslices * (64 * 16 + 20) + 8 : stored * 12 + (nslices + 1) * 8;
     }
 };
 
