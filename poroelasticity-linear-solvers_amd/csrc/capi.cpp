@@ -466,6 +466,10 @@ struct Handle {
         inner_pc = opt.str("pls.inner_pc_type", "hypre");
         timers.enabled = opt.flag("pls.timers", true);
         ctx.sell_d16 = opt.flag("pls.sell_d16", true);
+        ctx.d16_wide_lpr = (int)opt.integer("pls.d16_wide_lpr", 8);
+        if (ctx.d16_wide_lpr != 1 && ctx.d16_wide_lpr != 2 && ctx.d16_wide_lpr != 4 && ctx.d16_wide_lpr != 8 &&
+            ctx.d16_wide_lpr != 16 && ctx.d16_wide_lpr != 32 && ctx.d16_wide_lpr != 64)
+            throw Error("pls.d16_wide_lpr must be a power of two <= 64");
         g_d16_unroll = (int)opt.integer("pls.d16_unroll", 4);
     }
 };

@@ -139,9 +139,10 @@ static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<
             wide = spread > 4 * 63 && avg >= 16;
         }
         if (wide) {
-            for (int q = 0; q < 8; ++q) {
-                sfirst.push_back(r + 8 * q);
-                slpr.push_back(8);
+            const int l = c.d16_wide_lpr;
+            for (int q = 0; q < l; ++q) {
+                sfirst.push_back(r + (64 / l) * q);
+                slpr.push_back(l);
             }
         } else {
             sfirst.push_back(r);
