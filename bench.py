@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--blocks-fp", type=int, default=264)
     ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-copy-probe", action="store_true", help="skip the device-copy bandwidth probe")
     ap.add_argument("--cpu-N", type=int, default=30)  # ~10-15 s of single-thread oracle work
     ap.add_argument("--cpu-maxit", type=int, default=100)
     ap.add_argument("--sell-d16", type=int, default=1, help="1: SELL-64/D16 SpMV layout (16-bit column deltas)")
@@ -200,6 +201,23 @@ def main():
     fmt_bytes = mat_bytes + 8.0 * n + 8.0 * n  # + x once + y once
     h.rhs_device(7, d_b.p)
 
+    # achievable streaming bandwidth on this box: a 4 GiB
+    # device-to-device copy through torch, read + write bytes / time
+    copy_gbs = None
+    if rank == 0 and not args.no_copy_probe:
+        import torch
+        src = torch.empty(1 << 29, dtype=torch.float64, device=f"cuda:{local}")
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            dst.copy_(src)
+        e1.record()
+        e1.synchronize()
+        copy_gbs = 2 * src.numel() * 8 * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        del src, dst
+
     # HBM traffic of the same kernel from the committed PMC passes (tools/pmc.sh)
     traffic, traffic_src = None, None
     kname = ("void pls::k_d16_spmv<4, 1, false>" if d16 else "void pls::k_sell_spmv<8, 1, false>")
@@ -238,6 +256,7 @@ def main():
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "copy_gbs_measured": copy_gbs,
                          "kernel": ("k_d16_spmv<4,1,false>" if d16 else "k_sell_spmv<8,1,false>") + " (y = A x, outer MatMult)",
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_s": spmv_avg,
                          "isolated_spmv_gbs": alg_bytes / iso / 1e9,

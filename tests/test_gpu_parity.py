@@ -70,7 +70,7 @@ def _self_sensitivity(spec, params, db, b, ho, eps=1e-15, seeds=4):
     return worst
 
 
-def _compare_solve(spec, upd=None, db=None, sensitivity=False):
+def _compare_solve(spec, upd=None, db=None, sensitivity=False, b=None):
     """sensitivity=True: for configurations whose histories amplify rounding (a
     nonlinear PC such as inner Anderson mixing inside non-flexible GMRES), the
     history bound is 10x the oracle's own deviation under 1e-15 relative
@@ -79,7 +79,7 @@ def _compare_solve(spec, upd=None, db=None, sensitivity=False):
     params = dict(BASE)
     params.update(upd or {})
     db = dict(ILU_DB if db is None else db)
-    b = S.rhs(spec)
+    b = S.rhs(spec) if b is None else b
     o = _oracle(spec, params, db)
     xo = o.solve(b)
     h = _handle(spec, params, db)
@@ -470,3 +470,38 @@ def test_facade_set_up_detects_in_place_changes(gpu):
     assert its1 > 0 and solver.getIterationNumber() == o2.its
     assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
     popts.DB.clear()
+
+
+# ------------------------------------------------------------ edge cases ----
+@pytest.mark.parametrize("solver", ["gmres", "aar"])
+def test_zero_rhs(gpu, solver):
+    """b = 0: x = 0 without iterating (GMRES: ||r0|| = 0 -> CONVERGED_ATOL; AAR:
+    the first residual already meets atol), as in the oracle."""
+    spec = S.SynthSpec(2, 6)
+    params = dict(BASE, **{"solver type": solver})
+    b = np.zeros(spec.n)
+    o = _oracle(spec, params, ILU_DB)
+    xo = o.solve(b)
+    h = _handle(spec, params, ILU_DB)
+    x, r = h.solve(b)
+    assert r.its == o.its and r.reason == o.reason
+    assert not np.any(x) and not np.any(xo)
+
+
+@pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
+def test_smallest_system(gpu, pc_type):
+    """2-D N=1: 18 + 18 + 4 unknowns, slices far from full."""
+    _compare_solve(S.SynthSpec(2, 1), {"pc type": pc_type})
+
+
+def test_rtol_met_by_initial_residual(gpu):
+    _compare_solve(S.SynthSpec(2, 6), {"solver rtol": 2.0, "solver atol": 0.0})
+
+
+@pytest.mark.parametrize("nb", [1, 7, 64])
+def test_bjacobi_block_counts(gpu, nb):
+    db = dict(ILU_DB)
+    for pre in ("s_", "fp_"):
+        db[pre + "pc_type"] = "bjacobi"
+        db[pre + "pc_bjacobi_blocks"] = str(nb)
+    _compare_solve(S.SynthSpec(2, 7), db=db)
