@@ -470,7 +470,7 @@ struct Handle {
         if (ctx.d16_wide_lpr != 1 && ctx.d16_wide_lpr != 2 && ctx.d16_wide_lpr != 4 && ctx.d16_wide_lpr != 8 &&
             ctx.d16_wide_lpr != 16 && ctx.d16_wide_lpr != 32 && ctx.d16_wide_lpr != 64)
             throw Error("pls.d16_wide_lpr must be a power of two <= 64");
-        g_d16_unroll = (int)opt.integer("pls.d16_unroll", 4);
+        ctx.d16_unroll = (int)opt.integer("pls.d16_unroll", 4);
     }
 };
 

@@ -1275,15 +1275,14 @@ static void d16_dispatch(unsigned g, hipStream_t st, int64_t nrows, int64_t ns, 
         else k_d16_spmv<G2, 0, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
     }
 }
-int g_d16_unroll = 4;
 void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
                      const uint16_t *dl, const double *dv, const int32_t *seg, const double *x, double *y,
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
-                     hipStream_t st) {
+                     int unroll, hipStream_t st) {
     if (nslices <= 0) return;
     const unsigned g = grid_for(nslices, TPB / 64);
     const int32_t nl = (int32_t)nlocal;
-    switch (g_d16_unroll) {
+    switch (unroll) {
         case 1: d16_dispatch<1>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
         case 2: d16_dispatch<2>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
         default: d16_dispatch<4>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;

@@ -122,7 +122,6 @@ void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, c
                       int64_t nlocal, hipStream_t st);
 // SELL-64 / D16 (16-bit column deltas, D16_SEG segment bases per lane, 1 or 8 lanes per row)
 constexpr int D16_SEG = 4;
-extern int g_d16_unroll;  // entries per lane in flight / 8 (tuning knob, option pls.d16_unroll)
 void launch_d16_slice_len(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
                           int64_t nrows, int64_t *slen /* nslices+1 */, hipStream_t st);
 void launch_d16_count(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
@@ -134,7 +133,7 @@ void launch_first_col(int64_t nrows, const int64_t *rp, const int32_t *ci, int32
 void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
                      const uint16_t *dl, const double *dv, const int32_t *seg, const double *x, double *y,
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
-                     hipStream_t st);
+                     int unroll /* 8-entry groups per lane in flight: 1, 2 or 4 */, hipStream_t st);
 
 // Level-aligned SELL-64 triangular factors (see kernels.hip)
 void launch_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *slot_len, const int64_t *rp,

@@ -223,7 +223,7 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
     if (M.sell && M.sell->d16) {
         const DevSELL &S = *M.sell;
         launch_d16_spmv(M.nrows, S.nslices, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, x, y, alpha,
-                        beta, z, M.tag, ghost, nlocal, c.st);
+                        beta, z, M.tag, ghost, nlocal, c.d16_unroll, c.st);
         return;
     }
     if (M.sell) {

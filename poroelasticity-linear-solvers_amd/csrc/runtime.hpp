@@ -68,6 +68,7 @@ struct Ctx {
     double *hscal = nullptr;  // pinned host mirror
     bool sell_d16 = true;     // build SpMV layouts as SELL-64/D16 where every row fits
     int d16_wide_lpr = 8;     // lanes per row of D16 slices with wide rows (option pls.d16_wide_lpr)
+    int d16_unroll = 4;       // D16 SpMV 8-entry groups per lane in flight (option pls.d16_unroll)
     DBuf<char> scan_tmp;
     size_t scan_tmp_bytes = 0;
     Ctx();
