@@ -1,0 +1,61 @@
+"""Full-size GPU checks (BASELINE.json configs) through size-independent
+properties -- the CPU oracle cannot run these sizes in test time.
+
+* right-preconditioned GMRES's residual estimate |g_k| equals the true
+  residual ||b - A x|| (unpreconditioned norm; computed on the device) to
+  within accumulated rounding;
+* bitwise reproducibility: two solves of the same system give the same
+  history and solution (fixed-order reductions, no atomics in the Krylov path);
+* the D16 SpMV layout agrees with the int32 SELL-64 layout to 1e-13 (lane-
+  per-row slices bitwise, wide slices to summation-order rounding);
+* the solve converges (reason 2) in the iteration count recorded for this
+  build at the metric point (78 at N=59; a change flags a semantic change).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _opts(nb_s, nb_fp, extra=None):
+    o = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "s_ksp_type": "preonly", "s_pc_type": "bjacobi",
+         "s_pc_bjacobi_blocks": str(nb_s), "fp_ksp_type": "preonly", "fp_pc_type": "bjacobi",
+         "fp_pc_bjacobi_blocks": str(nb_fp), "pls.pc_type": "diagonal", "pls.solver_type": "gmres",
+         "pls.solver_rtol": "1e-6", "pls.solver_atol": "1e-8", "pls.solver_maxiter": "100",
+         "pls.inner_ksp_type": "preonly", "pls.inner_pc_type": "bjacobi"}
+    o.update(extra or {})
+    return o
+
+
+@pytest.mark.parametrize("N,nb_s,nb_fp,its", [(27, 64, 64, None), (59, 256, 264, 78)])
+def test_full_size_properties(gpu, N, nb_s, nb_fp, its):
+    import lib._native as Nt
+    from lib.handle import Handle
+    h = Handle.synthetic(3, N, 20261015, 0.05, _opts(nb_s, nb_fp))
+    n = h.n
+    b, x, r = Nt.DeviceArray(n), Nt.DeviceArray(n), Nt.DeviceArray(n)
+    h.rhs_device(7, b.p)
+    res = h.solve_device(b.p, x.p)
+    hist = h.history()
+    assert res.reason == 2
+    if its is not None:
+        assert res.its == its
+    h.matmult_device(x.p, r.p)
+    bh, rh, xh = b.download(), r.download(), x.download()
+    true = np.linalg.norm(bh - rh)
+    assert abs(true - hist[-1]) <= 1e-3 * hist[-1], (true, hist[-1])
+    assert hist[-1] <= 1e-6 * hist[0]
+    # bitwise reproducibility
+    x2 = Nt.DeviceArray(n)
+    res2 = h.solve_device(b.p, x2.p)
+    assert res2.its == res.its and np.array_equal(h.history(), hist) and np.array_equal(x2.download(), xh)
+    # D16 vs int32 SELL-64 products
+    h32 = Handle.synthetic(3, N, 20261015, 0.05, _opts(nb_s, nb_fp, {"pls.sell_d16": "0"}))
+    assert h.spmv_layout()[0] and not h32.spmv_layout()[0]
+    y32 = Nt.DeviceArray(n)
+    h32.matmult_device(x.p, y32.p)
+    assert np.max(np.abs(y32.download() - rh)) <= 1e-13 * np.max(np.abs(rh))
+    for a in (b, x, r, x2, y32):
+        a.free()
+    h.destroy()
+    h32.destroy()
