@@ -45,15 +45,19 @@ DELTA = 0.05
 
 
 def solver_options(args):
-    params = {"solver type": "gmres", "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": args.maxit,
-              "pc type": "diagonal", "inner ksp type": "preonly", "inner pc type": args.inner,
-              "inner accel order": 0}
-    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right",
-          "s_ksp_type": "preonly", "s_pc_type": args.inner,
-          "fp_ksp_type": "preonly", "fp_pc_type": args.inner}
-    if args.inner == "bjacobi":
-        db["s_pc_bjacobi_blocks"] = str(args.blocks_s)
-        db["fp_pc_bjacobi_blocks"] = str(args.blocks_fp)
+    three = args.pc_type == "diagonal 3-way"
+    params = {"solver type": args.solver, "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": args.maxit,
+              "pc type": args.pc_type, "inner ksp type": "preonly", "inner pc type": args.inner,
+              "inner accel order": 0, "AAR order": 10, "AAR p": 5, "AAR omega": 1.0, "AAR beta": 1.0}
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right"}
+    # block counts: every block solution fits one CU's LDS (<= 20480 rows)
+    blocks = {"s_": args.blocks_s, "fp_": args.blocks_fp, "f_": args.blocks_s, "p_": args.blocks_p,
+              "diff_": args.blocks_p}
+    for pre in (("s_", "f_", "p_", "diff_") if three else ("s_", "fp_")):
+        db[pre + "ksp_type"] = "preonly"
+        db[pre + "pc_type"] = args.inner
+        if args.inner == "bjacobi":
+            db[pre + "pc_bjacobi_blocks"] = str(blocks[pre])
     return params, db
 
 
@@ -66,10 +70,12 @@ def cpu_baseline(args, params, db):
     spec = S.SynthSpec(3, Ns, SEED, DELTA)
     t0 = time.perf_counter()
     A, P = S.matrix(spec, 0), S.matrix(spec, 1)
+    three = params["pc type"] == "diagonal 3-way"
+    Pd = S.matrix(spec, 2) if three else None
     is_s, is_f, is_p = S.field_major_index_sets(spec)
     p = dict(params)
     p["solver maxiter"] = args.cpu_maxit
-    o = OracleSolver(A, P, None, is_s, is_f, is_p, p, db, [])
+    o = OracleSolver(A, P, Pd, is_s, is_f, is_p, p, db, S.bcs_sub_pressure(spec) if three else [])
     b = S.rhs(spec)
     t_setup = time.perf_counter() - t0
     t1 = time.perf_counter()
@@ -80,7 +86,8 @@ def cpu_baseline(args, params, db):
     rate = o.its / dt
     return {"value": rate * n_sample / n_metric, "unit": "Krylov iters/s (scaled to the 10.33M-DoF system by DoF)",
             "cores": 1, "kind": "port",
-            "sample": (f"oracle (numpy/scipy + C kernels, 1 thread) 2-way GMRES solve of the N={Ns} 3-D "
+            "sample": (f"oracle (numpy/scipy + C kernels, 1 thread) {params['pc type']} / {params['solver type']} "
+                       f"solve of the N={Ns} 3-D "
                        f"system ({n_sample} DoF), {o.its} outer iterations in {dt:.1f}s "
                        f"(setup {t_setup:.1f}s), maxit {args.cpu_maxit}; iters/s x {n_sample}/{n_metric}"),
             "raw_iters_per_s": rate}
@@ -97,7 +104,11 @@ def main():
     # block so every block solution (<= 20480 doubles = 160 KiB) fits one CU's LDS
     ap.add_argument("--blocks-s", type=int, default=256)
     ap.add_argument("--blocks-fp", type=int, default=264)
+    ap.add_argument("--blocks-p", type=int, default=11, help="3-way p_ / diff_ blocks")
     ap.add_argument("--maxit", type=int, default=100)
+    ap.add_argument("--pc-type", default="diagonal", choices=["diagonal", "diagonal 3-way"],
+                    help="block preconditioner (the metric: 2-way 'diagonal')")
+    ap.add_argument("--solver", default="gmres", choices=["gmres", "aar"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the device-copy bandwidth probe")
     ap.add_argument("--cpu-N", type=int, default=30)  # ~10-15 s of single-thread oracle work
@@ -128,6 +139,7 @@ def main():
         N_glob = int(round(args.N * world ** (1.0 / 3.0)))
         args.blocks_s *= world
         args.blocks_fp *= world
+        args.blocks_p *= world
     params, db = solver_options(args)
     opts = dict(db)
     opts.update(params_to_options(params))
@@ -244,9 +256,12 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded SPD 3-field block system, SURVEY.md 8(d); generated in HBM)",
             "config": {
-                "workload": (f"swelling-3d-shaped 3-D N={N_glob} ({n_global} DoF): outer GMRES right-PC "
-                             f"rtol 1e-6 atol 1e-8 restart=maxit={args.maxit}, 2-way block PC, inner preonly+"
-                             f"{args.inner}" + (f"(ILU(0), {args.blocks_s}/{args.blocks_fp} blocks s/fp)" if args.inner == "bjacobi" else "")),
+                "workload": (f"swelling-3d-shaped 3-D N={N_glob} ({n_global} DoF): outer "
+                             + ("GMRES right-PC" if args.solver == "gmres" else "AAR(10, p=5)")
+                             + f" rtol 1e-6 atol 1e-8 maxit={args.maxit}, "
+                             + ("2-way" if args.pc_type == "diagonal" else "3-way") + " block PC, inner preonly+"
+                             + args.inner + (f"(ILU(0), {args.blocks_s}/{args.blocks_fp} blocks s/fp)"
+                                             if args.inner == "bjacobi" else "")),
                 "dim": 3, "N": N_glob, "dofs": n_global, "dofs_rank0": n, "nnz_A_rank0": nnz,
                 "parallelism": (f"row slabs x{world} ({args.comm})" if sharded else
                                 f"replicas x{world}" if world > 1 else "single GPU"),

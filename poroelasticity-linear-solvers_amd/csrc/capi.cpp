@@ -443,6 +443,14 @@ struct Handle {
     } aar;
     // work
     DBuf<double> t_fp, t_s, t_f, xpd, yfpd, ysd, vin, vout;
+    DBuf<double> t_s2, t_f2;              // DIFF-sweep temporaries (concurrent 3-way sweeps)
+    std::unique_ptr<Ctx> ctx2;            // second stream: the DIFF sweep runs beside the FS sweep
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    bool concurrent_3way = false;
+    ~Handle() {
+        if (ev_in) (void)hipEventDestroy(ev_in);
+        if (ev_out) (void)hipEventDestroy(ev_out);
+    }
     // result
     pls_result res{};
     std::vector<double> history;
@@ -492,6 +500,38 @@ void BlockPC::apply(const double *x, double *y, Ctx &c) {
         const double *xs = x, *xf = x + ns, *xp = x + ns + nf;
         double *ys = y, *yf = y + ns, *yp = y + ns + nf;
         double *yfd = H.yfpd.p, *ypd = H.yfpd.p + nf;
+        if (H.concurrent_3way) {
+            // FS sweep on the main stream, DIFF sweep on the second; join before the combination
+            Ctx &c2 = *H.ctx2;
+            HIPCHK(hipEventRecord(H.ev_in, c.st));
+            HIPCHK(hipStreamWaitEvent(c2.st, H.ev_in, 0));
+            launch_copy(np, xp, H.xpd.p, c2.st);                     // :172-173 BC rows of x_p zeroed
+            launch_zero_entries((int64_t)H.bcs.size(), H.dbcs.p, H.xpd.p, c2.st);
+            H.ksp_pd->solve(H.xpd.p, ypd, c2);                       // :174
+            spmv(H.Mf_p, ypd, H.t_f2.p, c2, -1.0, 1.0, xf);          // :184-185
+            H.ksp_f->solve(H.t_f2.p, yfd, c2);                       // :186
+            spmv(H.Ms_fp, yfd, H.t_s2.p, c2, -1.0, 1.0, xs);         // :198-201
+            H.ksp_s->solve(H.t_s2.p, H.ysd.p, c2);                   // :202
+            HIPCHK(hipEventRecord(H.ev_out, c2.st));
+            T.begin(T_PC_PRESS);
+            H.ksp_p->solve(xp, yp, c);                               // :170
+            T.end(T_PC_PRESS);
+            T.begin(T_PC_FLUID);
+            spmv(H.Mf_p, yp, H.t_f.p, c, -1.0, 1.0, xf);             // :180-181
+            H.ksp_f->solve(H.t_f.p, yf, c);                          // :182
+            T.end(T_PC_FLUID);
+            T.begin(T_PC_SOLID);
+            spmv(H.Ms_fp, yf, H.t_s.p, c, -1.0, 1.0, xs);            // :192-195
+            H.ksp_s->solve(H.t_s.p, ys, c);                          // :196
+            T.end(T_PC_SOLID);
+            HIPCHK(hipStreamWaitEvent(c.st, H.ev_out, 0));
+            launch_axpby(ns, 0.1, H.ysd.p, 1.0, ys, c.st);           // :207-212
+            launch_axpby(nf + np, 0.1, yfd, 1.0, yf, c.st);
+            if (H.mixer.order > 0) H.mixer.next(y, c);               // :248-249
+            T.end(T_PC_TOTAL);
+            H.pc_applies++;
+            return;
+        }
         T.begin(T_PC_PRESS);
         H.ksp_p->solve(xp, yp, c);                               // :170
         launch_copy(np, xp, H.xpd.p, c.st);                      // :172-173 BC rows of x_p zeroed
@@ -562,6 +602,26 @@ static void alloc_work(Handle &H) {
     H.ysd.alloc(std::max<int64_t>(H.ns, 1));
     H.vin.alloc(std::max<int64_t>(H.n, 1));
     H.vout.alloc(std::max<int64_t>(H.n, 1));
+    // 3-way: the FS (p -> f -> s) and DIFF sweeps are independent until the
+    // final w1/w2 combination (Preconditioner.py:150-212); with PREONLY inner
+    // solves (no host round trips) the DIFF sweep runs on a second stream.
+    // Not with several ranks: two streams would interleave halo exchanges on
+    // one communicator.
+    H.concurrent_3way = false;
+    if (H.three_way && !H.distributed && H.opt.flag("pls.concurrent_sweeps", true)) {
+        bool pre = true;
+        for (KSP *k : {H.ksp_s.get(), H.ksp_f.get(), H.ksp_p.get(), H.ksp_pd.get()}) pre = pre && k && k->type == "preonly";
+        if (pre) {
+            if (!H.ctx2) {
+                H.ctx2 = std::make_unique<Ctx>();
+                HIPCHK(hipEventCreateWithFlags(&H.ev_in, hipEventDisableTiming));
+                HIPCHK(hipEventCreateWithFlags(&H.ev_out, hipEventDisableTiming));
+            }
+            H.t_s2.alloc(std::max<int64_t>(H.ns, 1));
+            H.t_f2.alloc(std::max<int64_t>(H.nf, 1));
+            H.concurrent_3way = true;
+        }
+    }
 }
 
 static void do_setup(Handle &H) {
