@@ -62,33 +62,57 @@ def solver_options(args):
 
 
 def cpu_baseline(args, params, db):
-    """Oracle (CPU restatement) timed on host cores on a bounded sample."""
-    import numpy as np
+    """The same configuration on the host cores, timed on a bounded sample.
+
+    bench's configuration (2-way, GMRES, PREONLY + BJACOBI(ILU(0))) runs the
+    C/OpenMP restatement oracle/csrc/cpu_solver.c on all available cores
+    (SURVEY.md 8(d)'s planned baseline); other configurations fall back to the
+    single-thread Python oracle.  iters/s is scaled by DoF to the metric's
+    system (the per-iteration work is linear in n)."""
     from oracle import synthetic as S
-    from oracle.solver import OracleSolver
     Ns = args.cpu_N
     spec = S.SynthSpec(3, Ns, SEED, DELTA)
     t0 = time.perf_counter()
     A, P = S.matrix(spec, 0), S.matrix(spec, 1)
+    b = S.rhs(spec)
+    n_sample = spec.n
+    n_metric = S.SynthSpec(3, args.N).n if args.N != Ns else n_sample
+    c_path = (params["pc type"] == "diagonal" and params["solver type"] == "gmres" and args.inner == "bjacobi")
+    if c_path:
+        from oracle import native
+        try:
+            cores = len(os.sched_getaffinity(0))
+        except AttributeError:
+            cores = os.cpu_count() or 1
+        cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores) or cores))
+        t_gen = time.perf_counter() - t0
+        _, its, reason, _, t_setup, dt = native.cpu_gmres_2way(
+            A, P, spec.sizes()[0], args.blocks_s, args.blocks_fp, b, rtol=params["solver rtol"],
+            atol=params["solver atol"], maxit=args.cpu_maxit, nthreads=cores)
+        rate = its / dt
+        return {"value": rate * n_sample / n_metric,
+                "unit": "Krylov iters/s (scaled to the 10.33M-DoF system by DoF)", "cores": cores, "kind": "port",
+                "sample": (f"oracle/csrc/cpu_solver.c (C + OpenMP, {cores} threads): bench's configuration on "
+                           f"the N={Ns} 3-D system ({n_sample} DoF, {A.nnz} nnz), {its} GMRES iterations in "
+                           f"{dt:.1f}s (block setup {t_setup:.1f}s, generation {t_gen:.1f}s), reason {reason}; "
+                           f"iters/s x {n_sample}/{n_metric}"),
+                "raw_iters_per_s": rate}
+    from oracle.solver import OracleSolver
     three = params["pc type"] == "diagonal 3-way"
     Pd = S.matrix(spec, 2) if three else None
     is_s, is_f, is_p = S.field_major_index_sets(spec)
     p = dict(params)
     p["solver maxiter"] = args.cpu_maxit
     o = OracleSolver(A, P, Pd, is_s, is_f, is_p, p, db, S.bcs_sub_pressure(spec) if three else [])
-    b = S.rhs(spec)
     t_setup = time.perf_counter() - t0
     t1 = time.perf_counter()
     o.solve(b)
     dt = time.perf_counter() - t1
-    n_sample = spec.n
-    n_metric = S.SynthSpec(3, args.N).n if args.N != Ns else n_sample
     rate = o.its / dt
     return {"value": rate * n_sample / n_metric, "unit": "Krylov iters/s (scaled to the 10.33M-DoF system by DoF)",
             "cores": 1, "kind": "port",
             "sample": (f"oracle (numpy/scipy + C kernels, 1 thread) {params['pc type']} / {params['solver type']} "
-                       f"solve of the N={Ns} 3-D "
-                       f"system ({n_sample} DoF), {o.its} outer iterations in {dt:.1f}s "
+                       f"solve of the N={Ns} 3-D system ({n_sample} DoF), {o.its} outer iterations in {dt:.1f}s "
                        f"(setup {t_setup:.1f}s), maxit {args.cpu_maxit}; iters/s x {n_sample}/{n_metric}"),
             "raw_iters_per_s": rate}
 
@@ -111,7 +135,7 @@ def main():
     ap.add_argument("--solver", default="gmres", choices=["gmres", "aar"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the device-copy bandwidth probe")
-    ap.add_argument("--cpu-N", type=int, default=30)  # ~10-15 s of single-thread oracle work
+    ap.add_argument("--cpu-N", type=int, default=40)  # ~10-20 s of CPU solve on the box's cores
     ap.add_argument("--cpu-maxit", type=int, default=100)
     ap.add_argument("--sell-d16", type=int, default=1, help="1: SELL-64/D16 SpMV layout (16-bit column deltas)")
     ap.add_argument("--d16-unroll", type=int, default=0, help="D16 SpMV: 8-entry groups per lane in flight (tuning)")

@@ -18,8 +18,8 @@ _f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
 
 def build() -> str:
     """Compile the oracle C kernels (gcc, -ffp-contract=off)."""
-    src = os.path.join(_HERE, "csrc", "oracle.c")
-    if (not os.path.exists(_LIB)) or os.path.getmtime(_LIB) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, "csrc", f) for f in ("oracle.c", "cpu_solver.c")]
+    if (not os.path.exists(_LIB)) or os.path.getmtime(_LIB) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB
 
@@ -46,6 +46,10 @@ def lib():
     L.oracle_ilu0_solve.restype = None
     L.oracle_levels.argtypes = [C.c_int64, _i64p, _i32p, C.c_int, _i32p]
     L.oracle_levels.restype = C.c_int64
+    L.cpu_gmres_2way.argtypes = [C.c_int64, C.c_int64, _i64p, _i32p, _f64p, _i64p, _i32p, _f64p, C.c_int64,
+                                 C.c_int64, C.c_double, C.c_double, C.c_int, _f64p, _f64p, C.POINTER(C.c_int),
+                                 _f64p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.cpu_gmres_2way.restype = C.c_int
     _lib = L
     return L
 
@@ -94,3 +98,21 @@ def levels(M, lower: bool = True):
     lvl = np.zeros(M.shape[0], dtype=np.int32)
     nl = lib().oracle_levels(M.shape[0], rp, ci, 0 if lower else 1, lvl)
     return int(nl), lvl
+
+
+def cpu_gmres_2way(A, P, ns, nb_s, nb_fp, b, rtol=1e-6, atol=1e-8, maxit=100, nthreads=1):
+    """C/OpenMP restatement of bench.py's configuration (oracle/csrc/cpu_solver.c):
+    right-PC GMRES + 2-way block PC with PREONLY + BJACOBI(ILU(0)) inner solves
+    on a field-major system.  Returns (x, its, reason, history, t_setup, t_solve)."""
+    Ap, Ai, Av = csr_arrays(A)
+    Pp, Pi, Pv = csr_arrays(P)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros_like(b)
+    hist = np.zeros(maxit + 1)
+    reason = C.c_int(0)
+    ts, tv = C.c_double(0), C.c_double(0)
+    its = lib().cpu_gmres_2way(A.shape[0], ns, Ap, Ai, Av, Pp, Pi, Pv, nb_s, nb_fp, rtol, atol, maxit, b, x,
+                               C.byref(reason), hist, nthreads, C.byref(ts), C.byref(tv))
+    if its < 0:
+        raise RuntimeError("cpu_gmres_2way: ILU(0) failed (missing diagonal or zero pivot)")
+    return x, its, reason.value, hist[:its + 1], ts.value, tv.value

@@ -533,3 +533,28 @@ def test_fieldsplit_block_factorizations(ftype, fact):
     y = pc.apply(x)
     assert np.allclose(y[is_p], y0, rtol=1e-10, atol=1e-12)
     assert np.allclose(y[is_f], y1, rtol=1e-10, atol=1e-12)
+
+
+# ------------------------------------------------- C/OpenMP CPU baseline ----
+@pytest.mark.parametrize("threads", [1, 4])
+def test_cpu_baseline_solver_matches_oracle(threads):
+    """oracle/csrc/cpu_solver.c (bench.py's cpu_baseline) == the Python oracle
+    on bench's configuration: same iteration count and reason, history to
+    rounding (its inner products are OpenMP reductions)."""
+    spec = S.SynthSpec(2, 12)
+    A, P = S.matrix(spec, 0), S.matrix(spec, 1)
+    ns = spec.sizes()[0]
+    is_s, is_f, is_p = S.field_major_index_sets(spec)
+    params = {"solver type": "gmres", "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": 100,
+              "pc type": "diagonal", "inner ksp type": "preonly", "inner pc type": "bjacobi",
+              "inner accel order": 0}
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "s_ksp_type": "preonly",
+          "s_pc_type": "bjacobi", "s_pc_bjacobi_blocks": "5", "fp_ksp_type": "preonly",
+          "fp_pc_type": "bjacobi", "fp_pc_bjacobi_blocks": "3"}
+    o = OracleSolver(A, P, None, is_s, is_f, is_p, params, db, [])
+    b = S.rhs(spec)
+    xo = o.solve(b)
+    x, its, reason, hist, _, _ = native.cpu_gmres_2way(A, P, ns, 5, 3, b, nthreads=threads)
+    assert its == o.its and reason == o.reason
+    assert np.allclose(hist, o.history, rtol=1e-10, atol=0)
+    assert np.allclose(x, xo, rtol=1e-9, atol=1e-12)
