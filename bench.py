@@ -238,21 +238,14 @@ def main():
     h.rhs_device(7, d_b.p)
 
     # achievable streaming bandwidth on this box: a 4 GiB
-    # device-to-device copy through torch, read + write bytes / time
+    # device-to-device copy (pls_bench_copy), read + write bytes / time
     copy_gbs = None
     if rank == 0 and not args.no_copy_probe:
-        import torch
-        src = torch.empty(1 << 29, dtype=torch.float64, device=f"cuda:{local}")
-        dst = torch.empty_like(src)
-        dst.copy_(src)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            dst.copy_(src)
-        e1.record()
-        e1.synchronize()
-        copy_gbs = 2 * src.numel() * 8 * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
-        del src, dst
+        import ctypes as C
+        g, gr = C.c_double(), C.c_double()
+        Nat.check(Nat.lib().pls_bench_copy(1 << 32, 10, 0, C.byref(g)))
+        Nat.check(Nat.lib().pls_bench_copy(1 << 32, 10, 1, C.byref(gr)))
+        copy_gbs = {"copy": g.value, "read": gr.value}
 
     # HBM traffic of the same kernel from the committed PMC passes (tools/pmc.sh)
     traffic, traffic_src = None, None
@@ -295,7 +288,7 @@ def main():
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "copy_gbs_measured": copy_gbs,
+                         "stream_gbs_measured": copy_gbs,
                          "kernel": ("k_d16_spmv<4,1,false>" if d16 else "k_sell_spmv<8,1,false>") + " (y = A x, outer MatMult)",
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_s": spmv_avg,
                          "isolated_spmv_gbs": alg_bytes / iso / 1e9,

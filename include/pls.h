@@ -187,6 +187,11 @@ int pls_bench_spmv(pls_handle *h, const double *d_x, double *d_y, int32_t reps, 
  * from the matrix arrays (padding included).  Option "pls.sell_d16 0"
  * forces the int32 layout.                                                   */
 int pls_spmv_layout(pls_handle *h, int32_t *d16, int64_t *matrix_bytes);
+/* Streaming probe on the current device: per repetition `bytes` read (and,
+ * unless read_only, `bytes` written) with 16-B-per-lane nontemporal accesses;
+ * returns GB/s of bytes moved -- the achievable HBM rate beside the 8 TB/s
+ * peak.                                                     */
+int pls_bench_copy(int64_t bytes, int32_t reps, int32_t read_only, double *gbs);
 
 #ifdef __cplusplus
 }

@@ -1288,6 +1288,30 @@ int pls_update_matrices(pls_handle *hh, const pls_csr *A, const pls_csr *P, cons
     })
 }
 
+int pls_bench_copy(int64_t bytes, int32_t reps, int32_t read_only, double *gbs) {
+    PLS_TRY({
+        const int64_t n = std::max<int64_t>(bytes / 8, 2) & ~(int64_t)1;
+        DBuf<double> a(n), b(n);
+        hipStream_t st;
+        HIPCHK(hipStreamCreate(&st));
+        HIPCHK(hipMemsetAsync(a.p, 0, sizeof(double) * n, st));
+        launch_copy_probe(n, a.p, b.p, read_only ? 1 : 0, st);
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, st));
+        for (int r = 0; r < std::max(1, reps); ++r) launch_copy_probe(n, a.p, b.p, read_only ? 1 : 0, st);
+        HIPCHK(hipEventRecord(e1, st));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        *gbs = (read_only ? 1.0 : 2.0) * 8.0 * (double)n * std::max(1, reps) / (ms * 1e-3) / 1e9;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipStreamDestroy(st);
+    })
+}
+
 int pls_spmv_layout(pls_handle *hh, int32_t *d16, int64_t *matrix_bytes) {
     PLS_TRY({
         Handle &H = *reinterpret_cast<Handle *>(hh);

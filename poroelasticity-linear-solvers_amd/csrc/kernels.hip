@@ -433,6 +433,38 @@ static inline unsigned stream_grid(int64_t n) {
     return (unsigned)g;
 }
 
+// streaming probes (the achievable HBM rate): 16 B per lane,
+// four loads in flight per lane, nontemporal.  mode 0: copy (read + write),
+// mode 1: read-only (the SpMV's traffic mix is ~99 % reads)
+typedef double probe_d2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(TPB) void k_copy_probe(int64_t n2, const probe_d2 *__restrict__ x,
+                                                    probe_d2 *__restrict__ y, int mode, double *sink) {
+    const int64_t stride = (int64_t)gridDim.x * TPB;
+    probe_d2 acc = {0.0, 0.0};
+    for (int64_t i0 = (int64_t)blockIdx.x * TPB + threadIdx.x; i0 < n2; i0 += 4 * stride) {
+        probe_d2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + u * stride;
+            v[u] = i < n2 ? __builtin_nontemporal_load(x + i) : probe_d2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (mode == 0) {
+                if (i < n2) __builtin_nontemporal_store(v[u], y + i);
+            } else {
+                acc += v[u];
+            }
+        }
+    }
+    if (mode == 1 && acc.x + acc.y == 12345.678) sink[0] = acc.x;
+}
+void launch_copy_probe(int64_t n, const double *x, double *y, int mode, hipStream_t st) {
+    if (n > 1)
+        k_copy_probe<<<8192, TPB, 0, st>>>(n / 2, reinterpret_cast<const probe_d2 *>(x), reinterpret_cast<probe_d2 *>(y),
+                                            mode, y);
+}
 void launch_copy(int64_t n, const double *x, double *y, hipStream_t st) {
     if (n > 0) k_copy<<<stream_grid(n), TPB, 0, st>>>(n, x, y);
 }

@@ -53,6 +53,7 @@ void launch_spmv(int64_t nrows, int64_t nnz, const int64_t *rp, const int32_t *c
 
 // ----------------------------------------------------------------- BLAS-1 --
 void launch_copy(int64_t n, const double *x, double *y, hipStream_t st);
+void launch_copy_probe(int64_t n, const double *x, double *y, int mode /*0 copy, 1 read*/, hipStream_t st);
 void launch_set(int64_t n, double a, double *y, hipStream_t st);
 void launch_scale(int64_t n, double a, double *y, hipStream_t st);
 // y = a*x + b*y

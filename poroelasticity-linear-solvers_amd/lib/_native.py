@@ -45,6 +45,7 @@ EXPORTS = [
     "pls_get_timings", "pls_reset_timings", "pls_export_matrix", "pls_get_permutation",
     "pls_bench_spmv", "pls_rccl_unique_id", "pls_comm_create_rccl", "pls_comm_create_callback",
     "pls_comm_destroy", "pls_create_synthetic_dist", "pls_spmv_layout", "pls_update_matrices",
+    "pls_bench_copy",
 ]
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
@@ -92,6 +93,7 @@ def lib():
     L.pls_comm_create_callback.argtypes = [C.c_int, C.c_int, ALLGATHER_FN, vp, C.POINTER(vp)]
     L.pls_comm_destroy.argtypes = [vp]
     L.pls_update_matrices.argtypes = [vp, C.POINTER(pls_csr), C.POINTER(pls_csr), C.POINTER(pls_csr)]
+    L.pls_bench_copy.argtypes = [i64, i32, i32, C.POINTER(C.c_double)]
     L.pls_spmv_layout.argtypes = [vp, C.POINTER(i32), C.POINTER(i64)]
     L.pls_create_synthetic_dist.argtypes = [C.POINTER(pls_synth_spec), C.c_char_p, vp, C.POINTER(vp)]
     _lib = L
