@@ -147,6 +147,11 @@ def make_pc_of_type(t, M, db=None, prefix=""):
     if t == "bjacobi":
         return PCBJacobi(M, opt(db, prefix, "pc_bjacobi_blocks", 1, int),
                          opt(db, prefix + "sub_", "pc_type", "ilu"))
+    if t in ("gamg", "hypre"):
+        if t == "hypre" and str(db.get("pls.hypre", "gamg")) == "error":
+            raise NotImplementedError("PC type 'hypre' is not available (pls.hypre error)")
+        from .amg import PCAMG
+        return PCAMG(M, db, prefix, hypre=(t == "hypre"))
     raise NotImplementedError(f"PC type '{t}' is not restated by the oracle")
 
 

@@ -1,0 +1,419 @@
+// amg.cpp -- smoothed-aggregation algebraic multigrid (PCGAMG-like), the
+// device preconditioner behind -pc_type gamg and, by default, the stand-in for
+// -pc_type hypre (BoomerAMG is absent from this image; reference drivers
+// footing.py:73, swelling.py:70, swelling-3d.py:71 default "inner pc type" to
+// hypre, and petsc-options-inexact selects it for the s_/f_/p_ blocks).
+//
+// The algorithm is specified in oracle/amg.py (the test oracle); the setup
+// here reproduces it bit for bit -- every host sum runs in the order scipy's
+// sparsetools use (row-storage order, left to right, no contraction) and the
+// spectral estimate is rounded to float -- so the hierarchy (aggregates, P,
+// coarse operators) is identical to the oracle's and only the device V-cycle
+// rounding differs.
+//
+// Setup runs once on the host (aggregation is sequential by definition);
+// every level's A, P, R = P^T is then device resident in the SpMV layout and
+// one V-cycle is a fixed sequence of SpMVs and fused Chebyshev steps on the
+// context's stream; the coarsest level is a dense inverse (one SpMV) up to
+// 1024 rows, the device LU pipeline above that.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+
+#include "runtime.hpp"
+
+#pragma clang fp contract(off)
+
+namespace pls {
+namespace {
+
+HostCSR transpose(const HostCSR &A) {
+    HostCSR T;
+    T.nrows = A.ncols;
+    T.ncols = A.nrows;
+    T.rp.assign(A.ncols + 1, 0);
+    for (int32_t j : A.ci) ++T.rp[j + 1];
+    for (int64_t j = 0; j < A.ncols; ++j) T.rp[j + 1] += T.rp[j];
+    T.ci.resize(A.ci.size());
+    T.v.resize(A.v.size());
+    std::vector<int64_t> pos(T.rp.begin(), T.rp.end() - 1);
+    for (int64_t i = 0; i < A.nrows; ++i)
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+            const int64_t p = pos[A.ci[k]]++;
+            T.ci[p] = (int32_t)i;
+            T.v[p] = A.v[k];
+        }
+    return T;  // rows ascending (i visited in order)
+}
+
+// C = A B, row i accumulating over A's row in storage order (csr_matmat);
+// exact zero sums dropped; columns sorted.
+HostCSR spgemm(const HostCSR &A, const HostCSR &B) {
+    HostCSR C;
+    C.nrows = A.nrows;
+    C.ncols = B.ncols;
+    C.rp.assign(1, 0);
+    std::vector<double> acc(B.ncols, 0.0);
+    std::vector<char> mark(B.ncols, 0);
+    std::vector<int32_t> cols;
+    for (int64_t i = 0; i < A.nrows; ++i) {
+        cols.clear();
+        for (int64_t kk = A.rp[i]; kk < A.rp[i + 1]; ++kk) {
+            const int32_t k = A.ci[kk];
+            const double a = A.v[kk];
+            for (int64_t jj = B.rp[k]; jj < B.rp[k + 1]; ++jj) {
+                const int32_t j = B.ci[jj];
+                if (!mark[j]) {
+                    mark[j] = 1;
+                    acc[j] = 0.0;
+                    cols.push_back(j);
+                }
+                acc[j] += a * B.v[jj];
+            }
+        }
+        std::sort(cols.begin(), cols.end());
+        for (int32_t j : cols) {
+            if (acc[j] != 0.0) {
+                C.ci.push_back(j);
+                C.v.push_back(acc[j]);
+            }
+            mark[j] = 0;
+        }
+        C.rp.push_back((int64_t)C.ci.size());
+    }
+    return C;
+}
+
+// oracle/amg.py aggregate(): symmetric strength graph W = |A| + |A|^T (off
+// diagonal, zero weights dropped), three deterministic passes.
+std::vector<int32_t> aggregate(const HostCSR &A, double theta, int32_t &na) {
+    const int64_t n = A.nrows;
+    std::vector<double> d(n, 0.0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
+            if (A.ci[k] == i) d[i] = std::fabs(A.v[k]);
+    const HostCSR T = transpose(A);
+    std::vector<int64_t> wp(n + 1, 0);
+    std::vector<int32_t> wj;
+    std::vector<double> ww;
+    wj.reserve(A.ci.size());
+    ww.reserve(A.ci.size());
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t a = A.rp[i], ae = A.rp[i + 1], t = T.rp[i], te = T.rp[i + 1];
+        while (a < ae || t < te) {
+            int32_t j;
+            double w;
+            if (t >= te || (a < ae && A.ci[a] < T.ci[t])) {
+                j = A.ci[a];
+                w = std::fabs(A.v[a]) + 0.0;
+                ++a;
+            } else if (a >= ae || T.ci[t] < A.ci[a]) {
+                j = T.ci[t];
+                w = 0.0 + std::fabs(T.v[t]);
+                ++t;
+            } else {
+                j = A.ci[a];
+                w = std::fabs(A.v[a]) + std::fabs(T.v[t]);
+                ++a;
+                ++t;
+            }
+            if (j == i || w == 0.0) continue;
+            if (!(w > 2.0 * theta * std::sqrt(d[i] * d[j]))) continue;
+            wj.push_back(j);
+            ww.push_back(w);
+        }
+        wp[i + 1] = (int64_t)wj.size();
+    }
+    std::vector<int32_t> agg(n, -1);
+    na = 0;
+    for (int64_t i = 0; i < n; ++i) {  // pass 1
+        if (agg[i] >= 0) continue;
+        bool free_nb = true;
+        for (int64_t k = wp[i]; k < wp[i + 1] && free_nb; ++k) free_nb = agg[wj[k]] < 0;
+        if (!free_nb) continue;
+        agg[i] = na;
+        for (int64_t k = wp[i]; k < wp[i + 1]; ++k) agg[wj[k]] = na;
+        ++na;
+    }
+    const std::vector<int32_t> agg1 = agg;
+    for (int64_t i = 0; i < n; ++i) {  // pass 2
+        if (agg1[i] >= 0) continue;
+        int64_t best = -1;
+        double bw = -1.0;
+        for (int64_t k = wp[i]; k < wp[i + 1]; ++k)
+            if (agg1[wj[k]] >= 0 && ww[k] > bw) {
+                best = wj[k];
+                bw = ww[k];
+            }
+        if (best >= 0) agg[i] = agg1[best];
+    }
+    for (int64_t i = 0; i < n; ++i)  // pass 3
+        if (agg[i] < 0) agg[i] = na++;
+    return agg;
+}
+
+std::vector<double> jacobi_dinv(const HostCSR &A) {
+    std::vector<double> dinv(A.nrows, 1.0);
+    for (int64_t i = 0; i < A.nrows; ++i)
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
+            if (A.ci[k] == i && A.v[k] != 0.0) dinv[i] = 1.0 / A.v[k];
+    return dinv;
+}
+
+// power iteration on D^-1 A (oracle power_lambda), rounded to float so that
+// the hierarchy does not depend on the norms' summation order
+double power_lambda(const HostCSR &A, const std::vector<double> &dinv, int steps) {
+    const int64_t n = A.nrows;
+    std::vector<double> v(n, 1.0), w(n);
+    double lam = 1.0;
+    for (int s = 0; s < steps; ++s) {
+        double nw = 0.0, nv = 0.0;
+        for (int64_t i = 0; i < n; ++i) {
+            double acc = 0.0;
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) acc += A.v[k] * v[A.ci[k]];
+            w[i] = dinv[i] * acc;
+            nw += w[i] * w[i];
+            nv += v[i] * v[i];
+        }
+        nw = std::sqrt(nw);
+        nv = std::sqrt(nv);
+        if (nw == 0.0) return 1.0;
+        lam = nw / nv;
+        for (int64_t i = 0; i < n; ++i) v[i] = w[i] / nw;
+    }
+    return (double)(float)lam;
+}
+
+// dense inverse by Gauss-Jordan with partial pivoting (coarsest level)
+HostCSR dense_inverse(const HostCSR &A) {
+    const int64_t n = A.nrows;
+    std::vector<double> M(n * n, 0.0), X(n * n, 0.0);
+    for (int64_t i = 0; i < n; ++i) {
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) M[i * n + A.ci[k]] = A.v[k];
+        X[i * n + i] = 1.0;
+    }
+    for (int64_t c = 0; c < n; ++c) {
+        int64_t p = c;
+        for (int64_t r = c + 1; r < n; ++r)
+            if (std::fabs(M[r * n + c]) > std::fabs(M[p * n + c])) p = r;
+        if (M[p * n + c] == 0.0) throw Error("AMG: singular coarsest-level matrix");
+        if (p != c)
+            for (int64_t j = 0; j < n; ++j) {
+                std::swap(M[p * n + j], M[c * n + j]);
+                std::swap(X[p * n + j], X[c * n + j]);
+            }
+        const double inv = 1.0 / M[c * n + c];
+        for (int64_t j = 0; j < n; ++j) {
+            M[c * n + j] *= inv;
+            X[c * n + j] *= inv;
+        }
+        for (int64_t r = 0; r < n; ++r) {
+            if (r == c) continue;
+            const double f = M[r * n + c];
+            if (f == 0.0) continue;
+            for (int64_t j = 0; j < n; ++j) {
+                M[r * n + j] -= f * M[c * n + j];
+                X[r * n + j] -= f * X[c * n + j];
+            }
+        }
+    }
+    HostCSR D;
+    D.nrows = D.ncols = n;
+    D.rp.resize(n + 1);
+    D.ci.resize(n * n);
+    D.v = X;
+    for (int64_t i = 0; i <= n; ++i) D.rp[i] = i * n;
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t j = 0; j < n; ++j) D.ci[i * n + j] = (int32_t)j;
+    return D;
+}
+
+struct AmgLevel {
+    const DevCSR *A = nullptr;      // level 0: the PC's matrix; else Aown
+    std::unique_ptr<DevCSR> Aown;
+    DevCSR P, R;
+    DBuf<double> dinv, x, b, r, d;
+    int64_t n = 0, nc = 0;
+    double lam = 1.0;
+};
+
+struct PCAMG : PC {
+    std::vector<std::unique_ptr<AmgLevel>> lv;
+    int K = 2;
+    int64_t nco = 0;
+    DevCSR Cinv;                   // dense inverse of the coarsest operator
+    std::unique_ptr<PCILU> Clu;    // ... or its device LU
+    std::unique_ptr<DevCSR> Cmat;
+    DBuf<double> cx, cb;
+
+    PCAMG(const DevCSR &M, const Options &o, const std::string &prefix, bool hypre, Ctx &c) {
+        type = hypre ? "hypre" : "gamg";
+        n = M.nrows;
+        const double theta = o.num(prefix + "pc_gamg_threshold", 0.0);
+        const int64_t limit = o.integer(prefix + "pc_gamg_coarse_eq_limit", 50);
+        const int64_t maxlev = o.integer(prefix + "pc_mg_levels", 10);
+        // smoothing steps: PCMG's level KSP max_it; the hypre stand-in reads
+        // BoomerAMG's sweep count (reference petsc-options-inexact: 1)
+        const int64_t kdef = hypre ? o.integer(prefix + "pc_hypre_boomeramg_grid_sweeps_all", 1) : 2;
+        K = (int)o.integer(prefix + "mg_levels_ksp_max_it", kdef);
+        if (K < 1) throw Error(prefix + "mg_levels_ksp_max_it must be >= 1");
+        if (!M.sell) build_sell(const_cast<DevCSR &>(M), c);
+        HostCSR A = download(M, c);
+        std::unique_ptr<DevCSR> cur;  // device copy of A on levels > 0
+        while (A.nrows > limit && (int64_t)lv.size() < maxlev - 1) {
+            int32_t na = 0;
+            const std::vector<int32_t> agg = aggregate(A, theta, na);
+            if (na >= A.nrows || na == 0) break;
+            auto L = std::make_unique<AmgLevel>();
+            L->n = A.nrows;
+            L->nc = na;
+            std::vector<int64_t> sz(na, 0);
+            for (int32_t a : agg) ++sz[a];
+            HostCSR P0;
+            P0.nrows = A.nrows;
+            P0.ncols = na;
+            P0.rp.resize(A.nrows + 1);
+            P0.ci.resize(A.nrows);
+            P0.v.resize(A.nrows);
+            P0.rp[0] = 0;
+            for (int64_t i = 0; i < A.nrows; ++i) {
+                P0.rp[i + 1] = i + 1;
+                P0.ci[i] = agg[i];
+                P0.v[i] = 1.0 / std::sqrt((double)sz[agg[i]]);
+            }
+            const std::vector<double> dinv = jacobi_dinv(A);
+            L->lam = power_lambda(A, dinv, 15);
+            const double omega = 4.0 / (3.0 * L->lam);
+            const HostCSR AP0 = spgemm(A, P0);
+            HostCSR P;  // P0 - omega (D^-1 A P0), merged row by row (csr_binop)
+            P.nrows = A.nrows;
+            P.ncols = na;
+            auto put = [&P](int32_t j, double v) {
+                if (v != 0.0) {
+                    P.ci.push_back(j);
+                    P.v.push_back(v);
+                }
+            };
+            for (int64_t i = 0; i < A.nrows; ++i) {
+                const int32_t j0 = P0.ci[i];
+                bool done0 = false;
+                for (int64_t k = AP0.rp[i]; k < AP0.rp[i + 1]; ++k) {
+                    const int32_t j = AP0.ci[k];
+                    const double s = omega * (dinv[i] * AP0.v[k]);
+                    if (!done0 && j0 < j) {
+                        put(j0, P0.v[i] - 0.0);
+                        done0 = true;
+                    }
+                    if (j == j0) {
+                        put(j, P0.v[i] - s);
+                        done0 = true;
+                    } else {
+                        put(j, 0.0 - s);
+                    }
+                }
+                if (!done0) put(j0, P0.v[i] - 0.0);
+                P.rp.push_back((int64_t)P.ci.size());
+            }
+            const HostCSR R = transpose(P);
+            HostCSR Ac = spgemm(R, spgemm(A, P));
+            L->Aown = std::move(cur);
+            L->A = L->Aown ? L->Aown.get() : &M;
+            L->dinv.alloc(std::max<int64_t>(A.nrows, 1));
+            HIPCHK(hipMemcpyAsync(L->dinv.p, dinv.data(), sizeof(double) * A.nrows, hipMemcpyHostToDevice, c.st));
+            upload(P, L->P, c);
+            upload(R, L->R, c);
+            build_sell(L->P, c);
+            build_sell(L->R, c);
+            L->r.alloc(std::max<int64_t>(A.nrows, 1));
+            L->d.alloc(std::max<int64_t>(A.nrows, 1));
+            if (!lv.empty()) {
+                L->x.alloc(std::max<int64_t>(A.nrows, 1));
+                L->b.alloc(std::max<int64_t>(A.nrows, 1));
+            }
+            lv.push_back(std::move(L));
+            cur = std::make_unique<DevCSR>();
+            upload(Ac, *cur, c);
+            build_sell(*cur, c);
+            A = std::move(Ac);
+        }
+        nco = A.nrows;
+        cx.alloc(std::max<int64_t>(nco, 1));
+        cb.alloc(std::max<int64_t>(nco, 1));
+        if (nco > 0) {
+            if (nco <= 1024) {
+                upload(dense_inverse(A), Cinv, c);
+                build_sell(Cinv, c);
+            } else {
+                Cmat = std::move(cur);
+                Clu = std::make_unique<PCILU>(Cmat ? *Cmat : M, 1, c, true, o.flag("pls.ilu_lds", true));
+            }
+        }
+        c.sync();
+        if (o.flag("pls.amg_view", false)) {
+            fprintf(stderr, "[amg %s] levels %zu:", prefix.c_str(), lv.size() + 1);
+            for (auto &L : lv) fprintf(stderr, " %lld(lam %.6g)", (long long)L->n, L->lam);
+            fprintf(stderr, " coarse %lld\n", (long long)nco);
+        }
+    }
+
+    // K Chebyshev steps on level L from x (x_zero: x == 0 on entry, r = b)
+    void smooth(AmgLevel &L, const double *b, double *x, bool x_zero, Ctx &c) {
+        const double lmax = 1.1 * L.lam, lmin = 0.1 * L.lam;
+        const double th = (lmax + lmin) / 2.0, de = (lmax - lmin) / 2.0;
+        const double sigma = th / de;
+        double rho = 1.0 / sigma;
+        const double *r = b;
+        if (!x_zero) {
+            spmv(*L.A, x, L.r.p, c, -1.0, 1.0, b);
+            r = L.r.p;
+        }
+        launch_cheb_step(L.n, L.dinv.p, r, L.d.p, x, 0.0, 1.0 / th, x_zero ? 3 : 1, c.st);
+        for (int k = 1; k < K; ++k) {
+            spmv(*L.A, x, L.r.p, c, -1.0, 1.0, b);
+            const double rn = 1.0 / (2.0 * sigma - rho);
+            launch_cheb_step(L.n, L.dinv.p, L.r.p, L.d.p, x, rn * rho, 2.0 * rn / de, 0, c.st);
+            rho = rn;
+        }
+    }
+
+    void coarse_solve(const double *b, double *x, Ctx &c) {
+        if (nco == 0) return;
+        if (Clu) Clu->apply(b, x, c);
+        else spmv(Cinv, b, x, c);
+    }
+
+    void vcycle(size_t l, const double *b, double *x, Ctx &c) {
+        if (l == lv.size()) {
+            coarse_solve(b, x, c);
+            return;
+        }
+        AmgLevel &L = *lv[l];
+        const bool last = (l + 1 == lv.size());
+        double *bc = last ? cb.p : lv[l + 1]->b.p;
+        double *xc = last ? cx.p : lv[l + 1]->x.p;
+        smooth(L, b, x, true, c);
+        spmv(*L.A, x, L.r.p, c, -1.0, 1.0, b);
+        spmv(L.R, L.r.p, bc, c);
+        vcycle(l + 1, bc, xc, c);
+        spmv(L.P, xc, x, c, 1.0, 1.0, x);
+        smooth(L, b, x, false, c);
+    }
+
+    void apply(const double *x, double *y, Ctx &c) override {
+        if (n == 0) return;
+        if (lv.empty()) {
+            coarse_solve(x, y, c);
+            return;
+        }
+        vcycle(0, x, y, c);
+    }
+};
+
+}  // namespace
+
+std::unique_ptr<PC> make_amg(const DevCSR &M, const Options &o, const std::string &prefix, bool hypre, Ctx &c) {
+    if (M.halo) throw Error("PC type gamg/hypre (prefix " + prefix + "): multigrid is single-rank in this build");
+    return std::make_unique<PCAMG>(M, o, prefix, hypre, c);
+}
+
+}  // namespace pls

@@ -426,6 +426,20 @@ __global__ __launch_bounds__(TPB) void k_scatter(int64_t n, const int64_t *idx, 
         y[idx[i]] = x[i];
 }
 
+// AMG Chebyshev/Jacobi step (oracle/amg.py PCAMG._cheb), fused:
+// d = a d + bc (dinv . r), x += d;  flags 1: d not read (d = bc (dinv . r)),
+// flags 2: x not read (x = d)
+__global__ __launch_bounds__(TPB) void k_cheb_step(int64_t n, const double *__restrict__ dinv,
+                                                   const double *__restrict__ r, double *__restrict__ d,
+                                                   double *__restrict__ x, double a, double bc, int flags) {
+    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+        const double t = dinv[i] * r[i];
+        const double dn = (flags & 1) ? bc * t : a * d[i] + bc * t;
+        d[i] = dn;
+        x[i] = (flags & 2) ? dn : x[i] + dn;
+    }
+}
+
 static inline unsigned stream_grid(int64_t n) {
     int64_t g = (n + TPB - 1) / TPB;
     if (g > 8192) g = 8192;
@@ -482,6 +496,10 @@ void launch_waxpby(int64_t n, double a, const double *x, double b, const double 
 }
 void launch_pointwise_mult(int64_t n, const double *x, const double *d, double *y, hipStream_t st) {
     if (n > 0) k_pmult<<<stream_grid(n), TPB, 0, st>>>(n, x, d, y);
+}
+void launch_cheb_step(int64_t n, const double *dinv, const double *r, double *d, double *x, double a, double bc,
+                      int flags, hipStream_t st) {
+    if (n > 0) k_cheb_step<<<stream_grid(n), TPB, 0, st>>>(n, dinv, r, d, x, a, bc, flags);
 }
 void launch_zero_entries(int64_t m, const int32_t *idx, double *y, hipStream_t st) {
     if (m > 0) k_zero_entries<<<grid_for(m, TPB), TPB, 0, st>>>(m, idx, y);

@@ -62,6 +62,10 @@ void launch_axpby(int64_t n, double a, const double *x, double b, double *y, hip
 void launch_waxpby(int64_t n, double a, const double *x, double b, const double *y, double *w,
                    hipStream_t st);
 void launch_pointwise_mult(int64_t n, const double *x, const double *d, double *y, hipStream_t st);
+// AMG smoother step: d = a d + bc (dinv . r); x += d.  flags 1: d not read
+// (d = bc (dinv . r)); flags 2: x not read (x = d)
+void launch_cheb_step(int64_t n, const double *dinv, const double *r, double *d, double *x, double a, double bc,
+                      int flags, hipStream_t st);
 void launch_zero_entries(int64_t m, const int32_t *idx, double *y, hipStream_t st);
 void launch_gather(int64_t n, const int64_t *idx, const double *x, double *y, hipStream_t st);
 void launch_scatter(int64_t n, const int64_t *idx, const double *x, double *y, hipStream_t st);

@@ -743,8 +743,16 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         if (sub == "none") return std::make_unique<PCNone>(M.nrows);
         throw Error(prefix + "sub_pc_type " + sub + " is not available on the device");
     }
+    if (type == "gamg") return make_amg(M, o, prefix, false, c);
+    if (type == "hypre") {
+        // BoomerAMG is not in this image: the smoothed-aggregation AMG stands in
+        // (oracle/amg.py); pls.hypre error restores the refusal
+        if (o.str("pls.hypre", "gamg") == "error")
+            throw Error("PC type 'hypre' (prefix " + prefix + ") is not available (pls.hypre error)");
+        return make_amg(M, o, prefix, true, c);
+    }
     throw Error("PC type '" + type + "' (prefix " + prefix +
-                ") is not available in this build (supported: none, jacobi, ilu, bjacobi, lu)");
+                ") is not available in this build (supported: none, jacobi, ilu, bjacobi, lu, gamg, hypre)");
 }
 
 // ================================================================= KSP ===
@@ -1042,13 +1050,9 @@ std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const
 namespace pls {
 
 // =========================================================== fieldsplit ===
-namespace {
-struct HostCSR {
-    int64_t nrows = 0, ncols = 0;
-    std::vector<int64_t> rp{0};
-    std::vector<int32_t> ci;
-    std::vector<double> v;
-};
+void upload(const HostCSR &H, DevCSR &M, Ctx &c) {
+    upload_csr(M, H.nrows, H.ncols, H.rp.data(), H.ci.data(), H.v.data(), c);
+}
 
 HostCSR download(const DevCSR &M, Ctx &c) {
     HostCSR H;
@@ -1066,6 +1070,7 @@ HostCSR download(const DevCSR &M, Ctx &c) {
     return H;
 }
 
+namespace {
 // rows `rows`, columns mapped by cmap (-1: dropped); cmap is monotone on the
 // kept columns, so rows stay sorted (MatCreateSubMatrix with sorted ISs)
 HostCSR submatrix(const HostCSR &M, const std::vector<int32_t> &rows, const std::vector<int32_t> &cmap,
@@ -1146,9 +1151,6 @@ HostCSR selfp(const HostCSR &A, const HostCSR &B, const HostCSR &C, const HostCS
     return S;
 }
 
-void upload(const HostCSR &H, DevCSR &M, Ctx &c) {
-    upload_csr(M, H.nrows, H.ncols, H.rp.data(), H.ci.data(), H.v.data(), c);
-}
 
 // S x = A11 x - A10 A00^-1 A01 x (MatMult_SchurComplement; inner solve = the split-0 KSP)
 struct SchurOp : Op {

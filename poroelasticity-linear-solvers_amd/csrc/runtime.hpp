@@ -127,6 +127,16 @@ void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha = 1.0, double beta = 0.0,
           const double *z = nullptr);
 
+// Host copy of a CSR matrix (setup-time algebra: fieldsplit blocks, AMG hierarchy).
+struct HostCSR {
+    int64_t nrows = 0, ncols = 0;
+    std::vector<int64_t> rp{0};
+    std::vector<int32_t> ci;
+    std::vector<double> v;
+};
+HostCSR download(const DevCSR &M, Ctx &c);
+void upload(const HostCSR &H, DevCSR &M, Ctx &c);
+
 // ----------------------------------------------------------------- options --
 struct Options {
     std::map<std::string, std::string> kv;
@@ -232,6 +242,8 @@ struct PCILU : PC {
 };
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c);
+// Smoothed-aggregation AMG (amg.cpp; -pc_type gamg, and hypre unless pls.hypre error).
+std::unique_ptr<PC> make_amg(const DevCSR &M, const Options &o, const std::string &prefix, bool hypre, Ctx &c);
 
 // ---------------------------------------------------------------------- KSP --
 enum Reason {

@@ -343,13 +343,13 @@ def test_facade_with_repo_option_files(gpu):
 
 def test_unsupported_pc_fails_loudly(gpu):
     spec = S.SynthSpec(2, 4)
-    h = _handle(spec, BASE, dict(ILU_DB, s_pc_type="hypre"))
-    with pytest.raises(RuntimeError, match="hypre"):
+    h = _handle(spec, BASE, dict(ILU_DB, s_pc_type="asm"))
+    with pytest.raises(RuntimeError, match="asm"):
         h.setup()
 
 
 # ------------------------------------------------ fp fieldsplit (2-way) ----
-FS_INEXACT = {  # petsc-options-inexact:73-114 with BoomerAMG -> Jacobi / ILU(0) (hypre is not in this build)
+FS_INEXACT = {  # petsc-options-inexact:73-114 with BoomerAMG -> Jacobi / ILU(0) (the AMG stand-in: test_gpu_amg.py)
     "global_ksp_type": "gmres", "global_ksp_norm_type": "unpreconditioned",
     "s_ksp_type": "preonly", "s_pc_type": "ilu",
     "fp_ksp_type": "preonly", "fp_ksp_rtol": "1e-2", "fp_ksp_atol": "0.0",
