@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <map>
 
 #include "runtime.hpp"
 
@@ -232,9 +233,16 @@ struct AmgLevel {
     const DevCSR *A = nullptr;      // level 0: the PC's matrix; else Aown
     std::unique_ptr<DevCSR> Aown;
     DevCSR P, R;
-    DBuf<double> dinv, x, b, r, d;
+    DBuf<double> dinv;
     int64_t n = 0, nc = 0;
     double lam = 1.0;
+};
+
+// Work vectors of one V-cycle, one set per stream the PC is applied on (the
+// concurrent 3-way block PC applies the same s/f PCs on two streams at once).
+struct AmgWork {
+    std::vector<DBuf<double>> r, d, x, b;  // per level; x, b unused on level 0
+    DBuf<double> cx, cb;                   // coarsest level
 };
 
 struct PCAMG : PC {
@@ -244,7 +252,33 @@ struct PCAMG : PC {
     DevCSR Cinv;                   // dense inverse of the coarsest operator
     std::unique_ptr<PCILU> Clu;    // ... or its device LU
     std::unique_ptr<DevCSR> Cmat;
-    DBuf<double> cx, cb;
+    std::map<hipStream_t, std::unique_ptr<AmgWork>> work;
+
+    bool reentrant() const override { return true; }
+
+    AmgWork &work_for(Ctx &c) {
+        auto &w = work[c.st];
+        if (!w) {
+            w = std::make_unique<AmgWork>();
+            const size_t L = lv.size();
+            w->r.resize(L);
+            w->d.resize(L);
+            w->x.resize(L);
+            w->b.resize(L);
+            for (size_t l = 0; l < L; ++l) {
+                const size_t m = (size_t)std::max<int64_t>(lv[l]->n, 1);
+                w->r[l].alloc(m);
+                w->d[l].alloc(m);
+                if (l > 0) {
+                    w->x[l].alloc(m);
+                    w->b[l].alloc(m);
+                }
+            }
+            w->cx.alloc(std::max<int64_t>(nco, 1));
+            w->cb.alloc(std::max<int64_t>(nco, 1));
+        }
+        return *w;
+    }
 
     PCAMG(const DevCSR &M, const Options &o, const std::string &prefix, bool hypre, Ctx &c) {
         type = hypre ? "hypre" : "gamg";
@@ -324,12 +358,6 @@ struct PCAMG : PC {
             upload(R, L->R, c);
             build_sell(L->P, c);
             build_sell(L->R, c);
-            L->r.alloc(std::max<int64_t>(A.nrows, 1));
-            L->d.alloc(std::max<int64_t>(A.nrows, 1));
-            if (!lv.empty()) {
-                L->x.alloc(std::max<int64_t>(A.nrows, 1));
-                L->b.alloc(std::max<int64_t>(A.nrows, 1));
-            }
             lv.push_back(std::move(L));
             cur = std::make_unique<DevCSR>();
             upload(Ac, *cur, c);
@@ -337,8 +365,7 @@ struct PCAMG : PC {
             A = std::move(Ac);
         }
         nco = A.nrows;
-        cx.alloc(std::max<int64_t>(nco, 1));
-        cb.alloc(std::max<int64_t>(nco, 1));
+        work_for(c);
         if (nco > 0) {
             if (nco <= 1024) {
                 upload(dense_inverse(A), Cinv, c);
@@ -357,21 +384,23 @@ struct PCAMG : PC {
     }
 
     // K Chebyshev steps on level L from x (x_zero: x == 0 on entry, r = b)
-    void smooth(AmgLevel &L, const double *b, double *x, bool x_zero, Ctx &c) {
+    void smooth(size_t l, AmgWork &W, const double *b, double *x, bool x_zero, Ctx &c) {
+        const AmgLevel &L = *lv[l];
+        double *rw = W.r[l].p, *dw = W.d[l].p;
         const double lmax = 1.1 * L.lam, lmin = 0.1 * L.lam;
         const double th = (lmax + lmin) / 2.0, de = (lmax - lmin) / 2.0;
         const double sigma = th / de;
         double rho = 1.0 / sigma;
         const double *r = b;
         if (!x_zero) {
-            spmv(*L.A, x, L.r.p, c, -1.0, 1.0, b);
-            r = L.r.p;
+            spmv(*L.A, x, rw, c, -1.0, 1.0, b);
+            r = rw;
         }
-        launch_cheb_step(L.n, L.dinv.p, r, L.d.p, x, 0.0, 1.0 / th, x_zero ? 3 : 1, c.st);
+        launch_cheb_step(L.n, L.dinv.p, r, dw, x, 0.0, 1.0 / th, x_zero ? 3 : 1, c.st);
         for (int k = 1; k < K; ++k) {
-            spmv(*L.A, x, L.r.p, c, -1.0, 1.0, b);
+            spmv(*L.A, x, rw, c, -1.0, 1.0, b);
             const double rn = 1.0 / (2.0 * sigma - rho);
-            launch_cheb_step(L.n, L.dinv.p, L.r.p, L.d.p, x, rn * rho, 2.0 * rn / de, 0, c.st);
+            launch_cheb_step(L.n, L.dinv.p, rw, dw, x, rn * rho, 2.0 * rn / de, 0, c.st);
             rho = rn;
         }
     }
@@ -382,21 +411,21 @@ struct PCAMG : PC {
         else spmv(Cinv, b, x, c);
     }
 
-    void vcycle(size_t l, const double *b, double *x, Ctx &c) {
+    void vcycle(size_t l, AmgWork &W, const double *b, double *x, Ctx &c) {
         if (l == lv.size()) {
             coarse_solve(b, x, c);
             return;
         }
-        AmgLevel &L = *lv[l];
+        const AmgLevel &L = *lv[l];
         const bool last = (l + 1 == lv.size());
-        double *bc = last ? cb.p : lv[l + 1]->b.p;
-        double *xc = last ? cx.p : lv[l + 1]->x.p;
-        smooth(L, b, x, true, c);
-        spmv(*L.A, x, L.r.p, c, -1.0, 1.0, b);
-        spmv(L.R, L.r.p, bc, c);
-        vcycle(l + 1, bc, xc, c);
+        double *bc = last ? W.cb.p : W.b[l + 1].p;
+        double *xc = last ? W.cx.p : W.x[l + 1].p;
+        smooth(l, W, b, x, true, c);
+        spmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
+        spmv(L.R, W.r[l].p, bc, c);
+        vcycle(l + 1, W, bc, xc, c);
         spmv(L.P, xc, x, c, 1.0, 1.0, x);
-        smooth(L, b, x, false, c);
+        smooth(l, W, b, x, false, c);
     }
 
     void apply(const double *x, double *y, Ctx &c) override {
@@ -405,7 +434,7 @@ struct PCAMG : PC {
             coarse_solve(x, y, c);
             return;
         }
-        vcycle(0, x, y, c);
+        vcycle(0, work_for(c), x, y, c);
     }
 };
 

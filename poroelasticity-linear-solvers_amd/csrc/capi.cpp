@@ -611,6 +611,8 @@ static void alloc_work(Handle &H) {
     if (H.three_way && !H.distributed && H.opt.flag("pls.concurrent_sweeps", true)) {
         bool pre = true;
         for (KSP *k : {H.ksp_s.get(), H.ksp_f.get(), H.ksp_p.get(), H.ksp_pd.get()}) pre = pre && k && k->type == "preonly";
+        // the s and f PCs serve both sweeps at once: they must be reentrant
+        for (KSP *k : {H.ksp_s.get(), H.ksp_f.get()}) pre = pre && k->pc && k->pc->reentrant();
         if (pre) {
             if (!H.ctx2) {
                 H.ctx2 = std::make_unique<Ctx>();

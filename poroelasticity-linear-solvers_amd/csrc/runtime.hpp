@@ -189,14 +189,18 @@ struct PC {
     int64_t n = 0;
     virtual ~PC() = default;
     virtual void apply(const double *x, double *y, Ctx &c) = 0;
+    // apply() may run on two streams at once (no per-application device state)
+    virtual bool reentrant() const { return false; }
 };
 struct PCNone : PC {
     explicit PCNone(int64_t n_) { type = "none"; n = n_; }
+    bool reentrant() const override { return true; }
     void apply(const double *x, double *y, Ctx &c) override;
 };
 struct PCJacobi : PC {
     DBuf<double> dinv;
     PCJacobi(const DevCSR &M, Ctx &c);
+    bool reentrant() const override { return true; }
     void apply(const double *x, double *y, Ctx &c) override;
 };
 // Level-aligned SELL-64 strict triangular factor (see kernels.hip).
@@ -238,6 +242,7 @@ struct PCILU : PC {
     bool exact = false;     // envelope pattern: exact LU (PCLU)
     std::string profile_tag;  // non-empty: dump per-block sweep timings once (option pls.sweep_profile)
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0);
+    bool reentrant() const override { return profile_tag.empty(); }
     void apply(const double *x, double *y, Ctx &c) override;
 };
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
