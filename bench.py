@@ -44,12 +44,44 @@ SEED = 20261015
 DELTA = 0.05
 
 
+# reference petsc-options-inexact (BoomerAMG -> the device AMG stand-in,
+# MUMPS -> the device LU): CG on s/f/p, PREONLY on diff, Schur fieldsplit on fp
+INEXACT_DB = {
+    "global_ksp_type": "gmres", "global_ksp_norm_type": "unpreconditioned",
+    "s_ksp_type": "cg", "s_ksp_norm_type": "unpreconditioned", "s_ksp_atol": "0.0", "s_ksp_rtol": "1e-1",
+    "s_pc_type": "hypre", "s_pc_hypre_boomeramg_grid_sweeps_all": "1",
+    "f_ksp_type": "cg", "f_ksp_norm_type": "unpreconditioned", "f_ksp_atol": "0.0", "f_ksp_rtol": "1e-2",
+    "f_pc_type": "hypre", "f_pc_hypre_boomeramg_grid_sweeps_all": "1",
+    "p_ksp_type": "cg", "p_ksp_norm_type": "unpreconditioned", "p_ksp_atol": "0.0", "p_ksp_rtol": "1e-2",
+    "p_pc_type": "hypre", "diff_ksp_type": "preonly", "diff_pc_type": "hypre",
+    "fp_ksp_type": "preonly", "fp_pc_fieldsplit_type": "schur", "fp_pc_fieldsplit_schur_fact_type": "lower",
+    "fp_pc_fieldsplit_schur_precondition": "selfp",
+    "fp_fieldsplit_0_ksp_type": "cg", "fp_fieldsplit_0_ksp_rtol": "1e-4", "fp_fieldsplit_0_ksp_atol": "0.0",
+    "fp_fieldsplit_0_ksp_max_it": "10", "fp_fieldsplit_0_pc_type": "hypre",
+    "fp_fieldsplit_1_ksp_type": "preonly", "fp_fieldsplit_1_pc_type": "lu",
+}
+
+
 def solver_options(args):
     three = args.pc_type == "diagonal 3-way"
+    if args.inexact:
+        params = {"solver type": args.solver, "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": args.maxit,
+                  "pc type": args.pc_type, "inner ksp type": "cg", "inner pc type": "hypre",
+                  "inner accel order": 0, "AAR order": 10, "AAR p": 5, "AAR omega": 1.0, "AAR beta": 1.0}
+        return params, dict(INEXACT_DB)
     params = {"solver type": args.solver, "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": args.maxit,
               "pc type": args.pc_type, "inner ksp type": "preonly", "inner pc type": args.inner,
               "inner accel order": 0, "AAR order": 10, "AAR p": 5, "AAR omega": 1.0, "AAR beta": 1.0}
     db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right"}
+    if args.inner in ("gamg", "hypre"):
+        # AMG on the field blocks; the coupled 2-way fp block keeps BJACOBI(ILU(0))
+        for pre in (("s_", "f_", "p_", "diff_") if three else ("s_",)):
+            db[pre + "ksp_type"] = "preonly"
+            db[pre + "pc_type"] = args.inner
+        if not three:
+            db.update({"fp_ksp_type": "preonly", "fp_pc_type": "bjacobi", "fp_pc_bjacobi_blocks": str(args.blocks_fp)})
+            params["inner pc type"] = "bjacobi"
+        return params, db
     # block counts: every block solution fits one CU's LDS (<= 20480 rows)
     blocks = {"s_": args.blocks_s, "fp_": args.blocks_fp, "f_": args.blocks_s, "p_": args.blocks_p,
               "diff_": args.blocks_p}
@@ -77,7 +109,8 @@ def cpu_baseline(args, params, db):
     b = S.rhs(spec)
     n_sample = spec.n
     n_metric = S.SynthSpec(3, args.N).n if args.N != Ns else n_sample
-    c_path = (params["pc type"] == "diagonal" and params["solver type"] == "gmres" and args.inner == "bjacobi")
+    c_path = (params["pc type"] == "diagonal" and params["solver type"] == "gmres" and args.inner == "bjacobi"
+              and not args.inexact)
     if c_path:
         from oracle import native
         try:
@@ -123,14 +156,16 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--N", type=int, default=59)
-    ap.add_argument("--inner", default="bjacobi", choices=["bjacobi", "ilu", "jacobi"])
+    ap.add_argument("--inner", default="bjacobi", choices=["bjacobi", "ilu", "jacobi", "gamg", "hypre"])
+    ap.add_argument("--inexact", action="store_true",
+                    help="the reference's petsc-options-inexact set (CG + AMG blocks, Schur fieldsplit on fp)")
     # block counts: one block per CU (256) for the solid block; 264 for the fp
     # block so every block solution (<= 20480 doubles = 160 KiB) fits one CU's LDS
     ap.add_argument("--blocks-s", type=int, default=256)
     ap.add_argument("--blocks-fp", type=int, default=264)
     ap.add_argument("--blocks-p", type=int, default=11, help="3-way p_ / diff_ blocks")
     ap.add_argument("--maxit", type=int, default=100)
-    ap.add_argument("--pc-type", default="diagonal", choices=["diagonal", "diagonal 3-way"],
+    ap.add_argument("--pc-type", default="diagonal", choices=["diagonal", "diagonal 3-way", "3-way"],
                     help="block preconditioner (the metric: 2-way 'diagonal')")
     ap.add_argument("--solver", default="gmres", choices=["gmres", "aar"])
     ap.add_argument("--no-cpu", action="store_true")
@@ -144,6 +179,8 @@ def main():
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="host: host-staged gloo communicator (ranks may share a GPU; rehearsal only)")
     args = ap.parse_args()
+    if args.pc_type == "3-way":
+        args.pc_type = "diagonal 3-way"
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -276,9 +313,11 @@ def main():
                 "workload": (f"swelling-3d-shaped 3-D N={N_glob} ({n_global} DoF): outer "
                              + ("GMRES right-PC" if args.solver == "gmres" else "AAR(10, p=5)")
                              + f" rtol 1e-6 atol 1e-8 maxit={args.maxit}, "
-                             + ("2-way" if args.pc_type == "diagonal" else "3-way") + " block PC, inner preonly+"
-                             + args.inner + (f"(ILU(0), {args.blocks_s}/{args.blocks_fp} blocks s/fp)"
-                                             if args.inner == "bjacobi" else "")),
+                             + ("2-way" if args.pc_type == "diagonal" else "3-way") + " block PC, "
+                             + ("petsc-options-inexact (CG + AMG blocks, Schur fieldsplit fp)" if args.inexact else
+                                "inner preonly+" + args.inner
+                                + (f"(ILU(0), {args.blocks_s}/{args.blocks_fp} blocks s/fp)"
+                                   if args.inner == "bjacobi" else ""))),
                 "dim": 3, "N": N_glob, "dofs": n_global, "dofs_rank0": n, "nnz_A_rank0": nnz,
                 "parallelism": (f"row slabs x{world} ({args.comm})" if sharded else
                                 f"replicas x{world}" if world > 1 else "single GPU"),

@@ -17,9 +17,12 @@
 // context's stream; the coarsest level is a dense inverse (one SpMV) up to
 // 1024 rows, the device LU pipeline above that.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
+#include <thread>
 
 #include "runtime.hpp"
 
@@ -47,17 +50,55 @@ HostCSR transpose(const HostCSR &A) {
     return T;  // rows ascending (i visited in order)
 }
 
+// Host threads for the setup algebra (rows are independent, so results do
+// not depend on the count): OMP_NUM_THREADS if set, else the hardware's, <= 64.
+int setup_threads() {
+    int t = (int)std::thread::hardware_concurrency();
+    if (const char *e = std::getenv("OMP_NUM_THREADS")) t = std::atoi(e);
+    return std::max(1, std::min(t, 64));
+}
+
+// fn(t, i0, i1) on T contiguous row ranges, one thread each
+template <class F>
+void parallel_rows(int64_t n, int T, F fn) {
+    T = (int)std::max<int64_t>(1, std::min<int64_t>(T, n / 8));  // rows may be long (R = P^T)
+    if (T == 1) {
+        fn(0, (int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(fn, t, n * t / T, n * (t + 1) / T);
+    for (auto &x : th) x.join();
+}
+
+// Concatenate per-thread row ranges (ci/v/row lengths) into one CSR.
+void concat_rows(HostCSR &C, std::vector<HostCSR> &part) {
+    int64_t nnz = 0;
+    for (auto &p : part) nnz += (int64_t)p.ci.size();
+    C.rp.assign(1, 0);
+    C.rp.reserve(C.nrows + 1);
+    C.ci.resize(nnz);
+    C.v.resize(nnz);
+    int64_t off = 0;
+    for (auto &p : part) {
+        for (size_t k = 1; k < p.rp.size(); ++k) C.rp.push_back(off + p.rp[k]);
+        std::copy(p.ci.begin(), p.ci.end(), C.ci.begin() + off);
+        std::copy(p.v.begin(), p.v.end(), C.v.begin() + off);
+        off += (int64_t)p.ci.size();
+        HostCSR().rp.swap(p.rp);
+        std::vector<int32_t>().swap(p.ci);
+        std::vector<double>().swap(p.v);
+    }
+}
+
 // C = A B, row i accumulating over A's row in storage order (csr_matmat);
-// exact zero sums dropped; columns sorted.
-HostCSR spgemm(const HostCSR &A, const HostCSR &B) {
-    HostCSR C;
-    C.nrows = A.nrows;
-    C.ncols = B.ncols;
+// exact zero sums dropped; columns sorted.  Rows in parallel.
+void spgemm_rows(const HostCSR &A, const HostCSR &B, int64_t i0, int64_t i1, HostCSR &C) {
     C.rp.assign(1, 0);
     std::vector<double> acc(B.ncols, 0.0);
     std::vector<char> mark(B.ncols, 0);
     std::vector<int32_t> cols;
-    for (int64_t i = 0; i < A.nrows; ++i) {
+    for (int64_t i = i0; i < i1; ++i) {
         cols.clear();
         for (int64_t kk = A.rp[i]; kk < A.rp[i + 1]; ++kk) {
             const int32_t k = A.ci[kk];
@@ -82,6 +123,16 @@ HostCSR spgemm(const HostCSR &A, const HostCSR &B) {
         }
         C.rp.push_back((int64_t)C.ci.size());
     }
+}
+
+HostCSR spgemm(const HostCSR &A, const HostCSR &B) {
+    HostCSR C;
+    C.nrows = A.nrows;
+    C.ncols = B.ncols;
+    const int T = setup_threads();
+    std::vector<HostCSR> part(T);
+    parallel_rows(A.nrows, T, [&](int t, int64_t i0, int64_t i1) { spgemm_rows(A, B, i0, i1, part[t]); });
+    concat_rows(C, part);
     return C;
 }
 
@@ -167,12 +218,17 @@ double power_lambda(const HostCSR &A, const std::vector<double> &dinv, int steps
     const int64_t n = A.nrows;
     std::vector<double> v(n, 1.0), w(n);
     double lam = 1.0;
+    const int T = setup_threads();
     for (int s = 0; s < steps; ++s) {
+        parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+            for (int64_t i = i0; i < i1; ++i) {
+                double acc = 0.0;
+                for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) acc += A.v[k] * v[A.ci[k]];
+                w[i] = dinv[i] * acc;
+            }
+        });
         double nw = 0.0, nv = 0.0;
         for (int64_t i = 0; i < n; ++i) {
-            double acc = 0.0;
-            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) acc += A.v[k] * v[A.ci[k]];
-            w[i] = dinv[i] * acc;
             nw += w[i] * w[i];
             nv += v[i] * v[i];
         }
@@ -227,6 +283,13 @@ HostCSR dense_inverse(const HostCSR &A) {
     for (int64_t i = 0; i < n; ++i)
         for (int64_t j = 0; j < n; ++j) D.ci[i * n + j] = (int32_t)j;
     return D;
+}
+
+// SpMV layout for an AMG operator: SELL-64 for short rows; matrices of few
+// long rows (R = P^T, Galerkin coarse operators, the dense coarsest inverse)
+// stay CSR and take the workgroup-per-row kernel.
+void amg_layout(DevCSR &M, Ctx &c) {
+    if (M.nrows > 0 && M.nnz < 128 * M.nrows) build_sell(M, c);
 }
 
 struct AmgLevel {
@@ -292,11 +355,18 @@ struct PCAMG : PC {
         K = (int)o.integer(prefix + "mg_levels_ksp_max_it", kdef);
         if (K < 1) throw Error(prefix + "mg_levels_ksp_max_it must be >= 1");
         if (!M.sell) build_sell(const_cast<DevCSR &>(M), c);
+        const bool view = o.flag("pls.amg_view", false);
+        double tm[8] = {0};  // setup stage seconds (pls.amg_view)
+        auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+        double t0 = now();
         HostCSR A = download(M, c);
+        tm[0] += now() - t0;
         std::unique_ptr<DevCSR> cur;  // device copy of A on levels > 0
         while (A.nrows > limit && (int64_t)lv.size() < maxlev - 1) {
             int32_t na = 0;
+            t0 = now();
             const std::vector<int32_t> agg = aggregate(A, theta, na);
+            tm[1] += now() - t0;
             if (na >= A.nrows || na == 0) break;
             auto L = std::make_unique<AmgLevel>();
             L->n = A.nrows;
@@ -316,7 +386,10 @@ struct PCAMG : PC {
                 P0.v[i] = 1.0 / std::sqrt((double)sz[agg[i]]);
             }
             const std::vector<double> dinv = jacobi_dinv(A);
+            t0 = now();
             L->lam = power_lambda(A, dinv, 15);
+            tm[2] += now() - t0;
+            t0 = now();
             const double omega = 4.0 / (3.0 * L->lam);
             const HostCSR AP0 = spgemm(A, P0);
             HostCSR P;  // P0 - omega (D^-1 A P0), merged row by row (csr_binop)
@@ -349,37 +422,47 @@ struct PCAMG : PC {
                 P.rp.push_back((int64_t)P.ci.size());
             }
             const HostCSR R = transpose(P);
+            tm[3] += now() - t0;
+            t0 = now();
             HostCSR Ac = spgemm(R, spgemm(A, P));
+            tm[4] += now() - t0;
+            t0 = now();
             L->Aown = std::move(cur);
             L->A = L->Aown ? L->Aown.get() : &M;
             L->dinv.alloc(std::max<int64_t>(A.nrows, 1));
             HIPCHK(hipMemcpyAsync(L->dinv.p, dinv.data(), sizeof(double) * A.nrows, hipMemcpyHostToDevice, c.st));
             upload(P, L->P, c);
             upload(R, L->R, c);
-            build_sell(L->P, c);
-            build_sell(L->R, c);
+            amg_layout(L->P, c);
+            amg_layout(L->R, c);
             lv.push_back(std::move(L));
             cur = std::make_unique<DevCSR>();
             upload(Ac, *cur, c);
-            build_sell(*cur, c);
+            amg_layout(*cur, c);
             A = std::move(Ac);
+            c.sync();
+            tm[5] += now() - t0;
         }
         nco = A.nrows;
         work_for(c);
         if (nco > 0) {
             if (nco <= 1024) {
                 upload(dense_inverse(A), Cinv, c);
-                build_sell(Cinv, c);
+                amg_layout(Cinv, c);
             } else {
                 Cmat = std::move(cur);
                 Clu = std::make_unique<PCILU>(Cmat ? *Cmat : M, 1, c, true, o.flag("pls.ilu_lds", true));
             }
         }
         c.sync();
-        if (o.flag("pls.amg_view", false)) {
+        if (view) {
             fprintf(stderr, "[amg %s] levels %zu:", prefix.c_str(), lv.size() + 1);
             for (auto &L : lv) fprintf(stderr, " %lld(lam %.6g)", (long long)L->n, L->lam);
             fprintf(stderr, " coarse %lld\n", (long long)nco);
+            fprintf(stderr,
+                    "[amg %s] setup s: download %.2f aggregate %.2f lambda %.2f P/R %.2f RAP %.2f upload %.2f "
+                    "(%d threads)\n",
+                    prefix.c_str(), tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], setup_threads());
         }
     }
 

@@ -374,11 +374,52 @@ __global__ __launch_bounds__(TPB) void k_spmv_w64(int64_t nrows, int rpw, const 
     }
 }
 
+// Few, very long rows (AMG restriction R = P^T, Galerkin coarse operators,
+// the dense coarsest inverse): one 256-lane workgroup per row, U loads per
+// lane in flight, fixed-order wave + LDS reduction (deterministic).
+template <int U>
+__global__ __launch_bounds__(TPB) void k_spmv_wg(int64_t nrows, const int64_t *__restrict__ rp,
+                                                 const int32_t *__restrict__ ci, const double *__restrict__ val,
+                                                 const double *__restrict__ x, double *__restrict__ y, double alpha,
+                                                 double beta, const double *__restrict__ z) {
+    __shared__ double part[TPB / 64];
+    const int64_t row = blockIdx.x;
+    const int64_t s = rp[row], e = rp[row + 1];
+    double acc = 0.0;
+    for (int64_t k0 = s; k0 < e; k0 += U * TPB) {
+        int32_t c[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = k0 + u * TPB + threadIdx.x;
+            const int64_t kk = k < e ? k : s;
+            c[u] = __builtin_nontemporal_load(ci + kk);
+            const double vv = __builtin_nontemporal_load(val + kk);
+            v[u] = k < e ? vv : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u] * x[(uint32_t)c[u]];
+    }
+    acc = wave_reduce(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = part[0];
+#pragma unroll
+        for (int w = 1; w < TPB / 64; ++w) t += part[w];
+        double r = alpha * t;
+        if (beta != 0.0) r += beta * z[row];
+        y[row] = r;
+    }
+}
+
 void launch_spmv(int64_t nrows, int64_t nnz, const int64_t *rp, const int32_t *ci, const double *val,
                  const double *x, double *y, double alpha, double beta, const double *z, hipStream_t st) {
     if (nrows <= 0) return;
     const double mean = (double)nnz / (double)nrows;
-    if (mean >= 96.0) {
+    if (mean >= 512.0 || (mean >= 96.0 && nrows < 16384)) {
+        k_spmv_wg<4><<<(unsigned)nrows, TPB, 0, st>>>(nrows, rp, ci, val, x, y, alpha, beta, z);
+    } else if (mean >= 96.0) {
         const int rpw = 8;
         const int64_t waves = (nrows + rpw - 1) / rpw;
         k_spmv_w64<3><<<grid_for(waves, TPB / 64), TPB, 0, st>>>(nrows, rpw, rp, ci, val, x, y, alpha, beta, z);
