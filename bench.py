@@ -62,16 +62,71 @@ INEXACT_DB = {
 }
 
 
+# BASELINE.json "configs": named presets (dim, N, option set); the default is
+# configs[1] at the metric's size.  Only the metric's configuration is the
+# headline bench line; the others are measured and recorded in DESIGN.md.
+CONFIGS = {
+    # configs[0]: swelling.py 2-D N=32, exact block PC (petsc-options-exact:
+    # right-PC GMRES, PREONLY + LU on every block; MUMPS -> device LU),
+    # swelling.py:63-67 atol 1e-8 rtol 1e-6 maxit 500
+    "swelling2d-exact": dict(dim=2, N=32, maxit=500, atol=1e-8, preset="exact", cpu_N=32),
+    # configs[1] (metric: N=59 = 10.33M DoF; N=64 is the named size)
+    "swelling3d-bjacobi": dict(dim=3, N=59, maxit=100, atol=1e-8, preset=None),
+    # configs[2]: footing.py at N=128 (2-D in the reference: footing.py:18-19;
+    # its local refinement near the footing is not modelled by the synthetic
+    # system) with petsc-options-inexact and ILU(0) in place of BoomerAMG: CG
+    # blocks, Schur lower/selfp fieldsplit on fp (Schur block: device LU).
+    # footing.py:73-76 atol 1e-4 maxit 500.
+    "footing-inexact-ilu": dict(dim=2, N=128, maxit=500, atol=1e-4, preset="inexact-ilu", cpu_N=48),
+    # configs[4]: AAR depth m=5 (sharded across ranks under torchrun)
+    "aar-m5": dict(dim=3, N=59, maxit=100, atol=1e-8, preset=None, solver="aar", aar_order=5, cpu_N=20),
+}
+
+
+def _inexact_db(amg: str, blocks: int = 64):
+    """petsc-options-inexact with BoomerAMG replaced by ILU(0) blocks: block
+    Jacobi with ILU(0) sub-blocks (PETSc's parallel ILU; one workgroup per
+    block in LDS on the device), ``blocks`` blocks per inner PC."""
+    db = dict(INEXACT_DB)
+    if amg == "ilu":
+        for k in list(db):
+            if db[k] == "hypre":
+                pre = k[:-len("pc_type")]
+                db[k] = "bjacobi"
+                db[pre + "pc_bjacobi_blocks"] = str(blocks)
+                db[pre + "sub_pc_type"] = "ilu"
+            if "hypre" in k:
+                del db[k]
+    return db
+
+
 def solver_options(args):
     three = args.pc_type == "diagonal 3-way"
+    if args.preset == "exact":
+        params = {"solver type": args.solver, "solver atol": args.atol, "solver rtol": 1e-6,
+                  "solver maxiter": args.maxit, "pc type": args.pc_type, "inner ksp type": "preonly",
+                  "inner pc type": "lu", "inner accel order": 0, "AAR order": args.aar_order, "AAR p": 5,
+                  "AAR omega": 1.0, "AAR beta": 1.0}
+        db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right"}
+        for pre in (("s_", "f_", "p_", "diff_") if three else ("s_", "fp_")):
+            db[pre + "ksp_type"] = "preonly"
+            db[pre + "pc_type"] = "lu"
+        return params, db
+    if args.preset == "inexact-ilu":
+        params = {"solver type": args.solver, "solver atol": args.atol, "solver rtol": 1e-6,
+                  "solver maxiter": args.maxit, "pc type": args.pc_type, "inner ksp type": "cg",
+                  "inner pc type": "ilu", "inner accel order": 0, "AAR order": args.aar_order, "AAR p": 5,
+                  "AAR omega": 1.0, "AAR beta": 1.0}
+        return params, _inexact_db("ilu", args.blocks_inner)
     if args.inexact:
-        params = {"solver type": args.solver, "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": args.maxit,
-                  "pc type": args.pc_type, "inner ksp type": "cg", "inner pc type": "hypre",
-                  "inner accel order": 0, "AAR order": 10, "AAR p": 5, "AAR omega": 1.0, "AAR beta": 1.0}
+        params = {"solver type": args.solver, "solver atol": args.atol, "solver rtol": 1e-6,
+                  "solver maxiter": args.maxit, "pc type": args.pc_type, "inner ksp type": "cg",
+                  "inner pc type": "hypre", "inner accel order": 0, "AAR order": args.aar_order, "AAR p": 5,
+                  "AAR omega": 1.0, "AAR beta": 1.0}
         return params, dict(INEXACT_DB)
-    params = {"solver type": args.solver, "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": args.maxit,
+    params = {"solver type": args.solver, "solver atol": args.atol, "solver rtol": 1e-6, "solver maxiter": args.maxit,
               "pc type": args.pc_type, "inner ksp type": "preonly", "inner pc type": args.inner,
-              "inner accel order": 0, "AAR order": 10, "AAR p": 5, "AAR omega": 1.0, "AAR beta": 1.0}
+              "inner accel order": 0, "AAR order": args.aar_order, "AAR p": 5, "AAR omega": 1.0, "AAR beta": 1.0}
     db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right"}
     if args.inner in ("gamg", "hypre"):
         # AMG on the field blocks; the coupled 2-way fp block keeps BJACOBI(ILU(0))
@@ -103,14 +158,14 @@ def cpu_baseline(args, params, db):
     system (the per-iteration work is linear in n)."""
     from oracle import synthetic as S
     Ns = args.cpu_N
-    spec = S.SynthSpec(3, Ns, SEED, DELTA)
+    spec = S.SynthSpec(args.dim, Ns, SEED, DELTA)
     t0 = time.perf_counter()
     A, P = S.matrix(spec, 0), S.matrix(spec, 1)
     b = S.rhs(spec)
     n_sample = spec.n
-    n_metric = S.SynthSpec(3, args.N).n if args.N != Ns else n_sample
+    n_metric = S.SynthSpec(args.dim, args.N).n if args.N != Ns else n_sample
     c_path = (params["pc type"] == "diagonal" and params["solver type"] == "gmres" and args.inner == "bjacobi"
-              and not args.inexact)
+              and not args.inexact and args.preset is None)
     if c_path:
         from oracle import native
         try:
@@ -124,9 +179,9 @@ def cpu_baseline(args, params, db):
             atol=params["solver atol"], maxit=args.cpu_maxit, nthreads=cores)
         rate = its / dt
         return {"value": rate * n_sample / n_metric,
-                "unit": "Krylov iters/s (scaled to the 10.33M-DoF system by DoF)", "cores": cores, "kind": "port",
+                "unit": f"Krylov iters/s (scaled by DoF to the {n_metric}-DoF system)", "cores": cores, "kind": "port",
                 "sample": (f"oracle/csrc/cpu_solver.c (C + OpenMP, {cores} threads): bench's configuration on "
-                           f"the N={Ns} 3-D system ({n_sample} DoF, {A.nnz} nnz), {its} GMRES iterations in "
+                           f"the N={Ns} {args.dim}-D system ({n_sample} DoF, {A.nnz} nnz), {its} GMRES iterations in "
                            f"{dt:.1f}s (block setup {t_setup:.1f}s, generation {t_gen:.1f}s), reason {reason}; "
                            f"iters/s x {n_sample}/{n_metric}"),
                 "raw_iters_per_s": rate}
@@ -142,16 +197,21 @@ def cpu_baseline(args, params, db):
     o.solve(b)
     dt = time.perf_counter() - t1
     rate = o.its / dt
-    return {"value": rate * n_sample / n_metric, "unit": "Krylov iters/s (scaled to the 10.33M-DoF system by DoF)",
+    return {"value": rate * n_sample / n_metric, "unit": f"Krylov iters/s (scaled by DoF to the {n_metric}-DoF system)",
             "cores": 1, "kind": "port",
             "sample": (f"oracle (numpy/scipy + C kernels, 1 thread) {params['pc type']} / {params['solver type']} "
-                       f"solve of the N={Ns} 3-D system ({n_sample} DoF), {o.its} outer iterations in {dt:.1f}s "
+                       f"solve of the N={Ns} {args.dim}-D system ({n_sample} DoF), {o.its} outer iterations in {dt:.1f}s "
                        f"(setup {t_setup:.1f}s), maxit {args.cpu_maxit}; iters/s x {n_sample}/{n_metric}"),
             "raw_iters_per_s": rate}
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="swelling3d-bjacobi", choices=sorted(CONFIGS),
+                    help="BASELINE.json configuration preset (explicit flags override its fields)")
+    ap.add_argument("--dim", type=int, default=3, choices=[2, 3])
+    ap.add_argument("--atol", type=float, default=1e-8)
+    ap.add_argument("--aar-order", type=int, default=10)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
@@ -164,6 +224,7 @@ def main():
     ap.add_argument("--blocks-s", type=int, default=256)
     ap.add_argument("--blocks-fp", type=int, default=264)
     ap.add_argument("--blocks-p", type=int, default=11, help="3-way p_ / diff_ blocks")
+    ap.add_argument("--blocks-inner", type=int, default=64, help="footing preset: bjacobi blocks per inner PC")
     ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("--pc-type", default="diagonal", choices=["diagonal", "diagonal 3-way", "3-way"],
                     help="block preconditioner (the metric: 2-way 'diagonal')")
@@ -178,6 +239,9 @@ def main():
     ap.add_argument("--replicas", action="store_true", help="G independent N=59 solves instead of one sharded solve")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="host: host-staged gloo communicator (ranks may share a GPU; rehearsal only)")
+    pre, _ = ap.parse_known_args()
+    preset = dict(CONFIGS[pre.config])
+    ap.set_defaults(preset=preset.pop("preset"), **preset)
     args = ap.parse_args()
     if args.pc_type == "3-way":
         args.pc_type = "diagonal 3-way"
@@ -197,7 +261,7 @@ def main():
     sharded = world > 1 and not args.replicas
     N_glob = args.N
     if sharded:
-        N_glob = int(round(args.N * world ** (1.0 / 3.0)))
+        N_glob = int(round(args.N * world ** (1.0 / args.dim)))
         args.blocks_s *= world
         args.blocks_fp *= world
         args.blocks_p *= world
@@ -215,9 +279,9 @@ def main():
     if sharded:
         from lib.dist import Communicator
         comm = Communicator.rccl() if args.comm == "rccl" else Communicator.gloo()
-        h = Handle.synthetic_dist(3, N_glob, SEED, DELTA, opts, comm)
+        h = Handle.synthetic_dist(args.dim, N_glob, SEED, DELTA, opts, comm)
     else:
-        h = Handle.synthetic(3, args.N, SEED + rank, DELTA, opts)
+        h = Handle.synthetic(args.dim, args.N, SEED + rank, DELTA, opts)
     h.setup()
     h.create_solver()
     t_setup = time.perf_counter() - t0
@@ -310,15 +374,18 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded SPD 3-field block system, SURVEY.md 8(d); generated in HBM)",
             "config": {
-                "workload": (f"swelling-3d-shaped 3-D N={N_glob} ({n_global} DoF): outer "
-                             + ("GMRES right-PC" if args.solver == "gmres" else "AAR(10, p=5)")
-                             + f" rtol 1e-6 atol 1e-8 maxit={args.maxit}, "
+                "workload": (f"{args.config}: {args.dim}-D N={N_glob} ({n_global} DoF): outer "
+                             + ("GMRES right-PC" if args.solver == "gmres" else f"AAR({args.aar_order}, p=5)")
+                             + f" rtol 1e-6 atol {args.atol:g} maxit={args.maxit}, "
                              + ("2-way" if args.pc_type == "diagonal" else "3-way") + " block PC, "
-                             + ("petsc-options-inexact (CG + AMG blocks, Schur fieldsplit fp)" if args.inexact else
+                             + ("petsc-options-exact (PREONLY + LU blocks)" if args.preset == "exact" else
+                                "petsc-options-inexact with ILU(0) for BoomerAMG (CG blocks, Schur fieldsplit fp)"
+                                if args.preset == "inexact-ilu" else
+                                "petsc-options-inexact (CG + AMG blocks, Schur fieldsplit fp)" if args.inexact else
                                 "inner preonly+" + args.inner
                                 + (f"(ILU(0), {args.blocks_s}/{args.blocks_fp} blocks s/fp)"
                                    if args.inner == "bjacobi" else ""))),
-                "dim": 3, "N": N_glob, "dofs": n_global, "dofs_rank0": n, "nnz_A_rank0": nnz,
+                "dim": args.dim, "N": N_glob, "dofs": n_global, "dofs_rank0": n, "nnz_A_rank0": nnz,
                 "parallelism": (f"row slabs x{world} ({args.comm})" if sharded else
                                 f"replicas x{world}" if world > 1 else "single GPU"),
             },

@@ -313,7 +313,7 @@ struct PCAMG : PC {
     int K = 2;
     int64_t nco = 0;
     DevCSR Cinv;                   // dense inverse of the coarsest operator
-    std::unique_ptr<PCILU> Clu;    // ... or its device LU
+    std::unique_ptr<PC> Clu;       // ... or its device LU (dense inverse while it fits)
     std::unique_ptr<DevCSR> Cmat;
     std::map<hipStream_t, std::unique_ptr<AmgWork>> work;
 
@@ -451,7 +451,9 @@ struct PCAMG : PC {
                 amg_layout(Cinv, c);
             } else {
                 Cmat = std::move(cur);
-                Clu = std::make_unique<PCILU>(Cmat ? *Cmat : M, 1, c, true, o.flag("pls.ilu_lds", true));
+                const DevCSR &Cm = Cmat ? *Cmat : M;
+                if (nco <= o.integer("pls.lu_dense_max", 32768)) Clu = std::make_unique<PCDenseLU>(Cm, c);
+                else Clu = std::make_unique<PCILU>(Cm, 1, c, true, o.flag("pls.ilu_lds", true));
             }
         }
         c.sync();

@@ -909,11 +909,19 @@ __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ r
 }
 #pragma clang fp contract(on)
 
+int ilu0_max_row() { return 163840 / 12; }
 void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
-                       const int64_t *diag, double *dinv, int32_t *fail, hipStream_t st) {
-    // caller guarantees max row length * 12 B <= 64 KiB; dynamic LDS sized per launch by caller contract
+                       const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, hipStream_t st) {
+    // caller guarantees max_row <= ilu0_max_row(); LDS sized to the longest row (occupancy for short rows)
     if (nrows_level <= 0) return;
-    k_ilu0_level<<<(unsigned)nrows_level, 64, 65536, st>>>(rows, rp, ci, lu, diag, dinv, fail);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)k_ilu0_level, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)163840);
+        attr = true;
+    }
+    const size_t lds = (size_t)(((max_row < 1 ? 1 : max_row) * 12 + 15) & ~(int64_t)15);
+    k_ilu0_level<<<(unsigned)nrows_level, 64, lds, st>>>(rows, rp, ci, lu, diag, dinv, fail);
 }
 
 __global__ __launch_bounds__(TPB) void k_lvl_count(int64_t n, const int32_t *order, const int64_t *rp,

@@ -92,9 +92,11 @@ void launch_gram(int64_t n, int m, const double *const *cols_dev, const double *
 
 // -------------------------------------------------------------------- ILU --
 // Factor the rows of one level in place (original CSR): lu, diag pos, dinv.
+// max_row: longest row of the matrix (<= ilu0_max_row(); staged in LDS).
+int ilu0_max_row();
 void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp,
                        const int32_t *ci, double *lu, const int64_t *diag, double *dinv,
-                       int32_t *fail, hipStream_t st);
+                       int32_t *fail, int64_t max_row, hipStream_t st);
 void launch_find_diag(int64_t n, const int64_t *rp, const int32_t *ci, int64_t *diag, int32_t *fail,
                       hipStream_t st);
 // Level-ordered triangular factor storage ("row r of level order"): build
@@ -172,5 +174,15 @@ void launch_remap_cols(int64_t nnz, int32_t *ci, const int32_t *gmap, hipStream_
 void launch_sort_rows(int64_t n, const int64_t *rp, int32_t *ci, double *val, hipStream_t st);
 void launch_pack(int64_t m, const int32_t *idx, const double *x, double *buf, hipStream_t st);   // buf[k] = x[idx[k]]
 void launch_unpack(int64_t m, const int32_t *idx, const double *buf, double *x, hipStream_t st); // x[idx[k]] = buf[k]
+
+// ------------------------------------------------- dense exact LU (dense.hip) --
+// M: ld x ld row-major (ld = 64 * ceil(n / 64)); pads are identity rows.
+void launch_dense_from_csr(int64_t n, int64_t ld, const int64_t *rp, const int32_t *ci, const double *val, double *M,
+                           hipStream_t st);
+// In place M := M^-1 by blocked Gauss-Jordan (no pivoting); D: 64 x 64 scratch;
+// *fail |= 1 on a zero pivot.
+void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStream_t st);
+// y = M[:n, :n] x
+void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, double *y, hipStream_t st);
 
 }  // namespace pls

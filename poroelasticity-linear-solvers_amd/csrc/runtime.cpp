@@ -586,7 +586,9 @@ static void envelope_csr(const DevCSR &M, DevCSR &E, Ctx &c) {
         lo[i] = a;
         hi[i] = std::max<int64_t>(hmax, i);
         erp[i + 1] = erp[i] + (hi[i] - lo[i] + 1);
-        if (hi[i] - lo[i] + 1 > 5461) throw Error("lu: profile row longer than 5461 entries; use ilu/bjacobi");
+        if (hi[i] - lo[i] + 1 > ilu0_max_row())
+            throw Error("lu: profile row longer than " + std::to_string(ilu0_max_row()) +
+                        " entries; use ilu/bjacobi");
     }
     if (erp[n] > 400000000LL) throw Error("lu: profile fill exceeds 4e8 entries; use ilu/bjacobi on the device");
     std::vector<int32_t> eci(erp[n]);
@@ -615,7 +617,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
     }
     if (exact) envelope_csr(M, F, c);
     else extract_csr(M, 0, n, w, 0, n, F, c);
-    if (F.max_row * 12 > 65536) throw Error("ILU(0): row too long for the LDS-staged factorization");
+    if (F.max_row > ilu0_max_row()) throw Error("ILU(0): row too long for the LDS-staged factorization");
     diag.alloc(std::max<int64_t>(n, 1));
     dinv.alloc(std::max<int64_t>(n, 1));
     DBuf<int32_t> fail(1);
@@ -640,7 +642,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         HIPCHK(hipMemcpyAsync(rowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
         for (int64_t l = 0; l < nlev_L; ++l)
             launch_ilu0_level(Lptr[l + 1] - Lptr[l], rowsL.p + Lptr[l], F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p,
-                              fail.p, c.st);
+                              fail.p, F.max_row, c.st);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
         c.sync();
@@ -708,6 +710,26 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
     Uf.apply(y, y, c);
 }
 
+PCDenseLU::PCDenseLU(const DevCSR &M, Ctx &c) {
+    type = "lu";
+    n = M.nrows;
+    if (M.ncols != n) throw Error("lu: block is not square");
+    ld = std::max<int64_t>(64, (n + 63) / 64 * 64);
+    inv.alloc(ld * ld);
+    launch_dense_from_csr(n, ld, M.rp.p, M.ci.p, M.val.p, inv.p, c.st);
+    DBuf<double> D(64 * 64);
+    DBuf<int32_t> fail(1);
+    HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
+    launch_dense_invert(ld, inv.p, D.p, fail.p, c.st);
+    HIPCHK(hipGetLastError());
+    int32_t hfail = 0;
+    HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    if (hfail) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+}
+
+void PCDenseLU::apply(const double *x, double *y, Ctx &c) { launch_dense_gemv(n, ld, inv.p, x, y, c.st); }
+
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c) {
     if (type == "none") return std::make_unique<PCNone>(M.nrows);
@@ -722,6 +744,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         return std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true));
     }
     if (type == "lu" || type == "cholesky") {
+        if (M.nrows <= o.integer("pls.lu_dense_max", 32768)) return std::make_unique<PCDenseLU>(M, c);
         return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true));
     }
     if (type == "bjacobi") {

@@ -245,6 +245,16 @@ struct PCILU : PC {
     bool reentrant() const override { return profile_tag.empty(); }
     void apply(const double *x, double *y, Ctx &c) override;
 };
+// Exact LU of a block small enough for a dense inverse (dense.hip): K^-1 is
+// formed once (blocked Gauss-Jordan, no pivoting, like the sparse path) and
+// applied as one dense GEMV.  Chosen for -pc_type lu when n <= pls.lu_dense_max.
+struct PCDenseLU : PC {
+    int64_t ld = 0;
+    DBuf<double> inv;
+    PCDenseLU(const DevCSR &M, Ctx &c);
+    bool reentrant() const override { return true; }
+    void apply(const double *x, double *y, Ctx &c) override;
+};
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c);
 // Smoothed-aggregation AMG (amg.cpp; -pc_type gamg, and hypre unless pls.hypre error).

@@ -278,19 +278,30 @@ def test_facade_end_to_end(gpu):
     popts.DB.clear()
 
 
+# exact LU on the device: the dense Gauss-Jordan inverse (blocks up to
+# pls.lu_dense_max rows, default) and the envelope-pattern sparse LU
+LU_PATHS = {"dense": {}, "envelope": {"pls.lu_dense_max": "0"}}
+
+
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
-def test_exact_lu_inner_blocks(gpu, pc_type):
+@pytest.mark.parametrize("lu_path", sorted(LU_PATHS))
+def test_exact_lu_inner_blocks(gpu, pc_type, lu_path):
     """The reference's exact configuration: every block PREONLY + LU."""
     db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right"}
     for pre in ("s_", "f_", "p_", "diff_", "fp_"):
         db[pre + "ksp_type"] = "preonly"
         db[pre + "pc_type"] = "lu"
+    db.update(LU_PATHS[lu_path])
     _compare_solve(S.SynthSpec(2, 10), {"pc type": pc_type, "inner pc type": "lu"}, db=db)
 
 
-def test_exact_lu_pc_apply_is_exact(gpu):
-    spec = S.SynthSpec(3, 2)
+@pytest.mark.parametrize("lu_path,dim,N", [("dense", 3, 2), ("envelope", 3, 2), ("dense", 3, 3), ("dense", 2, 16)])
+def test_exact_lu_pc_apply_is_exact(gpu, lu_path, dim, N):
+    """||P_lower y - x|| at rounding level: multi-block Gauss-Jordan (n not a
+    multiple of 64) and the envelope LU."""
+    spec = S.SynthSpec(dim, N)
     db = {p + k: v for p in ("s_", "fp_") for k, v in (("ksp_type", "preonly"), ("pc_type", "lu"))}
+    db.update(LU_PATHS[lu_path])
     h = _handle(spec, dict(BASE, **{"inner pc type": "lu"}), db)
     P = S.matrix(spec, 1).toarray()
     ns = spec.sizes()[0]
