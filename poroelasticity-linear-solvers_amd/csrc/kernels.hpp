@@ -185,4 +185,20 @@ void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStr
 // y = M[:n, :n] x
 void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, double *y, hipStream_t st);
 
+// ------------------------------------------------- banded exact LU (band.hip) --
+// T: nb tile rows x (bl + bu + 1) tiles of 64 x 64 (see band.hip); padding
+// rows past n are identity rows.
+void launch_band_from_csr(int64_t n, int64_t nb, int64_t bl, int64_t bu, const int64_t *rp, const int32_t *ci,
+                          const double *val, double *T, hipStream_t st);
+// In place LU without pivoting; Dl / Du: nb inverted diagonal triangles;
+// *fail |= 1 on a zero pivot.
+void launch_band_factor(int64_t nb, int64_t bl, int64_t bu, double *T, double *Dl, double *Du, int32_t *fail,
+                        hipStream_t st);
+// One triangular sweep (upper 0: L with Dl, 1: U with Du), y != b.  epoch:
+// fresh per sweep, never 0; ticket_base: tickets drawn by earlier sweeps
+// (nb per sweep) on `ticket`; *fail |= 2 if a spin gave up.
+void launch_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu, const double *T, const double *Dinv,
+                       const double *b, double *y, int32_t *flags, uint64_t *ticket, uint64_t ticket_base,
+                       int32_t epoch, int upper, int32_t *fail, hipStream_t st);
+
 }  // namespace pls

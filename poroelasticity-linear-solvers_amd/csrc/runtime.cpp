@@ -730,6 +730,79 @@ PCDenseLU::PCDenseLU(const DevCSR &M, Ctx &c) {
 
 void PCDenseLU::apply(const double *x, double *y, Ctx &c) { launch_dense_gemv(n, ld, inv.p, x, y, c.st); }
 
+void csr_bandwidths(const DevCSR &M, int64_t &kl, int64_t &ku, Ctx &c) {
+    const int64_t n = M.nrows;
+    kl = ku = 0;
+    if (n == 0) return;
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> ci(M.nnz);
+    HIPCHK(hipMemcpyAsync(rp.data(), M.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, c.st));
+    if (M.nnz) HIPCHK(hipMemcpyAsync(ci.data(), M.ci.p, sizeof(int32_t) * M.nnz, hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    for (int64_t i = 0; i < n; ++i) {
+        if (rp[i + 1] == rp[i]) continue;
+        kl = std::max<int64_t>(kl, i - ci[rp[i]]);
+        ku = std::max<int64_t>(ku, ci[rp[i + 1] - 1] - i);
+    }
+}
+
+PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c) {
+    type = "lu";
+    n = M.nrows;
+    if (M.ncols != n) throw Error("lu: block is not square");
+    nb = (n + 63) / 64;
+    bl = (kl + 63) / 64;
+    bu = (ku + 63) / 64;
+    const int64_t W = bl + bu + 1;
+    T.alloc((size_t)(nb * W) * 4096);
+    Dl.alloc((size_t)nb * 4096);
+    Du.alloc((size_t)nb * 4096);
+    t.alloc(std::max<int64_t>(n, 1));
+    flags.alloc(std::max<int64_t>(nb, 1));
+    fail.alloc(1);
+    ticket.alloc(1);
+    HIPCHK(hipMemsetAsync(flags.p, 0, sizeof(int32_t) * flags.n, c.st));
+    HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
+    HIPCHK(hipMemsetAsync(ticket.p, 0, sizeof(uint64_t), c.st));
+    launch_band_from_csr(n, nb, bl, bu, M.rp.p, M.ci.p, M.val.p, T.p, c.st);
+    launch_band_factor(nb, bl, bu, T.p, Dl.p, Du.p, fail.p, c.st);
+    HIPCHK(hipGetLastError());
+    if (check_fail(c)) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+}
+
+int32_t PCBandLU::check_fail(Ctx &c) {
+    int32_t h = 0;
+    HIPCHK(hipMemcpyAsync(&h, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    return h;
+}
+
+void PCBandLU::apply(const double *x, double *y, Ctx &c) {
+    // epochs 2s+1, 2s+2 (never 0); each sweep draws nb tickets
+    launch_band_sweep(n, nb, bl, bu, T.p, Dl.p, x, t.p, flags.p, ticket.p, sweeps * nb, (int32_t)(sweeps + 1), 0,
+                      fail.p, c.st);
+    ++sweeps;
+    launch_band_sweep(n, nb, bl, bu, T.p, Du.p, t.p, y, flags.p, ticket.p, sweeps * nb, (int32_t)(sweeps + 1), 1,
+                      fail.p, c.st);
+    ++sweeps;
+}
+
+std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
+    const std::string path = o.str("pls.lu_path", "auto");
+    if (path != "auto" && path != "dense" && path != "band" && path != "envelope")
+        throw Error("pls.lu_path " + path + " (auto, dense, band, envelope)");
+    if (path == "dense" || (path == "auto" && M.nrows <= o.integer("pls.lu_dense_max", 32768)))
+        return std::make_unique<PCDenseLU>(M, c);
+    if (path == "band" || path == "auto") {
+        int64_t kl = 0, ku = 0;
+        csr_bandwidths(M, kl, ku, c);
+        const double nbt = (double)((M.nrows + 63) / 64), w = (double)((kl + 63) / 64 + (ku + 63) / 64 + 1);
+        const double gb = nbt * w * 4096.0 * 8.0 / 1e9;
+        if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 64.0)) return std::make_unique<PCBandLU>(M, kl, ku, c);
+    }
+    return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true));
+}
+
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c) {
     if (type == "none") return std::make_unique<PCNone>(M.nrows);
@@ -743,10 +816,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
             throw Error(prefix + "pc_factor_levels > 0: only ILU(0) is implemented");
         return std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true));
     }
-    if (type == "lu" || type == "cholesky") {
-        if (M.nrows <= o.integer("pls.lu_dense_max", 32768)) return std::make_unique<PCDenseLU>(M, c);
-        return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true));
-    }
+    if (type == "lu" || type == "cholesky") return make_lu(M, o, c);
     if (type == "bjacobi") {
         // total blocks over all ranks (PCBJacobiSetTotalBlocks): rank r gets
         // B / size (+1 for the first B % size ranks); at least one per rank

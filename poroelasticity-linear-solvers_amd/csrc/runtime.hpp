@@ -255,6 +255,26 @@ struct PCDenseLU : PC {
     bool reentrant() const override { return true; }
     void apply(const double *x, double *y, Ctx &c) override;
 };
+// Exact LU of a banded block past the dense-inverse size (band.hip): 64 x 64
+// tiles, right-looking factorization without pivoting, flag-chained sweeps.
+// Not reentrant (the sweeps share the flags, the ticket and t).
+struct PCBandLU : PC {
+    int64_t nb = 0, bl = 0, bu = 0;
+    DBuf<double> T, Dl, Du, t;
+    DBuf<int32_t> flags, fail;
+    DBuf<uint64_t> ticket;
+    uint64_t sweeps = 0;  // launched sweeps (ticket base = sweeps * nb)
+    PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c);
+    void apply(const double *x, double *y, Ctx &c) override;
+    int32_t check_fail(Ctx &c);  // synchronising: the fail word (2: a sweep spin gave up)
+};
+// Lower / upper bandwidth of a square CSR matrix with sorted rows.
+void csr_bandwidths(const DevCSR &M, int64_t &kl, int64_t &ku, Ctx &c);
+// -pc_type lu / cholesky (MUMPS in the reference): dense inverse up to
+// pls.lu_dense_max rows, else the band LU while its tiles fit
+// pls.lu_band_max_gb, else the envelope LU; pls.lu_path dense|band|envelope
+// forces one.
+std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c);
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c);
 // Smoothed-aggregation AMG (amg.cpp; -pc_type gamg, and hypre unless pls.hypre error).

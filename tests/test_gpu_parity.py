@@ -279,8 +279,9 @@ def test_facade_end_to_end(gpu):
 
 
 # exact LU on the device: the dense Gauss-Jordan inverse (blocks up to
-# pls.lu_dense_max rows, default) and the envelope-pattern sparse LU
-LU_PATHS = {"dense": {}, "envelope": {"pls.lu_dense_max": "0"}}
+# pls.lu_dense_max rows, default), the 64 x 64-tile band LU with flag-chained
+# sweeps, and the envelope-pattern sparse LU
+LU_PATHS = {"dense": {}, "band": {"pls.lu_path": "band"}, "envelope": {"pls.lu_path": "envelope"}}
 
 
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
@@ -295,10 +296,12 @@ def test_exact_lu_inner_blocks(gpu, pc_type, lu_path):
     _compare_solve(S.SynthSpec(2, 10), {"pc type": pc_type, "inner pc type": "lu"}, db=db)
 
 
-@pytest.mark.parametrize("lu_path,dim,N", [("dense", 3, 2), ("envelope", 3, 2), ("dense", 3, 3), ("dense", 2, 16)])
+@pytest.mark.parametrize("lu_path,dim,N", [("dense", 3, 2), ("envelope", 3, 2), ("dense", 3, 3), ("dense", 2, 16),
+                                           ("band", 3, 2), ("band", 2, 16), ("band", 2, 48), ("band", 3, 5)])
 def test_exact_lu_pc_apply_is_exact(gpu, lu_path, dim, N):
     """||P_lower y - x|| at rounding level: multi-block Gauss-Jordan (n not a
-    multiple of 64) and the envelope LU."""
+    multiple of 64), the band LU (2-D N=48: 295 / 343 tile rows, more than
+    one flag-chained hop per resident workgroup) and the envelope LU."""
     spec = S.SynthSpec(dim, N)
     db = {p + k: v for p in ("s_", "fp_") for k, v in (("ksp_type", "preonly"), ("pc_type", "lu"))}
     db.update(LU_PATHS[lu_path])
@@ -374,11 +377,13 @@ FS_INEXACT = {  # petsc-options-inexact:73-114 with BoomerAMG -> Jacobi / ILU(0)
 FS_PARAMS = {"inner ksp type": "cg", "inner pc type": "hypre"}
 
 
-@pytest.mark.parametrize("variant", ["inexact", "lower_ilu", "full_implicit", "upper", "diag", "multiplicative",
-                                     "additive", "default"])
+@pytest.mark.parametrize("variant", ["inexact", "inexact_band_lu", "lower_ilu", "full_implicit", "upper", "diag",
+                                     "multiplicative", "additive", "default"])
 def test_fieldsplit_fp(gpu, variant):
     db = dict(FS_INEXACT)
-    if variant == "lower_ilu":
+    if variant == "inexact_band_lu":  # the Schur block's LU on the band path (the footing configuration's)
+        db["pls.lu_path"] = "band"
+    elif variant == "lower_ilu":
         db.update({"fp_fieldsplit_0_ksp_type": "preonly", "fp_fieldsplit_0_pc_type": "ilu",
                    "fp_fieldsplit_1_pc_type": "ilu"})
     elif variant == "full_implicit":  # Schur KSP on the implicit S, preconditioned by ILU(selfp)
