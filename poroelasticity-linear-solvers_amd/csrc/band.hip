@@ -26,13 +26,12 @@
 // already running (no dispatch-order or residency assumption); each
 // accumulates its band tiles against the y blocks as they are published, the
 // nearest block last, and publishes y_I = Dinv_I r_I.  Hand-off (the producer
-// may sit on another XCD; cdna_hip_programming.md Guideline 16, R1): y stored
-// write-through (global sc1), every storing wave drains (vmcnt(0)), workgroup
-// barrier, one lane stores the tile row's flag (sc1); the consumer polls the
-// flag from one lane (sc1, bounded spin), joins a barrier, and reads y with
-// global sc1 loads only.  The sums run in a fixed order, so the result does
-// not depend on timing.  HBM traffic is the band once per sweep; the critical
-// path is one hop per 64 rows.
+// may sit on another XCD; cdna_hip_programming.md Guideline 16, R2): y_I is
+// published as tagged 8-byte granules (sc1 stores) that a consumer wave
+// re-reads (sc1 loads, bounded spin) until every tag carries this sweep's
+// epoch -- no flag, fence or drain.  The sums run in a fixed order, so the
+// result does not depend on timing.  HBM traffic is the band once per sweep;
+// the critical path is one hop per 64 rows.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -45,8 +44,7 @@ static constexpr int BT = 64;     // tile size
 static constexpr int BTPB = 256;  // threads per workgroup
 static constexpr int64_t TILE = BT * BT;
 
-typedef __attribute__((address_space(1))) double gf64;
-typedef __attribute__((address_space(1))) int32_t gi32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
 
 // ------------------------------------------------------------------ build --
 // identity on the padding diagonal (T zeroed first), then the CSR rows
@@ -84,8 +82,14 @@ __global__ __launch_bounds__(BTPB) void k_band_diag(int64_t W, int64_t bl, int64
     __shared__ double li[BT][BT + 1];
     __shared__ double ui[BT][BT + 1];
     double *src = T + (K * W + bl) * TILE;
-    for (int t = threadIdx.x; t < BT * BT; t += BTPB) a[t / BT][t % BT] = src[t];
+    for (int t = threadIdx.x; t < BT * BT; t += BTPB) {
+        const int i = t / BT, j = t % BT;
+        a[i][j] = src[t];
+        li[i][j] = ui[i][j] = (i == j) ? 1.0 : 0.0;
+    }
     __syncthreads();
+    // forward elimination of [A | I]: A -> L\U, I -> L^-1 (the same row
+    // operations); every thread updates 32 entries per step
     for (int p = 0; p < BT; ++p) {
         const double piv = a[p][p];
         if (piv == 0.0) {
@@ -94,33 +98,29 @@ __global__ __launch_bounds__(BTPB) void k_band_diag(int64_t W, int64_t bl, int64
         }
         if (p == BT - 1) break;
         __syncthreads();
-        // multipliers l_ip = a_ip / piv, then the trailing update
-        if (threadIdx.x > p && threadIdx.x < BT) a[threadIdx.x][p] = a[threadIdx.x][p] / piv;
+        if (threadIdx.x > p && threadIdx.x < BT) a[threadIdx.x][p] = a[threadIdx.x][p] / piv;  // l_ip
         __syncthreads();
-        for (int t = threadIdx.x; t < BT * BT; t += BTPB) {
+        for (int t = threadIdx.x; t < 2 * BT * BT; t += BTPB) {
+            const int i = t / (2 * BT), j = t % (2 * BT);
+            if (i <= p) continue;
+            if (j < BT) {
+                if (j > p) a[i][j] = a[i][j] - a[i][p] * a[p][j];
+            } else if (j - BT <= p) {
+                li[i][j - BT] = li[i][j - BT] - a[i][p] * li[p][j - BT];
+            }
+        }
+        __syncthreads();
+    }
+    // backward elimination of [U | I] -> U^-1 (U itself stays in a)
+    for (int p = BT - 1; p >= 0; --p) {
+        if (threadIdx.x >= p && threadIdx.x < BT) ui[p][threadIdx.x] = ui[p][threadIdx.x] / a[p][p];
+        __syncthreads();
+        for (int t = threadIdx.x; t < p * BT; t += BTPB) {
             const int i = t / BT, j = t % BT;
-            if (i > p && j > p) a[i][j] = a[i][j] - a[i][p] * a[p][j];
+            if (j >= p) ui[i][j] = ui[i][j] - a[i][p] * ui[p][j];
         }
         __syncthreads();
     }
-    // triangular inverses, one column per thread: L^-1 e_j by forward and
-    // U^-1 e_j by backward substitution
-    if (threadIdx.x < BT) {
-        const int j = threadIdx.x;
-        for (int i = 0; i < BT; ++i) {
-            double s = (i == j) ? 1.0 : 0.0;
-            for (int k = j; k < i; ++k) s = s - a[i][k] * li[k][j];
-            li[i][j] = (i < j) ? 0.0 : s;
-        }
-    } else if (threadIdx.x < 2 * BT) {
-        const int j = threadIdx.x - BT;
-        for (int i = BT - 1; i >= 0; --i) {
-            double s = (i == j) ? 1.0 : 0.0;
-            for (int k = i + 1; k <= j; ++k) s = s - a[i][k] * ui[k][j];
-            ui[i][j] = (i > j) ? 0.0 : s / a[i][i];
-        }
-    }
-    __syncthreads();
     for (int t = threadIdx.x; t < BT * BT; t += BTPB) {
         const int i = t / BT, j = t % BT;
         src[t] = a[i][j];
@@ -222,14 +222,19 @@ typedef double bd_d2 __attribute__((ext_vector_type(2)));
 // One triangle (upper = 0: forward with L and Dl; 1: backward with U and Du):
 // y_I = Dinv_I (b_I - sum_J T_IJ y_J).  Thread t owns row t / 4 and columns
 // 16 (t % 4) .. +16 of every tile; b and y have n entries (padding rows are 0
-// and never stored); b must not alias y.  flags[I] == epoch publishes y_I;
-// the caller passes a fresh epoch (never 0) and the ticket count of all
-// earlier sweeps on this counter as ticket_base.
+// and never stored); b must not alias y.
+// Hand-off (Guideline 16 R2, the data is the flag): y_I is published as 128
+// 8-byte granules {epoch, 32 bits of y} in G (tile row I: G[128 I + 2 r + h],
+// h = 0 low / 1 high half of row r), each written by ONE sc1 store; a
+// consumer wave re-reads a tile row's 128 granules with sc1 loads until every
+// tag equals this sweep's epoch (bounded spin), then stages y_J in LDS.  No
+// flag, no fence, no drain.  The caller passes a fresh epoch (never 0; G
+// starts zeroed) and the ticket count of all earlier sweeps as ticket_base.
 __global__ __launch_bounds__(BTPB) void k_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu,
                                                      const double *__restrict__ T, const double *__restrict__ Dinv,
-                                                     const double *__restrict__ b, double *y, int32_t *flags,
-                                                     uint64_t *ticket, uint64_t ticket_base, int32_t epoch, int upper,
-                                                     int32_t *fail) {
+                                                     const double *__restrict__ b, double *__restrict__ y,
+                                                     uint64_t *G, uint64_t *ticket, uint64_t ticket_base,
+                                                     uint32_t epoch, int upper, int32_t *fail) {
     __shared__ int64_t sI;
     __shared__ double ys[BT];
     __shared__ double rs[BT];
@@ -240,8 +245,7 @@ __global__ __launch_bounds__(BTPB) void k_band_sweep(int64_t n, int64_t nb, int6
     const int64_t I = upper ? nb - 1 - tk : tk;
     const int64_t W = bl + bu + 1;
     const int row = threadIdx.x >> 2, part = threadIdx.x & 3;
-    gf64 *gy = (gf64 *)y;
-    gi32 *gflag = (gi32 *)flags;
+    gu64 *gg = (gu64 *)G;
     const int64_t gi = I * BT + row;
     // everything off the dependency chain is loaded first
     const double bi = (part == 0 && gi < n) ? b[gi] : 0.0;
@@ -267,20 +271,22 @@ __global__ __launch_bounds__(BTPB) void k_band_sweep(int64_t n, int64_t nb, int6
         bd_d2 m[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) m[u] = __builtin_nontemporal_load(tile + u);
-        if (threadIdx.x == 0) {
-            int64_t spins = 0;
-            while (__hip_atomic_load(gflag + J, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1ll << 26)) {  // never expected: report instead of hanging the queue
-                    atomicOr(fail, 2);
+        if (threadIdx.x < 64) {  // wave 0 sweeps tile row J's granules
+            const int l = threadIdx.x;
+            gu64 *g = gg + J * 128 + 2 * l;
+            uint64_t lo = 0, hi = 0;
+            for (int64_t spins = 0;; ++spins) {
+                lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool ok = (uint32_t)(lo >> 32) == epoch && (uint32_t)(hi >> 32) == epoch;
+                if (__all(ok)) break;
+                if (spins > (1ll << 26)) {  // never expected: report instead of hanging the queue
+                    if (l == 0) atomicOr(fail, 2);
                     break;
                 }
+                __builtin_amdgcn_s_sleep(1);
             }
-        }
-        __syncthreads();
-        if (threadIdx.x < BT) {
-            const int64_t gj = J * BT + threadIdx.x;
-            ys[threadIdx.x] = gj < n ? __hip_atomic_load(gy + gj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+            ys[l] = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
         }
         __syncthreads();
 #pragma unroll
@@ -302,17 +308,21 @@ __global__ __launch_bounds__(BTPB) void k_band_sweep(int64_t n, int64_t nb, int6
     }
     z += __shfl_xor(z, 1);
     z += __shfl_xor(z, 2);
-    if (part == 0 && gi < n) __hip_atomic_store(gy + gi, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(gflag + I, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (part == 0) {
+        const uint64_t bits = gi < n ? (uint64_t)__double_as_longlong(z) : 0ull;  // padding rows publish 0
+        const uint64_t tag = (uint64_t)epoch << 32;
+        __hip_atomic_store(gg + I * 128 + 2 * row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gg + I * 128 + 2 * row + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (gi < n) y[gi] = z;
+    }
 }
 
 void launch_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu, const double *T, const double *Dinv,
-                       const double *b, double *y, int32_t *flags, uint64_t *ticket, uint64_t ticket_base,
-                       int32_t epoch, int upper, int32_t *fail, hipStream_t st) {
+                       const double *b, double *y, uint64_t *G, uint64_t *ticket, uint64_t ticket_base,
+                       uint32_t epoch, int upper, int32_t *fail, hipStream_t st) {
     if (nb > 0)
-        k_band_sweep<<<(unsigned)nb, BTPB, 0, st>>>(n, nb, bl, bu, T, Dinv, b, y, flags, ticket, ticket_base, epoch,
+        k_band_sweep<<<(unsigned)nb, BTPB, 0, st>>>(n, nb, bl, bu, T, Dinv, b, y, G, ticket, ticket_base, epoch,
                                                    upper, fail);
 }
 

@@ -194,11 +194,12 @@ void launch_band_from_csr(int64_t n, int64_t nb, int64_t bl, int64_t bu, const i
 // *fail |= 1 on a zero pivot.
 void launch_band_factor(int64_t nb, int64_t bl, int64_t bu, double *T, double *Dl, double *Du, int32_t *fail,
                         hipStream_t st);
-// One triangular sweep (upper 0: L with Dl, 1: U with Du), y != b.  epoch:
-// fresh per sweep, never 0; ticket_base: tickets drawn by earlier sweeps
-// (nb per sweep) on `ticket`; *fail |= 2 if a spin gave up.
+// One triangular sweep (upper 0: L with Dl, 1: U with Du), y != b.  G: 128
+// tagged granules per tile row (zeroed once); epoch: fresh per sweep, never 0;
+// ticket_base: tickets drawn by earlier sweeps (nb per sweep) on `ticket`;
+// *fail |= 2 if a spin gave up.
 void launch_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu, const double *T, const double *Dinv,
-                       const double *b, double *y, int32_t *flags, uint64_t *ticket, uint64_t ticket_base,
-                       int32_t epoch, int upper, int32_t *fail, hipStream_t st);
+                       const double *b, double *y, uint64_t *G, uint64_t *ticket, uint64_t ticket_base,
+                       uint32_t epoch, int upper, int32_t *fail, hipStream_t st);
 
 }  // namespace pls

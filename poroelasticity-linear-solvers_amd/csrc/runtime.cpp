@@ -758,10 +758,10 @@ PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c) {
     Dl.alloc((size_t)nb * 4096);
     Du.alloc((size_t)nb * 4096);
     t.alloc(std::max<int64_t>(n, 1));
-    flags.alloc(std::max<int64_t>(nb, 1));
+    G.alloc((size_t)std::max<int64_t>(nb, 1) * 128);
     fail.alloc(1);
     ticket.alloc(1);
-    HIPCHK(hipMemsetAsync(flags.p, 0, sizeof(int32_t) * flags.n, c.st));
+    HIPCHK(hipMemsetAsync(G.p, 0, sizeof(uint64_t) * G.n, c.st));
     HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
     HIPCHK(hipMemsetAsync(ticket.p, 0, sizeof(uint64_t), c.st));
     launch_band_from_csr(n, nb, bl, bu, M.rp.p, M.ci.p, M.val.p, T.p, c.st);
@@ -779,10 +779,10 @@ int32_t PCBandLU::check_fail(Ctx &c) {
 
 void PCBandLU::apply(const double *x, double *y, Ctx &c) {
     // epochs 2s+1, 2s+2 (never 0); each sweep draws nb tickets
-    launch_band_sweep(n, nb, bl, bu, T.p, Dl.p, x, t.p, flags.p, ticket.p, sweeps * nb, (int32_t)(sweeps + 1), 0,
+    launch_band_sweep(n, nb, bl, bu, T.p, Dl.p, x, t.p, G.p, ticket.p, sweeps * nb, (uint32_t)(sweeps + 1), 0,
                       fail.p, c.st);
     ++sweeps;
-    launch_band_sweep(n, nb, bl, bu, T.p, Du.p, t.p, y, flags.p, ticket.p, sweeps * nb, (int32_t)(sweeps + 1), 1,
+    launch_band_sweep(n, nb, bl, bu, T.p, Du.p, t.p, y, G.p, ticket.p, sweeps * nb, (uint32_t)(sweeps + 1), 1,
                       fail.p, c.st);
     ++sweeps;
 }

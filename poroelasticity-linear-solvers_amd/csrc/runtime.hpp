@@ -257,12 +257,12 @@ struct PCDenseLU : PC {
 };
 // Exact LU of a banded block past the dense-inverse size (band.hip): 64 x 64
 // tiles, right-looking factorization without pivoting, flag-chained sweeps.
-// Not reentrant (the sweeps share the flags, the ticket and t).
+// Not reentrant (the sweeps share the granules, the ticket and t).
 struct PCBandLU : PC {
     int64_t nb = 0, bl = 0, bu = 0;
     DBuf<double> T, Dl, Du, t;
-    DBuf<int32_t> flags, fail;
-    DBuf<uint64_t> ticket;
+    DBuf<int32_t> fail;
+    DBuf<uint64_t> G, ticket;  // G: 128 tagged granules per tile row (the sweeps' hand-off)
     uint64_t sweeps = 0;  // launched sweeps (ticket base = sweeps * nb)
     PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c);
     void apply(const double *x, double *y, Ctx &c) override;

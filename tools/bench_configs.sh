@@ -14,6 +14,7 @@ run() {  # run <name> <args...>
     echo "rc=$rc"; grep '^{' "gpurun_out/configs/$name.log" | cut -c1-900 || tail -n 20 "gpurun_out/configs/$name.log"
     [ $rc -eq 0 ] || exit $rc
 }
+run headline --steps 5
 run swelling2d-exact --config swelling2d-exact --steps 3 --no-copy-probe
 run footing-inexact-ilu --config footing-inexact-ilu --steps 2 --no-copy-probe
 run aar-m5 --config aar-m5 --steps 2 --no-copy-probe
