@@ -203,8 +203,29 @@ __global__ __launch_bounds__(BTPB) void k_band_update(int64_t nb, int64_t W, int
         }
 }
 
-void launch_band_factor(int64_t nb, int64_t bl, int64_t bu, double *T, double *Dl, double *Du, int32_t *fail,
-                        hipStream_t st) {
+// Near-tile products for the sweeps: Gl[I] = Dl_I L_{I,I-1} (I >= 1) and
+// Gu[I] = Du_I U_{I,I+1} (I <= nb - 2); blockIdx.y selects the triangle.
+__global__ __launch_bounds__(BTPB) void k_band_near(int64_t nb, int64_t bl, int64_t bu, const double *T,
+                                                    const double *Dl, const double *Du, double *Gl, double *Gu) {
+    __shared__ double at[BT][BT + 1];
+    __shared__ double b[BT][BT + 1];
+    const int64_t I = blockIdx.x, W = bl + bu + 1;
+    const bool up = blockIdx.y == 1;
+    if (up ? (I >= nb - 1 || bu == 0) : (I < 1 || bl == 0)) return;
+    const int64_t J = up ? I + 1 : I - 1;
+    double acc[4][4];
+    band_tile_mm((up ? Du : Dl) + I * TILE, T + (I * W + (J - I + bl)) * TILE, at, b, acc);
+    double *C = (up ? Gu : Gl) + I * TILE;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) C[(ty + 16 * r) * BT + tx + 16 * q] = acc[r][q];
+}
+
+void launch_band_factor(int64_t nb, int64_t bl, int64_t bu, double *T, double *Dl, double *Du, double *Gl,
+                        double *Gu, int32_t *fail, hipStream_t st) {
+    if (nb <= 0) return;
     const int64_t W = bl + bu + 1;
     for (int64_t K = 0; K < nb; ++K) {
         k_band_diag<<<1, BTPB, 0, st>>>(W, bl, K, T, Dl, Du, fail);
@@ -214,116 +235,179 @@ void launch_band_factor(int64_t nb, int64_t bl, int64_t bu, double *T, double *D
         k_band_panels<<<(unsigned)(bl + pu), BTPB, 0, st>>>(nb, W, bl, K, T, Dl, Du);
         if (pl > 0 && pu > 0) k_band_update<<<dim3((unsigned)pu, (unsigned)pl), BTPB, 0, st>>>(nb, W, bl, K, T);
     }
+    (void)hipMemsetAsync(Gl, 0, sizeof(double) * (size_t)(nb * TILE), st);
+    (void)hipMemsetAsync(Gu, 0, sizeof(double) * (size_t)(nb * TILE), st);
+    if (nb > 1) k_band_near<<<dim3((unsigned)nb, 2), BTPB, 0, st>>>(nb, bl, bu, T, Dl, Du, Gl, Gu);
 }
 
 // ------------------------------------------------------------------ sweeps --
 typedef double bd_d2 __attribute__((ext_vector_type(2)));
 
-// One triangle (upper = 0: forward with L and Dl; 1: backward with U and Du):
-// y_I = Dinv_I (b_I - sum_J T_IJ y_J).  Thread t owns row t / 4 and columns
-// 16 (t % 4) .. +16 of every tile; b and y have n entries (padding rows are 0
-// and never stored); b must not alias y.
+// One triangle (upper = 0: forward with L, Dl, Gl; 1: backward with U, Du,
+// Gu), walked in "positions" p (p = I forward, nb - 1 - I backward) so both
+// directions read alike.  A workgroup of SR x 256 threads takes SR = 2
+// consecutive positions (a super-row: one cross-workgroup hop per 128 rows);
+// group g (4 waves) owns position p0 + g, its thread t owns row t / 4 and
+// columns 16 (t % 4) .. +16 of every tile.  With bw tiles of the band on the
+// solved side,
+//     y_I = c_I - G_I y_near,   c_I = Dinv_I (b_I - sum_{J far} T_IJ y_J),
+// so the chain from the neighbouring tile row's y to y_I is one preloaded
+// tile product (G = Gl or Gu).  b and y have n entries (padding rows are 0
+// and never stored); b != y.
 // Hand-off (Guideline 16 R2, the data is the flag): y_I is published as 128
-// 8-byte granules {epoch, 32 bits of y} in G (tile row I: G[128 I + 2 r + h],
-// h = 0 low / 1 high half of row r), each written by ONE sc1 store; a
-// consumer wave re-reads a tile row's 128 granules with sc1 loads until every
-// tag equals this sweep's epoch (bounded spin), then stages y_J in LDS.  No
-// flag, no fence, no drain.  The caller passes a fresh epoch (never 0; G
-// starts zeroed) and the ticket count of all earlier sweeps as ticket_base.
-__global__ __launch_bounds__(BTPB) void k_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu,
-                                                     const double *__restrict__ T, const double *__restrict__ Dinv,
-                                                     const double *__restrict__ b, double *__restrict__ y,
-                                                     uint64_t *G, uint64_t *ticket, uint64_t ticket_base,
-                                                     uint32_t epoch, int upper, int32_t *fail) {
-    __shared__ int64_t sI;
-    __shared__ double ys[BT];
-    __shared__ double rs[BT];
-    if (threadIdx.x == 0) sI = (int64_t)(atomicAdd((unsigned long long *)ticket, 1ull) - ticket_base);
-    __syncthreads();
-    const int64_t tk = sI;
-    if (tk < 0 || tk >= nb) return;  // uniform
-    const int64_t I = upper ? nb - 1 - tk : tk;
-    const int64_t W = bl + bu + 1;
-    const int row = threadIdx.x >> 2, part = threadIdx.x & 3;
-    gu64 *gg = (gu64 *)G;
-    const int64_t gi = I * BT + row;
-    // everything off the dependency chain is loaded first
-    const double bi = (part == 0 && gi < n) ? b[gi] : 0.0;
-    bd_d2 dm[8];
-    {
-        const bd_d2 *dt = reinterpret_cast<const bd_d2 *>(Dinv + I * TILE + row * BT + part * 16);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) dm[u] = dt[u];
-    }
-    int64_t J0, nJ;  // tiles to accumulate, farthest first
-    if (upper) {
-        J0 = (I + bu < nb - 1) ? I + bu : nb - 1;
-        nJ = J0 - I;
-    } else {
-        J0 = (I - bl > 0) ? I - bl : 0;
-        nJ = I - J0;
-    }
-    double acc = 0.0;
-    for (int64_t s = 0; s < nJ; ++s) {
-        const int64_t J = upper ? J0 - s : J0 + s;
-        const bd_d2 *tile =
-            reinterpret_cast<const bd_d2 *>(T + (I * W + (J - I + bl)) * TILE + row * BT + part * 16);
-        bd_d2 m[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) m[u] = __builtin_nontemporal_load(tile + u);
-        if (threadIdx.x < 64) {  // wave 0 sweeps tile row J's granules
-            const int l = threadIdx.x;
-            gu64 *g = gg + J * 128 + 2 * l;
-            uint64_t lo = 0, hi = 0;
-            for (int64_t spins = 0;; ++spins) {
-                lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const bool ok = (uint32_t)(lo >> 32) == epoch && (uint32_t)(hi >> 32) == epoch;
-                if (__all(ok)) break;
-                if (spins > (1ll << 26)) {  // never expected: report instead of hanging the queue
-                    if (l == 0) atomicOr(fail, 2);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
+// 8-byte granules {epoch, 32 bits of y} in Gr (tile row I: Gr[128 I + 2 r +
+// h], h = 0 low / 1 high half of row r), each written by ONE sc1 store; wave
+// 0 re-reads a tile row's 128 granules with sc1 loads until every tag equals
+// this sweep's epoch (bounded spin), then stages y_J in LDS.  The caller
+// passes a fresh epoch (never 0; Gr starts zeroed) and the tickets drawn by
+// earlier sweeps (band_sweep_tickets(nb) each) as ticket_base.
+static constexpr int SR = 2;
+
+__device__ __forceinline__ void band_stage(const gu64 *gr, int64_t J, uint32_t epoch, double *ys, int32_t *fail) {
+    if (threadIdx.x < 64) {  // wave 0 sweeps tile row J's granules
+        const int l = threadIdx.x;
+        const gu64 *g = gr + J * 128 + 2 * l;
+        uint64_t lo = 0, hi = 0;
+        for (int64_t spins = 0;; ++spins) {
+            lo = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool ok = (uint32_t)(lo >> 32) == epoch && (uint32_t)(hi >> 32) == epoch;
+            if (__all(ok)) break;
+            if (spins > (1ll << 26)) {  // never expected: report instead of hanging the queue
+                if (l == 0) atomicOr(fail, 2);
+                break;
             }
-            ys[l] = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
+            __builtin_amdgcn_s_sleep(1);
         }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            acc += m[u].x * ys[part * 16 + 2 * u];
-            acc += m[u].y * ys[part * 16 + 2 * u + 1];
-        }
-        __syncthreads();  // ys is refilled for the next tile
+        ys[l] = __longlong_as_double((long long)((hi << 32) | (lo & 0xffffffffull)));
     }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (part == 0) rs[row] = bi - acc;
     __syncthreads();
-    double z = 0.0;
+}
+
+// partial row sum of a tile slice (16 entries per thread) against x in LDS
+__device__ __forceinline__ double band_dot16(const bd_d2 (&m)[8], const double *x, int part) {
+    double a = 0.0;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-        z += dm[u].x * rs[part * 16 + 2 * u];
-        z += dm[u].y * rs[part * 16 + 2 * u + 1];
+        a += m[u].x * x[part * 16 + 2 * u];
+        a += m[u].y * x[part * 16 + 2 * u + 1];
     }
-    z += __shfl_xor(z, 1);
-    z += __shfl_xor(z, 2);
-    if (part == 0) {
-        const uint64_t bits = gi < n ? (uint64_t)__double_as_longlong(z) : 0ull;  // padding rows publish 0
-        const uint64_t tag = (uint64_t)epoch << 32;
-        __hip_atomic_store(gg + I * 128 + 2 * row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gg + I * 128 + 2 * row + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (gi < n) y[gi] = z;
+    return a;
+}
+__device__ __forceinline__ double band_rowsum(double a) {  // over the 4 threads of a row; all get the sum
+    a += __shfl_xor(a, 1);
+    a += __shfl_xor(a, 2);
+    return a;
+}
+__device__ __forceinline__ void band_load16(bd_d2 (&m)[8], const double *p, bool nt) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+        m[u] = nt ? __builtin_nontemporal_load(reinterpret_cast<const bd_d2 *>(p) + u)
+                  : reinterpret_cast<const bd_d2 *>(p)[u];
+}
+// y_I to the granules and y (part-0 threads)
+__device__ __forceinline__ void band_publish(gu64 *gr, int64_t I, int row, int64_t gi, int64_t n, double v,
+                                             uint32_t epoch, double *y) {
+    const uint64_t bits = gi < n ? (uint64_t)__double_as_longlong(v) : 0ull;  // padding rows publish 0
+    const uint64_t tag = (uint64_t)epoch << 32;
+    __hip_atomic_store(gr + I * 128 + 2 * row, tag | (bits & 0xffffffffull), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gr + I * 128 + 2 * row + 1, tag | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gi < n) y[gi] = v;
+}
+
+__global__ __launch_bounds__(SR * 256) void k_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu,
+                                                        const double *__restrict__ T, const double *__restrict__ Dinv,
+                                                        const double *__restrict__ Gn, const double *__restrict__ b,
+                                                        double *__restrict__ y, uint64_t *Gr, uint64_t *ticket,
+                                                        uint64_t ticket_base, uint32_t epoch, int upper,
+                                                        int32_t *fail) {
+    static_assert(SR == 2, "the chain below is written for two positions per workgroup");
+    __shared__ int64_t sp;
+    __shared__ double ys[BT];
+    __shared__ double rs[SR][BT];
+    __shared__ double y0[BT];
+    if (threadIdx.x == 0) sp = (int64_t)(atomicAdd((unsigned long long *)ticket, 1ull) - ticket_base);
+    __syncthreads();
+    const int64_t nsr = (nb + SR - 1) / SR;
+    if (sp < 0 || sp >= nsr) return;  // uniform
+    const int64_t p0 = sp * SR;
+    const int g = threadIdx.x >> 8, lt = threadIdx.x & 255, row = lt >> 2, part = lt & 3;
+    const int64_t W = bl + bu + 1, bw = upper ? bu : bl;  // tiles on the solved side
+    const int64_t pI = p0 + g;
+    const bool act = pI < nb;
+    const int64_t I = upper ? nb - 1 - pI : pI;
+    const int64_t gi = I * BT + row;
+    gu64 *gr = (gu64 *)Gr;
+    auto tile_row = [&](int64_t pJ) { return upper ? nb - 1 - pJ : pJ; };
+    auto tile = [&](int64_t pJ) { return T + (I * W + (tile_row(pJ) - I + bl)) * TILE + row * BT + part * 16; };
+    // off the chain: b, Dinv and the near-tile product
+    const bool has_near = act && bw >= 1 && pI >= 1;
+    double bi = 0.0;
+    bd_d2 dm[8], gm[8];
+    if (act) {
+        bi = gi < n ? b[gi] : 0.0;
+        band_load16(dm, Dinv + I * TILE + row * BT + part * 16, false);
+    }
+    if (has_near) band_load16(gm, Gn + I * TILE + row * BT + part * 16, false);
+    // far tiles preceding the super-row: positions [p0 - bw, p0 - 2]; group g
+    // uses [pI - bw, pI - 2]
+    double acc = 0.0;
+    for (int64_t pJ = (p0 - bw > 0 ? p0 - bw : 0); pJ <= p0 - 2; ++pJ) {
+        const bool use = act && pJ >= pI - bw;
+        bd_d2 m[8];
+        if (use) band_load16(m, tile(pJ), true);
+        band_stage(gr, tile_row(pJ), epoch, ys, fail);
+        if (use) acc += band_dot16(m, ys, part);
+        __syncthreads();  // ys is refilled next
+    }
+    // group 0: c_0 = Dinv (b - far); group 1 loads its tile at p0 - 1 (far
+    // for it, near for group 0)
+    if (g == 0 && act) {
+        const double r = band_rowsum(acc);
+        if (part == 0) rs[0][row] = bi - r;
+    }
+    bd_d2 m1[8];
+    const bool use1 = act && g == 1 && p0 >= 1 && p0 - 1 >= pI - bw;
+    if (use1) band_load16(m1, tile(p0 - 1), true);
+    __syncthreads();
+    double c0 = 0.0;
+    if (g == 0 && act) c0 = band_rowsum(band_dot16(dm, rs[0], part));
+    if (p0 >= 1 && bw >= 1) {
+        band_stage(gr, tile_row(p0 - 1), epoch, ys, fail);  // the cross-workgroup hop
+        if (g == 0 && act) {
+            const double v = c0 - band_rowsum(band_dot16(gm, ys, part));
+            if (part == 0) {
+                y0[row] = v;
+                band_publish(gr, I, row, gi, n, v, epoch, y);
+            }
+        }
+        if (use1) acc += band_dot16(m1, ys, part);
+    } else if (g == 0 && act && part == 0) {  // nothing near precedes position p0
+        y0[row] = c0;
+        band_publish(gr, I, row, gi, n, c0, epoch, y);
+    }
+    // group 1: c_1, then its near tile against group 0's y (through LDS)
+    if (g == 1 && act) {
+        const double r = band_rowsum(acc);
+        if (part == 0) rs[1][row] = bi - r;
+    }
+    __syncthreads();
+    if (g == 1 && act) {
+        const double c1 = band_rowsum(band_dot16(dm, rs[1], part));
+        const double v = has_near ? c1 - band_rowsum(band_dot16(gm, y0, part)) : c1;
+        if (part == 0) band_publish(gr, I, row, gi, n, v, epoch, y);
     }
 }
 
+int64_t band_sweep_tickets(int64_t nb) { return (nb + SR - 1) / SR; }
+
 void launch_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu, const double *T, const double *Dinv,
-                       const double *b, double *y, uint64_t *G, uint64_t *ticket, uint64_t ticket_base,
-                       uint32_t epoch, int upper, int32_t *fail, hipStream_t st) {
+                       const double *Gn, const double *b, double *y, uint64_t *Gr, uint64_t *ticket,
+                       uint64_t ticket_base, uint32_t epoch, int upper, int32_t *fail, hipStream_t st) {
     if (nb > 0)
-        k_band_sweep<<<(unsigned)nb, BTPB, 0, st>>>(n, nb, bl, bu, T, Dinv, b, y, G, ticket, ticket_base, epoch,
-                                                   upper, fail);
+        k_band_sweep<<<(unsigned)band_sweep_tickets(nb), SR * 256, 0, st>>>(n, nb, bl, bu, T, Dinv, Gn, b, y, Gr,
+                                                                            ticket, ticket_base, epoch, upper, fail);
 }
 
 }  // namespace pls

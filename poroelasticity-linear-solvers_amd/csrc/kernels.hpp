@@ -191,15 +191,17 @@ void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, 
 void launch_band_from_csr(int64_t n, int64_t nb, int64_t bl, int64_t bu, const int64_t *rp, const int32_t *ci,
                           const double *val, double *T, hipStream_t st);
 // In place LU without pivoting; Dl / Du: nb inverted diagonal triangles;
+// Gl[I] = Dl_I L_{I,I-1}, Gu[I] = Du_I U_{I,I+1} (the sweeps' near tiles);
 // *fail |= 1 on a zero pivot.
-void launch_band_factor(int64_t nb, int64_t bl, int64_t bu, double *T, double *Dl, double *Du, int32_t *fail,
-                        hipStream_t st);
-// One triangular sweep (upper 0: L with Dl, 1: U with Du), y != b.  G: 128
-// tagged granules per tile row (zeroed once); epoch: fresh per sweep, never 0;
-// ticket_base: tickets drawn by earlier sweeps (nb per sweep) on `ticket`;
-// *fail |= 2 if a spin gave up.
+void launch_band_factor(int64_t nb, int64_t bl, int64_t bu, double *T, double *Dl, double *Du, double *Gl,
+                        double *Gu, int32_t *fail, hipStream_t st);
+// One triangular sweep (upper 0: L with Dl, Gl; 1: U with Du, Gu), y != b.
+// Gr: 128 tagged granules per tile row (zeroed once); epoch: fresh per sweep,
+// never 0; ticket_base: tickets drawn by earlier sweeps (band_sweep_tickets
+// per sweep) on `ticket`; *fail |= 2 if a spin gave up.
+int64_t band_sweep_tickets(int64_t nb);
 void launch_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu, const double *T, const double *Dinv,
-                       const double *b, double *y, uint64_t *G, uint64_t *ticket, uint64_t ticket_base,
-                       uint32_t epoch, int upper, int32_t *fail, hipStream_t st);
+                       const double *Gn, const double *b, double *y, uint64_t *Gr, uint64_t *ticket,
+                       uint64_t ticket_base, uint32_t epoch, int upper, int32_t *fail, hipStream_t st);
 
 }  // namespace pls

@@ -757,6 +757,8 @@ PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c) {
     T.alloc((size_t)(nb * W) * 4096);
     Dl.alloc((size_t)nb * 4096);
     Du.alloc((size_t)nb * 4096);
+    Gl.alloc((size_t)nb * 4096);
+    Gu.alloc((size_t)nb * 4096);
     t.alloc(std::max<int64_t>(n, 1));
     G.alloc((size_t)std::max<int64_t>(nb, 1) * 128);
     fail.alloc(1);
@@ -765,7 +767,7 @@ PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c) {
     HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
     HIPCHK(hipMemsetAsync(ticket.p, 0, sizeof(uint64_t), c.st));
     launch_band_from_csr(n, nb, bl, bu, M.rp.p, M.ci.p, M.val.p, T.p, c.st);
-    launch_band_factor(nb, bl, bu, T.p, Dl.p, Du.p, fail.p, c.st);
+    launch_band_factor(nb, bl, bu, T.p, Dl.p, Du.p, Gl.p, Gu.p, fail.p, c.st);
     HIPCHK(hipGetLastError());
     if (check_fail(c)) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
 }
@@ -778,11 +780,12 @@ int32_t PCBandLU::check_fail(Ctx &c) {
 }
 
 void PCBandLU::apply(const double *x, double *y, Ctx &c) {
-    // epochs 2s+1, 2s+2 (never 0); each sweep draws nb tickets
-    launch_band_sweep(n, nb, bl, bu, T.p, Dl.p, x, t.p, G.p, ticket.p, sweeps * nb, (uint32_t)(sweeps + 1), 0,
+    // epochs 2s+1, 2s+2 (never 0); each sweep draws band_sweep_tickets(nb) tickets
+    const uint64_t nt = (uint64_t)band_sweep_tickets(nb);
+    launch_band_sweep(n, nb, bl, bu, T.p, Dl.p, Gl.p, x, t.p, G.p, ticket.p, sweeps * nt, (uint32_t)(sweeps + 1), 0,
                       fail.p, c.st);
     ++sweeps;
-    launch_band_sweep(n, nb, bl, bu, T.p, Du.p, t.p, y, G.p, ticket.p, sweeps * nb, (uint32_t)(sweeps + 1), 1,
+    launch_band_sweep(n, nb, bl, bu, T.p, Du.p, Gu.p, t.p, y, G.p, ticket.p, sweeps * nt, (uint32_t)(sweeps + 1), 1,
                       fail.p, c.st);
     ++sweeps;
 }

@@ -260,10 +260,10 @@ struct PCDenseLU : PC {
 // Not reentrant (the sweeps share the granules, the ticket and t).
 struct PCBandLU : PC {
     int64_t nb = 0, bl = 0, bu = 0;
-    DBuf<double> T, Dl, Du, t;
+    DBuf<double> T, Dl, Du, Gl, Gu, t;  // Gl / Gu: near-tile products (band.hip)
     DBuf<int32_t> fail;
     DBuf<uint64_t> G, ticket;  // G: 128 tagged granules per tile row (the sweeps' hand-off)
-    uint64_t sweeps = 0;  // launched sweeps (ticket base = sweeps * nb)
+    uint64_t sweeps = 0;  // launched sweeps (ticket base = sweeps * band_sweep_tickets(nb))
     PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c);
     void apply(const double *x, double *y, Ctx &c) override;
     int32_t check_fail(Ctx &c);  // synchronising: the fail word (2: a sweep spin gave up)
