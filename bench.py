@@ -205,6 +205,13 @@ def cpu_baseline(args, params, db):
             "raw_iters_per_s": rate}
 
 
+def _progress(rank, msg):
+    """Progress on stderr (rank 0): long configurations stay visibly alive;
+    stdout carries only the JSON line."""
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="swelling3d-bjacobi", choices=sorted(CONFIGS),
@@ -286,12 +293,15 @@ def main():
     h.create_solver()
     t_setup = time.perf_counter() - t0
     n, nnz = h.n, h.nnz_A
+    _progress(rank, f"setup {t_setup:.2f} s ({n} DoF on this rank, nnz(A) {nnz})")
     d_b = Nat.DeviceArray(n)
     d_x = Nat.DeviceArray(n)
     h.rhs_device(7, d_b.p)
 
     for _ in range(args.warmup):
-        h.solve_device(d_b.p, d_x.p)
+        tw = time.perf_counter()
+        r = h.solve_device(d_b.p, d_x.p)
+        _progress(rank, f"warmup solve: {r.its} its, reason {r.reason}, {time.perf_counter() - tw:.3f} s")
     h.reset_timings()
 
     def barrier():
@@ -404,6 +414,7 @@ def main():
             "timings_s": {k: v for k, v in tm.items()},
         }
         if not args.no_cpu and world == 1:
+            _progress(rank, f"cpu baseline on the N={args.cpu_N} sample ...")
             out["cpu_baseline"] = cpu_baseline(args, params, db)
         print(json.dumps(out))
     d_b.free()
