@@ -137,14 +137,18 @@ HostCSR spgemm(const HostCSR &A, const HostCSR &B) {
 }
 
 // Galerkin product Ac = R (A P) with R = P^T, bitwise equal to
-// spgemm(R, AP): there every entry (a, b) sums R_ak (AP)_kb over R's row a in
-// storage order, k ascending -- the same sequence as visiting fine rows k in
-// order and scattering P_ka (AP)_kb.  This outer-product form streams P and AP
-// once per thread instead of gathering ~|aggregate neighbourhood| scattered
-// AP rows for every coarse row (the row-wise form is cache-miss bound: 85 s at
-// N=59).  Threads own coarse-row ranges with a dense accumulator each, so it
-// is used while nc^2 doubles stay small (max_bytes).
-bool galerkin_dense(const HostCSR &P, const HostCSR &AP, int64_t nc, double max_bytes, HostCSR &C) {
+// spgemm(R, spgemm(A, P)) (csr_matmat twice):
+//  * (AP)_kb is summed exactly as there (A's row k in storage order, P's rows
+//    in order), exact zeros dropped;
+//  * every Ac entry (a, b) sums R_ak (AP)_kb over R's row a in storage order,
+//    k ascending -- the same sequence as visiting fine rows k in order and
+//    scattering P_ka (AP)_kb.
+// This fused outer-product form never materialises AP (~950 entries per row
+// at N=59: ~57 GB) nor sorts its rows, and streams A and P once per thread.
+// Threads own coarse-row ranges with a dense accumulator each (a fine row
+// whose P row touches a range is expanded by that range's thread), so it is
+// used while nc^2 doubles stay small (max_bytes).
+bool galerkin_fused(const HostCSR &A, const HostCSR &P, int64_t nc, double max_bytes, HostCSR &C) {
     if ((double)nc * (double)nc * 8.0 > max_bytes) return false;
     C.nrows = C.ncols = nc;
     const int T = (int)std::max<int64_t>(1, std::min<int64_t>(setup_threads(), nc));
@@ -153,15 +157,37 @@ bool galerkin_dense(const HostCSR &P, const HostCSR &AP, int64_t nc, double max_
     for (int t = 0; t < T; ++t) {
         th.emplace_back([&, t] {
             const int64_t a0 = nc * t / T, a1 = nc * (t + 1) / T;
-            std::vector<double> acc((size_t)((a1 - a0) * nc), 0.0);
-            for (int64_t k = 0; k < P.nrows; ++k)
+            std::vector<double> acc((size_t)((a1 - a0) * nc), 0.0), ap(nc, 0.0);
+            std::vector<char> mark(nc, 0);
+            std::vector<int32_t> cols;
+            for (int64_t k = 0; k < P.nrows; ++k) {
+                bool touch = false;
+                for (int64_t q = P.rp[k]; q < P.rp[k + 1] && !touch; ++q) touch = P.ci[q] >= a0 && P.ci[q] < a1;
+                if (!touch) continue;
+                cols.clear();  // (AP)_k, as spgemm_rows sums it
+                for (int64_t kk = A.rp[k]; kk < A.rp[k + 1]; ++kk) {
+                    const int32_t kp = A.ci[kk];
+                    const double av = A.v[kk];
+                    for (int64_t jj = P.rp[kp]; jj < P.rp[kp + 1]; ++jj) {
+                        const int32_t b = P.ci[jj];
+                        if (!mark[b]) {
+                            mark[b] = 1;
+                            ap[b] = 0.0;
+                            cols.push_back(b);
+                        }
+                        ap[b] += av * P.v[jj];
+                    }
+                }
                 for (int64_t q = P.rp[k]; q < P.rp[k + 1]; ++q) {
                     const int64_t a = P.ci[q];
                     if (a < a0 || a >= a1) continue;
                     const double p = P.v[q];
                     double *row = acc.data() + (a - a0) * nc;
-                    for (int64_t jj = AP.rp[k]; jj < AP.rp[k + 1]; ++jj) row[AP.ci[jj]] += p * AP.v[jj];
+                    for (int32_t b : cols)
+                        if (ap[b] != 0.0) row[b] += p * ap[b];
                 }
+                for (int32_t b : cols) mark[b] = 0;
+            }
             HostCSR &out = part[t];
             out.rp.assign(1, 0);
             for (int64_t a = a0; a < a1; ++a) {
@@ -468,11 +494,8 @@ struct PCAMG : PC {
             const HostCSR R = transpose(P);
             tm[3] += now() - t0;
             t0 = now();
-            const HostCSR AP = spgemm(A, P);
-            tm[6] += now() - t0;
-            t0 = now();
             HostCSR Ac;
-            if (!galerkin_dense(P, AP, na, o.num("pls.amg_rap_dense_gb", 16.0) * 1e9, Ac)) Ac = spgemm(R, AP);
+            if (!galerkin_fused(A, P, na, o.num("pls.amg_rap_dense_gb", 16.0) * 1e9, Ac)) Ac = spgemm(R, spgemm(A, P));
             tm[4] += now() - t0;
             t0 = now();
             L->Aown = std::move(cur);
@@ -510,9 +533,9 @@ struct PCAMG : PC {
             for (auto &L : lv) fprintf(stderr, " %lld(lam %.6g)", (long long)L->n, L->lam);
             fprintf(stderr, " coarse %lld\n", (long long)nco);
             fprintf(stderr,
-                    "[amg %s] setup s: download %.2f aggregate %.2f lambda %.2f P/R %.2f AP %.2f R(AP) %.2f "
-                    "upload %.2f (%d threads)\n",
-                    prefix.c_str(), tm[0], tm[1], tm[2], tm[3], tm[6], tm[4], tm[5], setup_threads());
+                    "[amg %s] setup s: download %.2f aggregate %.2f lambda %.2f P/R %.2f RAP %.2f upload %.2f "
+                    "(%d threads)\n",
+                    prefix.c_str(), tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], setup_threads());
         }
     }
 
