@@ -273,8 +273,9 @@ __device__ __forceinline__ void band_stage(const gu64 *gr, int64_t J, uint32_t e
             hi = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const bool ok = (uint32_t)(lo >> 32) == epoch && (uint32_t)(hi >> 32) == epoch;
             if (__all(ok)) break;
-            if (spins > (1ll << 26)) {  // never expected: report instead of hanging the queue
-                if (l == 0) atomicOr(fail, 2);
+            if (spins > (1ll << 26)) {  // never expected: report instead of hanging the queue, and
+                if (l == 0) atomicOr(fail, 2);  // poison y so the Krylov loop stops (DIVERGED_NANORINF)
+                lo = hi = 0x7ff8000000000000ull;
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
