@@ -275,7 +275,8 @@ __device__ __forceinline__ void band_stage(const gu64 *gr, int64_t J, uint32_t e
             if (__all(ok)) break;
             if (spins > (1ll << 26)) {  // never expected: report instead of hanging the queue, and
                 if (l == 0) atomicOr(fail, 2);  // poison y so the Krylov loop stops (DIVERGED_NANORINF)
-                lo = hi = 0x7ff8000000000000ull;
+                hi = 0x7ff80000ull;  // high half of a quiet NaN
+                lo = 0;
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
