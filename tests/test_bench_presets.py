@@ -1,0 +1,82 @@
+"""bench.py's BASELINE.json presets (host logic, no GPU): each configuration
+maps to the reference's option sets as DESIGN.md §5 states.
+
+* swelling2d-exact: petsc-options-exact (right-PC GMRES, PREONLY + LU on every
+  block; reference petsc-options-exact:3-35), swelling.py:63-67 tolerances;
+* footing-inexact-ilu: petsc-options-inexact with every BoomerAMG block
+  replaced by BJACOBI(ILU(0)) and the Schur block's MUMPS LU kept as LU
+  (petsc-options-inexact:12-114), footing.py atol 1e-4;
+* swelling3d-bjacobi: the headline (2-way, PREONLY + BJACOBI(ILU(0)) 256 / 264
+  blocks), N = 59;
+* aar-m5: AAR with depth 5 (BASELINE configs[4]).
+"""
+import argparse
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _args(config, **over):
+    a = dict(bench.CONFIGS[config])
+    preset = a.pop("preset")
+    ns = argparse.Namespace(config=config, dim=3, atol=1e-8, aar_order=10, N=59, inner="bjacobi", inexact=False,
+                            blocks_s=256, blocks_fp=264, blocks_p=11, blocks_inner=64, maxit=100,
+                            pc_type="diagonal", solver="gmres", cpu_N=40, cpu_maxit=100, preset=preset)
+    for k, v in a.items():
+        setattr(ns, k, v)
+    for k, v in over.items():
+        setattr(ns, k, v)
+    return ns
+
+
+def test_every_preset_names_a_known_configuration():
+    assert set(bench.CONFIGS) == {"swelling2d-exact", "swelling3d-bjacobi", "footing-inexact-ilu", "aar-m5"}
+    assert bench.CONFIGS["swelling3d-bjacobi"]["N"] == 59  # the metric's 10.33M-DoF system
+
+
+def test_exact_preset_is_preonly_lu_everywhere():
+    params, db = bench.solver_options(_args("swelling2d-exact"))
+    assert params["solver maxiter"] == 500 and params["solver atol"] == 1e-8
+    assert db["global_ksp_pc_side"] == "right"
+    for pre in ("s_", "fp_"):
+        assert db[pre + "ksp_type"] == "preonly" and db[pre + "pc_type"] == "lu"
+    _, db3 = bench.solver_options(_args("swelling2d-exact", pc_type="diagonal 3-way"))
+    for pre in ("s_", "f_", "p_", "diff_"):
+        assert db3[pre + "pc_type"] == "lu"
+
+
+def test_footing_preset_replaces_boomeramg_by_ilu_blocks():
+    params, db = bench.solver_options(_args("footing-inexact-ilu"))
+    assert params["solver atol"] == 1e-4 and params["solver maxiter"] == 500
+    assert "hypre" not in db.values() and not any("hypre" in k for k in db)
+    for pre in ("s_", "f_", "p_", "diff_", "fp_fieldsplit_0_"):
+        assert db[pre + "pc_type"] == "bjacobi" and db[pre + "sub_pc_type"] == "ilu"
+        assert db[pre + "pc_bjacobi_blocks"] == "64"
+    # the rest of petsc-options-inexact is untouched
+    assert db["fp_pc_fieldsplit_type"] == "schur" and db["fp_pc_fieldsplit_schur_fact_type"] == "lower"
+    assert db["fp_pc_fieldsplit_schur_precondition"] == "selfp"
+    assert db["fp_fieldsplit_1_pc_type"] == "lu"  # MUMPS -> the device LU (band LU at N=128)
+    assert db["s_ksp_type"] == "cg" and db["s_ksp_rtol"] == "1e-1"
+    assert db["global_ksp_norm_type"] == "unpreconditioned"
+
+
+@pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
+def test_headline_preset_block_counts(pc_type):
+    _, db = bench.solver_options(_args("swelling3d-bjacobi", pc_type=pc_type))
+    if pc_type == "diagonal":
+        assert db["s_pc_bjacobi_blocks"] == "256" and db["fp_pc_bjacobi_blocks"] == "264"
+    else:
+        assert db["p_pc_bjacobi_blocks"] == "11" and db["diff_pc_bjacobi_blocks"] == "11"
+    assert all(db[p + "ksp_type"] == "preonly" for p in (("s_", "fp_") if pc_type == "diagonal" else
+                                                        ("s_", "f_", "p_", "diff_")))
+
+
+def test_aar_preset():
+    args = _args("aar-m5")
+    params, _ = bench.solver_options(args)
+    assert params["solver type"] == "aar" and params["AAR order"] == 5 and params["AAR p"] == 5
