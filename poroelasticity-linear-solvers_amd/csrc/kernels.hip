@@ -1229,7 +1229,7 @@ __global__ __launch_bounds__(TPB) void k_d16_count(int64_t nslices, const int64_
 __global__ __launch_bounds__(TPB) void k_d16_fill(int64_t nslices, const int64_t *sfirst, const int32_t *slpr,
                                                   const int64_t *rp, const int32_t *ci, const double *val,
                                                   int64_t nrows, const int64_t *sptr, uint16_t *dl, double *dv,
-                                                  int32_t *seg) {
+                                                  int32_t *seg, int nsegs) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl >= nslices) return;
@@ -1252,7 +1252,7 @@ __global__ __launch_bounds__(TPB) void k_d16_fill(int64_t nslices, const int64_t
             v = val[s0 + j];
             const int64_t gap = (int64_t)c - (int64_t)last;
             if (k == 0 || gap > 65535 || gap <= 0) {
-                seg[slot * D16_SEG + nseg++] = c;
+                seg[slot * nsegs + nseg++] = c;
             } else {
                 d = (uint16_t)gap;
             }
@@ -1261,8 +1261,8 @@ __global__ __launch_bounds__(TPB) void k_d16_fill(int64_t nslices, const int64_t
         dl[base + (k >> 3) * 512 + lane * 8 + (k & 7)] = d;
         dv[base + (k >> 1) * 128 + lane * 2 + (k & 1)] = v;
     }
-    if (nseg == 0) seg[slot * D16_SEG + nseg++] = 0;
-    for (int j = nseg; j < D16_SEG; ++j) seg[slot * D16_SEG + j] = seg[slot * D16_SEG + nseg - 1];
+    if (nseg == 0) seg[slot * nsegs + nseg++] = 0;
+    for (int j = nseg; j < nsegs; ++j) seg[slot * nsegs + j] = seg[slot * nsegs + nseg - 1];
 }
 
 // first column of every row (-1: empty row) -- input of the host slice plan
@@ -1275,7 +1275,7 @@ typedef int32_t d16_i4 __attribute__((ext_vector_type(4)));
 typedef uint32_t d16_u4 __attribute__((ext_vector_type(4)));
 typedef double d16_d2 __attribute__((ext_vector_type(2)));
 
-template <int G2, int TAG, bool HALO>
+template <int G2, int TAG, bool HALO, int SEG>
 __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *__restrict__ sptr,
                                                   const int64_t *__restrict__ sfirst,
                                                   const int32_t *__restrict__ slpr,
@@ -1284,7 +1284,7 @@ __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices
                                                   double *__restrict__ y, double alpha, double beta,
                                                   const double *__restrict__ z, const double *__restrict__ ghost,
                                                   int32_t nlocal) {
-    static_assert(D16_SEG == 4, "segment bases are one int4 per lane");
+    static_assert(SEG == 4 || SEG == 8, "segment bases are one or two int4 per lane");
     const int lane = threadIdx.x & 63;
     const int64_t sl = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
     if (sl >= nslices) return;
@@ -1293,7 +1293,9 @@ __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices
     const int lpr = slpr[sl];
     const int64_t r0 = sfirst[sl], r1 = sfirst[sl + 1];
     const int64_t row = r0 + lane / lpr;
-    const d16_i4 sb = __builtin_nontemporal_load(reinterpret_cast<const d16_i4 *>(seg) + sl * 64 + lane);
+    const d16_i4 sb = __builtin_nontemporal_load(reinterpret_cast<const d16_i4 *>(seg) + (sl * 64 + lane) * (SEG / 4));
+    d16_i4 sb2 = sb;
+    if (SEG == 8) sb2 = __builtin_nontemporal_load(reinterpret_cast<const d16_i4 *>(seg) + (sl * 64 + lane) * 2 + 1);
     const d16_u4 *dp = reinterpret_cast<const d16_u4 *>(dl + base) + lane;
     const d16_d2 *vp = reinterpret_cast<const d16_d2 *>(dv + base) + lane;
     int32_t col = 0;
@@ -1317,7 +1319,8 @@ __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int32_t dd = (int32_t)((w[e >> 1] >> ((e & 1) * 16)) & 0xffffu);
-                const int32_t b = si == 0 ? sb.x : si == 1 ? sb.y : si == 2 ? sb.z : sb.w;
+                int32_t b = si == 0 ? sb.x : si == 1 ? sb.y : si == 2 ? sb.z : sb.w;
+                if (SEG == 8 && si >= 4) b = si == 4 ? sb2.x : si == 5 ? sb2.y : si == 6 ? sb2.z : sb2.w;
                 col = dd == 0 ? b : col + dd;
                 si += dd == 0 ? 1 : 0;
                 const double a = (e & 1) ? v[u][e >> 1].y : v[u][e >> 1].x;
@@ -1353,39 +1356,47 @@ void launch_d16_count(int64_t nslices, const int64_t *sfirst, const int32_t *slp
 }
 void launch_d16_fill(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
                      const int32_t *ci, const double *val, int64_t nrows, const int64_t *sptr, uint16_t *dl,
-                     double *dv, int32_t *seg, hipStream_t st) {
+                     double *dv, int32_t *seg, int nsegs, hipStream_t st) {
     if (nslices > 0)
         k_d16_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, ci, val, nrows, sptr, dl,
-                                                                dv, seg);
+                                                                dv, seg, nsegs);
 }
 void launch_first_col(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *c0, hipStream_t st) {
     if (nrows > 0) k_first_col<<<grid_for(nrows, TPB), TPB, 0, st>>>(nrows, rp, ci, c0);
 }
-template <int G2>
+template <int G2, int SEG>
 static void d16_dispatch(unsigned g, hipStream_t st, int64_t nrows, int64_t ns, const int64_t *sptr,
                          const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
                          const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
                          int tag, const double *ghost, int32_t nl) {
     if (ghost) {
-        if (tag) k_d16_spmv<G2, 1, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-        else k_d16_spmv<G2, 0, true><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        if (tag) k_d16_spmv<G2, 1, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        else k_d16_spmv<G2, 0, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
     } else {
-        if (tag) k_d16_spmv<G2, 1, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-        else k_d16_spmv<G2, 0, false><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        if (tag) k_d16_spmv<G2, 1, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        else k_d16_spmv<G2, 0, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+    }
+}
+template <int SEG>
+static void d16_unrolled(int unroll, unsigned g, hipStream_t st, int64_t nrows, int64_t nslices, const int64_t *sptr,
+                         const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
+                         const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
+                         int tag, const double *ghost, int32_t nl) {
+    switch (unroll) {
+        case 1: d16_dispatch<1, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        case 2: d16_dispatch<2, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        default: d16_dispatch<4, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
     }
 }
 void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
-                     const uint16_t *dl, const double *dv, const int32_t *seg, const double *x, double *y,
+                     const uint16_t *dl, const double *dv, const int32_t *seg, int nsegs, const double *x, double *y,
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
                      int unroll, hipStream_t st) {
     if (nslices <= 0) return;
     const unsigned g = grid_for(nslices, TPB / 64);
     const int32_t nl = (int32_t)nlocal;
-    switch (unroll) {
-        case 1: d16_dispatch<1>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        case 2: d16_dispatch<2>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        default: d16_dispatch<4>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-    }
+    if (nsegs == 8) d16_unrolled<8>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl);
+    else d16_unrolled<4>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl);
 }
 
 // ================================================= level-aligned SELL-64 ====

@@ -170,7 +170,8 @@ void build_sell(DevCSR &M, Ctx &c) {
         int32_t h = 0;
         HIPCHK(hipMemcpyAsync(&h, mx.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
         c.sync();
-        S->d16 = h <= D16_SEG;
+        S->d16 = h <= D16_SEG_MAX;
+        S->nsegs = (h <= D16_SEG && c.d16_segs <= D16_SEG) ? D16_SEG : D16_SEG_MAX;
         if (S->d16) {
             S->nslices = ns;
             for (int32_t l : lp) S->wide_slices += (l > 1);
@@ -183,9 +184,9 @@ void build_sell(DevCSR &M, Ctx &c) {
             c.sync();
             S->val.alloc(std::max<int64_t>(S->stored, 2));
             S->dl.alloc(std::max<int64_t>(S->stored, 8));
-            S->seg.alloc(ns * 64 * D16_SEG);
+            S->seg.alloc(ns * 64 * S->nsegs);
             launch_d16_fill(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.ci.p, M.val.p, M.nrows, S->sptr.p, S->dl.p,
-                            S->val.p, S->seg.p, c.st);
+                            S->val.p, S->seg.p, S->nsegs, c.st);
             HIPCHK(hipGetLastError());
             c.sync();
             M.sell = std::move(S);
@@ -222,7 +223,7 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
     }
     if (M.sell && M.sell->d16) {
         const DevSELL &S = *M.sell;
-        launch_d16_spmv(M.nrows, S.nslices, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, x, y, alpha,
+        launch_d16_spmv(M.nrows, S.nslices, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y, alpha,
                         beta, z, M.tag, ghost, nlocal, c.d16_unroll, c.st);
         return;
     }

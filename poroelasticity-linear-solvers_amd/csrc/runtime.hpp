@@ -69,6 +69,7 @@ struct Ctx {
     bool sell_d16 = true;     // build SpMV layouts as SELL-64/D16 where every row fits
     int d16_wide_lpr = 8;     // lanes per row of D16 slices with wide rows (option pls.d16_wide_lpr)
     int d16_unroll = 4;       // D16 SpMV 8-entry groups per lane in flight (option pls.d16_unroll)
+    int d16_segs = D16_SEG;   // minimum D16 segment bases per lane (option pls.d16_segs; 8 where needed)
     DBuf<char> scan_tmp;
     size_t scan_tmp_bytes = 0;
     Ctx();
@@ -91,8 +92,9 @@ struct DevSELL {
     DBuf<int32_t> seg, slpr;  // D16: segment bases per lane, lanes per row per slice
     DBuf<int64_t> sfirst;     // D16: first row of each slice (nslices + 1)
     int64_t wide_slices = 0;  // D16 slices with 8 lanes per row
+    int nsegs = D16_SEG;      // D16 segment bases per lane: 4, or 8 when halo columns need them
     int64_t bytes() const {  // bytes one product streams from the matrix
-        return d16 ? stored * 10 + nslices * (64 * 16 + 20) + 8 : stored * 12 + (nslices + 1) * 8;
+        return d16 ? stored * 10 + nslices * (64 * 4 * nsegs + 20) + 8 : stored * 12 + (nslices + 1) * 8;
     }
 };
 

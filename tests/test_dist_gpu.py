@@ -43,6 +43,10 @@ CASES = [
     {"name": "twoway_2d", "dim": 2, "N": 12, "params": BASE, "db": _db()},
     {"name": "threeway_2d", "dim": 2, "N": 10, "params": dict(BASE, **{"pc type": "diagonal 3-way"}), "db": _db()},
     {"name": "twoway_3d", "dim": 3, "N": 4, "params": BASE, "db": _db({"s_": 4, "fp_": 4})},
+    # the SpMV layout with 8 segment bases per lane (what the halo rows of large
+    # sharded systems need: own s/f/p + a neighbour's s/f/p), forced here
+    {"name": "twoway_3d_seg8", "dim": 3, "N": 4, "params": BASE,
+     "db": dict(_db({"s_": 4, "fp_": 4}), **{"pls.d16_segs": "8"})},
     {"name": "aar_2d", "dim": 2, "N": 10, "params": dict(BASE, **{"solver type": "aar", "solver maxiter": 200}),
      "db": _db()},
     {"name": "jacobi_left_2d", "dim": 2, "N": 9, "params": BASE,

@@ -120,10 +120,12 @@ def test_synthetic_generator_bitwise(gpu, dim, N, variant):
     assert np.array_equal(M.data, R.data)  # bitwise
 
 
+@pytest.mark.parametrize("segs", ["4", "8"])
 @pytest.mark.parametrize("dim,N", [(2, 12), (3, 4)])
-def test_spmv_matches_scipy(gpu, dim, N):
+def test_spmv_matches_scipy(gpu, dim, N, segs):
+    """segs 8: the D16 layout with 8 segment bases per lane (sharded halo rows)."""
     spec = S.SynthSpec(dim, N)
-    h = _handle(spec, BASE, ILU_DB)
+    h = _handle(spec, BASE, dict(ILU_DB, **{"pls.d16_segs": segs}))
     A = S.matrix(spec, 0)
     rng = np.random.default_rng(1)
     x = rng.standard_normal(A.shape[0])
@@ -158,6 +160,10 @@ def test_gmres_right_2way_ilu(gpu):
 
 def test_gmres_right_2way_ilu_3d(gpu):
     _compare_solve(S.SynthSpec(3, 4))
+
+
+def test_gmres_right_2way_ilu_3d_seg8(gpu):
+    _compare_solve(S.SynthSpec(3, 4), db=dict(ILU_DB, **{"pls.d16_segs": "8"}))
 
 
 def test_gmres_left_default_norm(gpu):
