@@ -91,3 +91,31 @@ def test_band_lu_footing_size():
     f = native.ILU0(P[ns:, ns:].tocsr())
     assert np.linalg.norm(y[ns:] - f.solve(t)) <= 1e-12 * np.linalg.norm(y[ns:])
     h.destroy()
+
+
+def test_full_size_three_way():
+    """3-way block PC (FS + DIFF sweeps on two streams) at N=27 (~1M DoF):
+    converges, GMRES estimate = device true residual, bitwise reproducible
+    (the concurrent sweeps join before the w1/w2 combination, so stream timing
+    cannot reorder any sum)."""
+    import lib._native as Nt
+    from lib.handle import Handle
+    o = _opts(64, 64, {"pls.pc_type": "diagonal 3-way", "f_ksp_type": "preonly", "f_pc_type": "bjacobi",
+                       "f_pc_bjacobi_blocks": "64", "p_ksp_type": "preonly", "p_pc_type": "bjacobi",
+                       "p_pc_bjacobi_blocks": "8", "diff_ksp_type": "preonly", "diff_pc_type": "bjacobi",
+                       "diff_pc_bjacobi_blocks": "8"})
+    h = Handle.synthetic(3, 27, 20261015, 0.05, o)
+    n = h.n
+    b, x, r, x2 = (Nt.DeviceArray(n) for _ in range(4))
+    h.rhs_device(7, b.p)
+    res = h.solve_device(b.p, x.p)
+    hist = h.history()
+    assert res.reason == 2 and hist[-1] <= 1e-6 * hist[0]
+    h.matmult_device(x.p, r.p)
+    true = np.linalg.norm(b.download() - r.download())
+    assert abs(true - hist[-1]) <= 1e-3 * hist[-1], (true, hist[-1])
+    res2 = h.solve_device(b.p, x2.p)
+    assert res2.its == res.its and np.array_equal(h.history(), hist) and np.array_equal(x2.download(), x.download())
+    for a in (b, x, r, x2):
+        a.free()
+    h.destroy()
