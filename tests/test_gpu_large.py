@@ -100,7 +100,7 @@ def test_full_size_three_way():
     cannot reorder any sum)."""
     import lib._native as Nt
     from lib.handle import Handle
-    o = _opts(64, 64, {"pls.pc_type": "diagonal 3-way", "f_ksp_type": "preonly", "f_pc_type": "bjacobi",
+    o = _opts(64, 64, {"pls.pc_type": "diagonal_3-way", "f_ksp_type": "preonly", "f_pc_type": "bjacobi",
                        "f_pc_bjacobi_blocks": "64", "p_ksp_type": "preonly", "p_pc_type": "bjacobi",
                        "p_pc_bjacobi_blocks": "8", "diff_ksp_type": "preonly", "diff_pc_type": "bjacobi",
                        "diff_pc_bjacobi_blocks": "8"})
