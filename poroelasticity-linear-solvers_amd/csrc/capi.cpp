@@ -479,6 +479,7 @@ struct Handle {
             ctx.d16_wide_lpr != 16 && ctx.d16_wide_lpr != 32 && ctx.d16_wide_lpr != 64)
             throw Error("pls.d16_wide_lpr must be a power of two <= 64");
         ctx.d16_unroll = (int)opt.integer("pls.d16_unroll", 4);
+        ctx.halo_overlap = opt.flag("pls.halo_overlap", true);
         ctx.d16_segs = (int)opt.integer("pls.d16_segs", D16_SEG);  // 8: force the halo layout (tests)
         if (ctx.d16_segs != D16_SEG && ctx.d16_segs != D16_SEG_MAX) throw Error("pls.d16_segs must be 4 or 8");
     }

@@ -1283,11 +1283,14 @@ __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices
                                                   const int32_t *__restrict__ seg, const double *__restrict__ x,
                                                   double *__restrict__ y, double alpha, double beta,
                                                   const double *__restrict__ z, const double *__restrict__ ghost,
-                                                  int32_t nlocal) {
+                                                  int32_t nlocal, const int32_t *__restrict__ slist) {
     static_assert(SEG == 4 || SEG == 8, "segment bases are one or two int4 per lane");
     const int lane = threadIdx.x & 63;
-    const int64_t sl = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
-    if (sl >= nslices) return;
+    // nslices: slices this launch processes -- all of them, or the subset
+    // listed in slist (interior / halo rows of a distributed product)
+    const int64_t idx = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
+    if (idx >= nslices) return;
+    const int64_t sl = slist ? (int64_t)__builtin_amdgcn_readfirstlane(slist[idx]) : idx;
     const int64_t base = sptr[sl];
     const int64_t L = (sptr[sl + 1] - base) >> 6;  // multiple of 8
     const int lpr = slpr[sl];
@@ -1368,35 +1371,46 @@ template <int G2, int SEG>
 static void d16_dispatch(unsigned g, hipStream_t st, int64_t nrows, int64_t ns, const int64_t *sptr,
                          const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
                          const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
-                         int tag, const double *ghost, int32_t nl) {
+                         int tag, const double *ghost, int32_t nl, const int32_t *slist) {
     if (ghost) {
-        if (tag) k_d16_spmv<G2, 1, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-        else k_d16_spmv<G2, 0, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        if (tag) k_d16_spmv<G2, 1, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist);
+        else k_d16_spmv<G2, 0, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist);
     } else {
-        if (tag) k_d16_spmv<G2, 1, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
-        else k_d16_spmv<G2, 0, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl);
+        if (tag) k_d16_spmv<G2, 1, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist);
+        else k_d16_spmv<G2, 0, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist);
     }
 }
 template <int SEG>
 static void d16_unrolled(int unroll, unsigned g, hipStream_t st, int64_t nrows, int64_t nslices, const int64_t *sptr,
                          const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
                          const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
-                         int tag, const double *ghost, int32_t nl) {
+                         int tag, const double *ghost, int32_t nl, const int32_t *slist) {
     switch (unroll) {
-        case 1: d16_dispatch<1, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        case 2: d16_dispatch<2, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
-        default: d16_dispatch<4, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl); break;
+        case 1: d16_dispatch<1, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist); break;
+        case 2: d16_dispatch<2, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist); break;
+        default: d16_dispatch<4, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist); break;
     }
 }
 void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
                      const uint16_t *dl, const double *dv, const int32_t *seg, int nsegs, const double *x, double *y,
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
-                     int unroll, hipStream_t st) {
+                     int unroll, hipStream_t st, const int32_t *slist) {
     if (nslices <= 0) return;
     const unsigned g = grid_for(nslices, TPB / 64);
     const int32_t nl = (int32_t)nlocal;
-    if (nsegs == 8) d16_unrolled<8>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl);
-    else d16_unrolled<4>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl);
+    if (nsegs == 8) d16_unrolled<8>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist);
+    else d16_unrolled<4>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist);
+}
+
+// rows whose last (largest) column is a ghost column (rows sorted): flag 1
+__global__ __launch_bounds__(TPB) void k_row_has_ghost(int64_t nrows, const int64_t *rp, const int32_t *ci,
+                                                       int64_t nlocal, uint8_t *flag) {
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (r < nrows) flag[r] = (rp[r + 1] > rp[r] && ci[rp[r + 1] - 1] >= nlocal) ? 1 : 0;
+}
+void launch_row_has_ghost(int64_t nrows, const int64_t *rp, const int32_t *ci, int64_t nlocal, uint8_t *flag,
+                          hipStream_t st) {
+    if (nrows > 0) k_row_has_ghost<<<grid_for(nrows, TPB), TPB, 0, st>>>(nrows, rp, ci, nlocal, flag);
 }
 
 // ================================================= level-aligned SELL-64 ====

@@ -141,7 +141,11 @@ void launch_first_col(int64_t nrows, const int64_t *rp, const int32_t *ci, int32
 void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
                      const uint16_t *dl, const double *dv, const int32_t *seg, int nsegs, const double *x, double *y,
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
-                     int unroll /* 8-entry groups per lane in flight: 1, 2 or 4 */, hipStream_t st);
+                     int unroll /* 8-entry groups per lane in flight: 1, 2 or 4 */, hipStream_t st,
+                     const int32_t *slist = nullptr /* nslices entries: the slices to process */);
+// flag[r] = 1 when row r (sorted columns) references a ghost column (>= nlocal)
+void launch_row_has_ghost(int64_t nrows, const int64_t *rp, const int32_t *ci, int64_t nlocal, uint8_t *flag,
+                          hipStream_t st);
 
 // Level-aligned SELL-64 triangular factors (see kernels.hip)
 void launch_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *slot_len, const int64_t *rp,

@@ -32,6 +32,9 @@ Ctx::Ctx() {
 }
 Ctx::~Ctx() {
     if (hscal) (void)hipHostFree(hscal);
+    if (ev_x) (void)hipEventDestroy(ev_x);
+    if (ev_halo) (void)hipEventDestroy(ev_halo);
+    if (st_comm) (void)hipStreamDestroy(st_comm);
     if (st) (void)hipStreamDestroy(st);
 }
 void Ctx::ensure_scan(int64_t n) {
@@ -190,6 +193,7 @@ void build_sell(DevCSR &M, Ctx &c) {
             HIPCHK(hipGetLastError());
             c.sync();
             M.sell = std::move(S);
+            if (M.halo) classify_halo_slices(M, c);
             return;
         }
         S = std::make_unique<DevSELL>();
@@ -210,9 +214,62 @@ void build_sell(DevCSR &M, Ctx &c) {
     M.sell = std::move(S);
 }
 
+void classify_halo_slices(DevCSR &M, Ctx &c) {
+    if (!M.halo || !M.sell || !M.sell->d16) return;
+    DevSELL &S = *M.sell;
+    const int64_t n = M.nrows, ns = S.nslices;
+    DBuf<uint8_t> f(std::max<int64_t>(n, 1));
+    launch_row_has_ghost(n, M.rp.p, M.ci.p, M.halo->nlocal, f.p, c.st);
+    std::vector<uint8_t> hf(std::max<int64_t>(n, 1));
+    std::vector<int64_t> sf(ns + 1);
+    if (n) HIPCHK(hipMemcpyAsync(hf.data(), f.p, n, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipMemcpyAsync(sf.data(), S.sfirst.p, sizeof(int64_t) * (ns + 1), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    std::vector<int32_t> in, halo;
+    for (int64_t s = 0; s < ns; ++s) {
+        bool g = false;
+        for (int64_t r = sf[s]; r < std::min<int64_t>(sf[s + 1], n) && !g; ++r) g = hf[r] != 0;
+        (g ? halo : in).push_back((int32_t)s);
+    }
+    S.n_in = (int64_t)in.size();
+    S.n_halo = (int64_t)halo.size();
+    S.s_in.alloc(std::max<int64_t>(S.n_in, 1));
+    S.s_halo.alloc(std::max<int64_t>(S.n_halo, 1));
+    if (S.n_in) HIPCHK(hipMemcpyAsync(S.s_in.p, in.data(), sizeof(int32_t) * S.n_in, hipMemcpyHostToDevice, c.st));
+    if (S.n_halo)
+        HIPCHK(hipMemcpyAsync(S.s_halo.p, halo.data(), sizeof(int32_t) * S.n_halo, hipMemcpyHostToDevice, c.st));
+    c.sync();
+}
+
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z) {
     const double *ghost = nullptr;
     int64_t nlocal = M.ncols;
+    if (M.halo && c.halo_overlap && M.sell && M.sell->d16 && M.sell->n_halo + M.sell->n_in == M.sell->nslices) {
+        // interior slices on the solver stream while the pack + exchange run on
+        // the comm stream; the halo slices after the exchange.  Per-row sums
+        // are the kernel's as in the plain path (same result bitwise).  NCCL
+        // operations never overlap: the exchange waits for everything before
+        // this product on the solver stream, and the solver stream waits for
+        // the exchange before the halo slices (and any later collective).
+        Halo &H = *M.halo;
+        const DevSELL &S = *M.sell;
+        if (!c.st_comm) {
+            HIPCHK(hipStreamCreateWithFlags(&c.st_comm, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&c.ev_x, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&c.ev_halo, hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(c.ev_x, c.st));
+        HIPCHK(hipStreamWaitEvent(c.st_comm, c.ev_x, 0));
+        launch_d16_spmv(M.nrows, S.n_in, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y,
+                        alpha, beta, z, M.tag, nullptr, H.nlocal, c.d16_unroll, c.st, S.s_in.p);
+        launch_pack(H.nsend, H.send_idx.p, x, H.sendbuf.p, c.st_comm);
+        c.comm->exchange_dev(H.sendbuf.p, H.scnt, H.soff, H.ghost.p, H.rcnt, H.roff, c.st_comm);
+        HIPCHK(hipEventRecord(c.ev_halo, c.st_comm));
+        HIPCHK(hipStreamWaitEvent(c.st, c.ev_halo, 0));
+        launch_d16_spmv(M.nrows, S.n_halo, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y,
+                        alpha, beta, z, M.tag, H.ghost.p, H.nlocal, c.d16_unroll, c.st, S.s_halo.p);
+        return;
+    }
     if (M.halo) {
         Halo &H = *M.halo;
         launch_pack(H.nsend, H.send_idx.p, x, H.sendbuf.p, c.st);

@@ -70,6 +70,9 @@ struct Ctx {
     int d16_wide_lpr = 8;     // lanes per row of D16 slices with wide rows (option pls.d16_wide_lpr)
     int d16_unroll = 4;       // D16 SpMV 8-entry groups per lane in flight (option pls.d16_unroll)
     int d16_segs = D16_SEG;   // minimum D16 segment bases per lane (option pls.d16_segs; 8 where needed)
+    bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
+    hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
+    hipEvent_t ev_x = nullptr, ev_halo = nullptr;
     DBuf<char> scan_tmp;
     size_t scan_tmp_bytes = 0;
     Ctx();
@@ -93,6 +96,10 @@ struct DevSELL {
     DBuf<int64_t> sfirst;     // D16: first row of each slice (nslices + 1)
     int64_t wide_slices = 0;  // D16 slices with 8 lanes per row
     int nsegs = D16_SEG;      // D16 segment bases per lane: 4, or 8 when halo columns need them
+    // distributed products: slices without / with ghost columns (the first
+    // run while the halo exchange is in flight)
+    DBuf<int32_t> s_in, s_halo;
+    int64_t n_in = 0, n_halo = 0;
     int64_t bytes() const {  // bytes one product streams from the matrix
         return d16 ? stored * 10 + nslices * (64 * 4 * nsegs + 20) + 8 : stored * 12 + (nslices + 1) * 8;
     }
@@ -126,6 +133,10 @@ void upload_csr(DevCSR &M, int64_t nrows, int64_t ncols, const int64_t *rp, cons
 // Extract rows [r0, r1) with a column window (see WindowSpec), columns shifted.
 void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_t cshift, int64_t ncols,
                  DevCSR &dst, Ctx &c);
+// Distributed D16 matrices: split the slices into interior / halo lists (the
+// product overlaps the halo exchange with the interior slices).  build_sell
+// calls it for matrices with a halo.
+void classify_halo_slices(DevCSR &M, Ctx &c);
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha = 1.0, double beta = 0.0,
           const double *z = nullptr);
 
