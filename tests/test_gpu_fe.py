@@ -1,0 +1,161 @@
+"""GPU parity on true poromechanics systems: A, P, P_diff assembled by the
+P2-P2-P1 swelling assembler (lib/fe_swelling.py, lib/Assembler.py's forms)
+and handed to libpls.so through Handle.from_csr, against the CPU oracle on the
+same CSR.
+
+Bounds.  Iteration count and convergence reason exact.  The residual history:
+these systems are far worse conditioned than the synthetic SPD blocks (mass
+terms ~1e-2, elasticity ~4e3, the Darcy coupling phi0^2/kf = 1e5, Dirichlet
+unit rows; non-normal saddle-point operators), and GMRES amplifies
+summation-order rounding accordingly.  The oracle itself, with every inner PC
+output perturbed by 1e-15 relative, moves its own history by 1e-10 (diagonal,
+LU) to 1e-3 (undrained, LU) -- measured per case here by
+``_self_sensitivity`` (max over 4 seeds).  The bound is therefore
+max(RTOL_HIST = 1e-10, 10 x that noise floor) (the Anderson / AAR bounds of
+test_gpu_parity.py where larger); measured on the MI355X the device/oracle
+history deviation is 0.5-1.1x the oracle's own noise floor in every case.
+Independently of rounding, the device solution's true residual must meet the
+convergence test the history reports (||b - A x|| within 1e-2 relative of
+the last history entry) when the PC is linear."""
+import numpy as np
+import pytest
+
+from lib import fe_swelling as F
+from oracle.solver import OracleSolver
+
+pytestmark = pytest.mark.gpu
+
+RTOL_HIST = 1e-10
+
+BASE = {"solver type": "gmres", "solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": 300,
+        "pc type": "diagonal", "inner ksp type": "preonly", "inner pc type": "lu", "inner rtol": 1e-6,
+        "inner atol": 0, "inner maxiter": 1000, "inner monitor": False, "solver monitor": False,
+        "inner accel order": 0, "AAR order": 10, "AAR p": 5, "AAR omega": 1, "AAR beta": 1}
+
+
+def _db(inner, extra=None):
+    d = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right"}
+    for p in ("s_", "f_", "p_", "diff_", "fp_"):
+        d[p + "ksp_type"] = "preonly"
+        d[p + "pc_type"] = inner
+        if inner == "bjacobi":
+            d[p + "pc_bjacobi_blocks"] = "3"
+    d.update(extra or {})
+    return d
+
+
+def _self_sensitivity(s, params, db, ho, eps=1e-15, seeds=4):
+    """Max over seeds of the oracle's own history deviation when every inner
+    PC output is perturbed by eps (relative): the rounding noise floor."""
+    worst = 0.0
+    for seed in range(seeds):
+        o2 = OracleSolver(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, params, db, s.bcs_sub_pressure)
+        rng = np.random.default_rng(seed)
+        for name in ("ksp_s", "ksp_fp", "ksp_f", "ksp_p", "ksp_diff"):
+            ksp = getattr(o2.block_pc, name, None)
+            if ksp is None:
+                continue
+            orig = ksp.pc.apply
+            ksp.pc.apply = (lambda f: (lambda x: (lambda y: y * (1 + eps * rng.standard_normal(y.size)))(f(x))))(orig)
+        o2.solve(s.b)
+        h2 = np.asarray(o2.history)
+        n = min(len(h2), len(ho))
+        worst = max(worst, float(np.max(np.abs(h2[:n] - ho[:n]) / np.abs(ho[:n]))))
+    return worst
+
+
+def _compare(system, upd, db, linear_pc=True):
+    from lib.handle import Handle, params_to_options
+    params = dict(BASE, **upd)
+    s = system
+    o = OracleSolver(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, params, db, s.bcs_sub_pressure)
+    xo = o.solve(s.b)
+    opts = dict(db)
+    opts.update(params_to_options(params))
+    h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    x, r = h.solve(s.b)
+    hist, ho = h.history(), np.asarray(o.history)
+    assert r.its == o.its, f"its {r.its} vs oracle {o.its}"
+    assert r.reason == o.reason, f"reason {r.reason} vs oracle {o.reason}"
+    assert hist.shape == ho.shape
+    tol = RTOL_HIST
+    cond = max(getattr(o.solver, "max_cond", 1.0), getattr(o.block_pc.anderson, "max_cond", 1.0))
+    if cond > 1.0:
+        tol = max(RTOL_HIST, 50 * np.finfo(float).eps * cond)
+    tol = max(tol, 10 * _self_sensitivity(s, params, db, ho))
+    if params["solver type"] == "aar":
+        bound = tol * np.abs(ho) + 100 * np.finfo(float).eps * ho[0]
+        assert np.max(np.abs(hist - ho) / bound) <= 1.0
+    else:
+        rel = np.max(np.abs(hist - ho) / np.abs(ho))
+        assert rel <= tol, f"residual history rel diff {rel:.3e} (tol {tol:.1e})"
+    assert np.linalg.norm(x - xo) <= max(1e-8, tol) * np.linalg.norm(xo)
+    # AAR's history is ||M^-1 r||; with a nonlinear PC (inner Krylov) non-flexible
+    # GMRES's estimate is not the true residual -- in the reference too
+    if linear_pc and params["solver type"] != "aar" and r.reason > 0:
+        true_r = np.linalg.norm(s.b - s.A @ x)
+        assert abs(true_r - hist[-1]) <= 1e-2 * hist[-1] + 1e-12 * np.linalg.norm(s.b)
+    return r
+
+
+@pytest.mark.parametrize("dim,N,pc,inner,ordering", [
+    (2, 8, "diagonal", "lu", "field-major"),
+    (2, 8, "diagonal", "ilu", "interleaved"),
+    (2, 8, "diagonal 3-way", "ilu", "field-major"),
+    (2, 8, "diagonal 3-way", "lu", "interleaved"),
+    (2, 8, "undrained", "lu", "field-major"),
+    (3, 3, "diagonal", "ilu", "field-major"),
+    (3, 3, "diagonal 3-way", "lu", "interleaved"),
+])
+def test_gmres_on_assembled_swelling(gpu, dim, N, pc, inner, ordering):
+    s = F.assemble_swelling(dim, N, pc, ordering=ordering)
+    r = _compare(s, {"pc type": pc}, _db(inner))
+    assert r.reason > 0
+
+
+def test_gmres_not_converging_reason(gpu):
+    """undrained 3-way with ILU(0) blocks stalls on this system: DIVERGED_ITS
+    at maxit on both sides, histories equal to the last iteration.  (Block
+    Jacobi over 3 row slabs, which cuts the fp block's velocity-pressure
+    coupling, stalls too, but its stagnating history is rounding noise -- the
+    oracle's own 1e-15 sensitivity is 0.7 -- so it is not a parity case.)"""
+    s = F.assemble_swelling(2, 6, "undrained 3-way")
+    r = _compare(s, {"pc type": "undrained 3-way", "solver maxiter": 40}, _db("ilu"))
+    assert r.reason == -3 and r.its == 40
+
+
+def test_aar_on_assembled_swelling(gpu):
+    s = F.assemble_swelling(2, 8, "diagonal")
+    _compare(s, {"solver type": "aar", "solver maxiter": 200, "AAR order": 5, "AAR p": 3}, _db("lu"))
+
+
+def test_inner_cg_jacobi_on_assembled_swelling(gpu):
+    """Inner CG (unpreconditioned norm, rtol 1e-1) + Jacobi on the SPD solid
+    block, exact LU on fp: a nonlinear PC inside non-flexible GMRES."""
+    s = F.assemble_swelling(2, 6, "diagonal")
+    extra = {"s_ksp_type": "cg", "s_ksp_rtol": "1e-1", "s_ksp_norm_type": "unpreconditioned",
+             "s_pc_type": "jacobi"}
+    r = _compare(s, {"pc type": "diagonal", "solver maxiter": 100}, _db("lu", extra), linear_pc=False)
+    assert r.reason > 0
+
+
+@pytest.mark.parametrize("pc", ["diagonal", "diagonal 3-way", "undrained"])
+def test_swelling2d_n32_exact(gpu, pc):
+    """BASELINE.json configs[0] on true matrices: swelling.py's 2-D N=32 system
+    (17,989 dofs, 927,449 nnz -- dolfin's counts), the exact option set
+    (options/exact: right-PC GMRES, PREONLY + LU on every block) and
+    swelling.py:63-67's outer tolerances (atol 1e-8, rtol 1e-6, maxit 500)."""
+    s = F.assemble_swelling(2, 32, pc)
+    assert s.A.shape[0] == 17989 and s.A.nnz == 927449
+    r = _compare(s, {"pc type": pc, "solver maxiter": 500}, _db("lu"))
+    assert r.reason > 0
+
+
+@pytest.mark.parametrize("N,inner", [(8, "ilu"), (6, "lu")])
+def test_swelling3d_assembled(gpu, N, inner):
+    """swelling-3d.py's system (ks = 1e8, swelling-3d.py:95-107 boundary
+    conditions) at N=8 (30,207 dofs, 5.02M nnz) with ILU(0) blocks and N=6
+    with exact blocks, swelling-3d.py's maxit 100."""
+    s = F.assemble_swelling(3, N, "diagonal")
+    r = _compare(s, {"pc type": "diagonal", "solver maxiter": 100}, _db(inner))
+    assert r.reason > 0
