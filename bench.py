@@ -158,6 +158,8 @@ def cpu_baseline(args, params, db):
     system (the per-iteration work is linear in n)."""
     from oracle import synthetic as S
     Ns = args.cpu_N
+    if args.system == "fe":
+        return _cpu_baseline_fe(args, params, db)
     spec = S.SynthSpec(args.dim, Ns, SEED, DELTA)
     t0 = time.perf_counter()
     A, P = S.matrix(spec, 0), S.matrix(spec, 1)
@@ -205,6 +207,33 @@ def cpu_baseline(args, params, db):
             "raw_iters_per_s": rate}
 
 
+def _cpu_baseline_fe(args, params, db):
+    """--system fe: the Python oracle (1 thread) on the assembled swelling
+    system at N = cpu_N, iters/s scaled by DoF to the benched system."""
+    from lib.fe_swelling import assemble_swelling
+    from oracle.solver import OracleSolver
+    t0 = time.perf_counter()
+    fe = assemble_swelling(args.dim, args.cpu_N, params["pc type"])
+    n_sample = fe.A.shape[0]
+    n_metric = n_sample if args.N == args.cpu_N else (
+        6 * (2 * args.N + 1) ** 3 + (args.N + 1) ** 3 if args.dim == 3 else 4 * (2 * args.N + 1) ** 2 + (args.N + 1) ** 2)
+    p = dict(params)
+    p["solver maxiter"] = args.cpu_maxit
+    o = OracleSolver(fe.A, fe.P, fe.P_diff, fe.is_s, fe.is_f, fe.is_p, p, db, fe.bcs_sub_pressure)
+    o.solve(fe.b)  # first solve sets the inner PCs up (lazily, as PETSc does); time the second
+    t_setup = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    o.solve(fe.b)
+    dt = time.perf_counter() - t1
+    rate = o.its / dt
+    return {"value": rate * n_sample / n_metric, "unit": f"Krylov iters/s (scaled by DoF to the {n_metric}-DoF system)",
+            "cores": 1, "kind": "port",
+            "sample": (f"oracle (numpy/scipy + C kernels, 1 thread) {params['pc type']} / {params['solver type']} "
+                       f"solve of the assembled N={args.cpu_N} {args.dim}-D swelling system ({n_sample} DoF), {o.its} "
+                       f"outer iterations in {dt:.2f}s (second solve; assembly + setup + first solve {t_setup:.1f}s); iters/s x {n_sample}/{n_metric}"),
+            "raw_iters_per_s": rate}
+
+
 def _progress(rank, msg):
     """Progress on stderr (rank 0): long configurations stay visibly alive;
     stdout carries only the JSON line."""
@@ -244,6 +273,8 @@ def main():
     ap.add_argument("--d16-unroll", type=int, default=0, help="D16 SpMV: 8-entry groups per lane in flight (tuning)")
     ap.add_argument("--opt", action="append", default=[], help="extra library option key=value (diagnostics)")
     ap.add_argument("--replicas", action="store_true", help="G independent N=59 solves instead of one sharded solve")
+    ap.add_argument("--system", default="synthetic", choices=["synthetic", "fe"],
+                    help="fe: the P2-P2-P1 swelling system (lib/fe_swelling.py, assembled on the host; one GPU)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="host: host-staged gloo communicator (ranks may share a GPU; rehearsal only)")
     pre, _ = ap.parse_known_args()
@@ -266,6 +297,8 @@ def main():
     Nat.check(Nat.lib().pls_set_device(local if args.comm == "rccl" else 0))
 
     sharded = world > 1 and not args.replicas
+    if args.system == "fe" and world > 1:
+        raise SystemExit("--system fe runs on one GPU (the assembler is a host-side input generator)")
     N_glob = args.N
     if sharded:
         N_glob = int(round(args.N * world ** (1.0 / args.dim)))
@@ -283,10 +316,16 @@ def main():
         opts["pls.d16_unroll"] = str(args.d16_unroll)
     t0 = time.perf_counter()
     comm = None
+    fe = None
     if sharded:
         from lib.dist import Communicator
         comm = Communicator.rccl() if args.comm == "rccl" else Communicator.gloo()
         h = Handle.synthetic_dist(args.dim, N_glob, SEED, DELTA, opts, comm)
+    elif args.system == "fe":
+        from lib.fe_swelling import assemble_swelling
+        fe = assemble_swelling(args.dim, args.N, args.pc_type)
+        _progress(rank, f"assembled the {args.dim}-D N={args.N} swelling system in {time.perf_counter() - t0:.1f} s")
+        h = Handle.from_csr(fe.A, fe.P, fe.P_diff, fe.is_s, fe.is_f, fe.is_p, fe.bcs_sub_pressure, opts)
     else:
         h = Handle.synthetic(args.dim, args.N, SEED + rank, DELTA, opts)
     h.setup()
@@ -296,7 +335,13 @@ def main():
     _progress(rank, f"setup {t_setup:.2f} s ({n} DoF on this rank, nnz(A) {nnz})")
     d_b = Nat.DeviceArray(n)
     d_x = Nat.DeviceArray(n)
-    h.rhs_device(7, d_b.p)
+
+    def load_rhs():
+        if fe is not None:
+            d_b.upload(fe.b)
+        else:
+            h.rhs_device(7, d_b.p)
+    load_rhs()
 
     for _ in range(args.warmup):
         tw = time.perf_counter()
@@ -346,7 +391,7 @@ def main():
     iso = h.bench_spmv(d_x.p, d_b.p, 10)
     d16, mat_bytes = h.spmv_layout()
     fmt_bytes = mat_bytes + 8.0 * n + 8.0 * n  # + x once + y once
-    h.rhs_device(7, d_b.p)
+    load_rhs()
 
     # achievable streaming bandwidth on this box: a 4 GiB
     # device-to-device copy (pls_bench_copy), read + write bytes / time
@@ -362,7 +407,7 @@ def main():
     traffic, traffic_src = None, None
     kname = ("void pls::k_d16_spmv<4, 1, false>" if d16 else "void pls::k_sell_spmv<8, 1, false>")
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_N59_summary.json")
-    if os.path.exists(pmc) and n_global == 10326954 and world == 1:
+    if os.path.exists(pmc) and n_global == 10326954 and world == 1 and fe is None:
         for k, v in json.load(open(pmc)).items():
             if k.startswith(kname) and v.get("read_bytes"):
                 traffic = v["read_bytes"] + (v.get("write_bytes") or 0.0)
@@ -382,9 +427,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded SPD 3-field block system, SURVEY.md 8(d); generated in HBM)",
+            "data": ("synthetic (seeded SPD 3-field block system, SURVEY.md 8(d); generated in HBM)" if fe is None else
+                     "P2-P2-P1 swelling FE system (lib/fe_swelling.py: lib/Assembler.py's forms, first time step; "
+                     "assembled on the host, copied to HBM before timing)"),
             "config": {
-                "workload": (f"{args.config}: {args.dim}-D N={N_glob} ({n_global} DoF): outer "
+                "workload": (f"{args.config}{' on the assembled swelling FE system' if fe is not None else ''}: "
+                             f"{args.dim}-D N={N_glob} ({n_global} DoF): outer "
                              + ("GMRES right-PC" if args.solver == "gmres" else f"AAR({args.aar_order}, p=5)")
                              + f" rtol 1e-6 atol {args.atol:g} maxit={args.maxit}, "
                              + ("2-way" if args.pc_type == "diagonal" else "3-way") + " block PC, "

@@ -1660,6 +1660,8 @@ template <int LPR>
 __device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv, double acc) {
     if (LPR >= 2) acc += __shfl_xor(acc, 1);
     if (LPR >= 4) acc += __shfl_xor(acc, 2);
+    if (LPR >= 8) acc += __shfl_xor(acc, 4);
+    if (LPR >= 16) acc += __shfl_xor(acc, 8);
     const int32_t li = h & 0xFFFF;
     if ((x.lane % LPR) == 0 && li != 0xFFFF) x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
 }
@@ -1741,12 +1743,20 @@ __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int
     if (g0 >= g1) return;
     Sw2Ctx x{gslice, sptr, col, val, ys, g1, 0, 0, 0, 0, lane, wave, nw, upper};
     if (lpr == 4) sweep2<P, 4>(x, g0);
+    else if (lpr == 16) sweep2<P, 16>(x, g0);  // 8 / 16: long rows of the y-resident (gmem) sweep
+    else if (lpr == 8) sweep2<P, 8>(x, g0);
     else if (lpr == 2) sweep2<P, 2>(x, g0);
     else sweep2<P, 1>(x, g0);
 }
 
 static constexpr int SW_P = 7;  // factor entries per lane kept in registers per pipeline slot
 
+// GMEM: the block solution lives in y itself (global memory) instead of LDS --
+// blocks longer than the LDS holds (up to 65,534 rows: the 16-bit local row
+// index of the slice headers).  All waves of the workgroup share the CU's
+// vector L1, so y written by one wave before __syncthreads() is seen by the
+// others after it (workgroup-scope coherence, no cache maintenance needed).
+template <bool GMEM>
 __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *__restrict__ Lgoff,
                                                          const int64_t *__restrict__ Lgslice,
                                                          const int64_t *__restrict__ Lsptr,
@@ -1758,24 +1768,27 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
                                                          const int64_t *__restrict__ Usptr,
                                                          const int32_t *__restrict__ Ucol,
                                                          const double *__restrict__ Uval,
-                                                         const int32_t *__restrict__ Ulpr, const double *__restrict__ x,
-                                                         double *__restrict__ y, int64_t *__restrict__ prof) {
-    extern __shared__ __attribute__((aligned(16))) double ys[];
+                                                         const int32_t *__restrict__ Ulpr, const double *x,
+                                                         double *y, int64_t *__restrict__ prof) {
+    extern __shared__ __attribute__((aligned(16))) double lds_y[];
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
     const int64_t q = n / nblocks, r = n % nblocks;
     const int64_t b0 = blk * q + (blk < r ? blk : r);
+    double *ys = GMEM ? y + b0 : lds_y;
     const int64_t len = q + (blk < r ? 1 : 0);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int nw = blockDim.x >> 6;
     int64_t t0 = 0, t1 = 0;
     if (prof) t0 = wall_clock64();
-    for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
+    if (!GMEM || x != y)
+        for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
     __syncthreads();
     sweep_block<SW_P>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol, Lval, ys);
     if (prof) t1 = wall_clock64();
     sweep_block<SW_P>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol, Uval, ys);
-    for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
+    if (!GMEM)
+        for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
     if (prof && threadIdx.x == 0) {  // diagnostics (option pls.sweep_profile): 100 MHz wall clock
         int64_t *p = prof + blk * 8;
         p[0] = t0;
@@ -1790,22 +1803,29 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
 }
 
 int ilu_lds_max_rows() { return 163840 / 8; }
+int ilu_gmem_max_rows() { return 0xFFFE; }
 int ilu_lds_lane_entries() { return SW_P; }
 
 void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,
                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
-                           int64_t *prof) {
+                           int64_t *prof, bool gmem) {
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)163840);
         configured = true;
     }
+    if (gmem) {
+        k_ilu_blocks_lds<true><<<(unsigned)nblocks, 1024, 0, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
+                                                                   Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof);
+        return;
+    }
     const size_t bytes = (size_t)(n / nblocks + 1) * 8;
-    k_ilu_blocks_lds<<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr, Ugoff,
-                                                              Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof);
+    k_ilu_blocks_lds<false><<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval,
+                                                                     Llpr, Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y,
+                                                                     prof);
 }
 
 // =========================================================== distribution ====

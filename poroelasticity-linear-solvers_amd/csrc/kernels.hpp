@@ -158,14 +158,17 @@ void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t
                       const int32_t *col, const double *val, const double *sdinv, const double *b, double *y,
                       hipStream_t st);
 
-// Block-Jacobi ILU(0) apply, block solution resident in LDS (forward + backward
-// in one launch).  Valid when every block has <= ilu_lds_max_rows() rows.
+// Block-Jacobi ILU(0) apply, one workgroup per block, levels separated by
+// workgroup barriers (forward + backward in one launch).  Block solution
+// resident in LDS when every block has <= ilu_lds_max_rows() rows; gmem: kept
+// in y instead (blocks of up to ilu_gmem_max_rows() rows).
 int ilu_lds_max_rows();
+int ilu_gmem_max_rows();
 void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,
                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
-                           int64_t *prof = nullptr);
+                           int64_t *prof = nullptr, bool gmem = false);
 int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in registers
 // LDS-kernel stream layout (header entry per lane, lanes-per-row slices, block-local columns)
 void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,

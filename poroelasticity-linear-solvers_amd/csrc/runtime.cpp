@@ -554,7 +554,8 @@ static void build_tri_sell(const PCILU &P, const std::vector<int64_t> &rp, const
 // the lanes per row (1, 2 or 4) that fit every lane's share of the block's
 // longest row into the kernel's register window; slices of 64 / LPR rows of
 // one level; one header entry per lane.
-static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, const std::vector<int64_t> &rp,
+static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, int max_lpr,
+                          const std::vector<int64_t> &rp,
                           const std::vector<int64_t> &dg, const std::vector<int32_t> &order,
                           const std::vector<int64_t> &grp, const std::vector<int64_t> &goff, bool upper, LdsTri &D,
                           Ctx &c) {
@@ -569,8 +570,11 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
         // on short rows cost more in extra slices and headers than they gain)
         int64_t mx = 0;
         for (int64_t r = grp[goff[b]]; r < grp[goff[b + 1]]; ++r) mx = std::max(mx, rlen(order[r]));
+        // (the y-resident sweep, max_lpr 16: its y gathers miss LDS, so an
+        // in-level reload of a long row's tail costs an HBM round trip per
+        // level; up to 16 lanes keep every entry in the prefetched window)
         int l = 1;
-        while (l < 4 && (mx + l - 1) / l > W) l *= 2;
+        while (l < max_lpr && (mx + l - 1) / l > W) l *= 2;
         if (force_lpr) l = force_lpr;
         lpr[b] = l;
         const int64_t per = 64 / l;
@@ -658,7 +662,7 @@ static void envelope_csr(const DevCSR &M, DevCSR &E, Ctx &c) {
     upload_csr(E, n, n, erp.data(), eci.data(), ev.data(), c);
 }
 
-PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr) {
+PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr, int gmem_mode) {
     exact = exact_lu;
     allow_lds = lds;
     type = exact ? "lu" : (nb > 1 ? "bjacobi" : "ilu");
@@ -706,8 +710,17 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         c.sync();
     }
     if (hfail) throw Error("ILU(0): zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
-    const bool fits_lds = (n / nblocks + 1) <= ilu_lds_max_rows();
-    if (nblocks >= 64 || (fits_lds && allow_lds)) {
+    const int64_t blen = n / nblocks + 1;
+    const bool fits_lds = blen <= ilu_lds_max_rows() && gmem_mode != 1;
+    // Blocks too long for LDS: one workgroup per block with y itself as the
+    // block solution when levels are narrow -- FE blocks in a bandwidth-
+    // reducing order have ~30-150 rows per level and ~1,400 levels at 3-D
+    // N=12, where one launch per level is launch-latency bound (measured
+    // ~19 us per level).  Wide levels keep the grid-wide launch per level.
+    const bool narrow = nlev_L > 0 && n / nlev_L <= 2048;
+    const bool gmem = allow_lds && !fits_lds && gmem_mode >= 0 && blen <= ilu_gmem_max_rows() &&
+                      (narrow || nblocks >= 64 || gmem_mode == 1);
+    if (nblocks >= 64 || (fits_lds && allow_lds) || gmem) {
         std::vector<int32_t> oL, oU;
         std::vector<int64_t> gL, gU, fL, fU;
         block_level_groups(n, nblocks, rp, ci, false, oL, gL, fL);
@@ -715,10 +728,12 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         build_tri_sell(*this, rp, dg, oL, gL, &fL, false, Lf, c);
         build_tri_sell(*this, rp, dg, oU, gU, &fU, true, Uf, c);
         nlev_U = (int64_t)gU.size() - 1;
-        use_lds = allow_lds && fits_lds;
+        use_lds = (allow_lds && fits_lds) || gmem;
+        lds_gmem = gmem;
         if (use_lds) {
-            build_lds_tri(*this, n, nblocks, force_lpr, rp, dg, oL, gL, fL, false, Ls, c);
-            build_lds_tri(*this, n, nblocks, force_lpr, rp, dg, oU, gU, fU, true, Us, c);
+            const int max_lpr = gmem ? 16 : 4;
+            build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oL, gL, fL, false, Ls, c);
+            build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oU, gU, fU, true, Us, c);
         }
     } else {
         std::vector<int32_t> ordU;
@@ -734,7 +749,7 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
         DBuf<int64_t> prof;
         if (!profile_tag.empty()) prof.alloc(nblocks * 8);
         launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
-                              Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof.p);
+                              Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof.p, lds_gmem);
         if (!profile_tag.empty()) {
             // diagnostics: per-block sweep times (100 MHz wall clock), slowest first
             std::vector<int64_t> h(nblocks * 8);
@@ -861,7 +876,7 @@ std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
         const double gb = nbt * w * 4096.0 * 8.0 / 1e9;
         if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 64.0)) return std::make_unique<PCBandLU>(M, kl, ku, c);
     }
-    return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true));
+    return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true), 0, (int)o.integer("pls.ilu_gmem", 0));
 }
 
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
@@ -875,7 +890,8 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
     if (type == "ilu") {
         if (o.integer(prefix + "pc_factor_levels", 0) != 0)
             throw Error(prefix + "pc_factor_levels > 0: only ILU(0) is implemented");
-        return std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true));
+        return std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true), 0,
+                                       (int)o.integer("pls.ilu_gmem", 0));
     }
     if (type == "lu" || type == "cholesky") return make_lu(M, o, c);
     if (type == "bjacobi") {
@@ -889,7 +905,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
             if (o.integer(prefix + "sub_pc_factor_levels", 0) != 0)
                 throw Error(prefix + "sub_pc_factor_levels > 0: only ILU(0) is implemented");
             auto pc = std::make_unique<PCILU>(M, nb, c, false, o.flag("pls.ilu_lds", true),
-                                              (int)o.integer("pls.sweep_lpr", 0));
+                                              (int)o.integer("pls.sweep_lpr", 0), (int)o.integer("pls.ilu_gmem", 0));
             if (o.flag("pls.sweep_profile", false)) pc->profile_tag = prefix;
             return pc;
         }

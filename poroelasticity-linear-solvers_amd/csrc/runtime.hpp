@@ -249,12 +249,16 @@ struct PCILU : PC {
     DBuf<double> dinv;
     TriSELL Lf, Uf;
     LdsTri Ls, Us;            // built when the LDS kernel serves apply()
-    bool use_lds = false;
+    bool use_lds = false;  // one workgroup per block sweeps (k_ilu_blocks_lds)
+    bool lds_gmem = false;  // ... with the block solution kept in y (blocks too long for LDS)
     int64_t nlev_L = 0, nlev_U = 0;
     bool allow_lds = true;  // block solution resident in LDS when it fits
     bool exact = false;     // envelope pattern: exact LU (PCLU)
     std::string profile_tag;  // non-empty: dump per-block sweep timings once (option pls.sweep_profile)
-    PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0);
+    // gmem_mode (option pls.ilu_gmem): 0 auto, 1 force the y-resident
+    // workgroup sweep wherever blocks fit its 16-bit row index, -1 never
+    PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0,
+          int gmem_mode = 0);
     bool reentrant() const override { return profile_tag.empty(); }
     void apply(const double *x, double *y, Ctx &c) override;
 };

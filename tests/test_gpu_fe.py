@@ -159,3 +159,23 @@ def test_swelling3d_assembled(gpu, N, inner):
     s = F.assemble_swelling(3, N, "diagonal")
     r = _compare(s, {"pc type": "diagonal", "solver maxiter": 100}, _db(inner))
     assert r.reason > 0
+
+
+def test_swelling3d_n12_ilu_gmem_sweep(gpu):
+    """Whole-block ILU(0) on blocks longer than the LDS holds (3-D N=12: s
+    46,875 rows, fp 49,072 rows, ~1,440 levels per triangle): the
+    workgroup-per-block sweep with y-resident block solution, against the
+    oracle; and bitwise equal to the per-level launch path (pls.ilu_gmem -1)."""
+    from lib.handle import Handle, params_to_options
+    s = F.assemble_swelling(3, 12, "diagonal")
+    upd = {"pc type": "diagonal", "solver maxiter": 100}
+    r = _compare(s, upd, _db("ilu"))
+    assert r.reason > 0
+    opts = dict(_db("ilu"))
+    opts.update(params_to_options(dict(BASE, **upd)))
+    ha = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    hb = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure,
+                         dict(opts, **{"pls.ilu_gmem": "-1"}))
+    x = np.random.default_rng(5).standard_normal(s.A.shape[0])
+    ya, yb = ha.pc_apply(x), hb.pc_apply(x)
+    assert np.max(np.abs(ya - yb)) <= 1e-13 * np.max(np.abs(yb))

@@ -527,3 +527,32 @@ def test_bjacobi_block_counts(gpu, nb):
         db[pre + "pc_type"] = "bjacobi"
         db[pre + "pc_bjacobi_blocks"] = str(nb)
     _compare_solve(S.SynthSpec(2, 7), db=db)
+
+
+@pytest.mark.parametrize("inner,dim,N", [("ilu", 2, 10), ("bjacobi", 3, 3), ("lu", 2, 8)])
+def test_ilu_gmem_sweep(gpu, inner, dim, N):
+    """pls.ilu_gmem 1 forces the workgroup-per-block sweep with the block
+    solution kept in y (global memory; the path for blocks longer than the
+    LDS holds) on blocks that fit LDS.  It may give long rows 8 or 16 lanes
+    (the LDS sweep at most 4), which reorders each row's sum: <= 1e-13
+    relative; with the lanes per row pinned (pls.sweep_lpr, bjacobi) the
+    slices are the same and the apply is bitwise the LDS sweep's."""
+    spec = S.SynthSpec(dim, N)
+    db = dict(ILU_DB)
+    for pre in ("s_", "f_", "p_", "diff_", "fp_"):
+        db[pre + "pc_type"] = inner
+        if inner == "bjacobi":
+            db[pre + "pc_bjacobi_blocks"] = "3"
+    if inner == "lu":
+        db["pls.lu_path"] = "envelope"
+    if inner == "bjacobi":
+        db["pls.sweep_lpr"] = "4"
+    params = dict(BASE, **{"pc type": "diagonal 3-way"})
+    h0 = _handle(spec, params, db)
+    h1 = _handle(spec, params, dict(db, **{"pls.ilu_gmem": "1"}))
+    x = np.random.default_rng(3).standard_normal(spec.n)
+    y0, y1 = h0.pc_apply(x), h1.pc_apply(x)
+    if inner == "bjacobi":
+        assert np.array_equal(y0, y1)
+    else:
+        assert np.max(np.abs(y0 - y1)) <= 1e-13 * np.max(np.abs(y0))
