@@ -1540,15 +1540,19 @@ void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t
 // pressure blocks at the end of the fp ordering carry the most levels).
 // ------------------------------------------------ LDS sweep stream layout --
 // The block-Jacobi LDS kernel reads each level's slices as streams.  A block
-// whose rows are long gives each row LPR = 2 or 4 lanes (entries dealt round
-// robin, partial sums combined with two lane shuffles), so every lane's share
-// fits the P entries the pipeline keeps in registers; short-row blocks keep
-// LPR = 1.  Slice = 64 / LPR rows of one level.  Entry 0 of every lane is a
-// header -- col = (row - b0) | (entries of this lane << 16) (row 0xFFFF:
-// padding), val = 1/U_ii (upper factor) -- entries 1..L the lane's factor
+// whose rows are long gives each row LPR = 2 or 4 lanes (8 or 16 in the
+// y-resident variant; entries dealt round robin, partial sums combined with
+// lane shuffles), so every lane's share fits the P entries the pipeline keeps
+// in registers; short-row blocks keep LPR = 1.  Slice = 64 / LPR rows of one
+// level.  Entry 0 of every lane is a header -- col = (row - b0) | (entries of
+// this lane << SW_ROW_BITS) (row SW_ROW_PAD: padding; 14 bits hold the
+// longest row, ilu0_max_row()), val = 1/U_ii (upper factor) -- entries 1..L the lane's factor
 // entries with block-local columns.  The only metadata a level needs is where
 // its slice starts, known 64 levels ahead (see sweep2), so loads are issued D
 // levels before use without a dependent metadata hop.
+static constexpr int SW_ROW_BITS = 18;
+static constexpr int32_t SW_ROW_PAD = (1 << SW_ROW_BITS) - 1;  // local rows 0..262,142
+
 __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n,
                                                   const int32_t *s_lpr, const int32_t *order, const int64_t *rp,
                                                   const int32_t *ci, const double *lu, const int64_t *diag,
@@ -1570,7 +1574,7 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
         len = upper ? rp[i + 1] - diag[i] - 1 : diag[i] - rp[i];
     }
     const int64_t mine = len > sub ? (len - sub + lpr - 1) / lpr : 0;
-    ocol[base + lane] = (i >= 0 ? (int32_t)(i - b0) : 0xFFFF) | (int32_t)(mine << 16);
+    ocol[base + lane] = (i >= 0 ? (int32_t)(i - b0) : SW_ROW_PAD) | (int32_t)(mine << SW_ROW_BITS);
     oval[base + lane] = (upper && i >= 0) ? dinv[i] : 0.0;
     for (int64_t k = 1; k < L; ++k) {
         const int64_t j = (k - 1) * lpr + sub, pos = base + k * 64 + lane;
@@ -1662,8 +1666,8 @@ __device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv
     if (LPR >= 4) acc += __shfl_xor(acc, 2);
     if (LPR >= 8) acc += __shfl_xor(acc, 4);
     if (LPR >= 16) acc += __shfl_xor(acc, 8);
-    const int32_t li = h & 0xFFFF;
-    if ((x.lane % LPR) == 0 && li != 0xFFFF) x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
+    const int32_t li = h & SW_ROW_PAD;
+    if ((x.lane % LPR) == 0 && li != SW_ROW_PAD) x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
 }
 
 template <int LPR>
@@ -1671,7 +1675,7 @@ __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
     const int64_t base = x.sptr[sl], L = (x.sptr[sl + 1] - base) >> 6;
     const int32_t h = x.col[base + x.lane];
     const double dv = x.val[base + x.lane];
-    const int32_t len = (int32_t)((uint32_t)h >> 16);
+    const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
     double acc = 0.0;
     for (int64_t k = 1; k < L; ++k) {
         const int64_t pos = base + k * 64 + x.lane;
@@ -1688,7 +1692,7 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
     sw2_issue<P>(x, g + 2, ahead);
     if (cur.base >= 0) {
         const int32_t h = cur.c[0];
-        const int32_t len = (int32_t)((uint32_t)h >> 16);
+        const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
         double acc = 0.0;
 #pragma unroll
         for (int u = 1; u <= P; ++u) {
@@ -1752,7 +1756,7 @@ __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int
 static constexpr int SW_P = 7;  // factor entries per lane kept in registers per pipeline slot
 
 // GMEM: the block solution lives in y itself (global memory) instead of LDS --
-// blocks longer than the LDS holds (up to 65,534 rows: the 16-bit local row
+// blocks longer than the LDS holds (up to 262,142 rows: the 18-bit local row
 // index of the slice headers).  All waves of the workgroup share the CU's
 // vector L1, so y written by one wave before __syncthreads() is seen by the
 // others after it (workgroup-scope coherence, no cache maintenance needed).
@@ -1803,7 +1807,7 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
 }
 
 int ilu_lds_max_rows() { return 163840 / 8; }
-int ilu_gmem_max_rows() { return 0xFFFE; }
+int ilu_gmem_max_rows() { return SW_ROW_PAD - 1; }
 int ilu_lds_lane_entries() { return SW_P; }
 
 void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,
