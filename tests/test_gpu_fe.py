@@ -179,3 +179,41 @@ def test_swelling3d_n12_ilu_gmem_sweep(gpu):
     x = np.random.default_rng(5).standard_normal(s.A.shape[0])
     ya, yb = ha.pc_apply(x), hb.pc_apply(x)
     assert np.max(np.abs(ya - yb)) <= 1e-13 * np.max(np.abs(yb))
+
+
+@pytest.mark.parametrize("pc", ["diagonal", "diagonal 3-way"])
+def test_facade_time_loop_on_assembled_swelling(gpu, pc):
+    """swelling.py's driver sequence through the facades (lib/Poromechanics.py:
+    58-68 create, 88-98 per step: set_up + solve) on the assembled system with
+    options/exact loaded like the reference's -options_file: two time steps
+    (t = dt, 2 dt: new tractions, the same operators), each against the
+    oracle's persistent solver on the same right-hand side."""
+    import os
+    from lib import options as popts
+    from lib.IndexSet import IndexSet
+    from lib.Parser import load_options_lines
+    from lib.Preconditioner import Preconditioner
+    from lib.Solver import Solver
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lines = open(os.path.join(root, "options", "exact")).read().splitlines()
+    popts.DB.clear()
+    load_options_lines(lines)
+    params = dict(BASE, **{"pc type": pc, "solver maxiter": 500})
+    s = F.assemble_swelling(2, 12, pc)
+    index_map = IndexSet((s.is_s, s.is_f, s.is_p), two_way="3-way" not in pc)
+    prec = Preconditioner(index_map, s.A, s.P, s.P_diff, params, s.bcs_sub_pressure).get_pc()
+    solver = Solver(s.A, s.b, prec, params, index_map)
+    solver.create_solver(s.A, s.b, prec)
+    o = OracleSolver(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, params, _db("lu"), s.bcs_sub_pressure)
+    dt = F.SWELLING_2D["dt"]
+    try:
+        for step in (1, 2):
+            b = s.b if step == 1 else F.assemble_swelling(2, 12, pc, t=step * dt).b
+            solver.set_up()
+            x = np.zeros_like(b)
+            solver.solve(b, x)
+            xo = o.solve(b)
+            assert solver.getIterationNumber() == o.its
+            assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+    finally:
+        popts.DB.clear()
