@@ -1557,7 +1557,7 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
                                                   const int32_t *s_lpr, const int32_t *order, const int64_t *rp,
                                                   const int32_t *ci, const double *lu, const int64_t *diag,
                                                   const double *dinv, int upper, int64_t n, int64_t nb,
-                                                  const int64_t *sptr2, int32_t *ocol, double *oval) {
+                                                  const int64_t *sptr2, int32_t *ocol, double *oval, int wide) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl >= nslices) return;
@@ -1574,21 +1574,22 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
         len = upper ? rp[i + 1] - diag[i] - 1 : diag[i] - rp[i];
     }
     const int64_t mine = len > sub ? (len - sub + lpr - 1) / lpr : 0;
-    ocol[base + lane] = (i >= 0 ? (int32_t)(i - b0) : SW_ROW_PAD) | (int32_t)(mine << SW_ROW_BITS);
+    ocol[base + lane] = wide ? (i >= 0 ? (int32_t)(i - b0) : -1)
+                             : (i >= 0 ? (int32_t)(i - b0) : SW_ROW_PAD) | (int32_t)(mine << SW_ROW_BITS);
     oval[base + lane] = (upper && i >= 0) ? dinv[i] : 0.0;
     for (int64_t k = 1; k < L; ++k) {
         const int64_t j = (k - 1) * lpr + sub, pos = base + k * 64 + lane;
-        ocol[pos] = j < len ? (int32_t)(ci[src + j] - b0) : 0;
+        ocol[pos] = j < len ? (int32_t)(ci[src + j] - b0) : (wide && i >= 0 ? (int32_t)(i - b0) : 0);
         oval[pos] = j < len ? lu[src + j] : 0.0;
     }
 }
 void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,
                      const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu, const int64_t *diag,
                      const double *dinv, int upper, int64_t n, int64_t nb, const int64_t *sptr2, int32_t *ocol,
-                     double *oval, hipStream_t st) {
+                     double *oval, hipStream_t st, bool wide) {
     if (nslices > 0)
         k_lds_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, s_start, s_n, s_lpr, order, rp, ci, lu, diag,
-                                                                dinv, upper, n, nb, sptr2, ocol, oval);
+                                                                dinv, upper, n, nb, sptr2, ocol, oval, wide ? 1 : 0);
 }
 
 // One sweep over a block's levels.  Pipeline: the loads of level g+2 are
@@ -1660,17 +1661,20 @@ __device__ __forceinline__ void sw2_issue(Sw2Ctx &x, int64_t g, Sw2Slot<P> &s) {
     }
 }
 
-template <int LPR>
+// W (wide, the y-resident sweep): header col = local row (-1: padding lane),
+// a lane's padding entries point at its own row with value 0, so only the
+// slice length masks entries and blocks may have up to 2^31 rows.
+template <int LPR, bool W>
 __device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv, double acc) {
     if (LPR >= 2) acc += __shfl_xor(acc, 1);
     if (LPR >= 4) acc += __shfl_xor(acc, 2);
     if (LPR >= 8) acc += __shfl_xor(acc, 4);
     if (LPR >= 16) acc += __shfl_xor(acc, 8);
-    const int32_t li = h & SW_ROW_PAD;
-    if ((x.lane % LPR) == 0 && li != SW_ROW_PAD) x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
+    const int32_t li = W ? h : (h & SW_ROW_PAD);
+    if ((x.lane % LPR) == 0 && (W ? li >= 0 : li != SW_ROW_PAD)) x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
 }
 
-template <int LPR>
+template <int LPR, bool W>
 __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
     const int64_t base = x.sptr[sl], L = (x.sptr[sl + 1] - base) >> 6;
     const int32_t h = x.col[base + x.lane];
@@ -1681,18 +1685,18 @@ __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
         const int64_t pos = base + k * 64 + x.lane;
         const int32_t cc = x.col[pos];
         const double vv = x.val[pos];
-        if (k <= len) acc += vv * x.ys[cc];
+        if (W || k <= len) acc += vv * x.ys[cc];
     }
-    sw2_finish<LPR>(x, h, dv, acc);
+    sw2_finish<LPR, W>(x, h, dv, acc);
 }
 
-template <int P, int LPR>
+template <int P, int LPR, bool W>
 __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P> &cur, Sw2Slot<P> &ahead) {
     if (g + 2 >= x.gbase + 64) x.refill(g);
     sw2_issue<P>(x, g + 2, ahead);
     if (cur.base >= 0) {
         const int32_t h = cur.c[0];
-        const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
+        const int32_t len = W ? (int32_t)cur.L - 1 : (int32_t)((uint32_t)h >> SW_ROW_BITS);
         double acc = 0.0;
 #pragma unroll
         for (int u = 1; u <= P; ++u) {
@@ -1714,50 +1718,55 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
                 acc += (k0 + u <= len) ? t : 0.0;
             }
         }
-        sw2_finish<LPR>(x, h, cur.v[0], acc);
+        sw2_finish<LPR, W>(x, h, cur.v[0], acc);
         // levels with more slices than waves: the rest inline
         const int l = (int)(g - x.gbase);
         const int64_t s0 = readlane64(x.gv, l), s1 = readlane64(x.gv, l + 1);
-        for (int64_t sl = s0 + x.wave + x.nw; sl < s1; sl += x.nw) sw2_slice_inline<LPR>(x, sl);
+        for (int64_t sl = s0 + x.wave + x.nw; sl < s1; sl += x.nw) sw2_slice_inline<LPR, W>(x, sl);
     }
     __syncthreads();
 }
 
-template <int P, int LPR>
+template <int P, int LPR, bool W>
 __device__ __forceinline__ void sweep2(Sw2Ctx &x, int64_t g0) {
     x.refill(g0);
     Sw2Slot<P> s0, s1, s2;
     sw2_issue<P>(x, g0, s0);
     sw2_issue<P>(x, g0 + 1, s1);
     for (int64_t g = g0;;) {
-        sw2_level<P, LPR>(x, g, s0, s2);
+        sw2_level<P, LPR, W>(x, g, s0, s2);
         if (++g >= x.g1) break;
-        sw2_level<P, LPR>(x, g, s1, s0);
+        sw2_level<P, LPR, W>(x, g, s1, s0);
         if (++g >= x.g1) break;
-        sw2_level<P, LPR>(x, g, s2, s1);
+        sw2_level<P, LPR, W>(x, g, s2, s1);
         if (++g >= x.g1) break;
     }
 }
 
-template <int P>
+template <int P, bool W>
 __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int lane, int wave, int nw, bool upper,
                                             const int64_t *__restrict__ gslice, const int64_t *__restrict__ sptr,
                                             const int32_t *__restrict__ col, const double *__restrict__ val,
                                             double *ys) {
     if (g0 >= g1) return;
     Sw2Ctx x{gslice, sptr, col, val, ys, g1, 0, 0, 0, 0, lane, wave, nw, upper};
-    if (lpr == 4) sweep2<P, 4>(x, g0);
-    else if (lpr == 16) sweep2<P, 16>(x, g0);  // 8 / 16: long rows of the y-resident (gmem) sweep
-    else if (lpr == 8) sweep2<P, 8>(x, g0);
-    else if (lpr == 2) sweep2<P, 2>(x, g0);
-    else sweep2<P, 1>(x, g0);
+    if (W) {  // the y-resident sweep: 8 / 16 lanes for long rows
+        if (lpr == 16) sweep2<P, 16, W>(x, g0);
+        else if (lpr == 8) sweep2<P, 8, W>(x, g0);
+        else if (lpr == 4) sweep2<P, 4, W>(x, g0);
+        else if (lpr == 2) sweep2<P, 2, W>(x, g0);
+        else sweep2<P, 1, W>(x, g0);
+        return;
+    }
+    if (lpr == 4) sweep2<P, 4, W>(x, g0);
+    else if (lpr == 2) sweep2<P, 2, W>(x, g0);
+    else sweep2<P, 1, W>(x, g0);
 }
 
 static constexpr int SW_P = 7;  // factor entries per lane kept in registers per pipeline slot
 
 // GMEM: the block solution lives in y itself (global memory) instead of LDS --
-// blocks longer than the LDS holds (up to 262,142 rows: the 18-bit local row
-// index of the slice headers).  All waves of the workgroup share the CU's
+// blocks longer than the LDS holds, with the wide slice headers (W).  All waves of the workgroup share the CU's
 // vector L1, so y written by one wave before __syncthreads() is seen by the
 // others after it (workgroup-scope coherence, no cache maintenance needed).
 template <bool GMEM>
@@ -1788,9 +1797,9 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
     if (!GMEM || x != y)
         for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
     __syncthreads();
-    sweep_block<SW_P>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol, Lval, ys);
+    sweep_block<SW_P, GMEM>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol, Lval, ys);
     if (prof) t1 = wall_clock64();
-    sweep_block<SW_P>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol, Uval, ys);
+    sweep_block<SW_P, GMEM>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol, Uval, ys);
     if (!GMEM)
         for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
     if (prof && threadIdx.x == 0) {  // diagnostics (option pls.sweep_profile): 100 MHz wall clock
@@ -1807,7 +1816,7 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
 }
 
 int ilu_lds_max_rows() { return 163840 / 8; }
-int ilu_gmem_max_rows() { return SW_ROW_PAD - 1; }
+int ilu_gmem_max_rows() { return 0x7FFFFFFF; }
 int ilu_lds_lane_entries() { return SW_P; }
 
 void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,

@@ -174,7 +174,7 @@ int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in r
 void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,
                      const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu, const int64_t *diag,
                      const double *dinv, int upper, int64_t n, int64_t nb, const int64_t *sptr2, int32_t *ocol,
-                     double *oval, hipStream_t st);
+                     double *oval, hipStream_t st, bool wide = false);
 
 // distribution helpers
 void launch_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint8_t *flag, hipStream_t st);

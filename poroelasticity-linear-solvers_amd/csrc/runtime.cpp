@@ -611,7 +611,7 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
     D.col.alloc(std::max<int64_t>(sptr.back(), 1));
     D.val.alloc(std::max<int64_t>(sptr.back(), 1));
     launch_lds_fill(ns, d_start.p, d_n.p, d_lpr.p, d_order.p, P.F.rp.p, P.F.ci.p, P.F.val.p, P.diag.p, P.dinv.p,
-                    upper ? 1 : 0, n, nb, D.sptr.p, D.col.p, D.val.p, c.st);
+                    upper ? 1 : 0, n, nb, D.sptr.p, D.col.p, D.val.p, c.st, /*wide headers: y-resident sweep*/ max_lpr > 4);
     HIPCHK(hipGetLastError());
     c.sync();
 }

@@ -256,7 +256,7 @@ struct PCILU : PC {
     bool exact = false;     // envelope pattern: exact LU (PCLU)
     std::string profile_tag;  // non-empty: dump per-block sweep timings once (option pls.sweep_profile)
     // gmem_mode (option pls.ilu_gmem): 0 auto, 1 force the y-resident
-    // workgroup sweep wherever blocks fit its 18-bit row index, -1 never
+    // workgroup sweep (also on blocks that fit LDS), -1 never
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0,
           int gmem_mode = 0);
     bool reentrant() const override { return profile_tag.empty(); }

@@ -217,3 +217,22 @@ def test_facade_time_loop_on_assembled_swelling(gpu, pc):
             assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
     finally:
         popts.DB.clear()
+
+
+def test_wide_gmem_sweep_beyond_18bit_rows(gpu):
+    """3-D N=22: s block 273,375 rows, fp 285,768 rows -- past the 18-bit row
+    index of the LDS sweep's slice headers; the y-resident sweep's wide
+    headers serve them.  Its PC apply against the per-level launch path
+    (pls.ilu_gmem -1) on the same factors."""
+    from lib.handle import Handle, params_to_options
+    s = F.assemble_swelling(3, 22, "diagonal")
+    assert s.is_s.size > (1 << 18)
+    opts = dict(_db("ilu"))
+    opts.update(params_to_options(dict(BASE, **{"pc type": "diagonal"})))
+    ha = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    hb = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure,
+                         dict(opts, **{"pls.ilu_gmem": "-1"}))
+    x = np.random.default_rng(7).standard_normal(s.A.shape[0])
+    ya, yb = ha.pc_apply(x), hb.pc_apply(x)
+    assert np.all(np.isfinite(ya))
+    assert np.max(np.abs(ya - yb)) <= 1e-13 * np.max(np.abs(yb))
