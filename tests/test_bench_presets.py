@@ -80,3 +80,15 @@ def test_aar_preset():
     args = _args("aar-m5")
     params, _ = bench.solver_options(args)
     assert params["solver type"] == "aar" and params["AAR order"] == 5 and params["AAR p"] == 5
+
+
+def test_fe_cpu_baseline_runs_the_assembled_system():
+    """bench.py --system fe: the CPU baseline solves the assembled swelling
+    system (lib/fe_swelling.py) with the preset's options and scales by DoF."""
+    a = _args("swelling2d-exact", system="fe", N=8, cpu_N=4)
+    params, db = bench.solver_options(a)
+    out = bench.cpu_baseline(a, params, db)
+    assert out["kind"] == "port" and out["cores"] == 1 and out["value"] > 0
+    n4, n8 = 4 * 9 ** 2 + 5 ** 2, 4 * 17 ** 2 + 9 ** 2
+    assert abs(out["value"] - out["raw_iters_per_s"] * n4 / n8) <= 1e-9 * out["value"]
+    assert "assembled N=4 2-D swelling system" in out["sample"]
