@@ -183,3 +183,30 @@ def test_oracle_solves_assembled_system(dim, N, pc, inner, its):
     r = np.linalg.norm(s.A @ x - s.b)
     assert r <= max(1e-6 * np.linalg.norm(s.b), 1e-8) * 1.0001
     assert np.linalg.norm(x - xd) <= 0.1 * np.linalg.norm(xd)
+
+
+def _fe_golden():
+    import glob
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fe")
+    return sorted(glob.glob(os.path.join(here, "*.npz")))
+
+
+@pytest.mark.parametrize("path", _fe_golden(), ids=lambda p: p.rsplit("/", 1)[-1][:-4])
+def test_fe_golden_fixtures(path):
+    """tests/golden/fe (tests/golden/make_golden_fe.py): the assembler's matrix
+    checksums and the oracle's solve on the assembled system are reproduced."""
+    import json
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_golden_fe as G
+    z = np.load(path, allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    name = os.path.basename(path)[:-4]
+    s, params, db, o, x = G.run_case(name)
+    assert np.allclose(G.checksums(s), z["checksums"], rtol=1e-13, atol=0)
+    assert o.its == int(z["its"]) and o.reason == int(z["reason"])
+    assert np.allclose(o.history, z["history"], rtol=1e-9, atol=0)
+    assert np.allclose(x, z["x"], rtol=1e-8, atol=1e-12 * np.abs(z["x"]).max())
+    assert meta["pc"] == params["pc type"]

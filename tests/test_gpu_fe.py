@@ -236,3 +236,18 @@ def test_wide_gmem_sweep_beyond_18bit_rows(gpu):
     ya, yb = ha.pc_apply(x), hb.pc_apply(x)
     assert np.all(np.isfinite(ya))
     assert np.max(np.abs(ya - yb)) <= 1e-13 * np.max(np.abs(yb))
+
+
+@pytest.mark.parametrize("name", ["fe_swelling2d_N6_diagonal_lu", "fe_swelling2d_N6_3way_ilu",
+                                  "fe_swelling3d_N2_diagonal_ilu"])
+def test_device_reproduces_fe_golden(gpu, name):
+    """tests/golden/fe fixtures on the device: iteration count and reason of
+    the committed fixture, history within the noise-floor bound of _compare."""
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fe")
+    z = np.load(os.path.join(here, name + ".npz"), allow_pickle=False)
+    import json
+    meta = json.loads(str(z["meta"]))
+    s = F.assemble_swelling(meta["dim"], meta["N"], meta["pc"])
+    r = _compare(s, {"pc type": meta["pc"]}, meta["db"])
+    assert r.its == int(z["its"]) and r.reason == int(z["reason"])
