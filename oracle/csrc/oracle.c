@@ -202,6 +202,8 @@ int oracle_synth_rowptr(int dim, int N, uint64_t seed, int64_t *row_ptr) {
     if (rc) { synth_free(&S); return rc; }
     int64_t n = S.n[0] + S.n[1] + S.n[2];
     row_ptr[0] = 0;
+    /* rows are independent: the pattern does not depend on the thread count */
+#pragma omp parallel for schedule(static)
     for (int64_t g = 0; g < n; ++g) {
         int a = field_of(&S, g);
         row_ptr[g + 1] = synth_row(&S, a, g - S.off[a], NULL);
@@ -229,40 +231,47 @@ int oracle_synth_fill(int dim, int N, uint64_t seed, double delta, int variant,
         int64_t l = row_ptr[g + 1] - row_ptr[g];
         if (l > maxrow) maxrow = l;
     }
-    int64_t *cols = (int64_t *)malloc(sizeof(int64_t) * (size_t)(maxrow + 1));
     uint64_t sv = seed ^ SALT_VAL;
     uint64_t sd = seed ^ (variant == 0 ? SALT_DIAGA : SALT_DIAGP);
-    for (int64_t g = 0; g < n; ++g) {
-        int a = field_of(&S, g);
-        int64_t i = g - S.off[a];
-        int64_t c = synth_row(&S, a, i, cols);
-        int64_t base = row_ptr[g];
-        int bcrow = (variant == 2 && a == 2 && oracle_synth_is_bc(seed, i));
-        double sum = 0.0;
-        int64_t dpos = -1;
-        for (int64_t k = 0; k < c; ++k) {
-            int64_t gj = cols[k];
-            col[base + k] = (int32_t)gj;
-            if (gj == g) { dpos = k; val[base + k] = 0.0; continue; }
-            int b = field_of(&S, gj);
-            uint64_t lo = (uint64_t)(g < gj ? g : gj), hi = (uint64_t)(g < gj ? gj : g);
-            double u = u01(hash3(sv, lo, hi));
-            double v = (a == b) ? -u : -(0.1 * u);
-            val[base + k] = bcrow ? 0.0 : v;
-            sum = sum + fabs(v);
+    int bad = 0;
+    /* rows are independent (each sums its own diagonal in column order), so
+     * the values are bitwise the same for any thread count */
+#pragma omp parallel reduction(| : bad)
+    {
+        int64_t *cols = (int64_t *)malloc(sizeof(int64_t) * (size_t)(maxrow + 1));
+#pragma omp for schedule(static)
+        for (int64_t g = 0; g < n; ++g) {
+            int a = field_of(&S, g);
+            int64_t i = g - S.off[a];
+            int64_t c = synth_row(&S, a, i, cols);
+            int64_t base = row_ptr[g];
+            int bcrow = (variant == 2 && a == 2 && oracle_synth_is_bc(seed, i));
+            double sum = 0.0;
+            int64_t dpos = -1;
+            for (int64_t k = 0; k < c; ++k) {
+                int64_t gj = cols[k];
+                col[base + k] = (int32_t)gj;
+                if (gj == g) { dpos = k; val[base + k] = 0.0; continue; }
+                int b = field_of(&S, gj);
+                uint64_t lo = (uint64_t)(g < gj ? g : gj), hi = (uint64_t)(g < gj ? gj : g);
+                double u = u01(hash3(sv, lo, hi));
+                double v = (a == b) ? -u : -(0.1 * u);
+                val[base + k] = bcrow ? 0.0 : v;
+                sum = sum + fabs(v);
+            }
+            if (dpos < 0) { bad = 1; continue; }
+            if (bcrow) {
+                val[base + dpos] = 1.0;
+            } else {
+                double u = u01(hash3(sd, (uint64_t)g, (uint64_t)g));
+                double sh = delta * (1.0 + u);
+                val[base + dpos] = sum + sh;
+            }
         }
-        if (dpos < 0) { free(cols); synth_free(&S); return -3; }
-        if (bcrow) {
-            val[base + dpos] = 1.0;
-        } else {
-            double u = u01(hash3(sd, (uint64_t)g, (uint64_t)g));
-            double sh = delta * (1.0 + u);
-            val[base + dpos] = sum + sh;
-        }
+        free(cols);
     }
-    free(cols);
     synth_free(&S);
-    return 0;
+    return bad ? -3 : 0;
 }
 
 /* right-hand side b (field-major), uniform in [-1, 1) */

@@ -49,6 +49,10 @@ CASES = [
      "db": dict(_db({"s_": 4, "fp_": 4}), **{"pls.d16_segs": "8"})},
     {"name": "aar_2d", "dim": 2, "N": 10, "params": dict(BASE, **{"solver type": "aar", "solver maxiter": 200}),
      "db": _db()},
+    # configs[4]: AAR depth m=5, p=5 on a 3-D system, sharded
+    {"name": "aar_m5_3d", "dim": 3, "N": 4,
+     "params": dict(BASE, **{"solver type": "aar", "solver maxiter": 200, "AAR order": 5, "AAR p": 5}),
+     "db": _db({"s_": 4, "fp_": 4})},
     {"name": "jacobi_left_2d", "dim": 2, "N": 9, "params": BASE,
      "db": {"global_ksp_type": "gmres", "s_ksp_type": "preonly", "s_pc_type": "jacobi",
             "fp_ksp_type": "preonly", "fp_pc_type": "jacobi"}},
