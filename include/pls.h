@@ -127,6 +127,22 @@ int pls_comm_destroy(pls_comm *comm);
  * must be destroyed before its communicator.  Vectors of the device entry
  * points are rank-local ([s_r | f_r | p_r]).                                 */
 int pls_create_synthetic_dist(const pls_synth_spec *spec, const char *options, pls_comm *comm, pls_handle **out);
+/* Multi-rank pls_create from the caller's matrices -- what the reference
+ * drivers hold under mpirun (paper-scripts/robustness_2d.sh:29): on every rank
+ * A, P, P_diff are the rank's MPIAIJ rows (A.getValuesCSR() of the operator of
+ * lib/Solver.py:151: nrows = this rank's rows, ncols = the global n, global
+ * column indices), rows [row_start, row_start + ns + nf + np) of the global
+ * (dolfin) numbering; is_s / is_f / is_p are the global indices of the dofs
+ * this rank owns (dofmap().dofs(), lib/IndexSet.py:38-41; 2-way: fp = their
+ * sorted union, the all-gather of lib/IndexSet.py:49 happens inside);
+ * bcs_sub_p = positions inside this rank's p sub-vector
+ * (lib/Poromechanics.py:48-55).  Field blocks take the row ownership of the
+ * rank-local index sets, as PETSc's createSubMatrix (lib/Preconditioner.py:
+ * 61-74) gives them.  Collective over comm; host vectors of pls_solve /
+ * pls_pc_apply / pls_matmult are this rank's rows in the caller's order.   */
+int pls_create_dist(const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff, int64_t row_start, const int32_t *is_s,
+                    int64_t ns, const int32_t *is_f, int64_t nf, const int32_t *is_p, int64_t np,
+                    const int32_t *bcs_sub_p, int64_t nbc, const char *options, pls_comm *comm, pls_handle **out);
 
 int pls_setup(pls_handle *h);
 /* New values (or patterns) of A / P / P_diff (NULL: unchanged), caller's

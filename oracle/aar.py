@@ -19,6 +19,48 @@ from __future__ import annotations
 import numpy as np
 
 
+def _householder_r(A):
+    """R (m x m, upper) of a rows x m panel by the reflections libpls's k_tsqr
+    applies (LAPACK dlarfg conventions)."""
+    A = np.array(A, dtype=np.float64)
+    rows, m = A.shape
+    for j in range(min(m, rows)):
+        sigma = float(A[j + 1:, j] @ A[j + 1:, j])
+        alpha = A[j, j]
+        if sigma == 0.0:
+            continue
+        nrm = np.sqrt(alpha * alpha + sigma)
+        beta = -nrm if alpha >= 0.0 else nrm
+        tau, scal = (beta - alpha) / beta, 1.0 / (alpha - beta)
+        for k in range(j + 1, m):
+            w = A[j, k] + scal * float(A[j + 1:, j] @ A[j + 1:, k])
+            A[j, k] -= tau * w
+            A[j + 1:, k] -= tau * w * (A[j + 1:, j] * scal)
+        A[j, j] = beta
+    out = np.zeros((m, m))
+    k = min(m, rows)
+    out[:k] = np.triu(A[:k])
+    return out
+
+
+def tsqr_lstsq(F, f, rows_per_block=512):
+    """min ||f + F a|| the way libpls solves it (csrc/capi.cpp AndersonLS):
+    Householder TSQR of [F | f] over 512-row chunks, then of the stacked R's
+    until one is left; a = R^-1 (-z) with z the last column.  Used by the tests
+    to measure how far two backward-stable solvers of the same least squares
+    drift apart in a whole AAR history (the noise floor of the comparison)."""
+    P = np.column_stack([F, f])
+    m = P.shape[1]
+    while True:
+        n = P.shape[0]
+        nch = -(-n // rows_per_block)
+        P = np.vstack([_householder_r(P[b * rows_per_block:(b + 1) * rows_per_block]) for b in range(nch)])
+        if nch == 1:
+            break
+    L = m - 1
+    return np.linalg.solve(P[:L, :L], -P[:L, L])
+
+
 class AAR:
     def __init__(self, order, p, omega, beta, A, pc, atol=1e-12, rtol=1e-8, maxiter=1000,
                  monitor=None):
@@ -30,6 +72,7 @@ class AAR:
         self.it = 0
         self.history = []
         self.max_cond = 1.0  # largest cond(F) met in an Anderson least squares
+        self.lstsq = None  # tests only: another backward-stable solver of min ||f + F a|| (noise floor)
 
     def _update_residual(self, b, xk):
         temp = b - self.A @ xk
@@ -62,7 +105,7 @@ class AAR:
                 mk = min(self.order, it)
                 F = np.vstack(self.F0).T
                 Q, R = np.linalg.qr(F)
-                alpha = np.linalg.solve(R, -Q.T @ fk)
+                alpha = np.linalg.solve(R, -Q.T @ fk) if self.lstsq is None else self.lstsq(F, fk)
                 self.max_cond = max(self.max_cond, float(np.linalg.cond(R)))
                 xk = xk + self.beta * fk
                 for i in range(mk):
@@ -90,6 +133,7 @@ class AndersonAcceleration:
         self.k = 0
         self.F, self.X, self.F0 = [], [], []
         self.max_cond = 1.0
+        self.lstsq = None
 
     def get_next_vector(self, gk):
         gk = np.asarray(gk, dtype=np.float64)
@@ -114,7 +158,7 @@ class AndersonAcceleration:
                     self.F0.pop(0)
                 F = np.vstack(self.F0).T
                 Q, R = np.linalg.qr(F)
-                alpha = np.linalg.solve(R, -Q.T @ self.fk)
+                alpha = np.linalg.solve(R, -Q.T @ self.fk) if self.lstsq is None else self.lstsq(F, self.fk)
                 self.max_cond = max(self.max_cond, float(np.linalg.cond(R)))
                 self.xk = self.xk + 1.0 * self.fk
                 for i in range(mk):

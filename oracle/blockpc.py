@@ -36,7 +36,11 @@ def submatrix(M, isrow, iscol):
 class BlockPC:
     def __init__(self, P, P_diff, index_sets, dims, flag_3_way, db,
                  inner_ksp_type="gmres", inner_pc_type="lu", w1=1.0, w2=0.1,
-                 accel_order=0, bcs_sub_pressure=(), dist_size=1):
+                 accel_order=0, bcs_sub_pressure=(), dist_size=1, dist_owner=None):
+        """dist_size=G: the G-rank preconditioner libpls builds on a synthetic
+        field-major system (even slabs per field, oracle/dist.py);
+        dist_owner: the rank of every global row of a caller-assembled system
+        (pls_create_dist): each block's rows split by owner."""
         self.flag_3_way = flag_3_way
         self.w1, self.w2 = w1, w2
         self.ns, self.nf, self.np = dims
@@ -45,7 +49,11 @@ class BlockPC:
         self.anderson = AndersonAcceleration(accel_order)
         sizes = (self.ns, self.nf, self.np)
 
-        def inner(prefix, M, ksp_type, pc_type, fields):
+        if dist_owner is not None:
+            dist_owner = np.asarray(dist_owner)
+            dist_size = int(dist_owner.max()) + 1
+
+        def inner(prefix, M, ksp_type, pc_type, fields, rows=None):
             # G ranks: BJACOBI blocks live inside each rank's [field slabs] rows
             # (oracle/dist.py); other PC types are the same at any G
             pc = None
@@ -54,14 +62,15 @@ class BlockPC:
                 if ptype in ("ilu", "lu", "cholesky"):
                     raise ValueError(f"{prefix}pc_type {ptype} is not distributable; use bjacobi")
                 if ptype == "bjacobi":
-                    from .dist import PCBJacobiIndexed, bjacobi_blocks
+                    from .dist import PCBJacobiIndexed, bjacobi_blocks, bjacobi_blocks_owned
                     nbt = opt(db, prefix, "pc_bjacobi_blocks", dist_size, int)
-                    pc = PCBJacobiIndexed(M, bjacobi_blocks(sizes, fields, dist_size, nbt),
-                                          opt(db, prefix + "sub_", "pc_type", "ilu"))
+                    blocks = (bjacobi_blocks_owned(dist_owner[rows], dist_size, nbt) if dist_owner is not None
+                              else bjacobi_blocks(sizes, fields, dist_size, nbt))
+                    pc = PCBJacobiIndexed(M, blocks, opt(db, prefix + "sub_", "pc_type", "ilu"))
             return petsc.ksp_from_options(prefix, db, M, M, ksp_type, pc_type, pc=pc)
 
         Ms_s = submatrix(P, self.is_s, self.is_s)
-        self.ksp_s = inner("s_", Ms_s, inner_ksp_type, inner_pc_type, (0,))
+        self.ksp_s = inner("s_", Ms_s, inner_ksp_type, inner_pc_type, (0,), self.is_s)
         if flag_3_way:
             self.Ms_f = submatrix(P, self.is_s, self.is_f)
             self.Ms_p = submatrix(P, self.is_s, self.is_p)
@@ -69,14 +78,14 @@ class BlockPC:
             Mf_f = submatrix(P, self.is_f, self.is_f)
             Mp_p = submatrix(P, self.is_p, self.is_p)
             Mp_diff = submatrix(P_diff, self.is_p, self.is_p)
-            self.ksp_f = inner("f_", Mf_f, inner_ksp_type, inner_pc_type, (1,))
-            self.ksp_p = inner("p_", Mp_p, inner_ksp_type, inner_pc_type, (2,))
-            self.ksp_p_diff = inner("diff_", Mp_diff, inner_ksp_type, inner_pc_type, (2,))
+            self.ksp_f = inner("f_", Mf_f, inner_ksp_type, inner_pc_type, (1,), self.is_f)
+            self.ksp_p = inner("p_", Mp_p, inner_ksp_type, inner_pc_type, (2,), self.is_p)
+            self.ksp_p_diff = inner("diff_", Mp_diff, inner_ksp_type, inner_pc_type, (2,), self.is_p)
         else:
             self.Mfp_s = submatrix(P, self.is_fp, self.is_s)
             Mfp_fp = submatrix(P, self.is_fp, self.is_fp)
             if inner_pc_type == "lu":
-                self.ksp_fp = inner("fp_", Mfp_fp, inner_ksp_type, "lu", (1, 2))
+                self.ksp_fp = inner("fp_", Mfp_fp, inner_ksp_type, "lu", (1, 2), self.is_fp)
             else:
                 # setup_fieldsplit: GMRES + fieldsplit unless the options override the pc type
                 ptype = opt(db, "fp_", "pc_type", "fieldsplit")
@@ -88,7 +97,7 @@ class BlockPC:
                     fs = PCFieldSplit(Mfp_fp, self.is_p, self.is_f, db, "fp_")
                     self.ksp_fp = petsc.ksp_from_options("fp_", db, Mfp_fp, Mfp_fp, "gmres", "fieldsplit", pc=fs)
                 else:
-                    self.ksp_fp = inner("fp_", Mfp_fp, "gmres", ptype, (1, 2))
+                    self.ksp_fp = inner("fp_", Mfp_fp, "gmres", ptype, (1, 2), self.is_fp)
 
     def apply(self, x):
         x = np.asarray(x, dtype=np.float64)
@@ -123,7 +132,7 @@ class BlockPC:
         return y
 
 
-def make_block_pc(P, P_diff, index_sets, dims, parameters, db, bcs_sub_pressure, dist_size=1):
+def make_block_pc(P, P_diff, index_sets, dims, parameters, db, bcs_sub_pressure, dist_size=1, dist_owner=None):
     """Preconditioner(...).get_pc() restated (lib/Preconditioner.py:263-291)."""
     pc_type = parameters["pc type"]
     if pc_type not in PC_TYPES:
@@ -131,4 +140,4 @@ def make_block_pc(P, P_diff, index_sets, dims, parameters, db, bcs_sub_pressure,
     flag_3_way = pc_type in ("diagonal 3-way", "undrained 3-way")
     return BlockPC(P, P_diff, index_sets, dims, flag_3_way, db,
                    parameters["inner ksp type"], parameters["inner pc type"], 1.0, 0.1,
-                   parameters["inner accel order"], bcs_sub_pressure, dist_size)
+                   parameters["inner accel order"], bcs_sub_pressure, dist_size, dist_owner)

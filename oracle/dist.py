@@ -54,6 +54,32 @@ def bjacobi_blocks(sizes, fields, size, total_blocks):
     return blocks
 
 
+def bjacobi_blocks_owned(owner, size, total_blocks):
+    """BJACOBI blocks of a field block whose row i lives on rank owner[i] (a
+    caller-assembled system: PETSc's createSubMatrix keeps each rank's own IS
+    entries, so rank r's rows are the block rows it owns, in block order)."""
+    owner = np.asarray(owner)
+    blocks = []
+    for r in range(size):
+        loc = np.nonzero(owner == r)[0].astype(np.int64)
+        nb = max(1, total_blocks // size + (1 if r < total_blocks % size else 0))
+        lens = petsc.bjacobi_block_sizes(len(loc), nb) if len(loc) else []
+        b0 = 0
+        for ln in lens:
+            blocks.append(loc[b0:b0 + ln])
+            b0 += ln
+    return blocks
+
+
+def row_owner(n, size):
+    """Rank of each global row under PETSc's default MPIAIJ split of n rows."""
+    own = np.empty(n, dtype=np.int64)
+    for r in range(size):
+        lo, ln = slab(n, size, r)
+        own[lo:lo + ln] = r
+    return own
+
+
 class PCBJacobiIndexed:
     type = "bjacobi"
 

@@ -41,13 +41,15 @@ def index_sets(is_s, is_f, is_p, two_way):
 
 
 class OracleSolver:
-    def __init__(self, A, P, P_diff, is_s, is_f, is_p, parameters, db, bcs_sub_pressure=(), dist_size=1):
-        """dist_size=G: the preconditioner libpls builds on G ranks (oracle/dist.py)."""
+    def __init__(self, A, P, P_diff, is_s, is_f, is_p, parameters, db, bcs_sub_pressure=(), dist_size=1,
+                 dist_owner=None):
+        """dist_size=G: the preconditioner libpls builds on G ranks (oracle/dist.py);
+        dist_owner: rank of every global row (caller-assembled systems, pls_create_dist)."""
         pc_type = parameters["pc type"]
         two_way = "3-way" not in pc_type
         sets = index_sets(is_s, is_f, is_p, two_way)
         dims = (len(is_s), len(is_f), len(is_p))
-        self.block_pc = make_block_pc(P, P_diff, sets, dims, parameters, db, bcs_sub_pressure, dist_size)
+        self.block_pc = make_block_pc(P, P_diff, sets, dims, parameters, db, bcs_sub_pressure, dist_size, dist_owner)
         self.pc = petsc.PCShell(self.block_pc.apply)
         stype = parameters["solver type"]
         atol = parameters["solver atol"]

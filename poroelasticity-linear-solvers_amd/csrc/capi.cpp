@@ -89,95 +89,96 @@ struct SynthHost {
 };
 
 // ============================================================ Anderson ===
-// Least squares min ||f + F a|| for the Anderson steps (reference lib/AAR.py:
-// 102-105 and lib/AndersonAcceleration.py:62-65 use numpy Householder QR of F).
-// Here Cholesky-QR2 of F from two fused device Gram passes (no n x m panel is
-// ever gathered to one place):
-//   pass 1: G1 = F^T F = R1^T R1;
-//   pass 2: Gram of [Q1 | f] with Q1 = F R1^{-1} formed on the fly
-//           -> Q1^T Q1 = R2^T R2 and Q1^T f;
-//   R = R2 R1, Q^T f = R2^{-T} Q1^T f, a = R^{-1} (-Q^T f).
-// f never enters a Cholesky factor, so a nearly-consistent f (the regime where
-// Anderson works) does not degrade R.
+// Least squares min ||f + F a|| for the Anderson steps.  The reference
+// (lib/AAR.py:102-105, lib/AndersonAcceleration.py:62-65) gathers F and f to
+// rank 0 and runs numpy's Householder QR, then solve(R, -Q^T f).  Here a
+// Householder TSQR of the panel [F | f] on the device (k_tsqr: 512-row
+// chunks, then the stacked R's, a fixed tree), one m x m R per rank; across
+// ranks the R's are all-gathered (m^2 doubles each) and the stack is factored
+// on the host in rank order.  The last column of R~ = [[R, z], [0, rho]]
+// holds z = Q^T f in R's own sign convention, so a = R^-1 (-z) -- the same
+// quantity numpy computes, by a Householder QR, so it stays backward stable up
+// to cond(F) ~ 1/eps (no Gram matrix squares the condition number).  Only an
+// exactly singular R fails, as numpy.linalg.solve raises LinAlgError.
+static void householder_qr_host(std::vector<double> &A, int rows, int m) {  // column-major rows x m, in place
+    for (int j = 0; j < m && j < rows; ++j) {
+        double sigma = 0.0;
+        for (int r = j + 1; r < rows; ++r) sigma += A[(size_t)j * rows + r] * A[(size_t)j * rows + r];
+        const double alpha = A[(size_t)j * rows + j];
+        if (sigma == 0.0) continue;
+        const double nrm = std::sqrt(alpha * alpha + sigma);
+        const double beta = alpha >= 0.0 ? -nrm : nrm, tau = (beta - alpha) / beta, scal = 1.0 / (alpha - beta);
+        for (int k = j + 1; k < m; ++k) {
+            double s = 0.0;
+            for (int r = j + 1; r < rows; ++r) s += A[(size_t)j * rows + r] * A[(size_t)k * rows + r];
+            const double w = A[(size_t)k * rows + j] + scal * s;
+            A[(size_t)k * rows + j] -= tau * w;
+            for (int r = j + 1; r < rows; ++r) A[(size_t)k * rows + r] -= tau * w * (A[(size_t)j * rows + r] * scal);
+        }
+        A[(size_t)j * rows + j] = beta;
+    }
+}
+
 struct AndersonLS {
-    DBuf<const double *> dptr;
-    DBuf<double> dR;     // Rinv (extended) column-major
-    DBuf<double> dG;     // packed gram
+    DBuf<const double *> dptr;  // column pointers of every TSQR level
+    DBuf<double> lvl[2];        // ping-pong stacks of R's
+    DBuf<double> Rdev;          // m x m, then G x m x m gathered
     std::vector<double> solve(const std::vector<const double *> &cols, const double *f, int64_t n, Ctx &c) {
         const int L = (int)cols.size();
         if (L < 1) return {};
         if (L + 1 > 16) throw Error("Anderson order > 15 not supported");
-        if (dptr.n < 16) { dptr.alloc(16); dR.alloc(256); dG.alloc(256); }
-        std::vector<const double *> hp(cols);
-        hp.push_back(f);
-        HIPCHK(hipMemcpyAsync((void *)dptr.p, hp.data(), sizeof(double *) * (L + 1), hipMemcpyHostToDevice, c.st));
-        auto gram = [&](int m, const double *rinv_dev) {
-            launch_gram(n, m, dptr.p, rinv_dev, c.partial.p, dG.p, c.st);
-            const int np = m * (m + 1) / 2;
-            c.comm->global_sum_dev(dG.p, np, c.st);
-            HIPCHK(hipMemcpyAsync(c.hscal, dG.p, sizeof(double) * np, hipMemcpyDeviceToHost, c.st));
-            c.sync();
-            std::vector<double> G(m * m, 0.0);
-            int t = 0;
-            for (int r = 0; r < m; ++r)
-                for (int cc = r; cc < m; ++cc, ++t) G[r * m + cc] = G[cc * m + r] = c.hscal[t];
-            return G;
-        };
-        // Cholesky of the leading L x L block of G (stride m): G = R^T R, R upper row-major L x L
-        auto chol = [&](const std::vector<double> &G, int m, std::vector<double> &R) {
-            R.assign(L * L, 0.0);
-            for (int j = 0; j < L; ++j) {
-                double s = G[j * m + j];
-                for (int k = 0; k < j; ++k) s -= R[k * L + j] * R[k * L + j];
-                if (!(s > 0.0)) throw Error("Anderson least squares: rank-deficient history (numpy would raise LinAlgError)");
-                R[j * L + j] = std::sqrt(s);
-                for (int i = j + 1; i < L; ++i) {
-                    double t = G[j * m + i];
-                    for (int k = 0; k < j; ++k) t -= R[k * L + j] * R[k * L + i];
-                    R[j * L + i] = t / R[j * L + j];
-                }
-            }
-        };
-        std::vector<double> R1, R2;
-        chol(gram(L, nullptr), L, R1);
-        // extended inverse diag(R1^{-1}, 1), column-major (L+1) x (L+1)
         const int m = L + 1;
-        std::vector<double> X(L * L, 0.0);  // row-major R1^{-1}
-        for (int j = 0; j < L; ++j) {
-            X[j * L + j] = 1.0 / R1[j * L + j];
-            for (int i = j - 1; i >= 0; --i) {
-                double s = 0.0;
-                for (int k = i + 1; k <= j; ++k) s += R1[i * L + k] * X[k * L + j];
-                X[i * L + j] = -s / R1[i * L + i];
-            }
+        const int64_t C = tsqr_rows_per_block();
+        // the TSQR tree: level 0 reads [F | f]; level l > 0 reads level l-1's stacked R's
+        std::vector<int64_t> rows{std::max<int64_t>(n, 1)};
+        while ((rows.back() + C - 1) / C > 1) rows.push_back(((rows.back() + C - 1) / C) * m);
+        const int nlev = (int)rows.size();
+        const size_t cap = (size_t)((rows[0] + C - 1) / C) * m * m;
+        if (lvl[0].n < cap) { lvl[0].alloc(cap); lvl[1].alloc(cap); }
+        if (dptr.n < (size_t)nlev * 16) dptr.alloc((size_t)nlev * 16);
+        const int G = c.comm->size;
+        if (Rdev.n < (size_t)(G + 1) * m * m) Rdev.alloc((size_t)(G + 1) * m * m);
+        std::vector<const double *> hp((size_t)nlev * 16, nullptr);
+        for (int k = 0; k < L; ++k) hp[k] = cols[k];
+        hp[L] = f;
+        for (int l = 1; l < nlev; ++l)
+            for (int k = 0; k < m; ++k) hp[(size_t)l * 16 + k] = lvl[(l - 1) & 1].p + (size_t)k * rows[l];
+        HIPCHK(hipMemcpyAsync((void *)dptr.p, hp.data(), sizeof(double *) * hp.size(), hipMemcpyHostToDevice, c.st));
+        if (n == 0) HIPCHK(hipMemsetAsync(Rdev.p, 0, sizeof(double) * m * m, c.st));  // a rank without rows
+        for (int l = 0; l < nlev && n > 0; ++l) {
+            const bool last = l == nlev - 1;
+            double *out = last ? Rdev.p : lvl[l & 1].p;
+            const int64_t ldo = last ? m : ((rows[l] + C - 1) / C) * m;
+            launch_tsqr(rows[l], m, dptr.p + (size_t)l * 16, out, ldo, c.st);
         }
-        std::vector<double> ext(m * m, 0.0);
-        for (int r = 0; r < L; ++r)
-            for (int cc = 0; cc < L; ++cc) ext[cc * m + r] = X[r * L + cc];
-        ext[L * m + L] = 1.0;
-        HIPCHK(hipMemcpyAsync(dR.p, ext.data(), sizeof(double) * m * m, hipMemcpyHostToDevice, c.st));
-        std::vector<double> G2 = gram(m, dR.p);
-        chol(G2, m, R2);
-        // qtf = R2^{-T} (Q1^T f)
-        std::vector<double> qtf(L, 0.0);
-        for (int i = 0; i < L; ++i) {
-            double s = G2[i * m + L];
-            for (int k = 0; k < i; ++k) s -= R2[k * L + i] * qtf[k];
-            qtf[i] = s / R2[i * L + i];
+        std::vector<double> R((size_t)m * m);
+        if (G > 1) {
+            double *gat = Rdev.p + (size_t)m * m;
+            c.comm->allgather_dev(Rdev.p, m * m, gat, c.st);
+            std::vector<double> S((size_t)G * m * m);
+            HIPCHK(hipMemcpyAsync(S.data(), gat, sizeof(double) * S.size(), hipMemcpyDeviceToHost, c.st));
+            c.sync();
+            // stack the ranks' R's in rank order: (G m) x m column-major, then QR
+            const int rows_s = G * m;
+            std::vector<double> A((size_t)rows_s * m);
+            for (int g = 0; g < G; ++g)
+                for (int k = 0; k < m; ++k)
+                    for (int i = 0; i < m; ++i) A[(size_t)k * rows_s + g * m + i] = S[(size_t)g * m * m + (size_t)k * m + i];
+            householder_qr_host(A, rows_s, m);
+            for (int k = 0; k < m; ++k)
+                for (int i = 0; i < m; ++i) R[(size_t)k * m + i] = i <= k ? A[(size_t)k * rows_s + i] : 0.0;
+        } else {
+            HIPCHK(hipMemcpyAsync(R.data(), Rdev.p, sizeof(double) * R.size(), hipMemcpyDeviceToHost, c.st));
+            c.sync();
         }
-        // R = R2 R1 ; a = R^{-1} (-qtf)
-        std::vector<double> R(L * L, 0.0);
-        for (int i = 0; i < L; ++i)
-            for (int j = i; j < L; ++j) {
-                double s = 0.0;
-                for (int k = i; k <= j; ++k) s += R2[i * L + k] * R1[k * L + j];
-                R[i * L + j] = s;
-            }
+        // R~ column-major: R(i, k) = R[k m + i]; z = R~(0:L, L)
         std::vector<double> a(L, 0.0);
         for (int i = L - 1; i >= 0; --i) {
-            double s = -qtf[i];
-            for (int k = i + 1; k < L; ++k) s -= R[i * L + k] * a[k];
-            a[i] = s / R[i * L + i];
+            const double d = R[(size_t)i * m + i];
+            if (d == 0.0) throw Error("Anderson least squares: singular R (numpy.linalg.solve raises LinAlgError)");
+            double s = -R[(size_t)L * m + i];
+            for (int k = i + 1; k < L; ++k) s -= R[(size_t)k * m + i] * a[k];
+            a[i] = s / d;
         }
         return a;
     }
@@ -287,30 +288,53 @@ struct BlockPC : PC {
 
 // ========================================================== distribution ===
 // Row slabs per field (the analogue of PETSc MPIAIJ ownership ranges): rank r
-// owns rows [lo_f, lo_f + len_f) of every field f (PETSc split: the first
-// n % size ranks one row more); local layout [s_r | f_r | p_r].
+// owns rows [lo_f, lo_f + len_f) of every field f; local layout [s_r | f_r | p_r].
+// Synthetic systems use PETSc's split (the first n % size ranks one row
+// more); caller matrices (pls_create_dist) bring their own per-rank counts --
+// the rows each rank's index sets select, as PETSc's createSubMatrix keeps them.
 struct Dist {
     int rank = 0, size = 1;
     int64_t n[3] = {0, 0, 0}, off[3] = {0, 0, 0}, lo[3] = {0, 0, 0}, len[3] = {0, 0, 0}, loff[3] = {0, 0, 0};
     int64_t nloc = 0;
+    std::vector<int64_t> start[3];  // start[f][q]: first row of field f owned by rank q (size + 1 entries)
     static void slab(int64_t N, int size, int r, int64_t &lo, int64_t &len) {
         const int64_t q = N / size, rem = N % size;
         lo = r * q + std::min<int64_t>(r, rem);
         len = q + (r < rem ? 1 : 0);
     }
-    void init(const int64_t nf[3], int r, int s) {
+    void range(int f, int q, int64_t &lo_, int64_t &len_) const {
+        lo_ = start[f][q];
+        len_ = start[f][q + 1] - lo_;
+    }
+    // counts[f][q] = rows of field f on rank q
+    void init_counts(const std::vector<int64_t> counts[3], int r, int s) {
         rank = r;
         size = s;
         int64_t o = 0, lo_ = 0;
         for (int f = 0; f < 3; ++f) {
-            n[f] = nf[f];
+            start[f].assign(s + 1, 0);
+            for (int q = 0; q < s; ++q) start[f][q + 1] = start[f][q] + counts[f][q];
+            n[f] = start[f][s];
             off[f] = o;
-            o += nf[f];
-            slab(nf[f], s, r, lo[f], len[f]);
+            o += n[f];
+            lo[f] = start[f][r];
+            len[f] = counts[f][r];
             loff[f] = lo_;
             lo_ += len[f];
         }
         nloc = lo_;
+    }
+    void init(const int64_t nf[3], int r, int s) {
+        std::vector<int64_t> counts[3];
+        for (int f = 0; f < 3; ++f) {
+            counts[f].resize(s);
+            for (int q = 0; q < s; ++q) {
+                int64_t l0, l1;
+                slab(nf[f], s, q, l0, l1);
+                counts[f][q] = l1;
+            }
+        }
+        init_counts(counts, r, s);
     }
 };
 
@@ -350,7 +374,7 @@ static void make_dist(DevCSR &M, const Dist &D, int f0, int f1, Comm *comm, Ctx 
         if (q == D.rank) continue;
         for (int f = f0; f <= f1; ++f) {
             int64_t lo, len;
-            Dist::slab(D.n[f], D.size, q, lo, len);
+            D.range(f, q, lo, len);
             for (int64_t i = 0; i < len; ++i) {
                 const int64_t g = cs_off[f] + lo + i;
                 if (flag[g]) {
@@ -1053,6 +1077,156 @@ int pls_create_synthetic_dist(const pls_synth_spec *spec, const char *options, p
     PLS_TRY({
         if (!comm) throw Error("pls_create_synthetic_dist: communicator required");
         *out = reinterpret_cast<pls_handle *>(create_synthetic(spec, options, reinterpret_cast<Comm *>(comm)));
+    })
+}
+
+// Multi-rank drop-in from caller matrices: the reference runs under
+// `mpirun -np 8` (paper-scripts/robustness_2d.sh:29) where every rank holds the
+// MPIAIJ rows it owns (A.getValuesCSR() of lib/Solver.py:151's operator: local
+// rows, global columns) and the index sets of the dofs it owns
+// (lib/IndexSet.py:38-49).  PETSc's createSubMatrix (lib/Preconditioner.py:
+// 61-74) then gives every field block the row ownership of the rank-local IS
+// entries; the same here: field f of rank q is the contiguous internal range
+// start[f][q] .. start[f][q+1] (3-way fields s, f, p; 2-way s and
+// fp = sorted(f U p), PETSc's is_fp), columns renumbered to that field-major
+// global order, then make_dist builds the halo plan as for synthetic shards.
+static Handle *create_dist(const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff, int64_t row_start,
+                           const int32_t *is_s, int64_t ns, const int32_t *is_f, int64_t nf, const int32_t *is_p,
+                           int64_t np, const int32_t *bcs_sub_p, int64_t nbc, const char *options, Comm *cm) {
+    if (!A || !P) throw Error("pls_create_dist: A and P are required");
+    {
+        Options pre;
+        pre.parse(options);
+        validate_pc_type(pre);
+    }
+    auto H = std::make_unique<Handle>();
+    H->opt.parse(options);
+    H->parse_params();
+    H->timers.st = H->ctx.st;
+    H->ctx.comm = cm;
+    Ctx &c = H->ctx;
+    const int G = cm->size, r = cm->rank;
+    const int64_t nloc = ns + nf + np;
+    if (A->nrows != nloc || P->nrows != nloc || (Pdiff && Pdiff->nrows != nloc))
+        throw Error("pls_create_dist: local matrices must have ns + nf + np rows (this rank's rows)");
+    // this rank's rows are [row_start, row_start + nloc) of the caller's numbering
+    std::vector<char> seen(nloc, 0);
+    auto check_local = [&](const int32_t *is, int64_t m, const char *name) {
+        for (int64_t i = 0; i < m; ++i) {
+            const int64_t l = (int64_t)is[i] - row_start;
+            if (l < 0 || l >= nloc) throw Error(std::string(name) + ": index not owned by this rank");
+            if (i && is[i] <= is[i - 1]) throw Error(std::string(name) + ": must be sorted ascending and unique");
+            if (seen[l]) throw Error(std::string(name) + ": overlaps another field");
+            seen[l] = 1;
+        }
+    };
+    check_local(is_s, ns, "is_s");
+    check_local(is_f, nf, "is_f");
+    check_local(is_p, np, "is_p");
+    // internal local order and the field counts the Dist sees
+    std::vector<int64_t> order(is_s, is_s + ns);  // caller global indices in internal local order
+    int64_t cnt[3] = {ns, nf, np};
+    if (H->three_way) {
+        order.insert(order.end(), is_f, is_f + nf);
+        order.insert(order.end(), is_p, is_p + np);
+    } else {
+        std::vector<int64_t> fp(is_f, is_f + nf);
+        fp.insert(fp.end(), is_p, is_p + np);
+        std::sort(fp.begin(), fp.end());
+        std::vector<char> isf(nloc, 0);
+        for (int64_t i = 0; i < nf; ++i) isf[is_f[i] - row_start] = 1;
+        for (size_t t = 0; t < fp.size(); ++t) (isf[fp[t] - row_start] ? H->fp_is_f : H->fp_is_p).push_back((int32_t)t);
+        order.insert(order.end(), fp.begin(), fp.end());
+        cnt[1] = nf + np;
+        cnt[2] = 0;
+    }
+    // every rank's field counts -> ownership ranges of the internal numbering
+    std::vector<int64_t> all((size_t)3 * G);
+    cm->allgather_host(cnt, sizeof(int64_t) * 3, all.data());
+    std::vector<int64_t> counts[3];
+    int64_t maxloc = 0;
+    for (int f = 0; f < 3; ++f) counts[f].resize(G);
+    for (int q = 0; q < G; ++q) {
+        int64_t t = 0;
+        for (int f = 0; f < 3; ++f) t += (counts[f][q] = all[(size_t)q * 3 + f]);
+        maxloc = std::max(maxloc, t);
+    }
+    H->dist.init_counts(counts, r, G);
+    const Dist &D = H->dist;
+    const int64_t nglob = D.n[0] + D.n[1] + D.n[2];
+    if (A->ncols != nglob || P->ncols != nglob || (Pdiff && Pdiff->ncols != nglob))
+        throw Error("pls_create_dist: matrix columns must span the global system (sum of every rank's rows)");
+    // caller global index -> internal global index, from every rank's order
+    std::vector<int64_t> mine(maxloc, -1), every((size_t)maxloc * G);
+    std::copy(order.begin(), order.end(), mine.begin());
+    cm->allgather_host(mine.data(), sizeof(int64_t) * maxloc, every.data());
+    std::vector<int32_t> cmap(nglob, -1);
+    for (int q = 0; q < G; ++q) {
+        int64_t k = 0;
+        for (int f = 0; f < 3; ++f)
+            for (int64_t i = 0; i < counts[f][q]; ++i, ++k) {
+                const int64_t g = every[(size_t)q * maxloc + k];
+                if (g < 0 || g >= nglob || cmap[g] >= 0) throw Error("pls_create_dist: index sets do not partition 0..n-1");
+                cmap[g] = (int32_t)(D.off[f] + D.start[f][q] + i);
+            }
+    }
+    // local rows in internal order, columns in the internal global numbering
+    auto upload = [&](const pls_csr *M, DevCSR &out) {
+        std::vector<int64_t> rp(nloc + 1, 0);
+        for (int64_t i = 0; i < nloc; ++i) {
+            const int64_t o = order[i] - row_start;
+            rp[i + 1] = rp[i] + (M->row_ptr[o + 1] - M->row_ptr[o]);
+        }
+        std::vector<int32_t> ci(rp[nloc]);
+        std::vector<double> v(rp[nloc]);
+        std::vector<std::pair<int32_t, double>> row;
+        for (int64_t i = 0; i < nloc; ++i) {
+            const int64_t o = order[i] - row_start;
+            row.clear();
+            for (int64_t k = M->row_ptr[o]; k < M->row_ptr[o + 1]; ++k) {
+                const int32_t cc = M->col[k];
+                if (cc < 0 || cc >= nglob) throw Error("pls_create_dist: column index out of range");
+                row.emplace_back(cmap[cc], M->val[k]);
+            }
+            std::sort(row.begin(), row.end(), [](auto &a, auto &b) { return a.first < b.first; });
+            for (size_t t = 0; t < row.size(); ++t) {
+                ci[rp[i] + t] = row[t].first;
+                v[rp[i] + t] = row[t].second;
+            }
+        }
+        upload_csr(out, nloc, nglob, rp.data(), ci.data(), v.data(), c);
+    };
+    upload(A, H->A);
+    upload(P, H->P);
+    if (Pdiff) {
+        upload(Pdiff, H->Pd);
+        H->have_Pd = true;
+    }
+    H->ns = ns; H->nf = nf; H->np = np; H->n = nloc;
+    H->distributed = G > 1;
+    if (H->distributed) make_dist(H->A, D, 0, 2, cm, c);
+    H->perm.resize(nloc);
+    for (int64_t i = 0; i < nloc; ++i) H->perm[i] = order[i] - row_start;
+    H->dperm.alloc(std::max<int64_t>(nloc, 1));
+    HIPCHK(hipMemcpy(H->dperm.p, H->perm.data(), sizeof(int64_t) * nloc, hipMemcpyHostToDevice));
+    // bcs_sub_pressure: positions inside this rank's p sub-vector (what
+    // Poromechanics.py:48-55 computes from the rank's own dofs)
+    H->bcs.assign(bcs_sub_p, bcs_sub_p + nbc);
+    for (int32_t b : H->bcs)
+        if (b < 0 || b >= np) throw Error("bcs_sub_pressure: position out of range of the p sub-vector");
+    H->dbcs.alloc(std::max<int64_t>(nbc, 1));
+    if (nbc) HIPCHK(hipMemcpy(H->dbcs.p, H->bcs.data(), sizeof(int32_t) * nbc, hipMemcpyHostToDevice));
+    H->keep = H->opt.flag("pls.keep_matrices", true);
+    return H.release();
+}
+
+int pls_create_dist(const pls_csr *A, const pls_csr *P, const pls_csr *Pdiff, int64_t row_start, const int32_t *is_s,
+                    int64_t ns, const int32_t *is_f, int64_t nf, const int32_t *is_p, int64_t np,
+                    const int32_t *bcs_sub_p, int64_t nbc, const char *options, pls_comm *comm, pls_handle **out) {
+    PLS_TRY({
+        if (!comm || !out) throw Error("pls_create_dist: communicator and out are required");
+        *out = reinterpret_cast<pls_handle *>(create_dist(A, P, Pdiff, row_start, is_s, ns, is_f, nf, is_p, np,
+                                                          bcs_sub_p, nbc, options, reinterpret_cast<Comm *>(comm)));
     })
 }
 

@@ -755,84 +755,116 @@ void launch_lincomb(int64_t n, int k, const double *V, int64_t ldv, const double
     if (n > 0) k_lincomb<<<stream_grid(n), TPB, 0, st>>>(n, k, V, ldv, c_dev, y);
 }
 
-// Gram matrix of M <= 16 columns: G[a][b] for a <= b (packed upper, row-major),
-// optionally of Q = A * Rinv (Rinv upper triangular M x M, column-major) --
-// the second pass of Cholesky-QR2 for the Anderson least squares.
+// TSQR leaf / tree step for the Anderson least squares (numpy Householder QR
+// in the reference, lib/AAR.py:102-105): workgroup b takes rows
+// [b C, b C + C) of the m <= 16 columns cols[k] (rows >= n read as zero),
+// factors that C x m panel in LDS by m Householder reflections (LAPACK dlarfg
+// conventions: beta = -sign(alpha) ||x||, tau = (beta - alpha) / beta,
+// v = x / (alpha - beta) below the diagonal) and writes its m x m R (zero
+// below the diagonal) as rows [b m, b m + m) of a column-major matrix with
+// leading dimension ldo.  Stacked R's are factored again by the same kernel
+// until one R is left (a fixed tree: bitwise reproducible).  Each reflection
+// is one block reduction of the m - j dots sum_{r>j} A[j][r] A[k][r] (fixed
+// order: per-thread rows ascending, xor-shuffle tree, 4 waves in order).
+constexpr int TSQR_C = 512;
 template <int M>
-__global__ __launch_bounds__(TPB) void k_gram(int64_t n, const double *const *cols, const double *Rinv,
-                                              double *partial) {
-    __shared__ double lds[TPB / 64];
-    __shared__ double rinv[M * M];
-    if (Rinv)
-        for (int t = threadIdx.x; t < M * M; t += TPB) rinv[t] = Rinv[t];
-    __syncthreads();
-    const double *cp[M];
+__global__ __launch_bounds__(256) void k_tsqr(int64_t n, const double *const *cols, double *Rout, int64_t ldo) {
+    constexpr int C = TSQR_C, RPT = C / 256;
+    __shared__ double A[M * C];
+    __shared__ double red[4][M];
+    __shared__ double w[M];
+    __shared__ double cf[3];  // tau, scal, beta
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * C;
 #pragma unroll
-    for (int c = 0; c < M; ++c) cp[c] = cols[c];
-    int64_t s, e;
-    chunk_of(n, gridDim.x, blockIdx.x, s, e);
-    constexpr int NP = M * (M + 1) / 2;
-    double acc[NP];
+    for (int k = 0; k < M; ++k) {
+        const double *cp = cols[k];
 #pragma unroll
-    for (int t = 0; t < NP; ++t) acc[t] = 0.0;
-    for (int64_t i = s + threadIdx.x; i < e; i += TPB) {
-        double a[M];
-#pragma unroll
-        for (int c = 0; c < M; ++c) a[c] = cp[c][i];
-        if (Rinv) {
-            double q[M];
-#pragma unroll
-            for (int c = 0; c < M; ++c) {
-                double t = 0.0;
-#pragma unroll
-                for (int r = 0; r <= c; ++r) t += a[r] * rinv[c * M + r];
-                q[c] = t;
-            }
-#pragma unroll
-            for (int c = 0; c < M; ++c) a[c] = q[c];
+        for (int q = 0; q < RPT; ++q) {
+            const int r = tid + q * 256;
+            const int64_t g = r0 + r;
+            A[k * C + r] = g < n ? cp[g] : 0.0;
         }
-        int t = 0;
-#pragma unroll
-        for (int r = 0; r < M; ++r)
-#pragma unroll
-            for (int c = r; c < M; ++c) acc[t++] += a[r] * a[c];
     }
+    __syncthreads();
+    for (int j = 0; j < M; ++j) {
+        double p[M];
 #pragma unroll
-    for (int t = 0; t < NP; ++t) {
-        const double v = block_sum(acc[t], lds);
-        if (threadIdx.x == 0) partial[(int64_t)t * gridDim.x + blockIdx.x] = v;
+        for (int k = 0; k < M; ++k) p[k] = 0.0;
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int r = tid + q * 256;
+            if (r > j) {
+                const double vj = A[j * C + r];
+#pragma unroll
+                for (int k = 0; k < M; ++k)
+                    if (k >= j) p[k] += vj * A[k * C + r];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            if (k < j) continue;
+            double v = p[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0) red[wv][k] = v;
+        }
+        __syncthreads();
+        if (tid < M) {
+            const double sigma = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+            const double alpha = A[j * C + j];
+            double tau = 0.0, scal = 0.0, beta = alpha;
+            if (sigma != 0.0) {
+                const double nrm = sqrt(alpha * alpha + sigma);
+                beta = alpha >= 0.0 ? -nrm : nrm;
+                tau = (beta - alpha) / beta;
+                scal = 1.0 / (alpha - beta);
+            }
+            if (tid > j) {
+                const double sk = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+                w[tid] = A[tid * C + j] + scal * sk;
+            }
+            if (tid == 0) { cf[0] = tau; cf[1] = scal; cf[2] = beta; }
+        }
+        __syncthreads();
+        const double tau = cf[0], scal = cf[1];
+        if (tau != 0.0) {
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                const int r = tid + q * 256;
+                if (r > j) {
+                    const double v = A[j * C + r] * scal;
+#pragma unroll
+                    for (int k = 0; k < M; ++k)
+                        if (k > j) A[k * C + r] -= tau * w[k] * v;
+                } else if (r == j) {
+#pragma unroll
+                    for (int k = 0; k < M; ++k)
+                        if (k > j) A[k * C + j] -= tau * w[k];
+                }
+            }
+        }
+        if (tid == j) A[j * C + j] = cf[2];
+        __syncthreads();
+    }
+    for (int t = tid; t < M * M; t += 256) {
+        const int k = t / M, i = t % M;
+        Rout[(int64_t)k * ldo + (int64_t)blockIdx.x * M + i] = i <= k ? A[k * C + i] : 0.0;
     }
 }
 
-template <int M>
-static void gram_m(int nb, int64_t n, const double *const *cols, const double *Rinv, double *partial,
-                   hipStream_t st) {
-    k_gram<M><<<nb, TPB, 0, st>>>(n, cols, Rinv, partial);
-}
+int tsqr_rows_per_block() { return TSQR_C; }
 
-void launch_gram(int64_t n, int m, const double *const *cols_dev, const double *Rinv_dev, double *partial,
-                 double *out, hipStream_t st) {
-    const int nb = reduce_blocks(n);
+void launch_tsqr(int64_t n, int m, const double *const *cols_dev, double *Rout, int64_t ldo, hipStream_t st) {
+    const unsigned nb = (unsigned)((n + TSQR_C - 1) / TSQR_C);
+    if (nb == 0) return;
     switch (m) {
-        case 1: gram_m<1>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 2: gram_m<2>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 3: gram_m<3>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 4: gram_m<4>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 5: gram_m<5>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 6: gram_m<6>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 7: gram_m<7>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 8: gram_m<8>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 9: gram_m<9>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 10: gram_m<10>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 11: gram_m<11>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 12: gram_m<12>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 13: gram_m<13>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 14: gram_m<14>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 15: gram_m<15>(nb, n, cols_dev, Rinv_dev, partial, st); break;
-        case 16: gram_m<16>(nb, n, cols_dev, Rinv_dev, partial, st); break;
+#define PLS_TSQR(M) case M: k_tsqr<M><<<nb, 256, 0, st>>>(n, cols_dev, Rout, ldo); break;
+        PLS_TSQR(1) PLS_TSQR(2) PLS_TSQR(3) PLS_TSQR(4) PLS_TSQR(5) PLS_TSQR(6) PLS_TSQR(7) PLS_TSQR(8)
+        PLS_TSQR(9) PLS_TSQR(10) PLS_TSQR(11) PLS_TSQR(12) PLS_TSQR(13) PLS_TSQR(14) PLS_TSQR(15) PLS_TSQR(16)
+#undef PLS_TSQR
         default: return;
     }
-    k_final<<<m * (m + 1) / 2, TPB, 0, st>>>(nb, partial, out, 0);
 }
 
 // ================================================================ ILU(0) ===

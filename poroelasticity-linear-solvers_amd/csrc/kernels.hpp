@@ -85,10 +85,10 @@ void launch_maxpy_norm(int64_t n, int k, const double *V, int64_t ldv, const dou
 // y = sum_j c[j] * V[:, j] (c on device)
 void launch_lincomb(int64_t n, int k, const double *V, int64_t ldv, const double *c_dev, double *y,
                     hipStream_t st);
-// Gram of m columns (ptr list on device): G (upper, m*(m+1)/2) into out.
-// If Rinv != null, columns are first transformed q_row = a_row * Rinv (m x m upper, column-major).
-void launch_gram(int64_t n, int m, const double *const *cols_dev, const double *Rinv_dev,
-                 double *partial, double *out, hipStream_t st);
+// TSQR step (Anderson least squares): R of each TSQR rows-per-block row chunk of the
+// m <= 16 columns, written as rows [b m, b m + m) of a column-major matrix (leading dim ldo)
+int tsqr_rows_per_block();
+void launch_tsqr(int64_t n, int m, const double *const *cols_dev, double *Rout, int64_t ldo, hipStream_t st);
 
 // -------------------------------------------------------------------- ILU --
 // Factor the rows of one level in place (original CSR): lu, diag pos, dinv.

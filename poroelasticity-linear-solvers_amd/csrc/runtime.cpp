@@ -577,7 +577,15 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
         // measured slower: FE 3-D N=12 53 -> 44 it/s, N=20 unchanged)
         int l = 1;
         while (l < max_lpr && (mx + l - 1) / l > W) l *= 2;
-        if (force_lpr) l = force_lpr;
+        if (force_lpr) {
+            // pls.sweep_lpr: the sweep kernels are instantiated for 1/2/4 lanes per
+            // row (LDS) and 1/2/4/8/16 (y-resident); anything else would run slices
+            // under the wrong template and silently corrupt the apply
+            if (force_lpr < 1 || force_lpr > max_lpr || (force_lpr & (force_lpr - 1)))
+                throw Error("pls.sweep_lpr " + std::to_string(force_lpr) + " not supported by this sweep (allowed: 1.." +
+                            std::to_string(max_lpr) + ", powers of two)");
+            l = force_lpr;
+        }
         lpr[b] = l;
         const int64_t per = 64 / l;
         for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {

@@ -64,6 +64,39 @@ class Handle:
         return cls(out)
 
     @classmethod
+    def from_csr_dist(cls, A, P, P_diff, is_s, is_f, is_p, bcs_sub_pressure, options: dict, comm, row_start=None):
+        """This rank's share of a caller-assembled system (pls_create_dist):
+        A, P, P_diff = the rank's rows (global columns), is_* = the global
+        indices of the dofs it owns, bcs_sub_pressure = positions inside its p
+        sub-vector.  ``row_start`` (the rank's first global row) defaults to
+        the smallest owned index.  Collective over ``comm``; host vectors are
+        the rank's rows in the caller's order."""
+        keep = []
+        is_s, is_f, is_p = N.is_array(is_s), N.is_array(is_f), N.is_array(is_p)
+        nloc = is_s.size + is_f.size + is_p.size
+        if row_start is None:
+            row_start = int(min(a.min() for a in (is_s, is_f, is_p) if a.size)) if nloc else 0
+
+        def mk(M):
+            if M is None:
+                return None
+            ai, aj, av, _, nc = N.csr_of(M)
+            keep.extend([ai, aj, av])
+            return N.pls_csr(ai.size - 1, nc, ai.ctypes.data, aj.ctypes.data, av.ctypes.data)
+
+        cA, cP, cD = mk(A), mk(P), mk(P_diff)
+        bcs = np.ascontiguousarray(np.asarray(bcs_sub_pressure if bcs_sub_pressure is not None else [],
+                                              dtype=np.int32))
+        out = C.c_void_p()
+        N.check(N.lib().pls_create_dist(C.byref(cA), C.byref(cP), C.byref(cD) if cD is not None else None,
+                                        int(row_start), N.ptr(is_s), is_s.size, N.ptr(is_f), is_f.size,
+                                        N.ptr(is_p), is_p.size, N.ptr(bcs), bcs.size, options_text(options),
+                                        comm.ptr, C.byref(out)))
+        h = cls(out)
+        h._comm = comm
+        return h
+
+    @classmethod
     def synthetic(cls, dim, Nel, seed, delta, options: dict):
         spec = N.pls_synth_spec(int(dim), int(Nel), int(seed), float(delta))
         out = C.c_void_p()

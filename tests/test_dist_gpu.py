@@ -11,7 +11,7 @@ with the G-rank block-Jacobi structure (oracle/dist.py), itself checked against
 a G-process numpy emulation in tests/test_dist_cpu.py.  Tolerances as in
 tests/test_gpu_parity.py: synthetic rhs bitwise; SpMV / PC apply <= 1e-13
 relative; iteration count and reason exact; history h_k within
-1e-10 h_k + 100 eps h_0 (AAR: the cond(F)-scaled bound of test_gpu_parity).
+1e-10 h_k + 100 eps h_0 (AAR: the measured least-squares noise floor of test_gpu_parity).
 """
 import numpy as np
 import pytest
@@ -96,7 +96,17 @@ def test_dist_solve(ranks, case):
     xo = o.solve(b)
     ho = np.asarray(o.history)
     cond = getattr(o.solver, "max_cond", 1.0)
-    tol = max(1e-10, 50 * EPS * cond) if cond > 1.0 else 1e-10
+    tol = 1e-10
+    if cond > 1.0:
+        # measured noise floor of the Anderson least squares (test_gpu_parity):
+        # the oracle's history with numpy QR swapped for the device's TSQR
+        from oracle.aar import tsqr_lstsq
+        _, _, o2 = _oracle(case, G)
+        o2.solver.lstsq = tsqr_lstsq
+        o2.solve(b)
+        h2 = np.asarray(o2.history)
+        m = min(len(h2), len(ho))
+        tol = max(tol, 10 * float(np.max(np.abs(h2[:m] - ho[:m]) / (np.abs(ho[:m]) + 100 * EPS * ho[0]))))
     for p in parts:
         assert int(p["its"]) == o.its, (int(p["its"]), o.its)
         assert int(p["reason"]) == o.reason

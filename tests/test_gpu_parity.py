@@ -9,11 +9,11 @@ Tolerances (north star: iteration counts bit-exact, residual norms within
     residual-history entry within RTOL_HIST = 1e-10 relative.
   * Anderson steps (AAR, inner Anderson mixing): the least squares
     min ||f + F a|| is solved by numpy Householder QR in the reference and by a
-    device Cholesky-QR2 here; two backward-stable solvers agree only to
-    ~cond(F) * eps in a (measured: numpy QR vs CPU Cholesky-QR2 differ by 9e-9
-    in the AAR history at cond(F) = 6e7).  The history bound there is
-    max(RTOL_HIST, 50 * eps * max cond(F)) with cond(F) measured by the oracle;
-    iteration counts and reasons stay exact.
+    device Householder TSQR here; two backward-stable solvers agree only to
+    ~cond(F) * eps in a.  The history bound there is measured, not assumed:
+    max(RTOL_HIST, 10 x the deviation of the oracle's own history when its
+    numpy QR is swapped for a restatement of the device TSQR,
+    ``oracle.aar.tsqr_lstsq``); iteration counts and reasons stay exact.
 """
 import numpy as np
 import pytest
@@ -48,26 +48,48 @@ def _oracle(spec, params, db):
     return OracleSolver(A, P, Pd, is_s, is_f, is_p, params, db, S.bcs_sub_pressure(spec))
 
 
-def _self_sensitivity(spec, params, db, b, ho, eps=1e-15, seeds=4):
+def _self_sensitivity(spec, params, db, b, ho, eps=1e-15, seeds=4, o=None):
     """Max over a few seeds of the oracle's own history deviation when every
     inner PC output is perturbed by eps (relative) -- the rounding noise floor
     of configurations that amplify it (the deviation itself varies ~100x
-    between seeds, hence the max)."""
+    between seeds, hence the max).  ``o``: re-solve this oracle (its inner
+    factorizations are reused; GMRES keeps no state between solves) instead
+    of building one per seed."""
     worst = 0.0
     for seed in range(seeds):
-        o2 = _oracle(spec, params, db)
+        o2 = o if o is not None else _oracle(spec, params, db)
         rng = np.random.default_rng(seed)
+        saved = []
         for name in ("ksp_s", "ksp_fp", "ksp_f", "ksp_p"):
             ksp = getattr(o2.block_pc, name, None)
             if ksp is None:
                 continue
             orig = ksp.pc.apply
+            saved.append((ksp.pc, orig))
             ksp.pc.apply = (lambda f: (lambda x: (lambda y: y * (1 + eps * rng.standard_normal(y.size)))(f(x))))(orig)
         o2.solve(b)
+        for pc, orig in saved:
+            pc.apply = orig
         h2 = np.asarray(o2.history)
         n = min(len(h2), len(ho))
         worst = max(worst, float(np.max(np.abs(h2[:n] - ho[:n]) / np.abs(ho[:n]))))
     return worst
+
+
+def _ls_noise_floor(spec, params, db, b, ho):
+    """Deviation of the oracle's own history (relative, with AAR's absolute
+    floor) when its Anderson least squares uses the device's algorithm
+    (Householder TSQR, ``oracle.aar.tsqr_lstsq``) instead of numpy's QR."""
+    from oracle.aar import tsqr_lstsq
+    o2 = _oracle(spec, params, db)
+    if params["solver type"] == "aar":
+        o2.solver.lstsq = tsqr_lstsq
+    o2.block_pc.anderson.lstsq = tsqr_lstsq
+    o2.solve(b)
+    h2 = np.asarray(o2.history)
+    n = min(len(h2), len(ho))
+    floor = 100 * np.finfo(float).eps * ho[0] if params["solver type"] == "aar" else 0.0
+    return float(np.max(np.abs(h2[:n] - ho[:n]) / (np.abs(ho[:n]) + floor)))
 
 
 def _compare_solve(spec, upd=None, db=None, sensitivity=False, b=None):
@@ -92,9 +114,12 @@ def _compare_solve(spec, upd=None, db=None, sensitivity=False, b=None):
     tol = RTOL_HIST
     cond = max(getattr(o.solver, "max_cond", 1.0), getattr(o.block_pc.anderson, "max_cond", 1.0))
     if cond > 1.0:
-        tol = max(RTOL_HIST, 50 * np.finfo(float).eps * cond)
+        tol = max(RTOL_HIST, 10 * _ls_noise_floor(spec, params, db, b, ho))
     if sensitivity:
-        tol = max(tol, 10 * _self_sensitivity(spec, params, db, b, ho))
+        # AAR's F / X histories and inner Anderson mixing persist across solves
+        stateless = params["solver type"] != "aar" and not params.get("inner accel order")
+        reuse = o if stateless else None
+        tol = max(tol, 10 * _self_sensitivity(spec, params, db, b, ho, o=reuse))
     if params["solver type"] == "aar":
         # AAR's history is a recomputed residual ||M^-1 (b - A x_k)||: its attainable
         # absolute accuracy is ~eps * ||b|| = eps * h_0, not relative to h_k
@@ -223,6 +248,17 @@ def test_aar_ilu(gpu):
 
 def test_aar_order5(gpu):
     _compare_solve(S.SynthSpec(2, 8), {"solver type": "aar", "solver maxiter": 200, "AAR order": 5, "AAR p": 3})
+
+
+def test_aar_ill_conditioned_history(gpu):
+    """Anderson every 2nd step, depth 10, run to rtol 1e-10: the oracle's F
+    reaches cond(F) ~ 6e10 -- past where a Gram-based (Cholesky-QR) least
+    squares breaks down (the Gram squares it to ~1e21) and the regime numpy's
+    Householder QR in the reference still solves; the device TSQR must too."""
+    params = {"solver type": "aar", "solver maxiter": 300, "AAR order": 10, "AAR p": 2, "solver rtol": 1e-10,
+              "solver atol": 1e-14}
+    r, o = _compare_solve(S.SynthSpec(2, 8), params)
+    assert o.solver.max_cond > 1e10 and r.reason == 2
 
 
 def test_inner_anderson_order1(gpu):
