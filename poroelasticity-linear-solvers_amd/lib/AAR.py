@@ -4,8 +4,8 @@
 monitor_convergence)`` with ``solve(b, sol) -> it`` and ``getIterationNumber``.
 The iteration (46-128) runs in libpls.so on the PC's handle (the operator is
 the handle's A, which must be ``matA``); the Anderson least squares replaces the
-rank-0 numpy QR of full gathered vectors (85-108) with a device Cholesky-QR2 of
-the (order+1)^2 Gram matrix.  As in the reference, ``pc=None`` is an error
+rank-0 numpy QR of full gathered vectors (85-108) with a device Householder
+TSQR whose per-rank (order+1)^2 R factors are all-gathered.  As in the reference, ``pc=None`` is an error
 (the reference dereferences an undefined ``self.solver`` at 33-38).
 """
 from ._native import vec_array

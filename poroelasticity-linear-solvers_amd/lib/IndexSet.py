@@ -55,7 +55,15 @@ class IndexSet:
         self.dofmap_fp = np.sort(np.concatenate([self.dofmap_f, self.dofmap_p]))
         self.two_way = two_way
         if two_way:
-            self.dofmap_f, self.dofmap_p = get_local_fp_dofs(self.dofmap_fp, self.dofmap_f, self.dofmap_p)
+            # IndexSet.py:44-54: positions inside the all-gathered global fp list
+            dofs_fp_global = self.dofmap_fp
+            from .dist import world
+            if world()[1] > 1:
+                import torch.distributed as td
+                parts = [None] * world()[1]
+                td.all_gather_object(parts, self.dofmap_fp.tolist())
+                dofs_fp_global = np.asarray([d for part in parts for d in part], dtype=np.int64)
+            self.dofmap_f, self.dofmap_p = get_local_fp_dofs(dofs_fp_global, self.dofmap_f, self.dofmap_p)
         self.is_s = IS(self.dofmap_s)
         self.is_f = IS(self.dofmap_f)
         self.is_p = IS(self.dofmap_p)

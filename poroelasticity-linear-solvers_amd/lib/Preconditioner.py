@@ -5,12 +5,16 @@ validates the pc type exactly like the reference (263-280, ``sys.exit`` with
 the same message) and ``get_pc()`` builds the PC (282-291).  The work --
 sub-block extraction, inner KSP/PC setup (s_ f_ p_ diff_ fp_ prefixes, options
 win), and every ``apply`` (2-way 219-246, 3-way 150-218, inner Anderson
-248-249) -- runs in libpls.so on the GPU.
+248-249) -- runs in libpls.so on the GPU.  Inside a multi-rank job
+(torch.distributed initialised with world size G, the reference's
+``mpirun -np G``) the matrices are taken as this rank's rows and the handle is
+sharded over ``lib.dist.default_communicator()`` (pls_create_dist).
 """
 from time import perf_counter as time
 
 from . import options as _opts
 from ._native import csr_of, vec_array
+from .dist import default_communicator
 from .handle import Handle, params_to_options
 from .Printing import parprint
 
@@ -119,8 +123,15 @@ class Preconditioner:
         is_s, is_f, is_p = self.index_map.global_index_sets()
         opts = dict(_opts.DB)
         opts.update(params_to_options(self.parameters))
-        handle = Handle.from_csr(self.A, self.P, self.P_diff if flag_3_way else None, is_s, is_f, is_p,
-                                 self.bcs_sub_pressure, opts)
+        comm = default_communicator()
+        if comm is not None:
+            # one rank of G (mpirun -np G in the reference): the matrices are this
+            # rank's rows, the index sets the dofs it owns (pls_create_dist)
+            handle = Handle.from_csr_dist(self.A, self.P, self.P_diff if flag_3_way else None, is_s, is_f, is_p,
+                                          self.bcs_sub_pressure, opts, comm)
+        else:
+            handle = Handle.from_csr(self.A, self.P, self.P_diff if flag_3_way else None, is_s, is_f, is_p,
+                                     self.bcs_sub_pressure, opts)
         ctx = PreconditionerCC(handle, flag_3_way, (self.A, self.P, self.P_diff if flag_3_way else None))
         self.pc = PC(ctx)
         self.pc.setUp()

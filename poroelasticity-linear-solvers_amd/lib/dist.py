@@ -18,8 +18,11 @@ keeps a reference so the order holds).
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 from . import _native as N
+
+_DEFAULT = None
 
 
 class Communicator:
@@ -91,3 +94,43 @@ def torch_allgather(group=None):
         return [o.numpy().tobytes() for o in out]
 
     return allgather
+
+
+def world():
+    """(rank, size) of the torch.distributed job this process belongs to
+    ((0, 1) when none is initialised -- the single-process path)."""
+    try:
+        import torch.distributed as td
+        if td.is_available() and td.is_initialized():
+            return td.get_rank(), td.get_world_size()
+    except ImportError:
+        pass
+    return 0, 1
+
+
+def default_communicator():
+    """The communicator the facade shards over when the process is one rank of
+    a multi-rank job (the reference's ``mpirun -np G``; here torchrun /
+    torch.distributed), created once: RCCL on GPU ``LOCAL_RANK`` by default,
+    the host-staged gloo communicator when ``PLS_COMM=host`` (ranks sharing a
+    GPU).  None on a single rank."""
+    global _DEFAULT
+    rank, size = world()
+    if size <= 1:
+        return None
+    if _DEFAULT is None:
+        if os.environ.get("PLS_COMM", "rccl") == "host":
+            _DEFAULT = Communicator.gloo()
+        else:
+            N.check(N.lib().pls_set_device(int(os.environ.get("LOCAL_RANK", rank))))
+            _DEFAULT = Communicator.rccl()
+        import atexit
+        atexit.register(_release_default)
+    return _DEFAULT
+
+
+def _release_default():
+    global _DEFAULT
+    if _DEFAULT is not None:
+        _DEFAULT.destroy()
+        _DEFAULT = None

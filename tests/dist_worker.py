@@ -50,8 +50,26 @@ def run_callback(case, comm_ignored):
     return out
 
 
+def fe_rank_share(case, G, r):
+    """Rank r's share of an assembled swelling system under PETSc's default
+    MPIAIJ split of the global (dolfin-ordered) rows: its rows, the global
+    indices of the dofs it owns per field, its pressure-BC positions."""
+    from lib import fe_swelling as F
+    from oracle.dist import slab
+    s = F.assemble_swelling(case["dim"], case["N"], case["params"]["pc type"], ordering=case.get("ordering", "interleaved"))
+    lo, ln = slab(s.A.shape[0], G, r)
+    hi = lo + ln
+    own = [np.asarray(i)[(np.asarray(i) >= lo) & (np.asarray(i) < hi)] for i in (s.is_s, s.is_f, s.is_p)]
+    p_lo = int(np.searchsorted(np.asarray(s.is_p), lo))
+    bc = np.asarray(s.bcs_sub_pressure, dtype=np.int64)
+    bc_loc = bc[(bc >= p_lo) & (bc < p_lo + own[2].size)] - p_lo
+    return s, lo, hi, own, bc_loc
+
+
 def run_gpu(case, comm):
     import lib._native as N
+    if case.get("system") == "fe":
+        return run_gpu_fe(case, comm)
     from lib.handle import Handle, params_to_options
     from oracle import synthetic as S
     from oracle.dist import local_rows
@@ -77,6 +95,66 @@ def run_gpu(case, comm):
     x, r = h.solve(b)
     out = dict(x=x, rows=rows, its=r.its, reason=r.reason, hist=h.history(), b_dev=b_dev, b=b, Av=Av, Mv=Mv, v=v)
     h.destroy()
+    return out
+
+
+def run_gpu_fe(case, comm):
+    """pls_create_dist on a caller-assembled system (the reference's mpirun path)."""
+    import lib._native as N
+    from lib.handle import Handle, params_to_options
+    N.check(N.lib().pls_set_device(0))
+    s, lo, hi, own, bc_loc = fe_rank_share(case, comm.size, comm.rank)
+    opts = dict(case["db"])
+    opts.update(params_to_options(case["params"]))
+    three = "3-way" in case["params"]["pc type"]
+    if case.get("facade"):
+        return run_facade_fe(case, s, lo, hi, own, bc_loc)
+    h = Handle.from_csr_dist(s.A[lo:hi], s.P[lo:hi], s.P_diff[lo:hi] if three else None, own[0], own[1], own[2],
+                             bc_loc, opts, comm, row_start=lo)
+    rows = np.arange(lo, hi)
+    assert h.n == rows.size
+    v = np.random.default_rng(5).standard_normal(s.A.shape[0])
+    Av = h.matmult(v[rows])
+    h.setup()
+    Mv = h.pc_apply(v[rows])
+    x, r = h.solve(s.b[rows])
+    out = dict(x=x, rows=rows, its=r.its, reason=r.reason, hist=h.history(), Av=Av, Mv=Mv, v=v)
+    h.destroy()
+    return out
+
+
+def run_facade_fe(case, s, lo, hi, own, bc_loc):
+    """The reference driver's call sequence (lib/Poromechanics.py:58-98) on
+    every rank, unchanged: IndexSet -> Preconditioner(...).get_pc() ->
+    Solver(...).create_solver -> set_up -> solve; the facade sees the
+    torch.distributed job and shards (lib/dist.py default_communicator)."""
+    from lib import options as popts
+    from lib.IndexSet import IndexSet
+    from lib.Preconditioner import Preconditioner
+    from lib.Solver import Solver
+    os.environ["PLS_COMM"] = "host"  # ranks share the test box's one GPU
+    three = "3-way" in case["params"]["pc type"]
+    popts.DB.clear()
+    popts.DB.update(case["db"])
+    A, P = s.A[lo:hi], s.P[lo:hi]
+    Pd = s.P_diff[lo:hi] if three else None
+    index_map = IndexSet((own[0], own[1], own[2]), two_way=not three)
+    prec = Preconditioner(index_map, A, P, Pd, case["params"], bc_loc)
+    pc = prec.get_pc()
+    rows = np.arange(lo, hi)
+    v = np.random.default_rng(5).standard_normal(s.A.shape[0])
+    Av = pc.handle.matmult(v[rows])
+    Mv = np.zeros(rows.size)
+    pc.apply(v[rows].copy(), Mv)
+    b = s.b[rows].copy()
+    solver = Solver(A, b, pc, case["params"], index_map)
+    solver.create_solver(A, b, pc)
+    solver.set_up()
+    x = np.zeros_like(b)
+    solver.solve(b, x)
+    out = dict(x=x, rows=rows, its=solver.getIterationNumber(), reason=solver.getConvergedReason(),
+               hist=solver.history, Av=Av, Mv=Mv, v=v)
+    pc.handle.destroy()
     return out
 
 

@@ -59,6 +59,36 @@ CASES = [
 ]
 
 
+def _fe_db(G):
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right"}
+    for pre in ("s_", "f_", "p_", "diff_", "fp_"):
+        db[pre + "ksp_type"] = "preonly"
+        db[pre + "pc_type"] = "bjacobi"
+        db[pre + "pc_bjacobi_blocks"] = "3"
+    return db
+
+
+# caller-assembled swelling systems (lib/fe_swelling.py, dolfin-like interleaved
+# numbering) handed over rank by rank through pls_create_dist: every rank
+# passes its PETSc-split rows (global columns) and the index sets of the dofs
+# it owns -- the reference's mpirun path (paper-scripts/robustness_2d.sh:29)
+FE_BASE = dict(BASE, **{"solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": 60, "inner pc type": "bjacobi"})
+FE_CASES = [
+    {"name": "fe_threeway_2d", "system": "fe", "dim": 2, "N": 8,
+     "params": dict(FE_BASE, **{"pc type": "diagonal 3-way"}), "db": _fe_db(3)},
+    {"name": "fe_threeway_3d", "system": "fe", "dim": 3, "N": 3,
+     "params": dict(FE_BASE, **{"pc type": "diagonal 3-way"}), "db": _fe_db(3)},
+    {"name": "fe_twoway_3d", "system": "fe", "dim": 3, "N": 3,
+     "params": dict(FE_BASE, **{"pc type": "diagonal"}), "db": _fe_db(3)},
+    # the same through the unchanged facade call sequence (lib/Preconditioner.py,
+    # lib/Solver.py inside a torch.distributed job)
+    {"name": "fe_facade_threeway_2d", "system": "fe", "facade": True, "dim": 2, "N": 8,
+     "params": dict(FE_BASE, **{"pc type": "diagonal 3-way"}), "db": _fe_db(3)},
+    {"name": "fe_facade_twoway_3d", "system": "fe", "facade": True, "dim": 3, "N": 3,
+     "params": dict(FE_BASE, **{"pc type": "diagonal"}), "db": _fe_db(3)},
+]
+
+
 def _oracle(case, G):
     spec = S.SynthSpec(case["dim"], case["N"])
     A, P, Pd = S.matrix(spec, 0), S.matrix(spec, 1), S.matrix(spec, 2)
@@ -71,7 +101,7 @@ def _oracle(case, G):
 @pytest.fixture(scope="module", params=[2, 3])
 def ranks(request, tmp_path_factory):
     G = request.param
-    return G, launch("gpu", CASES, G, str(tmp_path_factory.mktemp(f"dist{G}")), timeout=900)
+    return G, launch("gpu", CASES + FE_CASES, G, str(tmp_path_factory.mktemp(f"dist{G}")), timeout=900)
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
@@ -114,6 +144,58 @@ def test_dist_solve(ranks, case):
         assert h.shape == ho.shape
         worst = np.max(np.abs(h - ho) / (tol * ho + 100 * EPS * ho[0]))
         assert worst <= 1.0, f"history off by {worst:.2f}x the bound"
+    x = assemble(parts)
+    assert np.linalg.norm(x - xo) <= max(1e-8, tol) * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("case", FE_CASES, ids=[c["name"] for c in FE_CASES])
+def test_dist_fe_caller_matrices(ranks, case):
+    """pls_create_dist vs OracleSolver(dist_owner=...): the G-rank block
+    Jacobi of a caller-assembled system splits every field block by the rows
+    each rank owns.  Bar: SpMV / PC apply <= 1e-13; its and reason exact;
+    history within max(1e-10, 10x the oracle's own deviation under 1e-15
+    relative perturbations of its inner PC outputs) -- these saddle-point
+    systems amplify rounding (tests/test_gpu_fe.py)."""
+    from lib import fe_swelling as F
+    from oracle.dist import row_owner
+    G, res = ranks
+    parts = res[case["name"]]
+    s = F.assemble_swelling(case["dim"], case["N"], case["params"]["pc type"], ordering="interleaved")
+    n = s.A.shape[0]
+    v = parts[0]["v"]
+    Av = assemble(parts, "Av")
+    assert np.max(np.abs(Av - s.A @ v) / (abs(s.A) @ np.abs(v) + 1e-300)) <= 1e-13
+
+    def oracle():
+        return OracleSolver(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, case["params"], case["db"],
+                            s.bcs_sub_pressure, dist_owner=row_owner(n, G))
+
+    o = oracle()
+    Mv = assemble(parts, "Mv")
+    Mo = o.block_pc.apply(v)
+    assert np.linalg.norm(Mv - Mo) <= 1e-13 * np.linalg.norm(Mo) * G
+    xo = o.solve(s.b)
+    ho = np.asarray(o.history)
+    # noise floor: the oracle's own history under 1e-15 perturbations of its inner PC outputs
+    worst = 0.0
+    for seed in range(3):
+        o2 = oracle()
+        rng = np.random.default_rng(seed)
+        for name in ("ksp_s", "ksp_fp", "ksp_f", "ksp_p", "ksp_p_diff"):
+            ksp = getattr(o2.block_pc, name, None)
+            if ksp is not None:
+                f = ksp.pc.apply
+                ksp.pc.apply = (lambda f: lambda x: (lambda y: y * (1 + 1e-15 * rng.standard_normal(y.size)))(f(x)))(f)
+        o2.solve(s.b)
+        h2 = np.asarray(o2.history)
+        m = min(len(h2), len(ho))
+        worst = max(worst, float(np.max(np.abs(h2[:m] - ho[:m]) / np.abs(ho[:m]))))
+    tol = max(1e-10, 10 * worst)
+    for p in parts:
+        assert int(p["its"]) == o.its and int(p["reason"]) == o.reason, (int(p["its"]), o.its)
+        h = p["hist"]
+        assert h.shape == ho.shape
+        assert np.max(np.abs(h - ho) / np.abs(ho)) <= tol
     x = assemble(parts)
     assert np.linalg.norm(x - xo) <= max(1e-8, tol) * np.linalg.norm(xo)
 
