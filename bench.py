@@ -12,11 +12,13 @@ value = whole-job Krylov iterations per second on the 10.33M-DoF system.  At
 G GPUs the solve is sharded the way the reference runs under MPI (one process
 per GPU, PETSc row slabs of every field, halo exchange before each SpMV,
 rank-ordered global sums, BJACOBI blocks inside each rank; RCCL over xGMI, see
-DESIGN.md §6) on a global system G times as large (3-D N = round(59 G^(1/3)),
-weak scaling: ~10.3M DoF per GPU, 256/264 s/fp blocks per GPU); one outer
-iteration there is worth n_global / 10,326,954 iterations of the metric's
-system, so value = outer iterations x n_global / 10,326,954 / max-over-ranks
-time.  ``--replicas`` instead runs G independent N=59 solves.
+DESIGN.md §6).  ``--scaling strong`` (the default at G > 1; north_star's
+"RCCL-dot scaling"): the same N=59 system on G GPUs with the same TOTAL
+BJACOBI block counts (PETSc's -pc_bjacobi_blocks is a total), value = outer
+iterations / max-over-ranks time.  ``--scaling weak``: a global system G
+times as large (3-D N = round(59 G^(1/3)), ~10.3M DoF and 256/264 blocks per
+GPU); one outer iteration there is worth n_global / 10,326,954 iterations of
+the metric's system.  ``--scaling replicas``: G independent N=59 solves.
 
 roofline: the dominant kernel is the CSR SpMV with A (one per outer
 iteration).  achieved = algorithmic bytes per launch
@@ -234,6 +236,23 @@ def _cpu_baseline_fe(args, params, db):
             "raw_iters_per_s": rate}
 
 
+def shard_plan(args, world):
+    """(sharded, global N) for G = world ranks; weak scaling also scales the
+    total BJACOBI block counts (blocks per GPU fixed), strong scaling keeps the
+    single-GPU system and its total block counts (PETSc's -pc_bjacobi_blocks
+    is a total over the ranks)."""
+    if args.replicas:
+        args.scaling = "replicas"
+    sharded = world > 1 and args.scaling != "replicas"
+    N_glob = args.N
+    if sharded and args.scaling == "weak":
+        N_glob = int(round(args.N * world ** (1.0 / args.dim)))
+        args.blocks_s *= world
+        args.blocks_fp *= world
+        args.blocks_p *= world
+    return sharded, N_glob
+
+
 def _progress(rank, msg):
     """Progress on stderr (rank 0): long configurations stay visibly alive;
     stdout carries only the JSON line."""
@@ -272,7 +291,9 @@ def main():
     ap.add_argument("--sell-d16", type=int, default=1, help="1: SELL-64/D16 SpMV layout (16-bit column deltas)")
     ap.add_argument("--d16-unroll", type=int, default=0, help="D16 SpMV: 8-entry groups per lane in flight (tuning)")
     ap.add_argument("--opt", action="append", default=[], help="extra library option key=value (diagnostics)")
-    ap.add_argument("--replicas", action="store_true", help="G independent N=59 solves instead of one sharded solve")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak", "replicas"],
+                    help="G > 1: strong (same system, same total block counts), weak (G x the DoF), replicas")
+    ap.add_argument("--replicas", action="store_true", help="alias of --scaling replicas")
     ap.add_argument("--system", default="synthetic", choices=["synthetic", "fe"],
                     help="fe: the P2-P2-P1 swelling system (lib/fe_swelling.py, assembled on the host; one GPU)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
@@ -296,15 +317,9 @@ def main():
     from lib.handle import Handle, params_to_options
     Nat.check(Nat.lib().pls_set_device(local if args.comm == "rccl" else 0))
 
-    sharded = world > 1 and not args.replicas
     if args.system == "fe" and world > 1:
         raise SystemExit("--system fe runs on one GPU (the assembler is a host-side input generator)")
-    N_glob = args.N
-    if sharded:
-        N_glob = int(round(args.N * world ** (1.0 / args.dim)))
-        args.blocks_s *= world
-        args.blocks_fp *= world
-        args.blocks_p *= world
+    sharded, N_glob = shard_plan(args, world)
     params, db = solver_options(args)
     opts = dict(db)
     opts.update(params_to_options(params))
@@ -389,6 +404,8 @@ def main():
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 8.0 * n + 8.0 * n
     achieved = alg_bytes / spmv_avg / 1e9 if spmv_avg > 0 else 0.0
     iso = h.bench_spmv(d_x.p, d_b.p, 10)
+    # latency of the solve's global sums: a CGS step's k+1 dots (k ~ its/2) and a norm
+    gsum_us = {"dots_40": 1e6 * h.bench_global_sum(40, 50), "norm_1": 1e6 * h.bench_global_sum(1, 50)}
     d16, mat_bytes = h.spmv_layout()
     fmt_bytes = mat_bytes + 8.0 * n + 8.0 * n  # + x once + y once
     load_rhs()
@@ -424,7 +441,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * dt / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if (world == 1 or args.scaling == "strong") else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic (seeded SPD 3-field block system, SURVEY.md 8(d); generated in HBM)" if fe is None else
@@ -444,10 +461,12 @@ def main():
                                 + (f"(ILU(0), {args.blocks_s}/{args.blocks_fp} blocks s/fp)"
                                    if args.inner == "bjacobi" else ""))),
                 "dim": args.dim, "N": N_glob, "dofs": n_global, "dofs_rank0": n, "nnz_A_rank0": nnz,
-                "parallelism": (f"row slabs x{world} ({args.comm})" if sharded else
+                "parallelism": (f"row slabs x{world} ({args.comm}, {args.scaling} scaling)" if sharded else
                                 f"replicas x{world}" if world > 1 else "single GPU"),
             },
             "its_per_solve": its / args.steps,
+            "comm": {"global_sum_latency_us": gsum_us, "spmv_gbs_rank0": achieved,
+                     "note": "per-rank SpMV includes the halo exchange it waits for"},
             "reasons": sorted(set(reasons)),
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -127,6 +127,10 @@ int pls_comm_destroy(pls_comm *comm);
  * must be destroyed before its communicator.  Vectors of the device entry
  * points are rank-local ([s_r | f_r | p_r]).                                 */
 int pls_create_synthetic_dist(const pls_synth_spec *spec, const char *options, pls_comm *comm, pls_handle **out);
+/* Mean latency of one global sum of `count` doubles (allgather + rank-ordered
+ * sum + the stream sync the Krylov loop performs), over `reps` calls; the
+ * reference's MPI_Allreduce inside VecMDot / VecNorm.                       */
+int pls_bench_global_sum(pls_handle *h, int32_t count, int32_t reps, double *sec_per_call);
 /* Multi-rank pls_create from the caller's matrices -- what the reference
  * drivers hold under mpirun (paper-scripts/robustness_2d.sh:29): on every rank
  * A, P, P_diff are the rank's MPIAIJ rows (A.getValuesCSR() of the operator of

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1433,6 +1434,28 @@ int pls_bench_spmv(pls_handle *hh, const double *d_x, double *d_y, int32_t reps,
         (void)hipEventDestroy(a);
         (void)hipEventDestroy(b);
         *sec_per_launch = (double)ms * 1e-3 / std::max(1, reps);
+    })
+}
+
+// Latency of the solve's global sums (one batched all-reduce per
+// CGS step, one per norm): reps x (global_sum_dev of `count` doubles + the
+// stream sync the Krylov loop does to read them on the host), host clock.
+int pls_bench_global_sum(pls_handle *hh, int32_t count, int32_t reps, double *sec_per_call) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        Ctx &c = H.ctx;
+        if (count < 1 || count > 4096) throw Error("pls_bench_global_sum: count must be in 1..4096");
+        DBuf<double> v(count);
+        HIPCHK(hipMemsetAsync(v.p, 0, sizeof(double) * count, c.st));
+        c.comm->global_sum_dev(v.p, count, c.st);  // warm (scratch allocation, first collective)
+        c.sync();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < reps; ++r) {
+            c.comm->global_sum_dev(v.p, count, c.st);
+            c.sync();
+        }
+        const auto t1 = std::chrono::steady_clock::now();
+        *sec_per_call = std::chrono::duration<double>(t1 - t0).count() / std::max(1, reps);
     })
 }
 

@@ -45,7 +45,7 @@ EXPORTS = [
     "pls_get_timings", "pls_reset_timings", "pls_export_matrix", "pls_get_permutation",
     "pls_bench_spmv", "pls_rccl_unique_id", "pls_comm_create_rccl", "pls_comm_create_callback",
     "pls_comm_destroy", "pls_create_synthetic_dist", "pls_spmv_layout", "pls_update_matrices",
-    "pls_bench_copy", "pls_create_dist",
+    "pls_bench_copy", "pls_create_dist", "pls_bench_global_sum",
 ]
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
@@ -96,6 +96,7 @@ def lib():
     L.pls_bench_copy.argtypes = [i64, i32, i32, C.POINTER(C.c_double)]
     L.pls_spmv_layout.argtypes = [vp, C.POINTER(i32), C.POINTER(i64)]
     L.pls_create_synthetic_dist.argtypes = [C.POINTER(pls_synth_spec), C.c_char_p, vp, C.POINTER(vp)]
+    L.pls_bench_global_sum.argtypes = [vp, i32, i32, C.POINTER(C.c_double)]
     L.pls_create_dist.argtypes = [C.POINTER(pls_csr), C.POINTER(pls_csr), C.POINTER(pls_csr), i64,
                                   vp, i64, vp, i64, vp, i64, vp, i64, C.c_char_p, vp, C.POINTER(vp)]
     _lib = L

@@ -190,6 +190,11 @@ class Handle:
         N.check(N.lib().pls_bench_spmv(self.ptr, d_x, d_y, int(reps), C.byref(s)))
         return s.value
 
+    def bench_global_sum(self, count, reps):
+        s = C.c_double()
+        N.check(N.lib().pls_bench_global_sum(self.ptr, int(count), int(reps), C.byref(s)))
+        return s.value
+
     def spmv_layout(self):
         """(is SELL-64/D16, matrix bytes streamed per product of A)."""
         d, b = C.c_int32(), C.c_int64()

@@ -92,3 +92,24 @@ def test_fe_cpu_baseline_runs_the_assembled_system():
     n4, n8 = 4 * 9 ** 2 + 5 ** 2, 4 * 17 ** 2 + 9 ** 2
     assert abs(out["value"] - out["raw_iters_per_s"] * n4 / n8) <= 1e-9 * out["value"]
     assert "assembled N=4 2-D swelling system" in out["sample"]
+
+
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+def test_strong_scaling_plan_keeps_the_system(G):
+    """--scaling strong (default): the N=59 system and its total block counts
+    at every G, so the outer iteration count does not grow with G."""
+    a = _args("swelling3d-bjacobi", scaling="strong", replicas=False)
+    sharded, N = bench.shard_plan(a, G)
+    assert sharded == (G > 1) and N == 59 and (a.blocks_s, a.blocks_fp) == (256, 264)
+
+
+@pytest.mark.parametrize("G,N", [(2, 74), (4, 94), (8, 118)])
+def test_weak_scaling_plan(G, N):
+    a = _args("swelling3d-bjacobi", scaling="weak", replicas=False)
+    sharded, Ng = bench.shard_plan(a, G)
+    assert sharded and Ng == N and (a.blocks_s, a.blocks_fp) == (256 * G, 264 * G)
+
+
+def test_replicas_plan():
+    a = _args("swelling3d-bjacobi", scaling="strong", replicas=True)
+    assert bench.shard_plan(a, 4) == (False, 59) and a.scaling == "replicas"
