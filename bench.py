@@ -155,9 +155,10 @@ def cpu_baseline(args, params, db):
 
     bench's configuration (2-way, GMRES, PREONLY + BJACOBI(ILU(0))) runs the
     C/OpenMP restatement oracle/csrc/cpu_solver.c on all available cores
-    (SURVEY.md 8(d)'s planned baseline); other configurations fall back to the
-    single-thread Python oracle.  iters/s is scaled by DoF to the metric's
-    system (the per-iteration work is linear in n)."""
+    (SURVEY.md 8(d)'s planned baseline) on the benched system itself (same
+    matrices, same iteration count); other configurations fall back to the
+    single-thread Python oracle on a smaller sample, iters/s scaled by DoF to
+    the benched system (the per-iteration work is linear in n)."""
     from oracle import synthetic as S
     Ns = args.cpu_N
     if args.system == "fe":
@@ -182,13 +183,15 @@ def cpu_baseline(args, params, db):
             A, P, spec.sizes()[0], args.blocks_s, args.blocks_fp, b, rtol=params["solver rtol"],
             atol=params["solver atol"], maxit=args.cpu_maxit, nthreads=cores)
         rate = its / dt
+        same = n_sample == n_metric
         return {"value": rate * n_sample / n_metric,
                 "unit": f"Krylov iters/s (scaled by DoF to the {n_metric}-DoF system)", "cores": cores, "kind": "port",
                 "sample": (f"oracle/csrc/cpu_solver.c (C + OpenMP, {cores} threads): bench's configuration on "
                            f"the N={Ns} {args.dim}-D system ({n_sample} DoF, {A.nnz} nnz), {its} GMRES iterations in "
-                           f"{dt:.1f}s (block setup {t_setup:.1f}s, generation {t_gen:.1f}s), reason {reason}; "
-                           f"iters/s x {n_sample}/{n_metric}"),
-                "raw_iters_per_s": rate}
+                           f"{dt:.1f}s (block setup {t_setup:.1f}s, generation {t_gen:.1f}s), reason {reason}"
+                           + ("; the benched system itself, no scaling" if same else
+                              f"; iters/s x {n_sample}/{n_metric}")),
+                "raw_iters_per_s": rate, "its": its, "petsc4py": _petsc_probe()}
     from oracle.solver import OracleSolver
     three = params["pc type"] == "diagonal 3-way"
     Pd = S.matrix(spec, 2) if three else None
@@ -207,6 +210,17 @@ def cpu_baseline(args, params, db):
                        f"solve of the N={Ns} {args.dim}-D system ({n_sample} DoF), {o.its} outer iterations in {dt:.1f}s "
                        f"(setup {t_setup:.1f}s), maxit {args.cpu_maxit}; iters/s x {n_sample}/{n_metric}"),
             "raw_iters_per_s": rate}
+
+
+def _petsc_probe():
+    """time the reference's own PETSc path if petsc4py is already
+    installed on the box (never installed here).  Records the outcome."""
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("petsc4py")
+    except (ImportError, ValueError):
+        spec = None
+    return "present (not timed: the reference's dolfin assembly is absent)" if spec else "absent on this host"
 
 
 def _cpu_baseline_fe(args, params, db):
@@ -286,7 +300,8 @@ def main():
     ap.add_argument("--solver", default="gmres", choices=["gmres", "aar"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the device-copy bandwidth probe")
-    ap.add_argument("--cpu-N", type=int, default=40)  # ~10-20 s of CPU solve on the box's cores
+    # default: the CPU baseline solves the benched system itself (N=59: ~20-30 s on the box's 16 cores)
+    ap.add_argument("--cpu-N", type=int, default=None)
     ap.add_argument("--cpu-maxit", type=int, default=100)
     ap.add_argument("--sell-d16", type=int, default=1, help="1: SELL-64/D16 SpMV layout (16-bit column deltas)")
     ap.add_argument("--d16-unroll", type=int, default=0, help="D16 SpMV: 8-entry groups per lane in flight (tuning)")
@@ -304,6 +319,8 @@ def main():
     args = ap.parse_args()
     if args.pc_type == "3-way":
         args.pc_type = "diagonal 3-way"
+    if args.cpu_N is None:
+        args.cpu_N = args.N
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -1210,22 +1210,25 @@ void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, c
 //   bases   seg[(slice * 64 + lane) * D16_SEG + j]        (one int4 per lane)
 //   slices  sfirst[slice] (first row), slpr[slice] (lanes per row)
 __device__ __forceinline__ void d16_lane(int64_t sl, int lane, const int64_t *sfirst, const int32_t *slpr,
-                                         int64_t nrows, int64_t &row, int &lpr, int &sub) {
+                                         int64_t nrows, int64_t &row, int &lpr, int &sub,
+                                         const int32_t *rowmap) {
     lpr = slpr[sl];
     row = sfirst[sl] + lane / lpr;
     sub = lane % lpr;
     if (row >= sfirst[sl + 1] || row >= nrows) row = -1;
+    else if (rowmap) row = rowmap[row];
 }
 
 __global__ __launch_bounds__(TPB) void k_d16_slice_len(int64_t nslices, const int64_t *sfirst, const int32_t *slpr,
-                                                       const int64_t *rp, int64_t nrows, int64_t *slen) {
+                                                       const int64_t *rp, int64_t nrows, int64_t *slen,
+                                                       const int32_t *rowmap) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl > nslices) return;
     if (sl == nslices) { if (lane == 0) slen[nslices] = 0; return; }
     int64_t row;
     int lpr, sub;
-    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub);
+    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub, rowmap);
     const int64_t len = row >= 0 ? rp[row + 1] - rp[row] : 0;
     int64_t mine = len > sub ? (len - sub + lpr - 1) / lpr : 0;
 #pragma unroll
@@ -1239,13 +1242,13 @@ __global__ __launch_bounds__(TPB) void k_d16_slice_len(int64_t nslices, const in
 // segments each lane's entry stream needs; *maxseg = max over lanes
 __global__ __launch_bounds__(TPB) void k_d16_count(int64_t nslices, const int64_t *sfirst, const int32_t *slpr,
                                                    const int64_t *rp, const int32_t *ci, int64_t nrows,
-                                                   int32_t *maxseg) {
+                                                   int32_t *maxseg, const int32_t *rowmap) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl >= nslices) return;
     int64_t row;
     int lpr, sub;
-    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub);
+    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub, rowmap);
     if (row < 0) return;
     const int64_t s = rp[row], e = rp[row + 1];
     int nseg = 0;
@@ -1261,13 +1264,13 @@ __global__ __launch_bounds__(TPB) void k_d16_count(int64_t nslices, const int64_
 __global__ __launch_bounds__(TPB) void k_d16_fill(int64_t nslices, const int64_t *sfirst, const int32_t *slpr,
                                                   const int64_t *rp, const int32_t *ci, const double *val,
                                                   int64_t nrows, const int64_t *sptr, uint16_t *dl, double *dv,
-                                                  int32_t *seg, int nsegs) {
+                                                  int32_t *seg, int nsegs, const int32_t *rowmap) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl >= nslices) return;
     int64_t row;
     int lpr, sub;
-    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub);
+    d16_lane(sl, lane, sfirst, slpr, nrows, row, lpr, sub, rowmap);
     const int64_t base = sptr[sl];
     const int64_t L = (sptr[sl + 1] - base) >> 6;
     const int64_t s0 = row >= 0 ? rp[row] : 0;
@@ -1307,6 +1310,8 @@ typedef int32_t d16_i4 __attribute__((ext_vector_type(4)));
 typedef uint32_t d16_u4 __attribute__((ext_vector_type(4)));
 typedef double d16_d2 __attribute__((ext_vector_type(2)));
 
+__constant__ int d16_xcd_map;  // set once by launch_d16_spmv (pls.d16_xcd)
+
 template <int G2, int TAG, bool HALO, int SEG>
 __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *__restrict__ sptr,
                                                   const int64_t *__restrict__ sfirst,
@@ -1315,12 +1320,21 @@ __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices
                                                   const int32_t *__restrict__ seg, const double *__restrict__ x,
                                                   double *__restrict__ y, double alpha, double beta,
                                                   const double *__restrict__ z, const double *__restrict__ ghost,
-                                                  int32_t nlocal, const int32_t *__restrict__ slist) {
+                                                  int32_t nlocal, const int32_t *__restrict__ slist,
+                                                  const int32_t *__restrict__ rowmap) {
     static_assert(SEG == 4 || SEG == 8, "segment bases are one or two int4 per lane");
     const int lane = threadIdx.x & 63;
     // nslices: slices this launch processes -- all of them, or the subset
     // listed in slist (interior / halo rows of a distributed product)
-    const int64_t idx = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
+    // d16_xcd_map (pls.d16_xcd 1): workgroup b runs on XCD b % 8; give each XCD a
+    // contiguous range of slices (its L2 then holds one window of x) instead
+    // of every 8th slice
+    unsigned blk = blockIdx.x;
+    if (d16_xcd_map) {
+        const unsigned per = (gridDim.x + 7) / 8;
+        blk = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    }
+    const int64_t idx = __builtin_amdgcn_readfirstlane((int)(blk * (TPB / 64) + (threadIdx.x >> 6)));
     if (idx >= nslices) return;
     const int64_t sl = slist ? (int64_t)__builtin_amdgcn_readfirstlane(slist[idx]) : idx;
     const int64_t base = sptr[sl];
@@ -1374,27 +1388,30 @@ __global__ __launch_bounds__(TPB) void k_d16_spmv(int64_t nrows, int64_t nslices
         if (lane % lpr) return;
     }
     if (row < r1) {
+        // rowmap: slices hold rows sorted by length inside windows (SELL-C-sigma);
+        // the lane's result goes to its row's place
+        const int64_t yr = rowmap ? (int64_t)rowmap[row] : row;
         double r = alpha * acc;
-        if (beta != 0.0) r += beta * z[row];
-        y[row] = r;
+        if (beta != 0.0) r += beta * z[yr];
+        y[yr] = r;
     }
 }
 
 void launch_d16_slice_len(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
-                          int64_t nrows, int64_t *slen, hipStream_t st) {
-    k_d16_slice_len<<<grid_for((nslices + 1) * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, nrows, slen);
+                          int64_t nrows, int64_t *slen, hipStream_t st, const int32_t *rowmap) {
+    k_d16_slice_len<<<grid_for((nslices + 1) * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, nrows, slen, rowmap);
 }
 void launch_d16_count(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
-                      const int32_t *ci, int64_t nrows, int32_t *maxseg, hipStream_t st) {
+                      const int32_t *ci, int64_t nrows, int32_t *maxseg, hipStream_t st, const int32_t *rowmap) {
     if (nslices > 0)
-        k_d16_count<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, ci, nrows, maxseg);
+        k_d16_count<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, ci, nrows, maxseg, rowmap);
 }
 void launch_d16_fill(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
                      const int32_t *ci, const double *val, int64_t nrows, const int64_t *sptr, uint16_t *dl,
-                     double *dv, int32_t *seg, int nsegs, hipStream_t st) {
+                     double *dv, int32_t *seg, int nsegs, hipStream_t st, const int32_t *rowmap) {
     if (nslices > 0)
         k_d16_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, sfirst, slpr, rp, ci, val, nrows, sptr, dl,
-                                                                dv, seg, nsegs);
+                                                                dv, seg, nsegs, rowmap);
 }
 void launch_first_col(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *c0, hipStream_t st) {
     if (nrows > 0) k_first_col<<<grid_for(nrows, TPB), TPB, 0, st>>>(nrows, rp, ci, c0);
@@ -1403,35 +1420,42 @@ template <int G2, int SEG>
 static void d16_dispatch(unsigned g, hipStream_t st, int64_t nrows, int64_t ns, const int64_t *sptr,
                          const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
                          const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
-                         int tag, const double *ghost, int32_t nl, const int32_t *slist) {
+                         int tag, const double *ghost, int32_t nl, const int32_t *slist, const int32_t *rm) {
     if (ghost) {
-        if (tag) k_d16_spmv<G2, 1, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist);
-        else k_d16_spmv<G2, 0, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist);
+        if (tag) k_d16_spmv<G2, 1, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
+        else k_d16_spmv<G2, 0, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
     } else {
-        if (tag) k_d16_spmv<G2, 1, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist);
-        else k_d16_spmv<G2, 0, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist);
+        if (tag) k_d16_spmv<G2, 1, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
+        else k_d16_spmv<G2, 0, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
     }
 }
 template <int SEG>
 static void d16_unrolled(int unroll, unsigned g, hipStream_t st, int64_t nrows, int64_t nslices, const int64_t *sptr,
                          const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
                          const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
-                         int tag, const double *ghost, int32_t nl, const int32_t *slist) {
+                         int tag, const double *ghost, int32_t nl, const int32_t *slist, const int32_t *rm) {
     switch (unroll) {
-        case 1: d16_dispatch<1, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist); break;
-        case 2: d16_dispatch<2, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist); break;
-        default: d16_dispatch<4, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist); break;
+        case 1: d16_dispatch<1, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm); break;
+        case 2: d16_dispatch<2, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm); break;
+        default: d16_dispatch<4, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm); break;
     }
+}
+static int d16_xcd_host = 0;
+void set_d16_xcd(int on) {
+    if (on == d16_xcd_host) return;
+    d16_xcd_host = on;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(d16_xcd_map), &on, sizeof(int)) != hipSuccess) d16_xcd_host = 0;
 }
 void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
                      const uint16_t *dl, const double *dv, const int32_t *seg, int nsegs, const double *x, double *y,
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
-                     int unroll, hipStream_t st, const int32_t *slist) {
+                     int unroll, hipStream_t st, const int32_t *slist, const int32_t *rowmap) {
     if (nslices <= 0) return;
-    const unsigned g = grid_for(nslices, TPB / 64);
+    unsigned g = grid_for(nslices, TPB / 64);
+    if (d16_xcd_host) g = (g + 7) / 8 * 8;  // every XCD range the same length (surplus blocks exit)
     const int32_t nl = (int32_t)nlocal;
-    if (nsegs == 8) d16_unrolled<8>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist);
-    else d16_unrolled<4>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist);
+    if (nsegs == 8) d16_unrolled<8>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rowmap);
+    else d16_unrolled<4>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rowmap);
 }
 
 // rows whose last (largest) column is a ghost column (rows sorted): flag 1

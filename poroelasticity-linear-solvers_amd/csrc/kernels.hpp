@@ -131,18 +131,24 @@ void launch_sell_spmv(int64_t nrows, const int64_t *sptr, const int32_t *scol, c
 constexpr int D16_SEG = 4;      // segment bases per lane (rows of a single rank)
 constexpr int D16_SEG_MAX = 8;  // ... with halo columns (own s/f/p + a neighbour's s/f/p)
 void launch_d16_slice_len(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
-                          int64_t nrows, int64_t *slen /* nslices+1 */, hipStream_t st);
+                          int64_t nrows, int64_t *slen /* nslices+1 */, hipStream_t st,
+                          const int32_t *rowmap = nullptr /* slice position -> row (SELL-C-sigma) */);
 void launch_d16_count(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
-                      const int32_t *ci, int64_t nrows, int32_t *maxseg, hipStream_t st);
+                      const int32_t *ci, int64_t nrows, int32_t *maxseg, hipStream_t st,
+                      const int32_t *rowmap = nullptr);
 void launch_d16_fill(int64_t nslices, const int64_t *sfirst, const int32_t *slpr, const int64_t *rp,
                      const int32_t *ci, const double *val, int64_t nrows, const int64_t *sptr, uint16_t *dl,
-                     double *dv, int32_t *seg, int nsegs /* D16_SEG or D16_SEG_MAX */, hipStream_t st);
+                     double *dv, int32_t *seg, int nsegs /* D16_SEG or D16_SEG_MAX */, hipStream_t st,
+                     const int32_t *rowmap = nullptr);
 void launch_first_col(int64_t nrows, const int64_t *rp, const int32_t *ci, int32_t *c0, hipStream_t st);
 void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
                      const uint16_t *dl, const double *dv, const int32_t *seg, int nsegs, const double *x, double *y,
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
                      int unroll /* 8-entry groups per lane in flight: 1, 2 or 4 */, hipStream_t st,
-                     const int32_t *slist = nullptr /* nslices entries: the slices to process */);
+                     const int32_t *slist = nullptr /* nslices entries: the slices to process */,
+                     const int32_t *rowmap = nullptr /* slice position -> row (SELL-C-sigma) */);
+// D16 SpMV workgroup -> slice order: 0 round-robin over the 8 XCDs (default), 1 XCD-contiguous ranges
+void set_d16_xcd(int on);
 // flag[r] = 1 when row r (sorted columns) references a ghost column (>= nlocal)
 void launch_row_has_ghost(int64_t nrows, const int64_t *rp, const int32_t *ci, int64_t nlocal, uint8_t *flag,
                           hipStream_t st);

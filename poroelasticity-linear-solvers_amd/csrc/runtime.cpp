@@ -13,6 +13,7 @@
 #include <climits>
 
 #include <algorithm>
+#include <numeric>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -123,7 +124,34 @@ void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_
 // group's rows are "wide" (first columns of neighbouring rows more than 4
 // apart on average, rows of 16+ entries: a lane-per-row gather would touch a
 // cache line per lane), else lane = row.
-static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<int32_t> &slpr, Ctx &c) {
+//
+// Rows of very different lengths in one slice pad every lane to the longest
+// (FE systems in a bandwidth-reducing order interleave P2 vertex, P2 edge and
+// P1 rows of 89..405 entries: ~100 % padding, 1.7x the CSR bytes).  When the
+// padding exceeds pls.d16_sigma_pad (15 %), the plan becomes SELL-C-sigma:
+// inside windows of pls.d16_sigma (1024) rows the rows are stably sorted by
+// length (rowmap[position] = row; the kernel writes y[rowmap[pos]]), and each
+// 64-row group of positions takes pls.d16_sorted_lpr (2) lanes per row when
+// its rows average 32+ entries (keeps a gather instruction on few cache
+// lines), else 1.  Per-row summation order is unchanged for lane-per-row
+// slices; it is the sorted plan only if it saves 15 % of the stored entries.
+static int64_t d16_plan_stored(const std::vector<int64_t> &rp, const std::vector<int64_t> &sfirst,
+                               const std::vector<int32_t> &slpr, const std::vector<int32_t> *rowmap) {
+    int64_t stored = 0;
+    for (size_t s = 0; s + 1 < sfirst.size(); ++s) {
+        const int l = slpr[s];
+        int64_t L = 0;
+        for (int64_t p = sfirst[s]; p < sfirst[s + 1]; ++p) {
+            const int64_t r = rowmap ? (*rowmap)[p] : p;
+            L = std::max<int64_t>(L, (rp[r + 1] - rp[r] + l - 1) / l);
+        }
+        stored += 64 * ((L + 7) & ~(int64_t)7);
+    }
+    return stored;
+}
+
+static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<int32_t> &slpr,
+                     std::vector<int32_t> &rowmap, Ctx &c) {
     const int64_t n = M.nrows;
     std::vector<int64_t> rp(n + 1);
     std::vector<int32_t> c0(n);
@@ -134,6 +162,7 @@ static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<
     c.sync();
     sfirst.clear();
     slpr.clear();
+    rowmap.clear();
     for (int64_t r = 0; r < n; r += 64) {
         bool wide = false;
         if (r + 64 <= n && c0[r] >= 0 && c0[r + 63] >= 0) {
@@ -153,6 +182,52 @@ static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<
         }
     }
     sfirst.push_back(n);
+    if (c.d16_sigma <= 0 || M.halo || n < 64) return;
+    const int64_t nnz = rp[n];
+    const int64_t stored = d16_plan_stored(rp, sfirst, slpr, nullptr);
+    if ((double)stored <= (1.0 + c.d16_sigma_pad) * (double)nnz) return;
+    // SELL-C-sigma
+    std::vector<int32_t> rm(n);
+    std::iota(rm.begin(), rm.end(), 0);
+    for (int64_t w = 0; w < n; w += c.d16_sigma) {
+        const int64_t e = std::min<int64_t>(n, w + c.d16_sigma);
+        std::stable_sort(rm.begin() + w, rm.begin() + e, [&](int32_t a, int32_t b) {
+            return rp[a + 1] - rp[a] > rp[b + 1] - rp[b];
+        });
+    }
+    std::vector<int64_t> sf;
+    std::vector<int32_t> sl;
+    // entries a group of positions [p, e) stores with l lanes per row
+    auto group_stored = [&](int64_t p, int64_t e, int l) {
+        int64_t st = 0;
+        for (int64_t q = p; q < e; q += 64 / l) {
+            int64_t L = 0;
+            for (int64_t t = q; t < std::min(e, q + 64 / l); ++t) L = std::max<int64_t>(L, (rp[rm[t] + 1] - rp[rm[t]] + l - 1) / l);
+            st += 64 * ((L + 7) & ~(int64_t)7);
+        }
+        return st;
+    };
+    for (int64_t p = 0; p < n; p += 64) {
+        const int64_t e = std::min<int64_t>(n, p + 64);
+        int64_t tot = 0;
+        for (int64_t q = p; q < e; ++q) tot += rp[rm[q] + 1] - rp[rm[q]];
+        // several lanes per row only for long rows, and only when the per-lane
+        // share's rounding to 8-entry groups costs little extra padding
+        int l = 1;
+        if (c.d16_sorted_lpr > 1 && tot >= 32 * (e - p) &&
+            (double)group_stored(p, e, c.d16_sorted_lpr) <= 1.05 * (double)group_stored(p, e, 1))
+            l = c.d16_sorted_lpr;
+        for (int64_t q = p; q < e; q += 64 / l) {
+            sf.push_back(q);
+            sl.push_back(l);
+        }
+    }
+    sf.push_back(n);
+    const int64_t stored2 = d16_plan_stored(rp, sf, sl, &rm);
+    if ((double)stored2 > 0.85 * (double)stored) return;
+    sfirst.swap(sf);
+    slpr.swap(sl);
+    rowmap.swap(rm);
 }
 
 void build_sell(DevCSR &M, Ctx &c) {
@@ -160,16 +235,22 @@ void build_sell(DevCSR &M, Ctx &c) {
     auto S = std::make_unique<DevSELL>();
     if (c.sell_d16 && M.nnz > 0) {
         std::vector<int64_t> sf;
-        std::vector<int32_t> lp;
-        d16_plan(M, sf, lp, c);
+        std::vector<int32_t> lp, rm;
+        d16_plan(M, sf, lp, rm, c);
         const int64_t ns = (int64_t)lp.size();
         S->sfirst.alloc(ns + 1);
         S->slpr.alloc(std::max<int64_t>(ns, 1));
         HIPCHK(hipMemcpyAsync(S->sfirst.p, sf.data(), sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, c.st));
         HIPCHK(hipMemcpyAsync(S->slpr.p, lp.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, c.st));
+        if (!rm.empty()) {
+            S->rowmap.alloc(rm.size());
+            S->nrows_mapped = (int64_t)rm.size();
+            HIPCHK(hipMemcpyAsync(S->rowmap.p, rm.data(), sizeof(int32_t) * rm.size(), hipMemcpyHostToDevice, c.st));
+        }
+        const int32_t *rmap = rm.empty() ? nullptr : S->rowmap.p;
         DBuf<int32_t> mx(1);
         HIPCHK(hipMemsetAsync(mx.p, 0, sizeof(int32_t), c.st));
-        launch_d16_count(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.ci.p, M.nrows, mx.p, c.st);
+        launch_d16_count(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.ci.p, M.nrows, mx.p, c.st, rmap);
         int32_t h = 0;
         HIPCHK(hipMemcpyAsync(&h, mx.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
         c.sync();
@@ -179,7 +260,7 @@ void build_sell(DevCSR &M, Ctx &c) {
             S->nslices = ns;
             for (int32_t l : lp) S->wide_slices += (l > 1);
             DBuf<int64_t> slen(ns + 1);
-            launch_d16_slice_len(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.nrows, slen.p, c.st);
+            launch_d16_slice_len(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.nrows, slen.p, c.st, rmap);
             S->sptr.alloc(ns + 1);
             c.ensure_scan(ns);
             exclusive_scan_i64(slen.p, S->sptr.p, ns, c.scan_tmp.p, c.scan_tmp_bytes, c.st);
@@ -189,7 +270,7 @@ void build_sell(DevCSR &M, Ctx &c) {
             S->dl.alloc(std::max<int64_t>(S->stored, 8));
             S->seg.alloc(ns * 64 * S->nsegs);
             launch_d16_fill(ns, S->sfirst.p, S->slpr.p, M.rp.p, M.ci.p, M.val.p, M.nrows, S->sptr.p, S->dl.p,
-                            S->val.p, S->seg.p, S->nsegs, c.st);
+                            S->val.p, S->seg.p, S->nsegs, c.st, rmap);
             HIPCHK(hipGetLastError());
             c.sync();
             M.sell = std::move(S);
@@ -261,13 +342,15 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
         HIPCHK(hipEventRecord(c.ev_x, c.st));
         HIPCHK(hipStreamWaitEvent(c.st_comm, c.ev_x, 0));
         launch_d16_spmv(M.nrows, S.n_in, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y,
-                        alpha, beta, z, M.tag, nullptr, H.nlocal, c.d16_unroll, c.st, S.s_in.p);
+                        alpha, beta, z, M.tag, nullptr, H.nlocal, c.d16_unroll, c.st, S.s_in.p,
+                        S.nrows_mapped ? S.rowmap.p : nullptr);
         launch_pack(H.nsend, H.send_idx.p, x, H.sendbuf.p, c.st_comm);
         c.comm->exchange_dev(H.sendbuf.p, H.scnt, H.soff, H.ghost.p, H.rcnt, H.roff, c.st_comm);
         HIPCHK(hipEventRecord(c.ev_halo, c.st_comm));
         HIPCHK(hipStreamWaitEvent(c.st, c.ev_halo, 0));
         launch_d16_spmv(M.nrows, S.n_halo, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y,
-                        alpha, beta, z, M.tag, H.ghost.p, H.nlocal, c.d16_unroll, c.st, S.s_halo.p);
+                        alpha, beta, z, M.tag, H.ghost.p, H.nlocal, c.d16_unroll, c.st, S.s_halo.p,
+                        S.nrows_mapped ? S.rowmap.p : nullptr);
         return;
     }
     if (M.halo) {
@@ -281,7 +364,8 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
     if (M.sell && M.sell->d16) {
         const DevSELL &S = *M.sell;
         launch_d16_spmv(M.nrows, S.nslices, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y, alpha,
-                        beta, z, M.tag, ghost, nlocal, c.d16_unroll, c.st);
+                        beta, z, M.tag, ghost, nlocal, c.d16_unroll, c.st, nullptr,
+                        S.nrows_mapped ? S.rowmap.p : nullptr);
         return;
     }
     if (M.sell) {

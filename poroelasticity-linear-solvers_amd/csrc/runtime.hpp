@@ -70,6 +70,9 @@ struct Ctx {
     int d16_wide_lpr = 8;     // lanes per row of D16 slices with wide rows (option pls.d16_wide_lpr)
     int d16_unroll = 4;       // D16 SpMV 8-entry groups per lane in flight (option pls.d16_unroll)
     int d16_segs = D16_SEG;   // minimum D16 segment bases per lane (option pls.d16_segs; 8 where needed)
+    int d16_sigma = 1024;         // SELL-C-sigma window (rows sorted by length; 0: never) (pls.d16_sigma)
+    double d16_sigma_pad = 0.15;  // ... used when the plain plan pads more than this fraction (pls.d16_sigma_pad)
+    int d16_sorted_lpr = 2;       // lanes per row of sorted slices with 32+ entries per row (pls.d16_sorted_lpr)
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
@@ -95,13 +98,18 @@ struct DevSELL {
     DBuf<int32_t> seg, slpr;  // D16: segment bases per lane, lanes per row per slice
     DBuf<int64_t> sfirst;     // D16: first row of each slice (nslices + 1)
     int64_t wide_slices = 0;  // D16 slices with 8 lanes per row
+    // SELL-C-sigma: slice positions hold rows sorted by length inside windows of
+    // sigma rows (rowmap[position] = row); empty when rows keep their order
+    DBuf<int32_t> rowmap;
+    int64_t nrows_mapped = 0;
     int nsegs = D16_SEG;      // D16 segment bases per lane: 4, or 8 when halo columns need them
     // distributed products: slices without / with ghost columns (the first
     // run while the halo exchange is in flight)
     DBuf<int32_t> s_in, s_halo;
     int64_t n_in = 0, n_halo = 0;
     int64_t bytes() const {  // bytes one product streams from the matrix
-        return d16 ? stored * 10 + nslices * (64 * 4 * nsegs + 20) + 8 : stored * 12 + (nslices + 1) * 8;
+        return d16 ? stored * 10 + nslices * (64 * 4 * nsegs + 20) + 8 + nrows_mapped * 4
+                   : stored * 12 + (nslices + 1) * 8;
     }
 };
 
