@@ -1613,7 +1613,8 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
                                                   const int32_t *s_lpr, const int32_t *order, const int64_t *rp,
                                                   const int32_t *ci, const double *lu, const int64_t *diag,
                                                   const double *dinv, int upper, int64_t n, int64_t nb,
-                                                  const int64_t *sptr2, int32_t *ocol, double *oval, int wide) {
+                                                  const int64_t *sptr2, int32_t *ocol, double *oval, int wide,
+                                                  const int32_t *posof, const int32_t *row_lo) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl >= nslices) return;
@@ -1630,22 +1631,48 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
         len = upper ? rp[i + 1] - diag[i] - 1 : diag[i] - rp[i];
     }
     const int64_t mine = len > sub ? (len - sub + lpr - 1) / lpr : 0;
-    ocol[base + lane] = wide ? (i >= 0 ? (int32_t)(i - b0) : -1)
-                             : (i >= 0 ? (int32_t)(i - b0) : SW_ROW_PAD) | (int32_t)(mine << SW_ROW_BITS);
+    // posof (ring sweep): rows and columns become block-local positions in the
+    // triangle's level order
+    const int32_t me = i >= 0 ? (posof ? posof[i] : (int32_t)(i - b0)) : -1;
+    // a padding lane's entries (value 0) read the slice's first row: in the
+    // ring sweep that position is in the LDS ring, never a global fallback
+    const int32_t pad = posof ? posof[order[s_start[sl]]] : 0;
+    ocol[base + lane] = wide ? me : (i >= 0 ? me : SW_ROW_PAD) | (int32_t)(mine << SW_ROW_BITS);
     oval[base + lane] = (upper && i >= 0) ? dinv[i] : 0.0;
+    if (row_lo) {
+        // ring sweep: only the row's near entries (position >= row_lo[i], in the
+        // LDS ring when the row runs), dealt round robin over its lanes; the far
+        // ones are applied to the row's input when its chunk is loaded
+        const int32_t lo = i >= 0 ? row_lo[i] : 0;
+        int64_t k = 1, m = 0;
+        for (int64_t j = 0; j < len; ++j) {
+            const int32_t pc = posof[ci[src + j]];
+            if (pc < lo) continue;
+            if (m++ % lpr != sub) continue;
+            ocol[base + k * 64 + lane] = pc;
+            oval[base + k * 64 + lane] = lu[src + j];
+            ++k;
+        }
+        for (; k < L; ++k) {
+            ocol[base + k * 64 + lane] = i >= 0 ? me : pad;
+            oval[base + k * 64 + lane] = 0.0;
+        }
+        return;
+    }
     for (int64_t k = 1; k < L; ++k) {
         const int64_t j = (k - 1) * lpr + sub, pos = base + k * 64 + lane;
-        ocol[pos] = j < len ? (int32_t)(ci[src + j] - b0) : (wide && i >= 0 ? (int32_t)(i - b0) : 0);
+        ocol[pos] = j < len ? (posof ? posof[ci[src + j]] : (int32_t)(ci[src + j] - b0)) : (wide && i >= 0 ? me : pad);
         oval[pos] = j < len ? lu[src + j] : 0.0;
     }
 }
 void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,
                      const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu, const int64_t *diag,
                      const double *dinv, int upper, int64_t n, int64_t nb, const int64_t *sptr2, int32_t *ocol,
-                     double *oval, hipStream_t st, bool wide) {
+                     double *oval, hipStream_t st, bool wide, const int32_t *posof, const int32_t *row_lo) {
     if (nslices > 0)
         k_lds_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, s_start, s_n, s_lpr, order, rp, ci, lu, diag,
-                                                                dinv, upper, n, nb, sptr2, ocol, oval, wide ? 1 : 0);
+                                                                dinv, upper, n, nb, sptr2, ocol, oval, wide ? 1 : 0,
+                                                                posof, row_lo);
 }
 
 // One sweep over a block's levels.  Pipeline: the loads of level g+2 are
@@ -1668,6 +1695,23 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// Ring sweep (R): the block solution lives in level-order position space; the
+// last RING_SLOTS positions sit in an LDS ring (slot p % RING_SLOTS), older
+// ones (far dependencies) were subtracted from the row's input when its chunk
+// loaded (from the position-ordered global copy ypos).  Positions are
+// processed in chunks of at most RING_CHUNK (level-aligned): at a chunk's first
+// level its inputs are loaded into their ring slots, after which every
+// position >= lo_ok = chunk end - RING_SLOTS is still in the ring.
+static constexpr int RING_SLOTS = 16384;
+static constexpr int RING_CHUNK = 4096;
+struct RingIn {
+    const int64_t *cg, *cp;   // per chunk: first level (group) / [start, end) positions (cp[2k], cp[2k+1])
+    const int32_t *src_idx;   // per position: index of its input value in src (block offset b0 included)
+    const double *src;        // L: x; U: the L sweep's ypos
+    const int64_t *frp;       // far dependencies per position (b0 + p): CSR row pointers
+    const int32_t *fcol;      // ... their block-local positions
+    const double *fval;       // ... factor values
+};
 struct Sw2Ctx {
     const int64_t *gslice, *sptr;
     const int32_t *col;
@@ -1677,6 +1721,10 @@ struct Sw2Ctx {
     int64_t gv, sb, se;  // lane l: gslice[gbase+l], sptr[gslice+wave], sptr[gslice+wave+1] (-1: none)
     int lane, wave, nw;
     bool upper;
+    // ring sweep only
+    double *ring, *ypos;     // LDS ring; this sweep's position-ordered output (block offset applied)
+    int64_t lo_ok, ck, cend, cnext, b0;
+    RingIn rin;
     __device__ __forceinline__ void refill(int64_t g) {
         gbase = g;
         const int64_t k = g + lane;
@@ -1720,17 +1768,35 @@ __device__ __forceinline__ void sw2_issue(Sw2Ctx &x, int64_t g, Sw2Slot<P> &s) {
 // W (wide, the y-resident sweep): header col = local row (-1: padding lane),
 // a lane's padding entries point at its own row with value 0, so only the
 // slice length masks entries and blocks may have up to 2^31 rows.
-template <int LPR, bool W>
+// the value of a dependency (block-local row, or position in the ring sweep)
+template <bool R>
+__device__ __forceinline__ double sw2_dep(const Sw2Ctx &x, int32_t c) {
+    // ring sweep: every stream entry is a near dependency, in the LDS ring (no
+    // global load in the level loop: vmcnt waits would drain the prefetches)
+    if (R) return x.ring[c & (RING_SLOTS - 1)];
+    return x.ys[c];
+}
+
+template <int LPR, bool W, bool R>
 __device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv, double acc) {
     if (LPR >= 2) acc += __shfl_xor(acc, 1);
     if (LPR >= 4) acc += __shfl_xor(acc, 2);
     if (LPR >= 8) acc += __shfl_xor(acc, 4);
     if (LPR >= 16) acc += __shfl_xor(acc, 8);
     const int32_t li = W ? h : (h & SW_ROW_PAD);
-    if ((x.lane % LPR) == 0 && (W ? li >= 0 : li != SW_ROW_PAD)) x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
+    if ((x.lane % LPR) == 0 && (W ? li >= 0 : li != SW_ROW_PAD)) {
+        if (R) {  // li: the row's position; its input sits in its ring slot
+            double *slot = x.ring + (li & (RING_SLOTS - 1));
+            const double v = x.upper ? (*slot - acc) * dv : *slot - acc;
+            *slot = v;
+            x.ypos[li] = v;
+        } else {
+            x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
+        }
+    }
 }
 
-template <int LPR, bool W>
+template <int LPR, bool W, bool R>
 __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
     const int64_t base = x.sptr[sl], L = (x.sptr[sl + 1] - base) >> 6;
     const int32_t h = x.col[base + x.lane];
@@ -1741,13 +1807,30 @@ __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
         const int64_t pos = base + k * 64 + x.lane;
         const int32_t cc = x.col[pos];
         const double vv = x.val[pos];
-        if (W || k <= len) acc += vv * x.ys[cc];
+        if (W || k <= len) acc += vv * sw2_dep<R>(x, cc);
     }
-    sw2_finish<LPR, W>(x, h, dv, acc);
+    sw2_finish<LPR, W, R>(x, h, dv, acc);
 }
 
-template <int P, int LPR, bool W>
+// ring sweep: at the first level of a chunk, its positions' inputs into the ring
+__device__ __forceinline__ void ring_chunk(Sw2Ctx &x, int64_t g) {
+    if (g != x.cnext) return;
+    const int64_t c0 = x.rin.cp[2 * x.ck], c1 = x.rin.cp[2 * x.ck + 1];
+    for (int64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
+        double v = x.rin.src[x.rin.src_idx[x.b0 + t]];
+        // far dependencies (older than the ring keeps, final before this chunk)
+        for (int64_t e = x.rin.frp[x.b0 + t]; e < x.rin.frp[x.b0 + t + 1]; ++e) v -= x.rin.fval[e] * x.ypos[x.rin.fcol[e]];
+        x.ring[t & (RING_SLOTS - 1)] = v;
+    }
+    __syncthreads();
+    x.lo_ok = c1 - RING_SLOTS;
+    ++x.ck;
+    x.cnext = x.ck < x.cend ? x.rin.cg[x.ck] : INT64_MAX;
+}
+
+template <int P, int LPR, bool W, bool R>
 __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P> &cur, Sw2Slot<P> &ahead) {
+    if (R) ring_chunk(x, g);
     if (g + 2 >= x.gbase + 64) x.refill(g);
     sw2_issue<P>(x, g + 2, ahead);
     if (cur.base >= 0) {
@@ -1756,7 +1839,7 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
         double acc = 0.0;
 #pragma unroll
         for (int u = 1; u <= P; ++u) {
-            const double t = cur.v[u] * x.ys[u <= len ? cur.c[u] : 0];
+            const double t = cur.v[u] * sw2_dep<R>(x, u <= len ? cur.c[u] : 0);
             acc += (u <= len) ? t : 0.0;
         }
         for (int64_t k0 = P + 1; k0 < cur.L; k0 += 8) {  // lanes with more than P entries: chunks of 8
@@ -1770,53 +1853,55 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const double t = vv[u] * x.ys[k0 + u <= len ? cc[u] : 0];
+                const double t = vv[u] * sw2_dep<R>(x, k0 + u <= len ? cc[u] : 0);
                 acc += (k0 + u <= len) ? t : 0.0;
             }
         }
-        sw2_finish<LPR, W>(x, h, cur.v[0], acc);
+        sw2_finish<LPR, W, R>(x, h, cur.v[0], acc);
         // levels with more slices than waves: the rest inline
         const int l = (int)(g - x.gbase);
         const int64_t s0 = readlane64(x.gv, l), s1 = readlane64(x.gv, l + 1);
-        for (int64_t sl = s0 + x.wave + x.nw; sl < s1; sl += x.nw) sw2_slice_inline<LPR, W>(x, sl);
+        for (int64_t sl = s0 + x.wave + x.nw; sl < s1; sl += x.nw) sw2_slice_inline<LPR, W, R>(x, sl);
     }
     __syncthreads();
 }
 
-template <int P, int LPR, bool W>
+template <int P, int LPR, bool W, bool R>
 __device__ __forceinline__ void sweep2(Sw2Ctx &x, int64_t g0) {
     x.refill(g0);
     Sw2Slot<P> s0, s1, s2;
     sw2_issue<P>(x, g0, s0);
     sw2_issue<P>(x, g0 + 1, s1);
     for (int64_t g = g0;;) {
-        sw2_level<P, LPR, W>(x, g, s0, s2);
+        sw2_level<P, LPR, W, R>(x, g, s0, s2);
         if (++g >= x.g1) break;
-        sw2_level<P, LPR, W>(x, g, s1, s0);
+        sw2_level<P, LPR, W, R>(x, g, s1, s0);
         if (++g >= x.g1) break;
-        sw2_level<P, LPR, W>(x, g, s2, s1);
+        sw2_level<P, LPR, W, R>(x, g, s2, s1);
         if (++g >= x.g1) break;
     }
 }
 
-template <int P, bool W>
+template <int P, bool W, bool R = false>
 __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int lane, int wave, int nw, bool upper,
                                             const int64_t *__restrict__ gslice, const int64_t *__restrict__ sptr,
                                             const int32_t *__restrict__ col, const double *__restrict__ val,
-                                            double *ys) {
+                                            double *ys, double *ring = nullptr, double *ypos = nullptr,
+                                            int64_t b0 = 0, int64_t ck0 = 0, int64_t ck1 = 0, RingIn rin = {}) {
     if (g0 >= g1) return;
-    Sw2Ctx x{gslice, sptr, col, val, ys, g1, 0, 0, 0, 0, lane, wave, nw, upper};
+    Sw2Ctx x{gslice, sptr, col, val, ys, g1, 0, 0, 0, 0, lane, wave, nw, upper,
+             ring, ypos, 0, ck0, ck1, ck0 < ck1 ? rin.cg[ck0] : INT64_MAX, b0, rin};
     if (W) {  // the y-resident sweep: 8 / 16 lanes for long rows
-        if (lpr == 16) sweep2<P, 16, W>(x, g0);
-        else if (lpr == 8) sweep2<P, 8, W>(x, g0);
-        else if (lpr == 4) sweep2<P, 4, W>(x, g0);
-        else if (lpr == 2) sweep2<P, 2, W>(x, g0);
-        else sweep2<P, 1, W>(x, g0);
+        if (lpr == 16) sweep2<P, 16, W, R>(x, g0);
+        else if (lpr == 8) sweep2<P, 8, W, R>(x, g0);
+        else if (lpr == 4) sweep2<P, 4, W, R>(x, g0);
+        else if (lpr == 2) sweep2<P, 2, W, R>(x, g0);
+        else sweep2<P, 1, W, R>(x, g0);
         return;
     }
-    if (lpr == 4) sweep2<P, 4, W>(x, g0);
-    else if (lpr == 2) sweep2<P, 2, W>(x, g0);
-    else sweep2<P, 1, W>(x, g0);
+    if (lpr == 4) sweep2<P, 4, W, R>(x, g0);
+    else if (lpr == 2) sweep2<P, 2, W, R>(x, g0);
+    else sweep2<P, 1, W, R>(x, g0);
 }
 
 static constexpr int SW_P = 7;  // factor entries per lane kept in registers per pipeline slot
@@ -1870,6 +1955,65 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
         p[7] = Llpr[blk] * 10 + Ulpr[blk];
     }
 }
+
+// The ring sweep (whole FE blocks in a bandwidth-reducing order: deep, narrow
+// level DAGs whose dependencies are recent in level order): per block, the L
+// sweep in L's level-order positions (inputs x[ordL]), outputs to yL (position
+// order); the U sweep in U's positions (inputs yL[mapUL]), outputs to yU; then
+// y[ordU[p]] = yU[p].  Dependency reads hit the LDS ring unless older than
+// RING_SLOTS - RING_CHUNK positions (then yL / yU in global memory, written by
+// this workgroup: workgroup-scope coherence as in the y-resident sweep), and
+// those "far" dependencies are known at setup: they are taken out of the
+// factor streams and subtracted from the row's input when its chunk loads.
+__global__ __launch_bounds__(1024) void k_ilu_blocks_ring(
+    int64_t n, int64_t nblocks, const int64_t *__restrict__ Lgoff, const int64_t *__restrict__ Lgslice,
+    const int64_t *__restrict__ Lsptr, const int32_t *__restrict__ Lcol, const double *__restrict__ Lval,
+    const int32_t *__restrict__ Llpr, const int64_t *__restrict__ Ugoff, const int64_t *__restrict__ Ugslice,
+    const int64_t *__restrict__ Usptr, const int32_t *__restrict__ Ucol, const double *__restrict__ Uval,
+    const int32_t *__restrict__ Ulpr, const int64_t *__restrict__ Lcoff, const int64_t *__restrict__ Lcg,
+    const int64_t *__restrict__ Lcp, const int64_t *__restrict__ Ucoff, const int64_t *__restrict__ Ucg,
+    const int64_t *__restrict__ Ucp, const int32_t *__restrict__ ordL, const int32_t *__restrict__ mapUL,
+    const int32_t *__restrict__ ordU, const int64_t *__restrict__ Lfrp, const int32_t *__restrict__ Lfcol,
+    const double *__restrict__ Lfval, const int64_t *__restrict__ Ufrp, const int32_t *__restrict__ Ufcol,
+    const double *__restrict__ Ufval, const double *x, double *y, double *yL, double *yU) {
+    extern __shared__ __attribute__((aligned(16))) double ring[];
+    const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
+    const int64_t q = n / nblocks, r = n % nblocks;
+    const int64_t b0 = blk * q + (blk < r ? blk : r);
+    const int64_t len = q + (blk < r ? 1 : 0);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    sweep_block<SW_P, true, true>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol,
+                                  Lval, nullptr, ring, yL + b0, b0, Lcoff[blk], Lcoff[blk + 1],
+                                  RingIn{Lcg, Lcp, ordL, x, Lfrp, Lfcol, Lfval});
+    __syncthreads();
+    sweep_block<SW_P, true, true>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol,
+                                  Uval, nullptr, ring, yU + b0, b0, Ucoff[blk], Ucoff[blk + 1],
+                                  RingIn{Ucg, Ucp, mapUL, yL, Ufrp, Ufcol, Ufval});
+    __syncthreads();
+    for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[ordU[b0 + t]] = yU[b0 + t];
+}
+
+void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,
+                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
+                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
+                            const double *Uval, const int32_t *Ulpr, const int64_t *Lcoff, const int64_t *Lcg,
+                            const int64_t *Lcp, const int64_t *Ucoff, const int64_t *Ucg, const int64_t *Ucp,
+                            const int32_t *ordL, const int32_t *mapUL, const int32_t *ordU, const int64_t *Lfrp,
+                            const int32_t *Lfcol, const double *Lfval, const int64_t *Ufrp, const int32_t *Ufcol,
+                            const double *Ufval, const double *x, double *y, double *yL, double *yU, hipStream_t st) {
+    static bool configured = false;
+    const int bytes = RING_SLOTS * 8;
+    if (!configured) {
+        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_ring, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        configured = true;
+    }
+    k_ilu_blocks_ring<<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
+                                                               Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, Lcoff, Lcg, Lcp,
+                                                               Ucoff, Ucg, Ucp, ordL, mapUL, ordU, Lfrp, Lfcol, Lfval,
+                                                               Ufrp, Ufcol, Ufval, x, y, yL, yU);
+}
+int ilu_ring_slots() { return RING_SLOTS; }
+int ilu_ring_chunk() { return RING_CHUNK; }
 
 int ilu_lds_max_rows() { return 163840 / 8; }
 int ilu_gmem_max_rows() { return 0x7FFFFFFF; }

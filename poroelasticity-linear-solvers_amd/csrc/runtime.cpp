@@ -642,10 +642,14 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
                           const std::vector<int64_t> &rp,
                           const std::vector<int64_t> &dg, const std::vector<int32_t> &order,
                           const std::vector<int64_t> &grp, const std::vector<int64_t> &goff, bool upper, LdsTri &D,
-                          Ctx &c) {
+                          Ctx &c, const std::vector<int32_t> *posof = nullptr,
+                          const std::vector<int32_t> *row_lo = nullptr, const std::vector<int32_t> *near_len = nullptr) {
     const int64_t ng = (int64_t)grp.size() - 1, nblk = (int64_t)goff.size() - 1;
     const int W = ilu_lds_lane_entries();
-    auto rlen = [&](int64_t i) { return upper ? rp[i + 1] - dg[i] - 1 : dg[i] - rp[i]; };
+    auto rlen = [&](int64_t i) -> int64_t {
+        if (near_len) return (*near_len)[i];  // ring sweep: the near entries only
+        return upper ? rp[i + 1] - dg[i] - 1 : dg[i] - rp[i];
+    };
     std::vector<int32_t> lpr(nblk, 1), s_start, s_n, s_lpr;
     std::vector<int64_t> gsl(ng + 1, 0), sptr(1, 0);
     for (int64_t b = 0; b < nblk; ++b) {
@@ -702,8 +706,12 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
     up(d_order, order);
     D.col.alloc(std::max<int64_t>(sptr.back(), 1));
     D.val.alloc(std::max<int64_t>(sptr.back(), 1));
+    DBuf<int32_t> d_posof, d_lo;
+    if (posof) up(d_posof, *posof);
+    if (row_lo) up(d_lo, *row_lo);
     launch_lds_fill(ns, d_start.p, d_n.p, d_lpr.p, d_order.p, P.F.rp.p, P.F.ci.p, P.F.val.p, P.diag.p, P.dinv.p,
-                    upper ? 1 : 0, n, nb, D.sptr.p, D.col.p, D.val.p, c.st, /*wide headers: y-resident sweep*/ max_lpr > 4);
+                    upper ? 1 : 0, n, nb, D.sptr.p, D.col.p, D.val.p, c.st, /*wide headers: y-resident sweep*/ max_lpr > 4,
+                    posof ? d_posof.p : nullptr, row_lo ? d_lo.p : nullptr);
     HIPCHK(hipGetLastError());
     c.sync();
 }
@@ -756,7 +764,76 @@ static void envelope_csr(const DevCSR &M, DevCSR &E, Ctx &c) {
     upload_csr(E, n, n, erp.data(), eci.data(), ev.data(), c);
 }
 
-PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr, int gmem_mode) {
+// Ring sweep tables of one triangle: block-local level-order positions of the
+// rows (posof), and level-aligned chunks of at most ilu_ring_chunk() positions.
+// A row's dependency at position q is "near" when q >= row_lo[row] = (end of
+// the row's chunk) - ilu_ring_slots(): still in the ring while the row runs.
+// Far ones go to a CSR over positions, applied when the row's chunk loads.
+static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order, const std::vector<int64_t> &grp,
+                        const std::vector<int64_t> &goff, const std::vector<int64_t> &rp, const std::vector<int32_t> &ci,
+                        const std::vector<int64_t> &dg, const std::vector<double> &fv, bool upper,
+                        std::vector<int32_t> &posof, std::vector<int32_t> &row_lo, std::vector<int32_t> &near_len,
+                        RingTri &T, Ctx &c) {
+    const int64_t q = n / nb, r = n % nb, C = ilu_ring_chunk(), R = ilu_ring_slots();
+    posof.assign(n, 0);
+    row_lo.assign(n, 0);
+    near_len.assign(n, 0);
+    std::vector<int64_t> coff(nb + 1, 0), cg, cp;
+    int64_t b0 = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t len = q + (b < r ? 1 : 0);
+        for (int64_t k = b0; k < b0 + len; ++k) posof[order[k]] = (int32_t)(k - b0);
+        coff[b] = (int64_t)cg.size();
+        for (int64_t g = goff[b]; g < goff[b + 1];) {
+            const int64_t c0 = grp[g] - b0;
+            int64_t e = g + 1;
+            while (e < goff[b + 1] && grp[e + 1] - b0 - c0 <= C) ++e;
+            cg.push_back(g);
+            cp.push_back(c0);
+            cp.push_back(grp[e] - b0);
+            for (int64_t k = grp[g]; k < grp[e]; ++k) row_lo[order[k]] = (int32_t)(grp[e] - b0 - R);
+            g = e;
+        }
+        b0 += len;
+    }
+    coff[nb] = (int64_t)cg.size();
+    // far dependencies, by position (b0 + p), in the row's entry order
+    std::vector<int64_t> frp(n + 1, 0);
+    std::vector<int32_t> fcol;
+    std::vector<double> fval;
+    for (int64_t k = 0; k < n; ++k) {
+        const int64_t i = order[k];
+        const int64_t s0 = upper ? dg[i] + 1 : rp[i], s1 = upper ? rp[i + 1] : dg[i];
+        int64_t near = 0;
+        for (int64_t e = s0; e < s1; ++e) {
+            const int32_t pc = posof[ci[e]];
+            if (pc >= row_lo[i]) {
+                ++near;
+            } else {
+                fcol.push_back(pc);
+                fval.push_back(fv[e]);
+            }
+        }
+        near_len[i] = (int32_t)near;
+        frp[k + 1] = (int64_t)fcol.size();
+    }
+    T.nfar = (int64_t)fcol.size();
+    auto up = [&](auto &d, const auto &v) {
+        d.alloc(std::max<size_t>(v.size(), 1));
+        if (!v.empty()) HIPCHK(hipMemcpyAsync(d.p, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, c.st));
+    };
+    up(T.coff, coff);
+    up(T.cg, cg);
+    up(T.cp, cp);
+    up(T.ord, order);
+    up(T.frp, frp);
+    up(T.fcol, fcol);
+    up(T.fval, fval);
+    c.sync();
+}
+
+PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr, int gmem_mode,
+             int ring_mode) {
     exact = exact_lu;
     allow_lds = lds;
     type = exact ? "lu" : (nb > 1 ? "bjacobi" : "ilu");
@@ -824,10 +901,39 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         nlev_U = (int64_t)gU.size() - 1;
         use_lds = (allow_lds && fits_lds) || gmem;
         lds_gmem = gmem;
+        // the ring sweep: y-resident blocks whose every level fits one chunk
+        if (gmem && ring_mode != 0) {
+            int64_t wmax = 0;
+            for (const auto *g : {&gL, &gU})
+                for (size_t k = 0; k + 1 < g->size(); ++k) wmax = std::max<int64_t>(wmax, (*g)[k + 1] - (*g)[k]);
+            ring = wmax <= ilu_ring_chunk();
+        }
         if (use_lds) {
             const int max_lpr = gmem ? 16 : 4;
-            build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oL, gL, fL, false, Ls, c);
-            build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oU, gU, fU, true, Us, c);
+            std::vector<int32_t> pL, pU, loL, loU, nlL, nlU;
+            if (ring) {
+                std::vector<double> fv(F.nnz);
+                if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
+                c.sync();
+                ring_tables(n, nblocks, oL, gL, fL, rp, ci, dg, fv, false, pL, loL, nlL, Lr, c);
+                ring_tables(n, nblocks, oU, gU, fU, rp, ci, dg, fv, true, pU, loU, nlU, Ur, c);
+                // mapUL[b0 + t] = b0 + (L position of the row at U position t)
+                std::vector<int32_t> m(n);
+                const int64_t q = n / nblocks, r = n % nblocks;
+                int64_t b0 = 0;
+                for (int64_t b = 0; b < nblocks; ++b) {
+                    const int64_t len = q + (b < r ? 1 : 0);
+                    for (int64_t t = b0; t < b0 + len; ++t) m[t] = (int32_t)(b0 + pL[oU[t]]);
+                    b0 += len;
+                }
+                mapUL.alloc(std::max<int64_t>(n, 1));
+                HIPCHK(hipMemcpyAsync(mapUL.p, m.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+                c.sync();
+            }
+            build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oL, gL, fL, false, Ls, c, ring ? &pL : nullptr,
+                          ring ? &loL : nullptr, ring ? &nlL : nullptr);
+            build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oU, gU, fU, true, Us, c, ring ? &pU : nullptr,
+                          ring ? &loU : nullptr, ring ? &nlU : nullptr);
         }
     } else {
         std::vector<int32_t> ordU;
@@ -839,6 +945,18 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
 }
 
 void PCILU::apply(const double *x, double *y, Ctx &c) {
+    if (use_lds && ring) {
+        auto &sc = ring_scratch[c.st];  // per stream: the concurrent 3-way sweeps share this PC
+        if (sc.first.n < (size_t)n) {
+            sc.first.alloc(std::max<int64_t>(n, 1));
+            sc.second.alloc(std::max<int64_t>(n, 1));
+        }
+        launch_ilu_blocks_ring(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
+                               Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, Lr.coff.p, Lr.cg.p, Lr.cp.p,
+                               Ur.coff.p, Ur.cg.p, Ur.cp.p, Lr.ord.p, mapUL.p, Ur.ord.p, Lr.frp.p, Lr.fcol.p,
+                               Lr.fval.p, Ur.frp.p, Ur.fcol.p, Ur.fval.p, x, y, sc.first.p, sc.second.p, c.st);
+        return;
+    }
     if (use_lds) {
         DBuf<int64_t> prof;
         if (!profile_tag.empty()) prof.alloc(nblocks * 8);
@@ -970,7 +1088,8 @@ std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
         const double gb = nbt * w * 4096.0 * 8.0 / 1e9;
         if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 64.0)) return std::make_unique<PCBandLU>(M, kl, ku, c);
     }
-    return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true), 0, (int)o.integer("pls.ilu_gmem", 0));
+    return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true), 0, (int)o.integer("pls.ilu_gmem", 0),
+                                   (int)o.integer("pls.ilu_ring", 1));
 }
 
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
@@ -985,7 +1104,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         if (o.integer(prefix + "pc_factor_levels", 0) != 0)
             throw Error(prefix + "pc_factor_levels > 0: only ILU(0) is implemented");
         return std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true), 0,
-                                       (int)o.integer("pls.ilu_gmem", 0));
+                                       (int)o.integer("pls.ilu_gmem", 0), (int)o.integer("pls.ilu_ring", 1));
     }
     if (type == "lu" || type == "cholesky") return make_lu(M, o, c);
     if (type == "bjacobi") {
@@ -999,7 +1118,8 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
             if (o.integer(prefix + "sub_pc_factor_levels", 0) != 0)
                 throw Error(prefix + "sub_pc_factor_levels > 0: only ILU(0) is implemented");
             auto pc = std::make_unique<PCILU>(M, nb, c, false, o.flag("pls.ilu_lds", true),
-                                              (int)o.integer("pls.sweep_lpr", 0), (int)o.integer("pls.ilu_gmem", 0));
+                                              (int)o.integer("pls.sweep_lpr", 0), (int)o.integer("pls.ilu_gmem", 0),
+                                              (int)o.integer("pls.ilu_ring", 1));
             if (o.flag("pls.sweep_profile", false)) pc->profile_tag = prefix;
             return pc;
         }

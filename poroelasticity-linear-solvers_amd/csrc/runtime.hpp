@@ -250,8 +250,23 @@ struct LdsTri {
     DBuf<int32_t> col, lpr;      // lpr: lanes per row, per block
     DBuf<double> val;
 };
+// Ring sweep tables of one triangle (kernels.hip, k_ilu_blocks_ring)
+struct RingTri {
+    DBuf<int64_t> coff, cg, cp;  // chunks per block / first level / [start, end) positions
+    DBuf<int32_t> ord;           // position -> row (the triangle's level order)
+    DBuf<int64_t> frp;           // far dependencies per position (CSR over b0 + p)
+    DBuf<int32_t> fcol;          // ... block-local positions
+    DBuf<double> fval;           // ... factor values
+    int64_t nfar = 0;
+};
 struct PCILU : PC {
     int64_t nblocks = 1;
+    // ring sweep (pls.ilu_ring, default on): y-resident blocks whose levels are
+    // narrow sweep in level-order position space with an LDS ring of recent values
+    bool ring = false;
+    RingTri Lr, Ur;
+    DBuf<int32_t> mapUL;  // U position -> index of the row's L-sweep value
+    std::map<hipStream_t, std::pair<DBuf<double>, DBuf<double>>> ring_scratch;  // per stream: yL, yU
     DevCSR F;                     // truncated matrix, factored in place
     DBuf<int64_t> diag;
     DBuf<double> dinv;
@@ -266,7 +281,7 @@ struct PCILU : PC {
     // gmem_mode (option pls.ilu_gmem): 0 auto, 1 force the y-resident
     // workgroup sweep (also on blocks that fit LDS), -1 never
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0,
-          int gmem_mode = 0);
+          int gmem_mode = 0, int ring_mode = 1);
     bool reentrant() const override { return profile_tag.empty(); }
     void apply(const double *x, double *y, Ctx &c) override;
 };

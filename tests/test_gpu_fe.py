@@ -305,3 +305,29 @@ def test_spmv_sigma_layout_on_assembled(gpu, dim, N, ordering):
     assert np.max(np.abs(hs.pc_apply(x) - hp.pc_apply(x))) <= 1e-12 * np.max(np.abs(hp.pc_apply(x)))
     hs.destroy()
     hp.destroy()
+
+
+@pytest.mark.parametrize("dim,N,blocks", [(3, 12, 1), (3, 8, 3), (2, 24, 1)])
+def test_ring_sweep_equals_y_resident(gpu, dim, N, blocks):
+    """The ring sweep (level-order positions, recent values in an LDS ring;
+    dependencies older than the ring keeps are subtracted from the row's input
+    when its chunk loads) against the y-resident sweep on the same factors:
+    equal to rounding (the far terms are summed first; rows without far
+    dependencies keep the same order).  3-D N=12 fp U reaches dependencies
+    46,596 positions back -- past the ring -- so the far path runs (11 % of
+    its entries)."""
+    from lib.handle import Handle, params_to_options
+    s = F.assemble_swelling(dim, N, "diagonal")
+    db = _db("ilu") if blocks == 1 else _db("bjacobi", {"s_pc_bjacobi_blocks": str(blocks),
+                                                        "fp_pc_bjacobi_blocks": str(blocks)})
+    opts = dict(db, **{"pls.ilu_gmem": "1"})
+    opts.update(params_to_options(dict(BASE, **{"pc type": "diagonal"})))
+    hr = Handle.from_csr(s.A, s.P, None, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    hy = Handle.from_csr(s.A, s.P, None, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, dict(opts, **{"pls.ilu_ring": "0"}))
+    x = np.random.default_rng(9).standard_normal(s.A.shape[0])
+    yr, yy = hr.pc_apply(x), hy.pc_apply(x)
+    assert np.all(np.isfinite(yr))
+    assert np.max(np.abs(yr - yy)) <= 1e-12 * np.max(np.abs(yy))
+    assert np.array_equal(hr.pc_apply(x), yr)  # repeatable (scratch reuse)
+    hr.destroy()
+    hy.destroy()
