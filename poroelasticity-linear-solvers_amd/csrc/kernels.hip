@@ -1687,6 +1687,7 @@ struct Sw2Slot {
     int32_t c[P + 1];
     double v[P + 1];
     int64_t base, L;  // L: entries incl. header; base < 0: this wave has no slice
+    int l2;           // ring sweep: log2 of the slice's lanes per row (slice starts carry it in bits 0-2)
 };
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
@@ -1723,7 +1724,7 @@ struct Sw2Ctx {
     bool upper;
     // ring sweep only
     double *ring, *ypos;     // LDS ring; this sweep's position-ordered output (block offset applied)
-    int64_t lo_ok, ck, cend, cnext, b0;
+    int64_t lo_ok, ck, cend, cnext, b0, ck0;
     RingIn rin;
     __device__ __forceinline__ void refill(int64_t g) {
         gbase = g;
@@ -1742,13 +1743,34 @@ struct Sw2Ctx {
     }
 };
 
-template <int P>
+template <int P, bool R>
 __device__ __forceinline__ void sw2_issue(Sw2Ctx &x, int64_t g, Sw2Slot<P> &s) {
     const int l = (int)(g - x.gbase);
-    const int64_t base = g < x.g1 ? readlane64(x.sb, l) : -1;
-    const int64_t L = base >= 0 ? (readlane64(x.se, l) - base) >> 6 : 0;
+    int64_t base = g < x.g1 ? readlane64(x.sb, l) : -1;
+    int64_t next = base >= 0 ? readlane64(x.se, l) : 0;
+    s.l2 = 0;
+    if (R) {  // slice starts are multiples of 64 entries; bits 0-2: log2(lanes per row)
+        s.l2 = base >= 0 ? (int)(base & 7) : 0;
+        base = base >= 0 ? (base & ~(int64_t)63) : -1;
+        next &= ~(int64_t)63;
+    }
+    const int64_t L = base >= 0 ? (next - base) >> 6 : 0;
     s.base = base;
     s.L = L;
+    if (R) {
+        // ring sweep: idle waves load too (the stream's first header, ignored):
+        // the same loads on every path keep the compiler's vmcnt bookkeeping
+        // exact, so using this slot two levels later waits for its own loads
+        // only (a branch around them made it wait for everything in flight)
+        const int64_t b = base >= 0 ? base : 0;
+#pragma unroll
+        for (int u = 0; u <= P; ++u) {
+            const int64_t pos = b + (u < L ? u : 0) * 64 + x.lane;
+            s.c[u] = __builtin_nontemporal_load(x.col + pos);
+            s.v[u] = __builtin_nontemporal_load(x.val + pos);
+        }
+        return;
+    }
     if (base < 0) {  // wave idle at this level: no loads (they would only queue in the CU's memory pipe)
 #pragma unroll
         for (int u = 0; u <= P; ++u) {
@@ -1777,19 +1799,32 @@ __device__ __forceinline__ double sw2_dep(const Sw2Ctx &x, int32_t c) {
     return x.ys[c];
 }
 
+// a double through a DPP lane permutation (no LDS round trip, unlike a shuffle)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// LPR = 0: lanes per row chosen per slice (ring sweep), 1 << l2
 template <int LPR, bool W, bool R>
-__device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv, double acc) {
-    if (LPR >= 2) acc += __shfl_xor(acc, 1);
-    if (LPR >= 4) acc += __shfl_xor(acc, 2);
-    if (LPR >= 8) acc += __shfl_xor(acc, 4);
-    if (LPR >= 16) acc += __shfl_xor(acc, 8);
+__device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv, double acc, int l2 = 0) {
+    // the LPR partial sums of a row: quad_perm xor 1, xor 2, then row_half_mirror
+    // and row_mirror -- after the quad steps every lane of a quad holds the same
+    // value, so mirroring pairs exactly the sums xor 4 / xor 8 would (a + b =
+    // b + a: bitwise the shuffle tree), without LDS round trips
+    const int lg = LPR ? (LPR >= 32 ? 5 : LPR >= 16 ? 4 : LPR >= 8 ? 3 : LPR >= 4 ? 2 : LPR >= 2 ? 1 : 0) : l2;
+    if (lg >= 1) acc += dpp_d<0xB1>(acc);
+    if (lg >= 2) acc += dpp_d<0x4E>(acc);
+    if (lg >= 3) acc += dpp_d<0x141>(acc);
+    if (lg >= 4) acc += dpp_d<0x140>(acc);
+    if (lg >= 5) acc += __shfl_xor(acc, 16);
     const int32_t li = W ? h : (h & SW_ROW_PAD);
-    if ((x.lane % LPR) == 0 && (W ? li >= 0 : li != SW_ROW_PAD)) {
+    if ((x.lane & ((1 << lg) - 1)) == 0 && (W ? li >= 0 : li != SW_ROW_PAD)) {
         if (R) {  // li: the row's position; its input sits in its ring slot
             double *slot = x.ring + (li & (RING_SLOTS - 1));
-            const double v = x.upper ? (*slot - acc) * dv : *slot - acc;
-            *slot = v;
-            x.ypos[li] = v;
+            *slot = x.upper ? (*slot - acc) * dv : *slot - acc;  // to ypos in bulk at the next chunk
         } else {
             x.ys[li] = x.upper ? (x.ys[li] - acc) * dv : x.ys[li] - acc;
         }
@@ -1798,7 +1833,9 @@ __device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv
 
 template <int LPR, bool W, bool R>
 __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
-    const int64_t base = x.sptr[sl], L = (x.sptr[sl + 1] - base) >> 6;
+    const int64_t enc = x.sptr[sl];
+    const int64_t base = R ? (enc & ~(int64_t)63) : enc;
+    const int64_t L = ((R ? (x.sptr[sl + 1] & ~(int64_t)63) : x.sptr[sl + 1]) - base) >> 6;
     const int32_t h = x.col[base + x.lane];
     const double dv = x.val[base + x.lane];
     const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
@@ -1809,12 +1846,20 @@ __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
         const double vv = x.val[pos];
         if (W || k <= len) acc += vv * sw2_dep<R>(x, cc);
     }
-    sw2_finish<LPR, W, R>(x, h, dv, acc);
+    sw2_finish<LPR, W, R>(x, h, dv, acc, R ? (int)(enc & 7) : 0);
 }
 
-// ring sweep: at the first level of a chunk, its positions' inputs into the ring
+// ring sweep: results of positions [p0, p1) from the ring to ypos (they stay in
+// the ring for RING_SLOTS - RING_CHUNK >= RING_CHUNK more positions)
+__device__ __forceinline__ void ring_flush(Sw2Ctx &x, int64_t p0, int64_t p1) {
+    for (int64_t t = p0 + threadIdx.x; t < p1; t += blockDim.x) x.ypos[t] = x.ring[t & (RING_SLOTS - 1)];
+}
+
+// ring sweep: at the first level of a chunk, the previous chunk's results to
+// ypos, then this chunk's inputs into the ring
 __device__ __forceinline__ void ring_chunk(Sw2Ctx &x, int64_t g) {
     if (g != x.cnext) return;
+    if (x.ck > x.ck0) ring_flush(x, x.rin.cp[2 * x.ck - 2], x.rin.cp[2 * x.ck - 1]);
     const int64_t c0 = x.rin.cp[2 * x.ck], c1 = x.rin.cp[2 * x.ck + 1];
     for (int64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
         double v = x.rin.src[x.rin.src_idx[x.b0 + t]];
@@ -1832,14 +1877,18 @@ template <int P, int LPR, bool W, bool R>
 __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P> &cur, Sw2Slot<P> &ahead) {
     if (R) ring_chunk(x, g);
     if (g + 2 >= x.gbase + 64) x.refill(g);
-    sw2_issue<P>(x, g + 2, ahead);
+    sw2_issue<P, R>(x, g + 2, ahead);
     if (cur.base >= 0) {
         const int32_t h = cur.c[0];
         const int32_t len = W ? (int32_t)cur.L - 1 : (int32_t)((uint32_t)h >> SW_ROW_BITS);
-        double acc = 0.0;
+        double acc = 0.0, d[P + 1];
+        // every dependency read issued before the first is consumed (they are
+        // independent; consuming in turn would serialise the LDS / L1 round trips)
+#pragma unroll
+        for (int u = 1; u <= P; ++u) d[u] = sw2_dep<R>(x, u <= len ? cur.c[u] : 0);
 #pragma unroll
         for (int u = 1; u <= P; ++u) {
-            const double t = cur.v[u] * sw2_dep<R>(x, u <= len ? cur.c[u] : 0);
+            const double t = cur.v[u] * d[u];
             acc += (u <= len) ? t : 0.0;
         }
         for (int64_t k0 = P + 1; k0 < cur.L; k0 += 8) {  // lanes with more than P entries: chunks of 8
@@ -1857,7 +1906,7 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
                 acc += (k0 + u <= len) ? t : 0.0;
             }
         }
-        sw2_finish<LPR, W, R>(x, h, cur.v[0], acc);
+        sw2_finish<LPR, W, R>(x, h, cur.v[0], acc, cur.l2);
         // levels with more slices than waves: the rest inline
         const int l = (int)(g - x.gbase);
         const int64_t s0 = readlane64(x.gv, l), s1 = readlane64(x.gv, l + 1);
@@ -1870,8 +1919,8 @@ template <int P, int LPR, bool W, bool R>
 __device__ __forceinline__ void sweep2(Sw2Ctx &x, int64_t g0) {
     x.refill(g0);
     Sw2Slot<P> s0, s1, s2;
-    sw2_issue<P>(x, g0, s0);
-    sw2_issue<P>(x, g0 + 1, s1);
+    sw2_issue<P, R>(x, g0, s0);
+    sw2_issue<P, R>(x, g0 + 1, s1);
     for (int64_t g = g0;;) {
         sw2_level<P, LPR, W, R>(x, g, s0, s2);
         if (++g >= x.g1) break;
@@ -1890,7 +1939,12 @@ __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int
                                             int64_t b0 = 0, int64_t ck0 = 0, int64_t ck1 = 0, RingIn rin = {}) {
     if (g0 >= g1) return;
     Sw2Ctx x{gslice, sptr, col, val, ys, g1, 0, 0, 0, 0, lane, wave, nw, upper,
-             ring, ypos, 0, ck0, ck1, ck0 < ck1 ? rin.cg[ck0] : INT64_MAX, b0, rin};
+             ring, ypos, 0, ck0, ck1, ck0 < ck1 ? rin.cg[ck0] : INT64_MAX, b0, ck0, rin};
+    if (R) {  // ring sweep: lanes per row per slice
+        sweep2<P, 0, true, true>(x, g0);
+        if (ck1 > ck0) ring_flush(x, rin.cp[2 * ck1 - 2], rin.cp[2 * ck1 - 1]);  // the last chunk
+        return;
+    }
     if (W) {  // the y-resident sweep: 8 / 16 lanes for long rows
         if (lpr == 16) sweep2<P, 16, W, R>(x, g0);
         else if (lpr == 8) sweep2<P, 8, W, R>(x, g0);

@@ -676,6 +676,33 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
         }
         lpr[b] = l;
         const int64_t per = 64 / l;
+        if (posof) {
+            // ring sweep: lanes per row chosen per slice (rows sorted longest first
+            // inside each level): the fewest that keep every lane's share within the
+            // register window, so short-row slices hold more rows and a level needs
+            // fewer slices than the workgroup has waves (no in-level reloads)
+            for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {
+                gsl[g] = (int64_t)s_start.size();
+                for (int64_t r0 = grp[g]; r0 < grp[g + 1];) {
+                    int ls = force_lpr ? force_lpr : 1;  // pls.sweep_lpr pins it
+                    int64_t r1 = 0, mxs = 0;
+                    for (;;) {
+                        r1 = std::min(grp[g + 1], r0 + 64 / ls);
+                        mxs = 0;
+                        for (int64_t r = r0; r < r1; ++r) mxs = std::max(mxs, rlen(order[r]));
+                        if ((mxs + ls - 1) / ls <= W || ls >= 32 || force_lpr) break;
+                        ls *= 2;
+                    }
+                    s_start.push_back((int32_t)r0);
+                    s_n.push_back((int32_t)(r1 - r0));
+                    s_lpr.push_back(ls);
+                    sptr.push_back(sptr.back() + 64 * ((mxs + ls - 1) / ls + 1));
+                    lpr[b] = std::max(lpr[b], ls);
+                    r0 = r1;
+                }
+            }
+            continue;
+        }
         for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {
             gsl[g] = (int64_t)s_start.size();
             for (int64_t r0 = grp[g]; r0 < grp[g + 1]; r0 += per) {
@@ -714,6 +741,15 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
                     posof ? d_posof.p : nullptr, row_lo ? d_lo.p : nullptr);
     HIPCHK(hipGetLastError());
     c.sync();
+    if (posof) {  // ring sweep: slice starts carry log2(lanes per row) in bits 0-2
+        for (int64_t k = 0; k < ns; ++k) {
+            int l2 = 0;
+            while ((1 << l2) < s_lpr[k]) ++l2;
+            sptr[k] |= l2;
+        }
+        HIPCHK(hipMemcpyAsync(D.sptr.p, sptr.data(), sizeof(int64_t) * sptr.size(), hipMemcpyHostToDevice, c.st));
+        c.sync();
+    }
 }
 
 void TriSELL::apply(const double *b, double *y, Ctx &c) const {
@@ -909,9 +945,19 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             ring = wmax <= ilu_ring_chunk();
         }
         if (use_lds) {
-            const int max_lpr = gmem ? 16 : 4;
+            const int max_lpr = gmem ? (ring ? 32 : 16) : 4;
             std::vector<int32_t> pL, pU, loL, loU, nlL, nlU;
             if (ring) {
+                // rows of a level longest first (slices then take fewer lanes per row
+                // as rows get shorter); positions follow this order
+                auto sort_levels = [&](std::vector<int32_t> &o, const std::vector<int64_t> &g, bool up) {
+                    auto len = [&](int32_t i) { return up ? rp[i + 1] - dg[i] - 1 : dg[i] - rp[i]; };
+                    for (size_t k = 0; k + 1 < g.size(); ++k)
+                        std::stable_sort(o.begin() + g[k], o.begin() + g[k + 1],
+                                         [&](int32_t a, int32_t b) { return len(a) > len(b); });
+                };
+                sort_levels(oL, gL, false);
+                sort_levels(oU, gU, true);
                 std::vector<double> fv(F.nnz);
                 if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
                 c.sync();
