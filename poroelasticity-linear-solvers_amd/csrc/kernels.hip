@@ -1703,6 +1703,9 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
 // processed in chunks of at most RING_CHUNK (level-aligned): at a chunk's first
 // level its inputs are loaded into their ring slots, after which every
 // position >= lo_ok = chunk end - RING_SLOTS is still in the ring.
+// diagnostics (pls.ring_probe; timing only, wrong results): bit 0 -- factor loads
+// range-checked away, bit 1 -- no compute, bit 2 -- no prefetch instructions
+__constant__ int ring_probe;
 static constexpr int RING_SLOTS = 16384;
 static constexpr int RING_CHUNK = 4096;
 struct RingIn {
@@ -1757,17 +1760,29 @@ __device__ __forceinline__ void sw2_issue(Sw2Ctx &x, int64_t g, Sw2Slot<P> &s) {
     const int64_t L = base >= 0 ? (next - base) >> 6 : 0;
     s.base = base;
     s.L = L;
+    if (R && (ring_probe & 4)) {  // diagnostics: no prefetch at all
+        s.base = base;
+#pragma unroll
+        for (int u = 0; u <= P; ++u) { s.c[u] = 0; s.v[u] = 0.0; }
+        return;
+    }
     if (R) {
-        // ring sweep: idle waves load too (the stream's first header, ignored):
-        // the same loads on every path keep the compiler's vmcnt bookkeeping
-        // exact, so using this slot two levels later waits for its own loads
-        // only (a branch around them made it wait for everything in flight)
+        // ring sweep: buffer loads through per-slot descriptors bounded to the
+        // slice (0 bytes for an idle wave): entries past the slice and idle
+        // waves' loads are range-checked away (no traffic, reads return 0),
+        // and every path issues the same loads, which keeps the compiler's
+        // vmcnt bookkeeping exact -- using this slot two levels later waits for
+        // its own loads only (a branch around them made it wait for everything
+        // in flight, the prefetch issued this level included)
         const int64_t b = base >= 0 ? base : 0;
+        const int nc = (base >= 0 && !(ring_probe & 1)) ? (int)(L * 64 * 4) : 0;
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void *)(x.col + b), (short)0, nc, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void *)(x.val + b), (short)0, 2 * nc, 0x00020000);
 #pragma unroll
         for (int u = 0; u <= P; ++u) {
-            const int64_t pos = b + (u < L ? u : 0) * 64 + x.lane;
-            s.c[u] = __builtin_nontemporal_load(x.col + pos);
-            s.v[u] = __builtin_nontemporal_load(x.val + pos);
+            const int off = u * 64 + x.lane;
+            s.c[u] = __builtin_amdgcn_raw_buffer_load_b32(rc, off * 4, 0, 0);
+            s.v[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, off * 8, 0, 0));
         }
         return;
     }
@@ -1878,18 +1893,28 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
     if (R) ring_chunk(x, g);
     if (g + 2 >= x.gbase + 64) x.refill(g);
     sw2_issue<P, R>(x, g + 2, ahead);
-    if (cur.base >= 0) {
+    if (cur.base >= 0 && !(R && (ring_probe & 2))) {  // (probe bit 1: no compute, diagnostics)
         const int32_t h = cur.c[0];
         const int32_t len = W ? (int32_t)cur.L - 1 : (int32_t)((uint32_t)h >> SW_ROW_BITS);
         double acc = 0.0, d[P + 1];
         // every dependency read issued before the first is consumed (they are
         // independent; consuming in turn would serialise the LDS / L1 round trips)
+        if (R) {
+            // ring sweep: entries past the slice were range-checked to col 0 /
+            // value 0 and padding entries carry value 0 on a written position,
+            // so no masking: 0 * (a finite ring value) adds nothing
 #pragma unroll
-        for (int u = 1; u <= P; ++u) d[u] = sw2_dep<R>(x, u <= len ? cur.c[u] : 0);
+            for (int u = 1; u <= P; ++u) d[u] = sw2_dep<R>(x, cur.c[u]);
 #pragma unroll
-        for (int u = 1; u <= P; ++u) {
-            const double t = cur.v[u] * d[u];
-            acc += (u <= len) ? t : 0.0;
+            for (int u = 1; u <= P; ++u) acc += __dmul_rn(cur.v[u], d[u]);  // no FMA: the other sweeps' rounding
+        } else {
+#pragma unroll
+            for (int u = 1; u <= P; ++u) d[u] = sw2_dep<R>(x, u <= len ? cur.c[u] : 0);
+#pragma unroll
+            for (int u = 1; u <= P; ++u) {
+                const double t = cur.v[u] * d[u];
+                acc += (u <= len) ? t : 0.0;
+            }
         }
         for (int64_t k0 = P + 1; k0 < cur.L; k0 += 8) {  // lanes with more than P entries: chunks of 8
             int32_t cc[8];
@@ -2066,6 +2091,7 @@ void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, co
                                                                Ucoff, Ucg, Ucp, ordL, mapUL, ordU, Lfrp, Lfcol, Lfval,
                                                                Ufrp, Ufcol, Ufval, x, y, yL, yU);
 }
+void set_ring_probe(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(ring_probe), &v, sizeof(int)); }
 int ilu_ring_slots() { return RING_SLOTS; }
 int ilu_ring_chunk() { return RING_CHUNK; }
 
