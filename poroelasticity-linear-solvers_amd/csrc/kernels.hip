@@ -1637,28 +1637,32 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
     // a padding lane's entries (value 0) read the slice's first row: in the
     // ring sweep that position is in the LDS ring, never a global fallback
     const int32_t pad = posof ? posof[order[s_start[sl]]] : 0;
-    ocol[base + lane] = wide ? me : (i >= 0 ? me : SW_ROW_PAD) | (int32_t)(mine << SW_ROW_BITS);
-    oval[base + lane] = (upper && i >= 0) ? dinv[i] : 0.0;
     if (row_lo) {
         // ring sweep: only the row's near entries (position >= row_lo[i], in the
         // LDS ring when the row runs), dealt round robin over its lanes; the far
-        // ones are applied to the row's input when its chunk is loaded
+        // ones are applied to the row's input when its chunk is loaded.  Lane-
+        // major layout: entry k of this lane at base + lane * L + k.
         const int32_t lo = i >= 0 ? row_lo[i] : 0;
+        const int64_t lb = base + (int64_t)lane * L;
+        ocol[lb] = me;
+        oval[lb] = (upper && i >= 0) ? dinv[i] : 0.0;
         int64_t k = 1, m = 0;
         for (int64_t j = 0; j < len; ++j) {
             const int32_t pc = posof[ci[src + j]];
             if (pc < lo) continue;
             if (m++ % lpr != sub) continue;
-            ocol[base + k * 64 + lane] = pc;
-            oval[base + k * 64 + lane] = lu[src + j];
+            ocol[lb + k] = pc;
+            oval[lb + k] = lu[src + j];
             ++k;
         }
         for (; k < L; ++k) {
-            ocol[base + k * 64 + lane] = i >= 0 ? me : pad;
-            oval[base + k * 64 + lane] = 0.0;
+            ocol[lb + k] = i >= 0 ? me : pad;
+            oval[lb + k] = 0.0;
         }
         return;
     }
+    ocol[base + lane] = wide ? me : (i >= 0 ? me : SW_ROW_PAD) | (int32_t)(mine << SW_ROW_BITS);
+    oval[base + lane] = (upper && i >= 0) ? dinv[i] : 0.0;
     for (int64_t k = 1; k < L; ++k) {
         const int64_t j = (k - 1) * lpr + sub, pos = base + k * 64 + lane;
         ocol[pos] = j < len ? (posof ? posof[ci[src + j]] : (int32_t)(ci[src + j] - b0)) : (wide && i >= 0 ? me : pad);
@@ -1774,15 +1778,25 @@ __device__ __forceinline__ void sw2_issue(Sw2Ctx &x, int64_t g, Sw2Slot<P> &s) {
         // vmcnt bookkeeping exact -- using this slot two levels later waits for
         // its own loads only (a branch around them made it wait for everything
         // in flight, the prefetch issued this level included)
+        static_assert((P + 1) % 8 == 0, "the ring sweep's slot is one lane's first P + 1 entries (a multiple of 8)");
         const int64_t b = base >= 0 ? base : 0;
         const int nc = (base >= 0 && !(ring_probe & 1)) ? (int)(L * 64 * 4) : 0;
         const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void *)(x.col + b), (short)0, nc, 0x00020000);
         const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void *)(x.val + b), (short)0, 2 * nc, 0x00020000);
+        const int off = x.lane * (int)L;  // lane-major, L a multiple of P + 1
 #pragma unroll
-        for (int u = 0; u <= P; ++u) {
-            const int off = u * 64 + x.lane;
-            s.c[u] = __builtin_amdgcn_raw_buffer_load_b32(rc, off * 4, 0, 0);
-            s.v[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, off * 8, 0, 0));
+        for (int q = 0; q < (P + 1) / 4; ++q) {
+            const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(rc, (off + 4 * q) * 4, 0, 0);
+            s.c[4 * q + 0] = (int32_t)c4[0];
+            s.c[4 * q + 1] = (int32_t)c4[1];
+            s.c[4 * q + 2] = (int32_t)c4[2];
+            s.c[4 * q + 3] = (int32_t)c4[3];
+        }
+#pragma unroll
+        for (int q = 0; q < (P + 1) / 2; ++q) {
+            const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rv, (off + 2 * q) * 8, 0, 0);
+            s.v[2 * q + 0] = __builtin_bit_cast(double, ((uint64_t)v4[1] << 32) | v4[0]);
+            s.v[2 * q + 1] = __builtin_bit_cast(double, ((uint64_t)v4[3] << 32) | v4[2]);
         }
         return;
     }
@@ -1822,6 +1836,14 @@ __device__ __forceinline__ double dpp_d(double v) {
     return __hiloint2double(hi, lo);
 }
 
+// index of entry k of a lane's stream: [k][lane] (LDS / y-resident sweeps) or,
+// in the ring sweep, lane-major [lane][k] with L (a multiple of 8) entries per
+// lane, so a slot's first 8 columns / values are 2 / 4 16-byte loads
+template <bool R>
+__device__ __forceinline__ int64_t sw2_at(int64_t base, int64_t L, int lane, int64_t k) {
+    return R ? base + (int64_t)lane * L + k : base + k * 64 + lane;
+}
+
 // LPR = 0: lanes per row chosen per slice (ring sweep), 1 << l2
 template <int LPR, bool W, bool R>
 __device__ __forceinline__ void sw2_finish(const Sw2Ctx &x, int32_t h, double dv, double acc, int l2 = 0) {
@@ -1851,12 +1873,12 @@ __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
     const int64_t enc = x.sptr[sl];
     const int64_t base = R ? (enc & ~(int64_t)63) : enc;
     const int64_t L = ((R ? (x.sptr[sl + 1] & ~(int64_t)63) : x.sptr[sl + 1]) - base) >> 6;
-    const int32_t h = x.col[base + x.lane];
-    const double dv = x.val[base + x.lane];
+    const int32_t h = x.col[sw2_at<R>(base, L, x.lane, 0)];
+    const double dv = x.val[sw2_at<R>(base, L, x.lane, 0)];
     const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
     double acc = 0.0;
     for (int64_t k = 1; k < L; ++k) {
-        const int64_t pos = base + k * 64 + x.lane;
+        const int64_t pos = sw2_at<R>(base, L, x.lane, k);
         const int32_t cc = x.col[pos];
         const double vv = x.val[pos];
         if (W || k <= len) acc += vv * sw2_dep<R>(x, cc);
@@ -1922,8 +1944,8 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int64_t k = k0 + u < cur.L ? k0 + u : cur.L - 1;
-                cc[u] = __builtin_nontemporal_load(x.col + cur.base + k * 64 + x.lane);
-                vv[u] = __builtin_nontemporal_load(x.val + cur.base + k * 64 + x.lane);
+                cc[u] = __builtin_nontemporal_load(x.col + sw2_at<R>(cur.base, cur.L, x.lane, k));
+                vv[u] = __builtin_nontemporal_load(x.val + sw2_at<R>(cur.base, cur.L, x.lane, k));
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -1984,6 +2006,10 @@ __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int
 }
 
 static constexpr int SW_P = 7;  // factor entries per lane kept in registers per pipeline slot
+// the ring sweep's slot and workgroup (measured: 512 threads with 15-entry
+// slots, which hold the wider N=20 levels without in-level reloads, were
+// slower at both N=12 (93 vs 138 it/s) and N=20 (16.6 vs 23.2))
+static constexpr int RING_P = 7, RING_TPB = 1024;
 
 // GMEM: the block solution lives in y itself (global memory) instead of LDS --
 // blocks longer than the LDS holds, with the wide slice headers (W).  All waves of the workgroup share the CU's
@@ -2044,7 +2070,7 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
 // this workgroup: workgroup-scope coherence as in the y-resident sweep), and
 // those "far" dependencies are known at setup: they are taken out of the
 // factor streams and subtracted from the row's input when its chunk loads.
-__global__ __launch_bounds__(1024) void k_ilu_blocks_ring(
+__global__ __launch_bounds__(RING_TPB) void k_ilu_blocks_ring(
     int64_t n, int64_t nblocks, const int64_t *__restrict__ Lgoff, const int64_t *__restrict__ Lgslice,
     const int64_t *__restrict__ Lsptr, const int32_t *__restrict__ Lcol, const double *__restrict__ Lval,
     const int32_t *__restrict__ Llpr, const int64_t *__restrict__ Ugoff, const int64_t *__restrict__ Ugslice,
@@ -2061,11 +2087,11 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_ring(
     const int64_t b0 = blk * q + (blk < r ? blk : r);
     const int64_t len = q + (blk < r ? 1 : 0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    sweep_block<SW_P, true, true>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol,
+    sweep_block<RING_P, true, true>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol,
                                   Lval, nullptr, ring, yL + b0, b0, Lcoff[blk], Lcoff[blk + 1],
                                   RingIn{Lcg, Lcp, ordL, x, Lfrp, Lfcol, Lfval});
     __syncthreads();
-    sweep_block<SW_P, true, true>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol,
+    sweep_block<RING_P, true, true>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol,
                                   Uval, nullptr, ring, yU + b0, b0, Ucoff[blk], Ucoff[blk + 1],
                                   RingIn{Ucg, Ucp, mapUL, yL, Ufrp, Ufcol, Ufval});
     __syncthreads();
@@ -2086,13 +2112,14 @@ void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, co
         (void)hipFuncSetAttribute((const void *)k_ilu_blocks_ring, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         configured = true;
     }
-    k_ilu_blocks_ring<<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
+    k_ilu_blocks_ring<<<(unsigned)nblocks, RING_TPB, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
                                                                Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, Lcoff, Lcg, Lcp,
                                                                Ucoff, Ucg, Ucp, ordL, mapUL, ordU, Lfrp, Lfcol, Lfval,
                                                                Ufrp, Ufcol, Ufval, x, y, yL, yU);
 }
 void set_ring_probe(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(ring_probe), &v, sizeof(int)); }
 int ilu_ring_slots() { return RING_SLOTS; }
+int ilu_ring_lane_entries() { return RING_P; }
 int ilu_ring_chunk() { return RING_CHUNK; }
 
 int ilu_lds_max_rows() { return 163840 / 8; }

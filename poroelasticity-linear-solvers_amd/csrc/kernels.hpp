@@ -181,6 +181,7 @@ int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in r
 // block, cg first level, cp [start, end) positions), level orders ordL / ordU
 // (position -> row), mapUL (U position -> yL index), scratch yL / yU (n each).
 int ilu_ring_slots();
+int ilu_ring_lane_entries();  // factor entries per lane per pipeline slot of the ring sweep
 void set_ring_probe(int v);  // diagnostics only (pls.ring_probe)
 int ilu_ring_chunk();
 void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,

@@ -684,19 +684,21 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
             for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {
                 gsl[g] = (int64_t)s_start.size();
                 for (int64_t r0 = grp[g]; r0 < grp[g + 1];) {
+                    const int WR = ilu_ring_lane_entries();
                     int ls = force_lpr ? force_lpr : 1;  // pls.sweep_lpr pins it
                     int64_t r1 = 0, mxs = 0;
                     for (;;) {
                         r1 = std::min(grp[g + 1], r0 + 64 / ls);
                         mxs = 0;
                         for (int64_t r = r0; r < r1; ++r) mxs = std::max(mxs, rlen(order[r]));
-                        if ((mxs + ls - 1) / ls <= W || ls >= 32 || force_lpr) break;
+                        if ((mxs + ls - 1) / ls <= WR || ls >= 32 || force_lpr) break;
                         ls *= 2;
                     }
                     s_start.push_back((int32_t)r0);
                     s_n.push_back((int32_t)(r1 - r0));
                     s_lpr.push_back(ls);
-                    sptr.push_back(sptr.back() + 64 * ((mxs + ls - 1) / ls + 1));
+                    // lane-major entries, a multiple of the slot (WR + 1) per lane (header included)
+                    sptr.push_back(sptr.back() + 64 * ((((mxs + ls - 1) / ls + 1) + WR) / (WR + 1) * (WR + 1)));
                     lpr[b] = std::max(lpr[b], ls);
                     r0 = r1;
                 }
