@@ -513,6 +513,7 @@ struct Handle {
         if (ctx.d16_sigma < 0 || ctx.d16_sigma % 64) throw Error("pls.d16_sigma must be a multiple of 64 (0: off)");
         ctx.d16_sigma_pad = opt.num("pls.d16_sigma_pad", 0.15);
         ctx.d16_sorted_lpr = (int)opt.integer("pls.d16_sorted_lpr", 2);
+        ctx.spmv_b3 = opt.flag("pls.spmv_b3", false);
         if (ctx.d16_sorted_lpr != 1 && ctx.d16_sorted_lpr != 2 && ctx.d16_sorted_lpr != 4 && ctx.d16_sorted_lpr != 8 &&
             ctx.d16_sorted_lpr != 16)
             throw Error("pls.d16_sorted_lpr must be 1, 2, 4, 8 or 16");

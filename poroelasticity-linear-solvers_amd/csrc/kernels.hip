@@ -1458,6 +1458,135 @@ void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const 
     else d16_unrolled<4>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rowmap);
 }
 
+// ============================================================ SELL/B3 ======
+// Row triples of FE vector fields: the 3 components of a P2 node have the same
+// sparsity pattern, so a triple shares one column list.  B3_LPT lanes per
+// triple (entry j of the triple's list on lane j % B3_LPT), slices of 64 /
+// B3_LPT triples (sorted by length inside windows, tmap[position] = the
+// triple's first row); per lane entry kk one column (one x gather serves 3
+// rows) and 3 values:  col[base + kk * 64 + lane],
+// val[3 * base + (3 kk + r) * 64 + lane].  The lanes' partial sums of a row
+// combine by DPP (quad_perm xor 1, xor 2).
+constexpr int B3_LPT = 4;
+
+// flag[r] = 1 when rows r, r + 1, r + 2 have the same column list
+__global__ __launch_bounds__(TPB) void k_triple_flags(int64_t n, const int64_t *rp, const int32_t *ci, uint8_t *flag) {
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (r >= n) return;
+    uint8_t f = 0;
+    if (r + 2 < n) {
+        const int64_t s0 = rp[r], len = rp[r + 1] - s0;
+        if (len > 0 && rp[r + 2] - rp[r + 1] == len && rp[r + 3] - rp[r + 2] == len) {
+            const int64_t s1 = rp[r + 1], s2 = rp[r + 2];
+            f = 1;
+            for (int64_t k = 0; k < len && f; ++k) f = (ci[s0 + k] == ci[s1 + k] && ci[s0 + k] == ci[s2 + k]) ? 1 : 0;
+        }
+    }
+    flag[r] = f;
+}
+void launch_triple_flags(int64_t n, const int64_t *rp, const int32_t *ci, uint8_t *flag, hipStream_t st) {
+    if (n > 0) k_triple_flags<<<grid_for(n, TPB), TPB, 0, st>>>(n, rp, ci, flag);
+}
+int b3_lanes_per_triple() { return B3_LPT; }
+
+__global__ __launch_bounds__(TPB) void k_b3_fill(int64_t nslices, int64_t ntrip, const int64_t *bptr,
+                                                 const int32_t *tmap, const int64_t *rp, const int32_t *ci,
+                                                 const double *val, int32_t *bcol, double *bval) {
+    const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63, sub = lane % B3_LPT;
+    if (sl >= nslices) return;
+    const int64_t base = bptr[sl], L = (bptr[sl + 1] - base) >> 6;
+    const int64_t pos = sl * (64 / B3_LPT) + lane / B3_LPT;
+    const int64_t h = pos < ntrip ? tmap[pos] : -1;
+    const int64_t s0 = h >= 0 ? rp[h] : 0, len = h >= 0 ? rp[h + 1] - s0 : 0;
+    const int32_t c0 = len > 0 ? ci[s0] : 0;
+    for (int64_t kk = 0; kk < L; ++kk) {
+        const int64_t k = kk * B3_LPT + sub;
+        const bool in = k < len;
+        bcol[base + kk * 64 + lane] = in ? ci[s0 + k] : c0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int64_t sj = h >= 0 ? rp[h + j] : 0;
+            bval[3 * base + (3 * kk + j) * 64 + lane] = in ? val[sj + k] : 0.0;
+        }
+    }
+}
+
+void launch_b3_fill(int64_t nslices, int64_t ntrip, const int64_t *bptr, const int32_t *tmap, const int64_t *rp,
+                    const int32_t *ci, const double *val, int32_t *bcol, double *bval, hipStream_t st) {
+    if (nslices > 0)
+        k_b3_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, ntrip, bptr, tmap, rp, ci, val, bcol, bval);
+}
+
+__device__ __forceinline__ double b3_dpp(double v, int ctrl_xor) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    if (ctrl_xor == 1)
+        return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, 0xB1, 0xF, 0xF, false),
+                                __builtin_amdgcn_update_dpp(0, lo, 0xB1, 0xF, 0xF, false));
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, 0x4E, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(0, lo, 0x4E, 0xF, 0xF, false));
+}
+
+template <int TAG>
+__global__ __launch_bounds__(TPB) void k_b3_spmv(int64_t nslices, int64_t ntrip, const int64_t *__restrict__ bptr,
+                                                 const int32_t *__restrict__ tmap, const int32_t *__restrict__ bcol,
+                                                 const double *__restrict__ bval, const double *__restrict__ x,
+                                                 double *__restrict__ y, double alpha, double beta,
+                                                 const double *__restrict__ z) {
+    const int64_t sl = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (TPB / 64) + (threadIdx.x >> 6)));
+    if (sl >= nslices) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t base = bptr[sl], L = (bptr[sl + 1] - base) >> 6;
+    const int32_t *cp = bcol + base + lane;
+    const double *vp = bval + 3 * base + lane;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    int64_t k = 0;
+    for (; k + 4 <= L; k += 4) {  // 4 entries per lane in flight
+        int32_t c[4];
+        double v[4][3], xv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = __builtin_nontemporal_load(cp + (k + u) * 64);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) v[u][j] = __builtin_nontemporal_load(vp + (3 * (k + u) + j) * 64);
+            xv[u] = x[(uint32_t)c[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a0 += v[u][0] * xv[u];
+            a1 += v[u][1] * xv[u];
+            a2 += v[u][2] * xv[u];
+        }
+    }
+    for (; k < L; ++k) {
+        const double xv = x[(uint32_t)cp[k * 64]];
+        a0 += vp[(3 * k) * 64] * xv;
+        a1 += vp[(3 * k + 1) * 64] * xv;
+        a2 += vp[(3 * k + 2) * 64] * xv;
+    }
+    static_assert(B3_LPT == 4, "two DPP steps combine the lanes of a triple");
+    a0 += b3_dpp(a0, 1); a1 += b3_dpp(a1, 1); a2 += b3_dpp(a2, 1);
+    a0 += b3_dpp(a0, 2); a1 += b3_dpp(a1, 2); a2 += b3_dpp(a2, 2);
+    const int64_t pos = sl * (64 / B3_LPT) + lane / B3_LPT;
+    if (pos >= ntrip || (lane % B3_LPT) >= 3) return;
+    // lanes 0, 1, 2 of a triple write its rows 0, 1, 2
+    const int j = lane % B3_LPT;
+    const int64_t row = tmap[pos] + j;
+    const double acc = j == 0 ? a0 : j == 1 ? a1 : a2;
+    double r = alpha * acc;
+    if (beta != 0.0) r += beta * z[row];
+    y[row] = r;
+}
+void launch_b3_spmv(int64_t nslices, int64_t ntrip, const int64_t *bptr, const int32_t *tmap, const int32_t *bcol,
+                    const double *bval, const double *x, double *y, double alpha, double beta, const double *z,
+                    int tag, hipStream_t st) {
+    if (nslices <= 0) return;
+    const unsigned g = grid_for(nslices, TPB / 64);
+    if (tag) k_b3_spmv<1><<<g, TPB, 0, st>>>(nslices, ntrip, bptr, tmap, bcol, bval, x, y, alpha, beta, z);
+    else k_b3_spmv<0><<<g, TPB, 0, st>>>(nslices, ntrip, bptr, tmap, bcol, bval, x, y, alpha, beta, z);
+}
+
 // rows whose last (largest) column is a ghost column (rows sorted): flag 1
 __global__ __launch_bounds__(TPB) void k_row_has_ghost(int64_t nrows, const int64_t *rp, const int32_t *ci,
                                                        int64_t nlocal, uint8_t *flag) {

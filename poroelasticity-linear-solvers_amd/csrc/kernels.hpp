@@ -147,6 +147,14 @@ void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const 
                      int unroll /* 8-entry groups per lane in flight: 1, 2 or 4 */, hipStream_t st,
                      const int32_t *slist = nullptr /* nslices entries: the slices to process */,
                      const int32_t *rowmap = nullptr /* slice position -> row (SELL-C-sigma) */);
+// SELL/B3: row triples sharing one column list (FE vector fields), see kernels.hip
+void launch_triple_flags(int64_t n, const int64_t *rp, const int32_t *ci, uint8_t *flag, hipStream_t st);
+int b3_lanes_per_triple();
+void launch_b3_fill(int64_t nslices, int64_t ntrip, const int64_t *bptr, const int32_t *tmap, const int64_t *rp,
+                    const int32_t *ci, const double *val, int32_t *bcol, double *bval, hipStream_t st);
+void launch_b3_spmv(int64_t nslices, int64_t ntrip, const int64_t *bptr, const int32_t *tmap, const int32_t *bcol,
+                    const double *bval, const double *x, double *y, double alpha, double beta, const double *z,
+                    int tag, hipStream_t st);
 // D16 SpMV workgroup -> slice order: 0 round-robin over the 8 XCDs (default), 1 XCD-contiguous ranges
 void set_d16_xcd(int on);
 // flag[r] = 1 when row r (sorted columns) references a ghost column (>= nlocal)

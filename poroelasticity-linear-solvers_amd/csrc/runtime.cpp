@@ -151,7 +151,7 @@ static int64_t d16_plan_stored(const std::vector<int64_t> &rp, const std::vector
 }
 
 static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<int32_t> &slpr,
-                     std::vector<int32_t> &rowmap, Ctx &c) {
+                     std::vector<int32_t> &rowmap, Ctx &c, const std::vector<int32_t> *subset = nullptr) {
     const int64_t n = M.nrows;
     std::vector<int64_t> rp(n + 1);
     std::vector<int32_t> c0(n);
@@ -163,6 +163,29 @@ static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<
     sfirst.clear();
     slpr.clear();
     rowmap.clear();
+    if (subset) {
+        // the rows left to the D16 part by the B3 layout: always the sorted plan
+        std::vector<int32_t> rm(*subset);
+        const int64_t m = (int64_t)rm.size();
+        for (int64_t w = 0; w < m; w += std::max(c.d16_sigma, 64)) {
+            const int64_t e = std::min<int64_t>(m, w + std::max(c.d16_sigma, 64));
+            std::stable_sort(rm.begin() + w, rm.begin() + e,
+                             [&](int32_t a, int32_t b) { return rp[a + 1] - rp[a] > rp[b + 1] - rp[b]; });
+        }
+        for (int64_t p = 0; p < m; p += 64) {
+            const int64_t e = std::min<int64_t>(m, p + 64);
+            int64_t tot = 0;
+            for (int64_t q = p; q < e; ++q) tot += rp[rm[q] + 1] - rp[rm[q]];
+            const int l = (c.d16_sorted_lpr > 1 && tot >= 32 * (e - p)) ? c.d16_sorted_lpr : 1;
+            for (int64_t q = p; q < e; q += 64 / l) {
+                sfirst.push_back(q);
+                slpr.push_back(l);
+            }
+        }
+        sfirst.push_back(m);
+        rowmap.swap(rm);
+        return;
+    }
     for (int64_t r = 0; r < n; r += 64) {
         bool wide = false;
         if (r + 64 <= n && c0[r] >= 0 && c0[r + 63] >= 0) {
@@ -230,14 +253,77 @@ static void d16_plan(const DevCSR &M, std::vector<int64_t> &sfirst, std::vector<
     rowmap.swap(rm);
 }
 
+// SELL/B3: row triples with one column list (the components of a P2 node in
+// an FE vector field).  Used when such triples hold >= half the entries; the
+// other rows go to a D16 part (returned in `singles`).  Triples are sorted by
+// length inside windows of 512 (SELL-C-sigma); slices of 64 / b3_lanes_per_triple() triples.
+static bool build_b3(const DevCSR &M, DevSELL &S, std::vector<int32_t> &singles, Ctx &c) {
+    const int64_t n = M.nrows;
+    if (!c.spmv_b3 || M.halo || n < 192) return false;
+    DBuf<uint8_t> df(n);
+    launch_triple_flags(n, M.rp.p, M.ci.p, df.p, c.st);
+    std::vector<uint8_t> f(n);
+    std::vector<int64_t> rp(n + 1);
+    HIPCHK(hipMemcpyAsync(f.data(), df.p, n, hipMemcpyDeviceToHost, c.st));
+    HIPCHK(hipMemcpyAsync(rp.data(), M.rp.p, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost, c.st));
+    c.sync();
+    std::vector<int32_t> heads;
+    singles.clear();
+    int64_t tnnz = 0;
+    for (int64_t r = 0; r < n;) {
+        if (f[r]) {
+            heads.push_back((int32_t)r);
+            tnnz += 3 * (rp[r + 1] - rp[r]);
+            r += 3;
+        } else {
+            singles.push_back((int32_t)r);
+            r += 1;
+        }
+    }
+    if (2 * tnnz < M.nnz) return false;
+    const int64_t nt = (int64_t)heads.size(), W = 512;
+    for (int64_t w = 0; w < nt; w += W) {
+        const int64_t e = std::min(nt, w + W);
+        std::stable_sort(heads.begin() + w, heads.begin() + e,
+                         [&](int32_t a, int32_t b) { return rp[a + 1] - rp[a] > rp[b + 1] - rp[b]; });
+    }
+    const int64_t lpt = b3_lanes_per_triple(), per = 64 / lpt, ns = (nt + per - 1) / per;
+    std::vector<int64_t> bptr(ns + 1, 0);
+    for (int64_t sl = 0; sl < ns; ++sl) {
+        int64_t L = 0;
+        for (int64_t t = sl * per; t < std::min(nt, sl * per + per); ++t)
+            L = std::max<int64_t>(L, (rp[heads[t] + 1] - rp[heads[t]] + lpt - 1) / lpt);
+        bptr[sl + 1] = bptr[sl] + 64 * L;
+    }
+    S.b3_nslices = ns;
+    S.b3_ntrip = nt;
+    S.b3_stored = bptr[ns];
+    S.b3ptr.alloc(ns + 1);
+    S.b3map.alloc(std::max<int64_t>(nt, 1));
+    S.b3col.alloc(std::max<int64_t>(S.b3_stored, 1));
+    S.b3val.alloc(std::max<int64_t>(3 * S.b3_stored, 1));
+    HIPCHK(hipMemcpyAsync(S.b3ptr.p, bptr.data(), sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(S.b3map.p, heads.data(), sizeof(int32_t) * nt, hipMemcpyHostToDevice, c.st));
+    launch_b3_fill(ns, nt, S.b3ptr.p, S.b3map.p, M.rp.p, M.ci.p, M.val.p, S.b3col.p, S.b3val.p, c.st);
+    HIPCHK(hipGetLastError());
+    c.sync();
+    return true;
+}
+
 void build_sell(DevCSR &M, Ctx &c) {
     if (M.sell || M.nrows == 0) return;
     auto S = std::make_unique<DevSELL>();
     if (c.sell_d16 && M.nnz > 0) {
         std::vector<int64_t> sf;
-        std::vector<int32_t> lp, rm;
-        d16_plan(M, sf, lp, rm, c);
+        std::vector<int32_t> lp, rm, singles;
+        const bool b3 = build_b3(M, *S, singles, c);
+        d16_plan(M, sf, lp, rm, c, b3 ? &singles : nullptr);
         const int64_t ns = (int64_t)lp.size();
+        if (ns == 0) {  // every row in a triple: the B3 part is the whole product
+            S->d16 = true;
+            M.sell = std::move(S);
+            return;
+        }
         S->sfirst.alloc(ns + 1);
         S->slpr.alloc(std::max<int64_t>(ns, 1));
         HIPCHK(hipMemcpyAsync(S->sfirst.p, sf.data(), sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, c.st));
@@ -275,6 +361,13 @@ void build_sell(DevCSR &M, Ctx &c) {
             c.sync();
             M.sell = std::move(S);
             if (M.halo) classify_halo_slices(M, c);
+            return;
+        }
+        if (b3) {  // the other rows do not fit D16: plain layouts for the whole matrix
+            const bool keep = c.spmv_b3;
+            c.spmv_b3 = false;
+            build_sell(M, c);
+            c.spmv_b3 = keep;
             return;
         }
         S = std::make_unique<DevSELL>();
@@ -363,6 +456,9 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
     }
     if (M.sell && M.sell->d16) {
         const DevSELL &S = *M.sell;
+        if (S.b3_nslices)
+            launch_b3_spmv(S.b3_nslices, S.b3_ntrip, S.b3ptr.p, S.b3map.p, S.b3col.p, S.b3val.p, x, y, alpha, beta, z,
+                           M.tag, c.st);
         launch_d16_spmv(M.nrows, S.nslices, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y, alpha,
                         beta, z, M.tag, ghost, nlocal, c.d16_unroll, c.st, nullptr,
                         S.nrows_mapped ? S.rowmap.p : nullptr);

@@ -73,6 +73,7 @@ struct Ctx {
     int d16_sigma = 1024;         // SELL-C-sigma window (rows sorted by length; 0: never) (pls.d16_sigma)
     double d16_sigma_pad = 0.15;  // ... used when the plain plan pads more than this fraction (pls.d16_sigma_pad)
     int d16_sorted_lpr = 2;       // lanes per row of sorted slices with 32+ entries per row (pls.d16_sorted_lpr)
+    bool spmv_b3 = false;         // row-triple layout for FE vector fields (pls.spmv_b3; measured slower)
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
@@ -102,14 +103,21 @@ struct DevSELL {
     // sigma rows (rowmap[position] = row); empty when rows keep their order
     DBuf<int32_t> rowmap;
     int64_t nrows_mapped = 0;
+    // SELL/B3 (FE vector fields): row triples with one shared column list, lane =
+    // triple; the D16 part above then holds only the other rows (through rowmap)
+    int64_t b3_nslices = 0, b3_ntrip = 0, b3_stored = 0;
+    DBuf<int64_t> b3ptr;
+    DBuf<int32_t> b3map, b3col;
+    DBuf<double> b3val;
     int nsegs = D16_SEG;      // D16 segment bases per lane: 4, or 8 when halo columns need them
     // distributed products: slices without / with ghost columns (the first
     // run while the halo exchange is in flight)
     DBuf<int32_t> s_in, s_halo;
     int64_t n_in = 0, n_halo = 0;
     int64_t bytes() const {  // bytes one product streams from the matrix
-        return d16 ? stored * 10 + nslices * (64 * 4 * nsegs + 20) + 8 + nrows_mapped * 4
-                   : stored * 12 + (nslices + 1) * 8;
+        return (d16 ? stored * 10 + nslices * (64 * 4 * nsegs + 20) + 8 + nrows_mapped * 4
+                    : stored * 12 + (nslices + 1) * 8) +
+               b3_stored * 28 + b3_ntrip * 4 + (b3_nslices + 1) * 8;
     }
 };
 

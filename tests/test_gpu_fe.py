@@ -280,7 +280,8 @@ def test_device_reproduces_fe_golden(gpu, name):
 
 @pytest.mark.parametrize("dim,N,ordering", [(3, 6, "field-major"), (3, 6, "interleaved"), (2, 16, "interleaved")])
 def test_spmv_sigma_layout_on_assembled(gpu, dim, N, ordering):
-    """SELL-C-sigma (rows sorted by length inside 1024-row windows, results
+    """SELL/B3 (opt-in pls.spmv_b3; row triples of the P2 vector fields share
+    one column list: one x gather serves 3 rows) and SELL-C-sigma (the default) (rows sorted by length inside 1024-row windows, results
     written through the row map): the FE matrices' mixed P2-vertex / P2-edge /
     P1 row lengths pad the plain SELL-64 plan by ~100 %.  Products of A and of
     the PC's coupling block against scipy (<= 1e-14 of |A||x|), the sorted plan
@@ -290,21 +291,29 @@ def test_spmv_sigma_layout_on_assembled(gpu, dim, N, ordering):
     s = F.assemble_swelling(dim, N, "diagonal", ordering=ordering)
     opts = dict(_db("ilu"))
     opts.update(params_to_options(dict(BASE, **{"pc type": "diagonal"})))
+    # pls.spmv_b3=1 (opt-in, measured slower): SELL/B3 row triples + a SELL-C-sigma
+    # D16 part; default: SELL-C-sigma D16 for every row; plain: neither
+    hb = Handle.from_csr(s.A, s.P, None, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, dict(opts, **{"pls.spmv_b3": "1"}))
     hs = Handle.from_csr(s.A, s.P, None, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
     hp = Handle.from_csr(s.A, s.P, None, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, dict(opts, **{"pls.d16_sigma": "0"}))
     rng = np.random.default_rng(3)
     x = rng.standard_normal(s.A.shape[0])
-    ys, yp = hs.matmult(x), hp.matmult(x)
+    yb, ys, yp = hb.matmult(x), hs.matmult(x), hp.matmult(x)
     ref = s.A @ x
     scale = abs(s.A) @ np.abs(x)
-    assert np.max(np.abs(ys - ref) / scale) <= 1e-14
+    for y in (yb, ys, yp):
+        assert np.max(np.abs(y - ref) / scale) <= 1e-14
     assert np.max(np.abs(ys - yp) / scale) <= 1e-14
-    (d16s, bs), (d16p, bp) = hs.spmv_layout(), hp.spmv_layout()
+    (d16b, bb), (d16s, bs), (d16p, bp) = hb.spmv_layout(), hs.spmv_layout(), hp.spmv_layout()
     assert d16s and d16p and bs < 0.9 * bp, (bs, bp)
-    # the PC's P_fp,s product (t = x_fp - P_fp,s y_s) through the same layout: PC applies agree
-    assert np.max(np.abs(hs.pc_apply(x) - hp.pc_apply(x))) <= 1e-12 * np.max(np.abs(hp.pc_apply(x)))
-    hs.destroy()
-    hp.destroy()
+    if dim == 3:  # 3-D: most entries sit in P2 vector-field triples
+        assert bb < bs, (bb, bs)
+    # the PC's P_fp,s product (t = x_fp - P_fp,s y_s) through the same layouts: PC applies agree
+    yref = hp.pc_apply(x)
+    for h in (hb, hs):
+        assert np.max(np.abs(h.pc_apply(x) - yref)) <= 1e-12 * np.max(np.abs(yref))
+    for h in (hb, hs, hp):
+        h.destroy()
 
 
 @pytest.mark.parametrize("dim,N,blocks", [(3, 12, 1), (3, 8, 3), (2, 24, 1)])
