@@ -47,7 +47,7 @@ DELTA = 0.05
 RHS_SEED = 7  # the seed of the device-generated right-hand side (pls_synthetic_rhs_device)
 
 
-# reference petsc-options-inexact (BoomerAMG -> the device AMG stand-in,
+# reference petsc-options-inexact (BoomerAMG -> the device classical AMG,
 # MUMPS -> the device LU): CG on s/f/p, PREONLY on diff, Schur fieldsplit on fp
 INEXACT_DB = {
     "global_ksp_type": "gmres", "global_ksp_norm_type": "unpreconditioned",
@@ -63,6 +63,12 @@ INEXACT_DB = {
     "fp_fieldsplit_0_ksp_max_it": "10", "fp_fieldsplit_0_pc_type": "hypre",
     "fp_fieldsplit_1_ksp_type": "preonly", "fp_fieldsplit_1_pc_type": "lu",
 }
+# petsc-options-inexact's BoomerAMG settings (:16-24 and the other blocks)
+BOOMER = {"pc_hypre_boomeramg_P_max": "4", "pc_hypre_boomeramg_agg_nl": "1", "pc_hypre_boomeramg_agg_num_paths": "2",
+          "pc_hypre_boomeramg_coarsen_type": "HMIS", "pc_hypre_boomeramg_interp_type": "ext+i",
+          "pc_hypre_boomeramg_no_CF": "true"}
+for _pre in ("s_", "f_", "p_", "diff_", "fp_fieldsplit_0_"):
+    INEXACT_DB.update({_pre + k: v for k, v in BOOMER.items()})
 
 
 # BASELINE.json "configs": named presets (dim, N, option set); the default is
@@ -136,6 +142,8 @@ def solver_options(args):
         for pre in (("s_", "f_", "p_", "diff_") if three else ("s_",)):
             db[pre + "ksp_type"] = "preonly"
             db[pre + "pc_type"] = args.inner
+            if args.inner == "hypre":
+                db.update({pre + k: v for k, v in BOOMER.items()})
         if not three:
             db.update({"fp_ksp_type": "preonly", "fp_pc_type": "bjacobi", "fp_pc_bjacobi_blocks": str(args.blocks_fp)})
             params["inner pc type"] = "bjacobi"

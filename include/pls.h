@@ -198,6 +198,34 @@ int pls_export_matrix(pls_handle *h, int which, int64_t *nrows, int64_t *nnz,
 /* Export the field-major permutation: perm[internal] = caller index.         */
 int pls_get_permutation(pls_handle *h, int64_t *perm);
 
+/* Host-only query of the classical AMG behind -pc_type hypre (no device
+ * needed; test and inspection entry): level `level` of the hierarchy that
+ * options' <prefix>pc_hypre_boomeramg_* build from A (petsc-options-inexact:
+ * 16-24): n, nc, nnz of P (of the coarsest operator when level ==
+ * *nlevels - 1); when non-NULL, cf[n] (1 C / -1 F) and P's CSR arrays
+ * (p_rp[n + 1], p_ci[nnz], p_v[nnz]).                                        */
+int pls_boomeramg_host_level(const pls_csr *A, const char *options, const char *prefix, int64_t level,
+                             int64_t *nlevels, int64_t *n, int64_t *nc, int64_t *p_nnz, int8_t *cf, int64_t *p_rp,
+                             int32_t *p_ci, double *p_v);
+
+/* Standalone inner Anderson mixing (lib/AndersonAcceleration.py:8-78): the
+ * object a caller's own fixed-point loop holds, as the reference's
+ * PreconditionerCC holds one per inner block (lib/Preconditioner.py:248-249).
+ *   pls_anderson_create   AndersonAcceleration(order), vectors of length n
+ *                         (AndersonAcceleration.py:8-17)
+ *   pls_anderson_next     get_next_vector(gk) (AndersonAcceleration.py:19-78):
+ *                         d_gk (device, length n) is replaced by the mixed
+ *                         iterate x_k, in place as the reference's
+ *                         self.xk.copy(gk); F / X histories persist across
+ *                         calls, the least squares is Householder QR (TSQR)
+ *   pls_anderson_destroy  frees the object and its stream.
+ * Single-rank: the reference's scatter-to-rank-0 least squares over MPI is
+ * the handle's inner accel path (option pls.inner_accel_order) at G > 1.    */
+typedef struct pls_anderson pls_anderson;
+int pls_anderson_create(int32_t order, int64_t n, pls_anderson **out);
+int pls_anderson_next(pls_anderson *a, double *d_gk);
+int pls_anderson_destroy(pls_anderson *a);
+
 /* Kernel micro-entry points used by bench.py's roofline leg (device ptrs):
  * y = A x on the handle's A, repeated `reps` times; returns the mean device
  * time per launch in seconds measured with HIP events on the solver stream. */

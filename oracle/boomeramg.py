@@ -1,0 +1,427 @@
+"""Classical AMG as BoomerAMG is configured by the reference (TEST INFRASTRUCTURE ONLY,
+see oracle/__init__.py).
+
+``-X_pc_type hypre -X_pc_hypre_type boomeramg`` with the reference's
+``petsc-options-inexact:16-24`` (and the f_ / p_ / diff_ / fp_fieldsplit_0_
+blocks, :32-40, :48-56, :63-71, :92-100): ``coarsen_type HMIS``,
+``interp_type ext+i``, ``P_max 4``, ``agg_nl 1``, ``agg_num_paths 2``,
+``grid_sweeps_all 1``, ``no_CF``.  hypre itself is absent from this image and
+from the reference tree: this module restates the published
+algorithms those options select (Ruge & Stueben 1987; De Sterck, Yang & Heys
+2006 -- HMIS; De Sterck, Falgout, Nolting & Yang 2008 -- extended+i; Stueben
+2001, App. A -- aggressive coarsening and multipass interpolation) with
+PETSc's PCHYPRE defaults for everything the options leave open.  It is the
+exact specification libpls's device AMG follows (csrc/boomeramg.cpp builds the
+same hierarchy bit for bit: every sum below runs in the order written, no
+contraction) and the oracle its GPU tests compare with.  Parity against hypre
+is unpinned.
+
+Setup, level l (A_l square CSR, sorted columns), single rank:
+* strength (hypre CreateS, theta = strong_threshold 0.25, mu = max_row_sum
+  0.9): row i with diagonal d and off-diagonal entries a_ij; no off-diagonals,
+  or mu < 1 and |sum_j a_ij| > mu |d| (row sum incl. d, storage order): no
+  strong dependencies; else d >= 0: s = min_j a_ij, j strong iff a_ij < theta s;
+  d < 0: s = max_j a_ij, j strong iff a_ij > theta s.  S_i = strong j
+  (ascending), S^T its transpose (influences).
+* HMIS on one rank = the Ruge-Stueben first pass (hypre's HMIS runs RS pass 1
+  inside each process, then PMIS only across process boundaries):
+  lambda_i = |S^T_i|; points with S_i empty and lambda_i = 0 are F; then in
+  ascending order every undecided point with lambda_i = 0 becomes F; then
+  repeatedly the undecided point of largest lambda (ties: smallest index)
+  becomes C, its undecided influencees j in S^T_i become F, and a point j that
+  becomes F raises lambda_k by 1 for its undecided dependencies k in S_j (in
+  order); the undecided dependencies k in S_i of the new C point lose 1, and
+  one reaching 0 becomes F.  Left-over undecided points are F.
+* aggressive coarsening on the first agg_nl levels (agg_num_paths p): HMIS on
+  S gives C1; S2 on C1: j in C1 (j != i) is a strong dependency of i in C1
+  iff [j in S_i] + #{k in S_i : j in S_k} >= p; HMIS on S2 (C1's points in
+  ascending order) gives C.
+* interpolation: C points inject (P_i = e_c(i), coarse points numbered in
+  ascending order).  Aggressive levels: multipass (Stueben A.4.3): pass 0 = C;
+  pass p = the undecided F points with a strong dependency assigned in an
+  earlier pass (decided from the passes before p); Q_i = those
+  dependencies (ascending); with a^- = min(a, 0), a^+ = max(a, 0) summed over
+  the row's off-diagonals (storage order) and over Q_i: a negative (positive)
+  Q-sum of 0 adds the row's negative (positive) sum to d~ = a_ii, else
+  alpha = row sum / Q sum for that sign; P_i = sum_{k in Q_i} (-alpha_sign(a_ik)
+  a_ik / d~) P_k (Q order, then P_k's storage order); points never reached
+  interpolate nothing.  Other levels: extended+i: C^_i = strong C neighbours
+  plus the strong C neighbours of strong F neighbours; w_j starts at a_ij for
+  j in C^_i (row storage order; weak neighbours in C^_i included) and d~ = a_ii
+  plus every other weak a_in; each strong F neighbour k (ascending) spreads
+  a_ik over bar(a_kl) = a_kl if a_kl a_kk < 0 else 0: D = sum over k's row
+  (storage order) of bar(a_kl) for l in C^_i or l = i; D = 0 adds a_ik to
+  d~, else w_l += a_ik bar(a_kl) / D for l in C^_i and d~ += a_ik bar(a_ki) / D;
+  P_ij = -w_j / d~.  Then P_max truncation: rows with more than P_max entries
+  keep the P_max largest |P_ij| (ties: smaller j), rescaled by (row sum) /
+  (kept sum) (both in column order) when the kept sum is nonzero.  Exact
+  zeros are dropped.
+* R = P^T, A_{l+1} = R (A P) (scipy's csr_matmat order);
+* levels stop when n <= 9 (hypre's max_coarse_size) or max_levels (25) is
+  reached, or when coarsening selects no or every point; the coarsest level is
+  solved exactly (hypre's relax type 9, Gaussian elimination).
+V-cycle (one PC application, x = 0): per level, grid_sweeps_all sweeps of
+hybrid symmetric Gauss-Seidel (PETSc's PCHYPRE default relax type, hypre 6;
+one rank: forward then backward GS), lexicographic with no_CF, else over the
+C points then the F points going down and F then C going up (hypre's CF
+relaxation order); restricted to a point set I, forward is
+x_I += (D + L)_II^-1 (b - A x)_I and backward x_I += (D + U)_II^-1 (b - A x)_I;
+r = b - A x; recurse on R r from 0; x += P e; post-smooth.
+"""
+from __future__ import annotations
+
+import heapq
+
+import numpy as np
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+from .options import get as opt
+
+_SUPPORTED_COARSEN = ("HMIS",)
+_SUPPORTED_INTERP = ("ext+i",)
+
+
+def _rows(A):
+    A = A.tocsr()
+    A.sort_indices()
+    return A, A.indptr, A.indices, A.data
+
+
+def strength(A, theta=0.25, max_row_sum=0.9):
+    """S as a list of int arrays (strong dependencies of each row, ascending)."""
+    A, rp, ci, v = _rows(A)
+    n = A.shape[0]
+    S = []
+    for i in range(n):
+        cols, vals = ci[rp[i]:rp[i + 1]], v[rp[i]:rp[i + 1]]
+        d = 0.0
+        rs = 0.0
+        off = []
+        for j, a in zip(cols.tolist(), vals.tolist()):
+            rs += a
+            if j == i:
+                d = a
+            else:
+                off.append((j, a))
+        if not off or (max_row_sum < 1.0 and abs(rs) > max_row_sum * abs(d)):
+            S.append(np.zeros(0, dtype=np.int64))
+            continue
+        if d >= 0.0:
+            s = min(a for _, a in off)
+            st = [j for j, a in off if a < theta * s]
+        else:
+            s = max(a for _, a in off)
+            st = [j for j, a in off if a > theta * s]
+        S.append(np.asarray(st, dtype=np.int64))
+    return S
+
+
+def transpose_lists(S, n):
+    T = [[] for _ in range(n)]
+    for i, row in enumerate(S):
+        for j in row.tolist():
+            T[j].append(i)
+    return [np.asarray(t, dtype=np.int64) for t in T]
+
+
+U, F, C = 0, -1, 1
+
+
+def rs_first_pass(S, n):
+    """C/F marker (1 / -1) of the Ruge-Stueben first pass (HMIS on one rank)."""
+    ST = transpose_lists(S, n)
+    lam = [len(t) for t in ST]
+    state = [U] * n
+    heap = []
+
+    def make_f(j):
+        state[j] = F
+        for k in S[j].tolist():
+            if state[k] == U:
+                lam[k] += 1
+                heapq.heappush(heap, (-lam[k], k))
+
+    for i in range(n):
+        if len(S[i]) == 0 and lam[i] == 0:
+            state[i] = F
+    for i in range(n):
+        if state[i] == U and lam[i] == 0:
+            make_f(i)
+    for i in range(n):
+        if state[i] == U:
+            heapq.heappush(heap, (-lam[i], i))
+    while heap:
+        nl, i = heapq.heappop(heap)
+        if state[i] != U or -nl != lam[i]:
+            continue
+        state[i] = C
+        for j in ST[i].tolist():
+            if state[j] == U:
+                make_f(j)
+        for k in S[i].tolist():
+            if state[k] == U:
+                lam[k] -= 1
+                if lam[k] == 0:
+                    make_f(k)
+                else:
+                    heapq.heappush(heap, (-lam[k], k))
+    return np.asarray([C if s == C else F for s in state], dtype=np.int64)
+
+
+def second_strength(S, cf, num_paths):
+    """S2 over the C points (local numbering, ascending original index)."""
+    cpts = np.flatnonzero(cf == C)
+    loc = -np.ones(len(cf), dtype=np.int64)
+    loc[cpts] = np.arange(len(cpts))
+    S2 = []
+    for i in cpts.tolist():
+        cnt = {}
+        for k in S[i].tolist():
+            if loc[k] >= 0 and k != i:
+                cnt[k] = cnt.get(k, 0) + 1
+        for k in S[i].tolist():
+            for j in S[k].tolist():
+                if loc[j] >= 0 and j != i:
+                    cnt[j] = cnt.get(j, 0) + 1
+        S2.append(np.asarray(sorted(loc[j] for j, c in cnt.items() if c >= num_paths), dtype=np.int64))
+    return S2, cpts
+
+
+def coarsen(S, n, aggressive, num_paths):
+    cf = rs_first_pass(S, n)
+    if aggressive:
+        S2, cpts = second_strength(S, cf, num_paths)
+        cf2 = rs_first_pass(S2, len(cpts))
+        cf = np.full(n, F, dtype=np.int64)
+        cf[cpts[cf2 == C]] = C
+    return cf
+
+
+def _csr_from_rows(rows, ncols):
+    rp, ci, v = [0], [], []
+    for row in rows:
+        for j in sorted(row):
+            if row[j] != 0.0:
+                ci.append(j)
+                v.append(row[j])
+        rp.append(len(ci))
+    return sp.csr_matrix((np.asarray(v, dtype=np.float64), np.asarray(ci, dtype=np.int64),
+                          np.asarray(rp, dtype=np.int64)), shape=(len(rows), ncols))
+
+
+def multipass_interp(A, S, cf):
+    A, rp, ci, v = _rows(A)
+    n = A.shape[0]
+    cidx = np.cumsum(cf == C) - 1
+    npass = np.where(cf == C, 0, -1)
+    order = []
+    p = 1
+    while True:
+        new = [i for i in range(n) if npass[i] < 0 and any(0 <= npass[k] < p for k in S[i].tolist())]
+        if not new:
+            break
+        for i in new:
+            npass[i] = p
+        order.append(new)
+        p += 1
+    rows = [dict() for _ in range(n)]
+    for i in np.flatnonzero(cf == C).tolist():
+        rows[i][int(cidx[i])] = 1.0
+    for p, pts in enumerate(order, start=1):
+        for i in pts:
+            Q = [k for k in S[i].tolist() if 0 <= npass[k] < p]
+            qs = set(Q)
+            d = 0.0
+            neg_all = pos_all = neg_q = pos_q = 0.0
+            aik = {}
+            for j, a in zip(ci[rp[i]:rp[i + 1]].tolist(), v[rp[i]:rp[i + 1]].tolist()):
+                if j == i:
+                    d = a
+                    continue
+                neg_all += min(a, 0.0)
+                pos_all += max(a, 0.0)
+                if j in qs:
+                    aik[j] = a
+            for k in Q:
+                a = aik.get(k, 0.0)
+                neg_q += min(a, 0.0)
+                pos_q += max(a, 0.0)
+            alpha = beta = 0.0
+            if neg_q == 0.0:
+                d += neg_all
+            else:
+                alpha = neg_all / neg_q
+            if pos_q == 0.0:
+                d += pos_all
+            else:
+                beta = pos_all / pos_q
+            row = {}
+            for k in Q:
+                a = aik.get(k, 0.0)
+                if a == 0.0:
+                    continue
+                w = -(alpha if a < 0.0 else beta) * a / d
+                for j, pv in rows[k].items():
+                    row[j] = row.get(j, 0.0) + w * pv
+            rows[i] = row
+    return _csr_from_rows(rows, int((cf == C).sum()))
+
+
+def ext_i_interp(A, S, cf):
+    A, rp, ci, v = _rows(A)
+    n = A.shape[0]
+    cidx = np.cumsum(cf == C) - 1
+    diag = np.zeros(n)
+    for i in range(n):
+        for j, a in zip(ci[rp[i]:rp[i + 1]].tolist(), v[rp[i]:rp[i + 1]].tolist()):
+            if j == i:
+                diag[i] = a
+    rows = []
+    for i in range(n):
+        if cf[i] == C:
+            rows.append({int(cidx[i]): 1.0})
+            continue
+        Si = S[i].tolist()
+        sset = set(Si)
+        chat = set(j for j in Si if cf[j] == C)
+        for k in Si:
+            if cf[k] == F:
+                chat.update(l for l in S[k].tolist() if cf[l] == C)
+        w = {}
+        dt = 0.0
+        for j, a in zip(ci[rp[i]:rp[i + 1]].tolist(), v[rp[i]:rp[i + 1]].tolist()):
+            if j == i:
+                dt += a
+            elif j in chat:
+                w[j] = w.get(j, 0.0) + a
+            elif j in sset:
+                continue
+            else:
+                dt += a
+        arow = dict(zip(ci[rp[i]:rp[i + 1]].tolist(), v[rp[i]:rp[i + 1]].tolist()))
+        for k in Si:
+            if cf[k] != F:
+                continue
+            a_ik = arow[k]
+            dk = diag[k]
+            kc, kv = ci[rp[k]:rp[k + 1]].tolist(), v[rp[k]:rp[k + 1]].tolist()
+            D = 0.0
+            for l, a in zip(kc, kv):
+                if (l in chat or l == i) and a * dk < 0.0:
+                    D += a
+            if D == 0.0:
+                dt += a_ik
+                continue
+            for l, a in zip(kc, kv):
+                if a * dk >= 0.0:
+                    continue
+                if l in chat:
+                    w[l] = w.get(l, 0.0) + a_ik * a / D
+                elif l == i:
+                    dt += a_ik * a / D
+        rows.append({int(cidx[j]): -wv / dt for j, wv in w.items()} if dt != 0.0 else {})
+    return _csr_from_rows(rows, int((cf == C).sum()))
+
+
+def truncate(P, pmax):
+    if pmax <= 0:
+        return P
+    P = P.tocsr()
+    P.sort_indices()
+    rows = []
+    for i in range(P.shape[0]):
+        cols = P.indices[P.indptr[i]:P.indptr[i + 1]].tolist()
+        vals = P.data[P.indptr[i]:P.indptr[i + 1]].tolist()
+        if len(cols) <= pmax:
+            rows.append(dict(zip(cols, vals)))
+            continue
+        keep = sorted(range(len(cols)), key=lambda t: (-abs(vals[t]), cols[t]))[:pmax]
+        keep.sort()
+        tot = 0.0
+        for x in vals:
+            tot += x
+        kept = 0.0
+        for t in keep:
+            kept += vals[t]
+        s = tot / kept if kept != 0.0 else 1.0
+        rows.append({cols[t]: vals[t] * s for t in keep})
+    return _csr_from_rows(rows, P.shape[1])
+
+
+def _tri(A, lower):
+    return (sp.tril(A) if lower else sp.triu(A)).tocsr()
+
+
+class PCBoomerAMG:
+    type = "hypre"
+
+    def __init__(self, A, db=None, prefix=""):
+        db = db or {}
+        g = lambda k, d, t=str: opt(db, prefix, "pc_hypre_boomeramg_" + k, d, t)  # noqa: E731
+        self.theta = g("strong_threshold", 0.25, float)
+        self.mu = g("max_row_sum", 0.9, float)
+        self.pmax = g("P_max", 0, int)
+        self.agg_nl = g("agg_nl", 0, int)
+        self.npaths = g("agg_num_paths", 1, int)
+        self.K = g("grid_sweeps_all", 1, int)
+        self.max_levels = g("max_levels", 25, int)
+        self.no_cf = g("no_CF", False, bool)
+        coarsen_t = g("coarsen_type", "HMIS")
+        interp_t = g("interp_type", "ext+i")
+        if coarsen_t not in _SUPPORTED_COARSEN or interp_t not in _SUPPORTED_INTERP:
+            raise NotImplementedError(f"boomeramg coarsen_type {coarsen_t} / interp_type {interp_t}")
+        if self.K < 1:
+            raise ValueError("grid_sweeps_all must be >= 1")
+        A = A.tocsr()
+        A.sort_indices()
+        self.levels = []
+        while A.shape[0] > 9 and len(self.levels) < self.max_levels - 1:
+            n = A.shape[0]
+            S = strength(A, self.theta, self.mu)
+            aggressive = len(self.levels) < self.agg_nl
+            cf = coarsen(S, n, aggressive, self.npaths)
+            nc = int((cf == C).sum())
+            if nc == 0 or nc == n:
+                break
+            P = multipass_interp(A, S, cf) if aggressive else truncate(ext_i_interp(A, S, cf), self.pmax)
+            P.sort_indices()
+            R = P.T.tocsr()
+            R.sort_indices()
+            Ac = (R @ (A @ P)).tocsr()
+            Ac.sort_indices()
+            self.levels.append({"A": A, "P": P, "R": R, "cf": cf})
+            A = Ac
+        self.coarse = A
+        self.coarse_lu = spla.splu(sp.csc_matrix(A)) if A.shape[0] else None
+
+    def _relax(self, L, b, x, order):
+        A = L["A"]
+        sets = [None] if self.no_cf else [np.flatnonzero(L["cf"] == (C if o == "C" else F)) for o in order]
+        for _ in range(self.K):
+            for idx in sets:
+                for lower in (True, False):
+                    r = b - A @ x
+                    if idx is None:
+                        x = x + spla.spsolve_triangular(_tri(A, lower), r, lower=lower)
+                    elif len(idx):
+                        Asub = A[idx][:, idx]
+                        x = x.copy()
+                        x[idx] += spla.spsolve_triangular(_tri(Asub, lower), r[idx], lower=lower)
+        return x
+
+    def _vcycle(self, l, b):
+        if l == len(self.levels):
+            return self.coarse_lu.solve(b) if self.coarse_lu is not None else b.copy()
+        L = self.levels[l]
+        x = self._relax(L, b, np.zeros_like(b), "CF")
+        r = b - L["A"] @ x
+        e = self._vcycle(l + 1, L["R"] @ r)
+        x = x + L["P"] @ e
+        return self._relax(L, b, x, "FC")
+
+    def apply(self, b):
+        b = np.asarray(b, dtype=np.float64)
+        if b.size == 0:
+            return b.copy()
+        return self._vcycle(0, b)

@@ -147,11 +147,18 @@ def make_pc_of_type(t, M, db=None, prefix=""):
     if t == "bjacobi":
         return PCBJacobi(M, opt(db, prefix, "pc_bjacobi_blocks", 1, int),
                          opt(db, prefix + "sub_", "pc_type", "ilu"))
-    if t in ("gamg", "hypre"):
-        if t == "hypre" and str(db.get("pls.hypre", "gamg")) == "error":
+    if t == "hypre":
+        h = str(db.get("pls.hypre", "boomeramg"))
+        if h == "error":
             raise NotImplementedError("PC type 'hypre' is not available (pls.hypre error)")
+        if h in ("sa", "gamg"):
+            from .amg import PCAMG
+            return PCAMG(M, db, prefix, hypre=True)
+        from .boomeramg import PCBoomerAMG
+        return PCBoomerAMG(M, db, prefix)
+    if t == "gamg":
         from .amg import PCAMG
-        return PCAMG(M, db, prefix, hypre=(t == "hypre"))
+        return PCAMG(M, db, prefix)
     raise NotImplementedError(f"PC type '{t}' is not restated by the oracle")
 
 

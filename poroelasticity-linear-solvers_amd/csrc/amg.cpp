@@ -24,12 +24,12 @@
 #include <map>
 #include <thread>
 
-#include "runtime.hpp"
+#include "amg_host.hpp"
 
 #pragma clang fp contract(off)
 
 namespace pls {
-namespace {
+namespace amgh {
 
 HostCSR transpose(const HostCSR &A) {
     HostCSR T;
@@ -56,19 +56,6 @@ int setup_threads() {
     int t = (int)std::thread::hardware_concurrency();
     if (const char *e = std::getenv("OMP_NUM_THREADS")) t = std::atoi(e);
     return std::max(1, std::min(t, 64));
-}
-
-// fn(t, i0, i1) on T contiguous row ranges, one thread each
-template <class F>
-void parallel_rows(int64_t n, int T, F fn) {
-    T = (int)std::max<int64_t>(1, std::min<int64_t>(T, n / 8));  // rows may be long (R = P^T)
-    if (T == 1) {
-        fn(0, (int64_t)0, n);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; ++t) th.emplace_back(fn, t, n * t / T, n * (t + 1) / T);
-    for (auto &x : th) x.join();
 }
 
 // Concatenate per-thread row ranges (ci/v/row lengths) into one CSR.
@@ -361,6 +348,11 @@ HostCSR dense_inverse(const HostCSR &A) {
 void amg_layout(DevCSR &M, Ctx &c) {
     if (M.nrows > 0 && M.nnz < 128 * M.nrows) build_sell(M, c);
 }
+
+}  // namespace amgh
+
+namespace {
+using namespace amgh;
 
 struct AmgLevel {
     const DevCSR *A = nullptr;      // level 0: the PC's matrix; else Aown

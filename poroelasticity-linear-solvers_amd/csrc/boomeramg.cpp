@@ -1,0 +1,834 @@
+// boomeramg.cpp -- classical algebraic multigrid as the reference configures
+// hypre BoomerAMG (-X_pc_type hypre, petsc-options-inexact:16-24, :32-40,
+// :48-56, :63-71, :92-100): strength of connection (strong_threshold,
+// max_row_sum), HMIS coarsening (one rank: the Ruge-Stueben first pass),
+// aggressive coarsening on the first agg_nl levels with agg_num_paths and
+// multipass interpolation there, extended+i interpolation with P_max
+// truncation elsewhere, Galerkin coarse operators, hybrid symmetric
+// Gauss-Seidel smoothing (PCHYPRE's default relax type) in lexicographic
+// (no_CF) or C/F order, Gaussian elimination on the coarsest level.
+//
+// The algorithm is specified in oracle/boomeramg.py (the test oracle); the
+// setup here builds the same hierarchy bit for bit -- C/F splittings,
+// interpolation weights and coarse operators -- by running every host sum in
+// the order the spec writes it, without contraction.  Row-local stages
+// (strength, S2, interpolation rows, truncation, Galerkin products) run on
+// host threads (row results do not depend on the thread count); the
+// coarsening pass is sequential by definition.  Each level's Gauss-Seidel
+// half-sweep is a device triangular solve: (D + L)^-1 r is the ILU(0) apply of
+// the lower triangle tril(A) (its ILU(0) factors are exact: I + L D^-1 and D),
+// (D + U)^-1 r that of triu(A), on libpls's level-scheduled sweeps.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <limits>
+#include <map>
+#include <queue>
+
+#include "amg_host.hpp"
+#include "kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace pls {
+namespace {
+using namespace amgh;
+
+struct Pattern {  // CSR sparsity (strong dependencies)
+    int64_t n = 0;
+    std::vector<int64_t> rp{0};
+    std::vector<int32_t> ci;
+    int64_t len(int64_t i) const { return rp[i + 1] - rp[i]; }
+};
+
+// concatenate per-thread pattern parts (rows in order)
+Pattern concat_pattern(int64_t n, std::vector<Pattern> &part) {
+    Pattern S;
+    S.n = n;
+    S.rp.reserve(n + 1);
+    int64_t off = 0;
+    for (auto &p : part) {
+        for (size_t k = 1; k < p.rp.size(); ++k) S.rp.push_back(off + p.rp[k]);
+        S.ci.insert(S.ci.end(), p.ci.begin(), p.ci.end());
+        off += (int64_t)p.ci.size();
+        Pattern().rp.swap(p.rp);
+        std::vector<int32_t>().swap(p.ci);
+    }
+    return S;
+}
+
+// oracle strength(): hypre CreateS with strong_threshold theta, max_row_sum mu
+Pattern strength(const HostCSR &A, double theta, double mu) {
+    const int64_t n = A.nrows;
+    const int T = setup_threads();
+    std::vector<Pattern> part(T);
+    parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
+        Pattern &P = part[t];
+        P.rp.assign(1, 0);
+        for (int64_t i = i0; i < i1; ++i) {
+            double d = 0.0, rs = 0.0;
+            double smin = std::numeric_limits<double>::infinity(), smax = -smin;
+            int64_t noff = 0;
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                const double a = A.v[k];
+                rs += a;
+                if (A.ci[k] == i) {
+                    d = a;
+                } else {
+                    ++noff;
+                    smin = std::min(smin, a);
+                    smax = std::max(smax, a);
+                }
+            }
+            if (noff > 0 && !(mu < 1.0 && std::fabs(rs) > mu * std::fabs(d))) {
+                const bool pos = d >= 0.0;
+                const double thr = theta * (pos ? smin : smax);
+                for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                    if (A.ci[k] == i) continue;
+                    const double a = A.v[k];
+                    if (pos ? a < thr : a > thr) P.ci.push_back(A.ci[k]);
+                }
+            }
+            P.rp.push_back((int64_t)P.ci.size());
+        }
+    });
+    return concat_pattern(n, part);
+}
+
+Pattern transpose(const Pattern &S) {
+    Pattern T;
+    T.n = S.n;
+    T.rp.assign(S.n + 1, 0);
+    for (int32_t j : S.ci) ++T.rp[j + 1];
+    for (int64_t j = 0; j < S.n; ++j) T.rp[j + 1] += T.rp[j];
+    T.ci.resize(S.ci.size());
+    std::vector<int64_t> pos(T.rp.begin(), T.rp.end() - 1);
+    for (int64_t i = 0; i < S.n; ++i)
+        for (int64_t k = S.rp[i]; k < S.rp[i + 1]; ++k) T.ci[pos[S.ci[k]]++] = (int32_t)i;
+    return T;
+}
+
+constexpr int8_t UND = 0, FPT = -1, CPT = 1;
+
+// oracle rs_first_pass(): HMIS on one rank.  The lazily updated max-heap
+// selects argmax (lambda, -i) over the undecided points, as the oracle's heapq.
+std::vector<int8_t> rs_first_pass(const Pattern &S) {
+    const int64_t n = S.n;
+    const Pattern ST = transpose(S);
+    std::vector<int64_t> lam(n);
+    for (int64_t i = 0; i < n; ++i) lam[i] = ST.len(i);
+    std::vector<int8_t> st(n, UND);
+    std::priority_queue<std::pair<int64_t, int64_t>> heap;
+    auto make_f = [&](int64_t j) {
+        st[j] = FPT;
+        for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q) {
+            const int32_t k = S.ci[q];
+            if (st[k] == UND) heap.push({++lam[k], -(int64_t)k});
+        }
+    };
+    for (int64_t i = 0; i < n; ++i)
+        if (S.len(i) == 0 && lam[i] == 0) st[i] = FPT;
+    for (int64_t i = 0; i < n; ++i)
+        if (st[i] == UND && lam[i] == 0) make_f(i);
+    for (int64_t i = 0; i < n; ++i)
+        if (st[i] == UND) heap.push({lam[i], -i});
+    while (!heap.empty()) {
+        const auto top = heap.top();
+        heap.pop();
+        const int64_t i = -top.second;
+        if (st[i] != UND || top.first != lam[i]) continue;
+        st[i] = CPT;
+        for (int64_t q = ST.rp[i]; q < ST.rp[i + 1]; ++q)
+            if (st[ST.ci[q]] == UND) make_f(ST.ci[q]);
+        for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+            const int32_t k = S.ci[q];
+            if (st[k] != UND) continue;
+            if (--lam[k] == 0) make_f(k);
+            else heap.push({lam[k], -(int64_t)k});
+        }
+    }
+    for (auto &s : st)
+        if (s == UND) s = FPT;
+    return st;
+}
+
+// oracle second_strength(): S2 over the C points (local numbering)
+Pattern second_strength(const Pattern &S, const std::vector<int8_t> &cf, int paths, std::vector<int32_t> &cpts) {
+    const int64_t n = S.n;
+    std::vector<int32_t> loc(n, -1);
+    cpts.clear();
+    for (int64_t i = 0; i < n; ++i)
+        if (cf[i] == CPT) {
+            loc[i] = (int32_t)cpts.size();
+            cpts.push_back((int32_t)i);
+        }
+    const int64_t m = (int64_t)cpts.size();
+    const int T = setup_threads();
+    std::vector<Pattern> part(T);
+    parallel_rows(m, T, [&](int t, int64_t c0, int64_t c1) {
+        Pattern &P = part[t];
+        P.rp.assign(1, 0);
+        std::vector<int32_t> cnt(n, 0), touched;
+        for (int64_t c = c0; c < c1; ++c) {
+            const int64_t i = cpts[c];
+            touched.clear();
+            auto bump = [&](int32_t j) {
+                if (loc[j] < 0 || j == i) return;
+                if (cnt[j]++ == 0) touched.push_back(j);
+            };
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) bump(S.ci[q]);
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+                const int32_t k = S.ci[q];
+                for (int64_t r = S.rp[k]; r < S.rp[k + 1]; ++r) bump(S.ci[r]);
+            }
+            std::vector<int32_t> row;
+            for (int32_t j : touched) {
+                if (cnt[j] >= paths) row.push_back(loc[j]);
+                cnt[j] = 0;
+            }
+            std::sort(row.begin(), row.end());
+            P.ci.insert(P.ci.end(), row.begin(), row.end());
+            P.rp.push_back((int64_t)P.ci.size());
+        }
+    });
+    return concat_pattern(m, part);
+}
+
+std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths) {
+    std::vector<int8_t> cf = rs_first_pass(S);
+    if (!aggressive) return cf;
+    std::vector<int32_t> cpts;
+    const Pattern S2 = second_strength(S, cf, paths, cpts);
+    const std::vector<int8_t> cf2 = rs_first_pass(S2);
+    std::vector<int8_t> out(S.n, FPT);
+    for (size_t c = 0; c < cpts.size(); ++c)
+        if (cf2[c] == CPT) out[cpts[c]] = CPT;
+    return out;
+}
+
+// rows (sorted column, value) -> HostCSR; exact zeros dropped
+struct RowSet {
+    std::vector<std::vector<int32_t>> col;
+    std::vector<std::vector<double>> val;
+};
+HostCSR to_csr(const RowSet &R, int64_t ncols) {
+    HostCSR P;
+    P.nrows = (int64_t)R.col.size();
+    P.ncols = ncols;
+    P.rp.assign(1, 0);
+    for (size_t i = 0; i < R.col.size(); ++i) {
+        for (size_t k = 0; k < R.col[i].size(); ++k)
+            if (R.val[i][k] != 0.0) {
+                P.ci.push_back(R.col[i][k]);
+                P.v.push_back(R.val[i][k]);
+            }
+        P.rp.push_back((int64_t)P.ci.size());
+    }
+    return P;
+}
+
+// dense accumulator of one thread: first-touch order kept, sorted on output
+struct Acc {
+    std::vector<double> v;
+    std::vector<char> on;
+    std::vector<int32_t> touched;
+    explicit Acc(int64_t n) : v(n, 0.0), on(n, 0) {}
+    void add(int32_t j, double x) {
+        if (!on[j]) {
+            on[j] = 1;
+            v[j] = 0.0;
+            touched.push_back(j);
+        }
+        v[j] += x;
+    }
+    void clear() {
+        for (int32_t j : touched) on[j] = 0;
+        touched.clear();
+    }
+};
+
+std::vector<int32_t> coarse_index(const std::vector<int8_t> &cf, int64_t &nc) {
+    std::vector<int32_t> ci(cf.size(), -1);
+    nc = 0;
+    for (size_t i = 0; i < cf.size(); ++i)
+        if (cf[i] == CPT) ci[i] = (int32_t)nc++;
+    return ci;
+}
+
+// oracle multipass_interp()
+HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> &cf) {
+    const int64_t n = A.nrows;
+    int64_t nc = 0;
+    const std::vector<int32_t> cidx = coarse_index(cf, nc);
+    std::vector<int32_t> pass(n, -1);
+    for (int64_t i = 0; i < n; ++i)
+        if (cf[i] == CPT) pass[i] = 0;
+    RowSet R;
+    R.col.resize(n);
+    R.val.resize(n);
+    for (int64_t i = 0; i < n; ++i)
+        if (cf[i] == CPT) {
+            R.col[i] = {cidx[i]};
+            R.val[i] = {1.0};
+        }
+    const int T = setup_threads();
+    for (int p = 1;; ++p) {
+        std::vector<int32_t> pts;
+        for (int64_t i = 0; i < n; ++i) {
+            if (pass[i] >= 0) continue;
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+                const int32_t k = S.ci[q];
+                if (pass[k] >= 0 && pass[k] < p) {
+                    pts.push_back((int32_t)i);
+                    break;
+                }
+            }
+        }
+        if (pts.empty()) break;
+        for (int32_t i : pts) pass[i] = p;
+        parallel_rows((int64_t)pts.size(), T, [&](int, int64_t t0, int64_t t1) {
+            Acc acc(nc);
+            std::vector<int32_t> Q;
+            std::vector<double> aq;
+            for (int64_t t = t0; t < t1; ++t) {
+                const int64_t i = pts[t];
+                Q.clear();
+                aq.clear();
+                for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+                    const int32_t k = S.ci[q];
+                    if (pass[k] >= 0 && pass[k] < p) Q.push_back(k);
+                }
+                double d = 0.0, neg_all = 0.0, pos_all = 0.0, neg_q = 0.0, pos_q = 0.0;
+                size_t qi = 0;
+                aq.assign(Q.size(), 0.0);
+                for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                    const int32_t j = A.ci[k];
+                    const double a = A.v[k];
+                    if (j == i) {
+                        d = a;
+                        continue;
+                    }
+                    neg_all += std::min(a, 0.0);
+                    pos_all += std::max(a, 0.0);
+                    while (qi < Q.size() && Q[qi] < j) ++qi;
+                    if (qi < Q.size() && Q[qi] == j) aq[qi] = a;
+                }
+                for (size_t u = 0; u < Q.size(); ++u) {
+                    neg_q += std::min(aq[u], 0.0);
+                    pos_q += std::max(aq[u], 0.0);
+                }
+                double alpha = 0.0, beta = 0.0;
+                if (neg_q == 0.0) d += neg_all;
+                else alpha = neg_all / neg_q;
+                if (pos_q == 0.0) d += pos_all;
+                else beta = pos_all / pos_q;
+                for (size_t u = 0; u < Q.size(); ++u) {
+                    const double a = aq[u];
+                    if (a == 0.0) continue;
+                    const double w = -(a < 0.0 ? alpha : beta) * a / d;
+                    const auto &pc = R.col[Q[u]];
+                    const auto &pv = R.val[Q[u]];
+                    for (size_t e = 0; e < pc.size(); ++e) acc.add(pc[e], w * pv[e]);
+                }
+                std::sort(acc.touched.begin(), acc.touched.end());
+                std::vector<int32_t> cc;
+                std::vector<double> vv;
+                for (int32_t j : acc.touched) {
+                    cc.push_back(j);
+                    vv.push_back(acc.v[j]);
+                }
+                acc.clear();
+                R.col[i] = std::move(cc);
+                R.val[i] = std::move(vv);
+            }
+        });
+    }
+    return to_csr(R, nc);
+}
+
+// oracle ext_i_interp()
+HostCSR ext_i(const HostCSR &A, const Pattern &S, const std::vector<int8_t> &cf) {
+    const int64_t n = A.nrows;
+    int64_t nc = 0;
+    const std::vector<int32_t> cidx = coarse_index(cf, nc);
+    std::vector<double> diag(n, 0.0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
+            if (A.ci[k] == i) diag[i] = A.v[k];
+    RowSet R;
+    R.col.resize(n);
+    R.val.resize(n);
+    const int T = setup_threads();
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        std::vector<char> chat(n, 0), strong(n, 0);
+        std::vector<int32_t> chat_list;
+        Acc w(n);
+        for (int64_t i = i0; i < i1; ++i) {
+            if (cf[i] == CPT) {
+                R.col[i] = {cidx[i]};
+                R.val[i] = {1.0};
+                continue;
+            }
+            chat_list.clear();
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+                const int32_t k = S.ci[q];
+                strong[k] = 1;
+                if (cf[k] == CPT) {
+                    if (!chat[k]) chat_list.push_back(k);
+                    chat[k] = 1;
+                } else {
+                    for (int64_t r = S.rp[k]; r < S.rp[k + 1]; ++r) {
+                        const int32_t l = S.ci[r];
+                        if (cf[l] == CPT && !chat[l]) {
+                            chat[l] = 1;
+                            chat_list.push_back(l);
+                        }
+                    }
+                }
+            }
+            double dt = 0.0;
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                const int32_t j = A.ci[k];
+                const double a = A.v[k];
+                if (j == i) dt += a;
+                else if (chat[j]) w.add(j, a);
+                else if (strong[j]) continue;
+                else dt += a;
+            }
+            int64_t ak = A.rp[i];  // A's row i is sorted and S_i ascending: merge for a_ik
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+                const int32_t k = S.ci[q];
+                if (cf[k] != FPT) continue;
+                while (A.ci[ak] < k) ++ak;
+                const double a_ik = A.v[ak];
+                const double dk = diag[k];
+                double D = 0.0;
+                for (int64_t r = A.rp[k]; r < A.rp[k + 1]; ++r) {
+                    const int32_t l = A.ci[r];
+                    const double a = A.v[r];
+                    if ((chat[l] || l == i) && a * dk < 0.0) D += a;
+                }
+                if (D == 0.0) {
+                    dt += a_ik;
+                    continue;
+                }
+                for (int64_t r = A.rp[k]; r < A.rp[k + 1]; ++r) {
+                    const int32_t l = A.ci[r];
+                    const double a = A.v[r];
+                    if (a * dk >= 0.0) continue;
+                    if (chat[l]) w.add(l, a_ik * a / D);
+                    else if (l == i) dt += a_ik * a / D;
+                }
+            }
+            std::sort(w.touched.begin(), w.touched.end());
+            if (dt != 0.0)
+                for (int32_t j : w.touched) {
+                    R.col[i].push_back(cidx[j]);
+                    R.val[i].push_back(-w.v[j] / dt);
+                }
+            w.clear();
+            for (int32_t l : chat_list) chat[l] = 0;
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) strong[S.ci[q]] = 0;
+        }
+    });
+    return to_csr(R, nc);
+}
+
+// oracle truncate(): keep the pmax largest |P_ij| (ties: smaller j), rescale
+HostCSR truncate(const HostCSR &P, int64_t pmax) {
+    if (pmax <= 0) return P;
+    RowSet R;
+    R.col.resize(P.nrows);
+    R.val.resize(P.nrows);
+    parallel_rows(P.nrows, setup_threads(), [&](int, int64_t i0, int64_t i1) {
+        std::vector<int64_t> idx;
+        for (int64_t i = i0; i < i1; ++i) {
+            const int64_t b = P.rp[i], e = P.rp[i + 1];
+            if (e - b <= pmax) {
+                R.col[i].assign(P.ci.begin() + b, P.ci.begin() + e);
+                R.val[i].assign(P.v.begin() + b, P.v.begin() + e);
+                continue;
+            }
+            idx.resize(e - b);
+            for (int64_t k = b; k < e; ++k) idx[k - b] = k;
+            std::sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) {
+                const double ax = std::fabs(P.v[x]), ay = std::fabs(P.v[y]);
+                return ax != ay ? ax > ay : P.ci[x] < P.ci[y];
+            });
+            idx.resize(pmax);
+            std::sort(idx.begin(), idx.end());
+            double tot = 0.0, kept = 0.0;
+            for (int64_t k = b; k < e; ++k) tot += P.v[k];
+            for (int64_t k : idx) kept += P.v[k];
+            const double s = kept != 0.0 ? tot / kept : 1.0;
+            for (int64_t k : idx) {
+                R.col[i].push_back(P.ci[k]);
+                R.val[i].push_back(P.v[k] * s);
+            }
+        }
+    });
+    return to_csr(R, P.ncols);
+}
+
+// rows / columns `idx` of A (idx ascending; empty: all), lower or upper triangle with the diagonal
+HostCSR triangle(const HostCSR &A, const std::vector<int32_t> &idx, bool lower) {
+    const int64_t n = A.nrows;
+    std::vector<int32_t> loc;
+    const bool all = idx.empty();
+    if (!all) {
+        loc.assign(n, -1);
+        for (size_t t = 0; t < idx.size(); ++t) loc[idx[t]] = (int32_t)t;
+    }
+    const int64_t m = all ? n : (int64_t)idx.size();
+    HostCSR T;
+    T.nrows = T.ncols = m;
+    T.rp.assign(1, 0);
+    for (int64_t r = 0; r < m; ++r) {
+        const int64_t i = all ? r : idx[r];
+        bool has_diag = false;
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+            const int32_t j = all ? A.ci[k] : loc[A.ci[k]];
+            if (j < 0 || (lower ? j > r : j < r)) continue;
+            if (j == r) {
+                if (A.v[k] == 0.0) break;
+                has_diag = true;
+            }
+            T.ci.push_back(j);
+            T.v.push_back(A.v[k]);
+        }
+        if (!has_diag) throw Error("boomeramg: zero diagonal entry on a Gauss-Seidel level (row " + std::to_string(i) + ")");
+        T.rp.push_back((int64_t)T.ci.size());
+    }
+    return T;
+}
+
+struct BParams {
+    double theta = 0.25, mu = 0.9, rap_bytes = 16e9;
+    int64_t pmax = 0, agg_nl = 0, max_levels = 25;
+    int paths = 1, K = 1;
+    bool no_cf = false;
+};
+
+BParams parse_params(const Options &o, const std::string &prefix) {
+    const std::string pre = prefix + "pc_hypre_boomeramg_";
+    BParams p;
+    p.theta = o.num(pre + "strong_threshold", 0.25);
+    p.mu = o.num(pre + "max_row_sum", 0.9);
+    p.pmax = o.integer(pre + "P_max", 0);
+    p.agg_nl = o.integer(pre + "agg_nl", 0);
+    p.paths = (int)o.integer(pre + "agg_num_paths", 1);
+    p.max_levels = o.integer(pre + "max_levels", 25);
+    p.K = (int)o.integer(pre + "grid_sweeps_all", 1);
+    p.no_cf = o.flag(pre + "no_CF", false);
+    p.rap_bytes = o.num("pls.amg_rap_dense_gb", 16.0) * 1e9;
+    const std::string ct = o.str(pre + "coarsen_type", "HMIS"), it = o.str(pre + "interp_type", "ext+i");
+    if (ct != "HMIS") throw Error(pre + "coarsen_type " + ct + ": only HMIS is implemented");
+    if (it != "ext+i") throw Error(pre + "interp_type " + it + ": only ext+i is implemented");
+    const std::string rt = o.str(pre + "relax_type_all", "symmetric-SOR/Jacobi");
+    if (rt != "symmetric-SOR/Jacobi") throw Error(pre + "relax_type_all " + rt + ": only symmetric-SOR/Jacobi is implemented");
+    if (p.K < 1) throw Error(pre + "grid_sweeps_all must be >= 1");
+    if (p.paths < 1) throw Error(pre + "agg_num_paths must be >= 1");
+    return p;
+}
+
+// The host setup (oracle PCBoomerAMG.__init__): on_level(A, cf, P, R, nc) for
+// every level, then the coarsest operator is returned.  tm: stage seconds.
+template <class F>
+HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    int64_t nlev = 0;
+    while (A.nrows > 9 && nlev < p.max_levels - 1) {
+        double t0 = now();
+        const Pattern S = strength(A, p.theta, p.mu);
+        tm[1] += now() - t0;
+        t0 = now();
+        const bool aggressive = nlev < p.agg_nl;
+        const std::vector<int8_t> cf = coarsen(S, aggressive, p.paths);
+        tm[2] += now() - t0;
+        int64_t nc = 0;
+        for (int8_t v : cf) nc += v == CPT;
+        if (nc == 0 || nc == A.nrows) break;
+        t0 = now();
+        const HostCSR P = aggressive ? multipass(A, S, cf) : truncate(ext_i(A, S, cf), p.pmax);
+        const HostCSR R = amgh::transpose(P);
+        tm[3] += now() - t0;
+        t0 = now();
+        HostCSR Ac;
+        if (!galerkin_fused(A, P, nc, p.rap_bytes, Ac)) Ac = spgemm(R, spgemm(A, P));
+        tm[4] += now() - t0;
+        on_level(A, cf, P, R, nc);
+        A = std::move(Ac);
+        ++nlev;
+    }
+    return A;
+}
+
+struct RelaxSet {  // the points one Gauss-Seidel pass visits (all, C or F)
+    int64_t m = 0;
+    bool all = true;
+    DBuf<int64_t> idx;
+    DevCSR lo, up;
+    std::unique_ptr<PCILU> fwd, bwd;
+};
+
+struct BLevel {
+    const DevCSR *A = nullptr;  // level 0: the PC's matrix; else Aown
+    std::unique_ptr<DevCSR> Aown;
+    DevCSR P, R;
+    int64_t n = 0, nc = 0;
+    std::vector<std::unique_ptr<RelaxSet>> sets;  // no_CF: {all}; else {C, F}
+};
+
+struct BWork {
+    std::vector<DBuf<double>> r, t, x, b, xs, rs, ts;
+    DBuf<double> cx, cb;
+};
+
+struct PCBoomer : PC {
+    std::vector<std::unique_ptr<BLevel>> lv;
+    int K = 1;
+    bool no_cf = false;
+    int64_t nco = 0;
+    DevCSR Cinv;
+    std::unique_ptr<PC> Clu;
+    std::unique_ptr<DevCSR> Cmat;
+    std::map<hipStream_t, std::unique_ptr<BWork>> work;
+
+    bool reentrant() const override { return true; }
+
+    BWork &work_for(Ctx &c) {
+        auto &w = work[c.st];
+        if (!w) {
+            w = std::make_unique<BWork>();
+            const size_t L = lv.size();
+            for (auto *v : {&w->r, &w->t, &w->x, &w->b, &w->xs, &w->rs, &w->ts}) v->resize(L);
+            for (size_t l = 0; l < L; ++l) {
+                const size_t m = (size_t)std::max<int64_t>(lv[l]->n, 1);
+                w->r[l].alloc(m);
+                w->t[l].alloc(m);
+                if (l > 0) {
+                    w->x[l].alloc(m);
+                    w->b[l].alloc(m);
+                }
+                if (!no_cf) {
+                    w->xs[l].alloc(m);
+                    w->rs[l].alloc(m);
+                    w->ts[l].alloc(m);
+                }
+            }
+            w->cx.alloc(std::max<int64_t>(nco, 1));
+            w->cb.alloc(std::max<int64_t>(nco, 1));
+        }
+        return *w;
+    }
+
+    PCBoomer(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c) {
+        type = "hypre";
+        n = M.nrows;
+        const BParams prm = parse_params(o, prefix);
+        K = prm.K;
+        no_cf = prm.no_cf;
+        if (!M.sell) build_sell(const_cast<DevCSR &>(M), c);
+        const bool view = o.flag("pls.amg_view", false);
+        const bool allow_lds = o.flag("pls.ilu_lds", true);
+        const int gmem = (int)o.integer("pls.ilu_gmem", 0), ring = (int)o.integer("pls.ilu_ring", 1);
+        double tm[7] = {0};
+        auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+        double t0 = now();
+        std::unique_ptr<DevCSR> cur;
+        HostCSR A = host_setup(download(M, c), prm, [&](const HostCSR &Al, const std::vector<int8_t> &cf, const HostCSR &P,
+                                                        const HostCSR &R, int64_t nc) {
+            const double t1 = now();
+            auto L = std::make_unique<BLevel>();
+            L->n = Al.nrows;
+            L->nc = nc;
+            if (lv.empty()) {
+                L->A = &M;
+            } else {  // the level's Galerkin operator
+                L->Aown = std::make_unique<DevCSR>();
+                upload(Al, *L->Aown, c);
+                amg_layout(*L->Aown, c);
+                L->A = L->Aown.get();
+            }
+            upload(P, L->P, c);
+            upload(R, L->R, c);
+            amg_layout(L->P, c);
+            amg_layout(L->R, c);
+            std::vector<std::vector<int32_t>> groups;
+            if (no_cf) {
+                groups.emplace_back();
+            } else {
+                groups.resize(2);
+                for (int64_t i = 0; i < Al.nrows; ++i) groups[cf[i] == CPT ? 0 : 1].push_back((int32_t)i);
+            }
+            for (auto &g : groups) {
+                auto rs = std::make_unique<RelaxSet>();
+                rs->all = no_cf;
+                rs->m = no_cf ? Al.nrows : (int64_t)g.size();
+                if (rs->m > 0) {
+                    if (!no_cf) {
+                        std::vector<int64_t> gi(g.begin(), g.end());
+                        rs->idx.alloc(gi.size());
+                        HIPCHK(hipMemcpyAsync(rs->idx.p, gi.data(), sizeof(int64_t) * gi.size(), hipMemcpyHostToDevice, c.st));
+                    }
+                    upload(triangle(Al, g, true), rs->lo, c);
+                    upload(triangle(Al, g, false), rs->up, c);
+                    rs->fwd = std::make_unique<PCILU>(rs->lo, 1, c, false, allow_lds, 0, gmem, ring);
+                    rs->bwd = std::make_unique<PCILU>(rs->up, 1, c, false, allow_lds, 0, gmem, ring);
+                }
+                L->sets.push_back(std::move(rs));
+            }
+            lv.push_back(std::move(L));
+            c.sync();
+            tm[5] += now() - t1;
+        }, tm);
+        tm[0] = now() - t0 - (tm[1] + tm[2] + tm[3] + tm[4] + tm[5]);
+        if (!lv.empty()) {
+            cur = std::make_unique<DevCSR>();
+            upload(A, *cur, c);
+            amg_layout(*cur, c);
+        }
+        t0 = now();
+        nco = A.nrows;
+        work_for(c);
+        if (nco > 0) {
+            if (nco <= 1024) {
+                upload(dense_inverse(A), Cinv, c);
+                amg_layout(Cinv, c);
+            } else {
+                Cmat = std::move(cur);
+                const DevCSR &Cm = Cmat ? *Cmat : M;
+                if (nco <= o.integer("pls.lu_dense_max", 32768)) Clu = std::make_unique<PCDenseLU>(Cm, c);
+                else Clu = std::make_unique<PCILU>(Cm, 1, c, true, allow_lds);
+            }
+        }
+        c.sync();
+        tm[6] += now() - t0;
+        // the V-cycle's vectors are sized from these: check the chain before any launch
+        for (size_t l = 0; l < lv.size(); ++l) {
+            const BLevel &L = *lv[l];
+            const int64_t next = l + 1 < lv.size() ? lv[l + 1]->n : nco;
+            if (L.A->nrows != L.n || L.P.nrows != L.n || L.P.ncols != L.nc || L.R.nrows != L.nc || L.R.ncols != L.n ||
+                next != L.nc)
+                throw Error("boomeramg: inconsistent hierarchy at level " + std::to_string(l));
+            for (const auto &s : L.sets)
+                if (s->m > 0 && (s->lo.nrows != s->m || s->up.nrows != s->m)) throw Error("boomeramg: smoother size mismatch");
+        }
+        if (view) {
+            fprintf(stderr, "[boomeramg %s] levels %zu:", prefix.c_str(), lv.size() + 1);
+            for (auto &L : lv) fprintf(stderr, " %lld(P nnz %lld)", (long long)L->n, (long long)L->P.nnz);
+            fprintf(stderr, " coarse %lld\n", (long long)nco);
+            fprintf(stderr,
+                    "[boomeramg %s] setup s: download/other %.2f strength %.2f coarsen %.2f interp %.2f RAP %.2f "
+                    "smoothers+upload %.2f coarse %.2f (%d threads)\n",
+                    prefix.c_str(), tm[0], tm[1], tm[2], tm[3], tm[4], tm[5], tm[6], setup_threads());
+        }
+    }
+
+    // one Gauss-Seidel half-sweep over set s: x_I += T_II^-1 (b - A x)_I
+    // (x_zero: x == 0 on entry, so the residual is b and x_I is written)
+    void half_sweep(BLevel &L, size_t l, RelaxSet &s, bool lower, BWork &W, const double *b, double *x, bool x_zero,
+                    Ctx &c) {
+        if (s.m == 0) return;
+        PCILU &T = lower ? *s.fwd : *s.bwd;
+        const double *r = b;
+        if (!x_zero) {
+            spmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
+            r = W.r[l].p;
+        }
+        if (s.all) {
+            if (x_zero) {
+                T.apply(r, x, c);
+            } else {
+                T.apply(r, W.t[l].p, c);
+                launch_axpby(L.n, 1.0, W.t[l].p, 1.0, x, c.st);
+            }
+            return;
+        }
+        launch_gather(s.m, s.idx.p, r, W.rs[l].p, c.st);
+        T.apply(W.rs[l].p, W.ts[l].p, c);
+        launch_gather(s.m, s.idx.p, x, W.xs[l].p, c.st);
+        launch_axpby(s.m, 1.0, W.ts[l].p, 1.0, W.xs[l].p, c.st);
+        launch_scatter(s.m, s.idx.p, W.xs[l].p, x, c.st);
+    }
+
+    // grid_sweeps_all hybrid symmetric GS sweeps; down: C then F, up: F then C
+    void relax(size_t l, BWork &W, const double *b, double *x, bool down, bool x_zero, Ctx &c) {
+        BLevel &L = *lv[l];
+        if (x_zero && !no_cf) launch_set(L.n, 0.0, x, c.st);
+        for (int k = 0; k < K; ++k)
+            for (size_t g = 0; g < L.sets.size(); ++g) {
+                RelaxSet &s = *L.sets[down ? g : L.sets.size() - 1 - g];
+                half_sweep(L, l, s, true, W, b, x, x_zero && no_cf, c);
+                x_zero = false;
+                half_sweep(L, l, s, false, W, b, x, false, c);
+            }
+    }
+
+    void coarse_solve(const double *b, double *x, Ctx &c) {
+        if (nco == 0) return;
+        if (Clu) Clu->apply(b, x, c);
+        else spmv(Cinv, b, x, c);
+    }
+
+    void vcycle(size_t l, BWork &W, const double *b, double *x, Ctx &c) {
+        if (l == lv.size()) {
+            coarse_solve(b, x, c);
+            return;
+        }
+        BLevel &L = *lv[l];
+        const bool last = (l + 1 == lv.size());
+        double *bc = last ? W.cb.p : W.b[l + 1].p;
+        double *xc = last ? W.cx.p : W.x[l + 1].p;
+        relax(l, W, b, x, true, true, c);
+        spmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
+        spmv(L.R, W.r[l].p, bc, c);
+        vcycle(l + 1, W, bc, xc, c);
+        spmv(L.P, xc, x, c, 1.0, 1.0, x);
+        relax(l, W, b, x, false, false, c);
+    }
+
+    void apply(const double *x, double *y, Ctx &c) override {
+        if (n == 0) return;
+        if (lv.empty()) {
+            coarse_solve(x, y, c);
+            return;
+        }
+        vcycle(0, work_for(c), x, y, c);
+    }
+};
+
+}  // namespace
+
+std::unique_ptr<PC> make_boomeramg(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c) {
+    if (M.halo) throw Error("PC type hypre (prefix " + prefix + "): multigrid is single-rank in this build");
+    return std::make_unique<PCBoomer>(M, o, prefix, c);
+}
+
+// Host-only hierarchy query for the CPU tests (pls_boomeramg_host_level):
+// level `level`'s n, nc, C/F marker and P (CSR) of the setup on the host matrix.
+void boomeramg_host_level(const HostCSR &A, const Options &o, const std::string &prefix, int64_t level,
+                          int64_t &nlevels, int64_t &n, int64_t &nc, std::vector<int8_t> &cf, HostCSR &P) {
+    const BParams prm = parse_params(o, prefix);
+    double tm[7] = {0};
+    int64_t l = 0;
+    n = nc = 0;
+    HostCSR coarse = host_setup(A, prm, [&](const HostCSR &Al, const std::vector<int8_t> &cfl, const HostCSR &Pl,
+                                            const HostCSR &, int64_t ncl) {
+        if (l == level) {
+            n = Al.nrows;
+            nc = ncl;
+            cf = cfl;
+            P = Pl;
+        }
+        ++l;
+    }, tm);
+    nlevels = l + 1;
+    if (level == l) {  // the coarsest operator (P empty)
+        n = coarse.nrows;
+        P = coarse;
+    }
+}
+
+}  // namespace pls

@@ -1447,6 +1447,63 @@ int pls_bench_spmv(pls_handle *hh, const double *d_x, double *d_y, int32_t reps,
     })
 }
 
+// Host-only query of the classical-AMG setup (no device): level `level` of
+// the hierarchy built from A with the options' prefix_pc_hypre_boomeramg_*
+// values.  Outputs n, nc, P's nnz (the coarsest operator when level ==
+// nlevels - 1); cf (n int8: 1 C, -1 F) and P's CSR arrays are written when
+// non-NULL (call once for the sizes, then with buffers).
+int pls_boomeramg_host_level(const pls_csr *A, const char *options, const char *prefix, int64_t level,
+                             int64_t *nlevels, int64_t *n, int64_t *nc, int64_t *p_nnz, int8_t *cf, int64_t *p_rp,
+                             int32_t *p_ci, double *p_v) {
+    PLS_TRY({
+        if (!A || A->nrows != A->ncols) throw Error("pls_boomeramg_host_level: square A required");
+        Options o;
+        o.parse(options);
+        HostCSR H;
+        H.nrows = H.ncols = A->nrows;
+        H.rp.assign(A->row_ptr, A->row_ptr + A->nrows + 1);
+        H.ci.assign(A->col, A->col + H.rp.back());
+        H.v.assign(A->val, A->val + H.rp.back());
+        std::vector<int8_t> cfv;
+        HostCSR P;
+        boomeramg_host_level(H, o, prefix ? prefix : "", level, *nlevels, *n, *nc, cfv, P);
+        *p_nnz = (int64_t)P.ci.size();
+        if (cf && !cfv.empty()) std::copy(cfv.begin(), cfv.end(), cf);
+        if (p_rp && P.nrows > 0) std::copy(P.rp.begin(), P.rp.end(), p_rp);
+        if (p_ci) std::copy(P.ci.begin(), P.ci.end(), p_ci);
+        if (p_v) std::copy(P.v.begin(), P.v.end(), p_v);
+    })
+}
+
+// Standalone AndersonAcceleration (lib/AndersonAcceleration.py:8-78) on its
+// own stream and a single-rank communicator; the same mixer the block PC runs
+// for "inner accel order" > 0.
+struct AndersonObj {
+    Ctx ctx;
+    AndersonMixer mix;
+};
+int pls_anderson_create(int32_t order, int64_t n, pls_anderson **out) {
+    PLS_TRY({
+        if (!out) throw Error("pls_anderson_create: out is NULL");
+        if (order < 0 || order > 15) throw Error("pls_anderson_create: order must be in 0..15");
+        if (n < 0) throw Error("pls_anderson_create: negative length");
+        auto *a = new AndersonObj();
+        a->mix.init(order, n);
+        *out = reinterpret_cast<pls_anderson *>(a);
+    })
+}
+int pls_anderson_next(pls_anderson *aa, double *d_gk) {
+    PLS_TRY({
+        if (!aa) throw Error("pls_anderson_next: NULL object");
+        AndersonObj &a = *reinterpret_cast<AndersonObj *>(aa);
+        if (a.mix.n > 0 && !d_gk) throw Error("pls_anderson_next: NULL vector");
+        // order 0: mk = 0 every call, x_k = g_k (AndersonAcceleration.py:69-70)
+        if (a.mix.order > 0) a.mix.next(d_gk, a.ctx);
+        a.ctx.sync();
+    })
+}
+int pls_anderson_destroy(pls_anderson *a) { PLS_TRY(delete reinterpret_cast<AndersonObj *>(a)) }
+
 // Latency of the solve's global sums (one batched all-reduce per
 // CGS step, one per norm): reps x (global_sum_dev of `count` doubles + the
 // stream sync the Krylov loop does to read them on the host), host clock.

@@ -1273,11 +1273,15 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
     }
     if (type == "gamg") return make_amg(M, o, prefix, false, c);
     if (type == "hypre") {
-        // BoomerAMG is not in this image: the smoothed-aggregation AMG stands in
-        // (oracle/amg.py); pls.hypre error restores the refusal
-        if (o.str("pls.hypre", "gamg") == "error")
+        // hypre is not in this image: classical AMG restating BoomerAMG as the
+        // reference configures it (oracle/boomeramg.py); pls.hypre sa selects
+        // the smoothed-aggregation AMG instead, pls.hypre error the refusal
+        const std::string h = o.str("pls.hypre", "boomeramg");
+        if (h == "error")
             throw Error("PC type 'hypre' (prefix " + prefix + ") is not available (pls.hypre error)");
-        return make_amg(M, o, prefix, true, c);
+        if (h == "sa" || h == "gamg") return make_amg(M, o, prefix, true, c);
+        if (h != "boomeramg") throw Error("pls.hypre " + h + ": expected boomeramg, sa or error");
+        return make_boomeramg(M, o, prefix, c);
     }
     throw Error("PC type '" + type + "' (prefix " + prefix +
                 ") is not available in this build (supported: none, jacobi, ilu, bjacobi, lu, gamg, hypre)");

@@ -325,8 +325,12 @@ void csr_bandwidths(const DevCSR &M, int64_t &kl, int64_t &ku, Ctx &c);
 std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c);
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c);
-// Smoothed-aggregation AMG (amg.cpp; -pc_type gamg, and hypre unless pls.hypre error).
+// Smoothed-aggregation AMG (amg.cpp; -pc_type gamg, and hypre with pls.hypre sa).
 std::unique_ptr<PC> make_amg(const DevCSR &M, const Options &o, const std::string &prefix, bool hypre, Ctx &c);
+// Classical AMG as the reference configures BoomerAMG (boomeramg.cpp; -pc_type hypre).
+std::unique_ptr<PC> make_boomeramg(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c);
+void boomeramg_host_level(const HostCSR &A, const Options &o, const std::string &prefix, int64_t level,
+                          int64_t &nlevels, int64_t &n, int64_t &nc, std::vector<int8_t> &cf, HostCSR &P);
 
 // ---------------------------------------------------------------------- KSP --
 enum Reason {

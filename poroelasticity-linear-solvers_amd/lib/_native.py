@@ -45,7 +45,8 @@ EXPORTS = [
     "pls_get_timings", "pls_reset_timings", "pls_export_matrix", "pls_get_permutation",
     "pls_bench_spmv", "pls_rccl_unique_id", "pls_comm_create_rccl", "pls_comm_create_callback",
     "pls_comm_destroy", "pls_create_synthetic_dist", "pls_spmv_layout", "pls_update_matrices",
-    "pls_bench_copy", "pls_create_dist", "pls_bench_global_sum",
+    "pls_bench_copy", "pls_create_dist", "pls_bench_global_sum", "pls_anderson_create",
+    "pls_anderson_next", "pls_anderson_destroy", "pls_boomeramg_host_level",
 ]
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
@@ -97,6 +98,11 @@ def lib():
     L.pls_spmv_layout.argtypes = [vp, C.POINTER(i32), C.POINTER(i64)]
     L.pls_create_synthetic_dist.argtypes = [C.POINTER(pls_synth_spec), C.c_char_p, vp, C.POINTER(vp)]
     L.pls_bench_global_sum.argtypes = [vp, i32, i32, C.POINTER(C.c_double)]
+    L.pls_anderson_create.argtypes = [i32, i64, C.POINTER(vp)]
+    L.pls_anderson_next.argtypes = [vp, vp]
+    L.pls_anderson_destroy.argtypes = [vp]
+    L.pls_boomeramg_host_level.argtypes = [C.POINTER(pls_csr), C.c_char_p, C.c_char_p, i64, C.POINTER(i64),
+                                           C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), vp, vp, vp, vp]
     L.pls_create_dist.argtypes = [C.POINTER(pls_csr), C.POINTER(pls_csr), C.POINTER(pls_csr), i64,
                                   vp, i64, vp, i64, vp, i64, vp, i64, C.c_char_p, vp, C.POINTER(vp)]
     _lib = L

@@ -235,3 +235,27 @@ class Handle:
         p = np.zeros(self.n, dtype=np.int64)
         N.check(N.lib().pls_get_permutation(self.ptr, N.ptr(p)))
         return p
+
+
+def boomeramg_host_level(A, options: dict, prefix: str, level: int):
+    """Level ``level`` of the classical AMG hierarchy (-pc_type hypre) that
+    libpls builds from ``A`` on the host (``pls_boomeramg_host_level``; no
+    device needed): (nlevels, n, nc, cf int8[n], P scipy CSR); on the coarsest
+    level cf is empty and P is the coarsest operator."""
+    import scipy.sparse as sp
+    ai, aj, av, nr, nc_ = N.csr_of(A)
+    m = N.pls_csr(nr, nc_, ai.ctypes.data_as(C.c_void_p), aj.ctypes.data_as(C.c_void_p), av.ctypes.data_as(C.c_void_p))
+    nl, n, nc, nnz = (C.c_int64() for _ in range(4))
+    args = [C.byref(m), options_text(options), prefix.encode(), int(level), C.byref(nl), C.byref(n), C.byref(nc),
+            C.byref(nnz)]
+    N.check(N.lib().pls_boomeramg_host_level(*args, None, None, None, None))
+    cf = np.zeros(n.value if level < nl.value - 1 else 0, dtype=np.int8)
+    rp = np.zeros(n.value + 1, dtype=np.int64)
+    ci = np.zeros(max(nnz.value, 1), dtype=np.int32)
+    v = np.zeros(max(nnz.value, 1), dtype=np.float64)
+    N.check(N.lib().pls_boomeramg_host_level(*args, cf.ctypes.data_as(C.c_void_p) if cf.size else None,
+                                             rp.ctypes.data_as(C.c_void_p), ci.ctypes.data_as(C.c_void_p),
+                                             v.ctypes.data_as(C.c_void_p)))
+    ncols = nc.value if level < nl.value - 1 else n.value
+    P = sp.csr_matrix((v[:nnz.value], ci[:nnz.value], rp), shape=(n.value, ncols))
+    return nl.value, n.value, nc.value, cf, P
