@@ -22,6 +22,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <map>
 #include <queue>
@@ -111,41 +112,77 @@ Pattern transpose(const Pattern &S) {
 
 constexpr int8_t UND = 0, FPT = -1, CPT = 1;
 
-// oracle rs_first_pass(): HMIS on one rank.  The lazily updated max-heap
-// selects argmax (lambda, -i) over the undecided points, as the oracle's heapq.
+// oracle rs_first_pass(): HMIS on one rank.  The oracle's lazily updated heap
+// selects argmax (lambda, -i) over the undecided points; here a tournament
+// tree over the points holds that argmax (O(log n) per lambda change, no
+// allocation), the same selection.
+struct Tournament {
+    int64_t size = 1;
+    std::vector<int32_t> node;  // best point of each subtree, -1: none
+    const std::vector<int64_t> &lam;
+    const std::vector<int8_t> &st;
+    Tournament(int64_t n, const std::vector<int64_t> &l, const std::vector<int8_t> &s) : lam(l), st(s) {
+        while (size < n) size <<= 1;
+        node.assign(2 * size, -1);
+        for (int64_t i = 0; i < n; ++i) node[size + i] = s[i] == 0 ? (int32_t)i : -1;
+        for (int64_t v = size - 1; v >= 1; --v) node[v] = better(node[2 * v], node[2 * v + 1]);
+    }
+    int32_t better(int32_t a, int32_t b) const {
+        if (a < 0) return b;
+        if (b < 0) return a;
+        if (lam[a] != lam[b]) return lam[a] > lam[b] ? a : b;
+        return a < b ? a : b;
+    }
+    void update(int64_t i) {  // after lam[i] or st[i] changed
+        int64_t v = size + i;
+        node[v] = st[i] == 0 ? (int32_t)i : -1;
+        for (v >>= 1; v >= 1; v >>= 1) {
+            const int32_t b = better(node[2 * v], node[2 * v + 1]);
+            if (node[v] == b && b != (int32_t)i) break;  // unchanged above
+            node[v] = b;
+        }
+    }
+};
+
 std::vector<int8_t> rs_first_pass(const Pattern &S) {
     const int64_t n = S.n;
     const Pattern ST = transpose(S);
     std::vector<int64_t> lam(n);
     for (int64_t i = 0; i < n; ++i) lam[i] = ST.len(i);
     std::vector<int8_t> st(n, UND);
-    std::priority_queue<std::pair<int64_t, int64_t>> heap;
-    auto make_f = [&](int64_t j) {
-        st[j] = FPT;
-        for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q) {
-            const int32_t k = S.ci[q];
-            if (st[k] == UND) heap.push({++lam[k], -(int64_t)k});
-        }
-    };
     for (int64_t i = 0; i < n; ++i)
         if (S.len(i) == 0 && lam[i] == 0) st[i] = FPT;
-    for (int64_t i = 0; i < n; ++i)
-        if (st[i] == UND && lam[i] == 0) make_f(i);
-    for (int64_t i = 0; i < n; ++i)
-        if (st[i] == UND) heap.push({lam[i], -i});
-    while (!heap.empty()) {
-        const auto top = heap.top();
-        heap.pop();
-        const int64_t i = -top.second;
-        if (st[i] != UND || top.first != lam[i]) continue;
+    // prepass: undecided points with lambda 0 become F in ascending order
+    // (their dependencies' lambda grow, possibly above 0 before their turn)
+    for (int64_t j = 0; j < n; ++j) {
+        if (st[j] != UND || lam[j] != 0) continue;
+        st[j] = FPT;
+        for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q)
+            if (st[S.ci[q]] == UND) ++lam[S.ci[q]];
+    }
+    Tournament T(n, lam, st);
+    auto make_f = [&](int64_t j) {
+        st[j] = FPT;
+        T.update(j);
+        for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q) {
+            const int32_t k = S.ci[q];
+            if (st[k] == UND) {
+                ++lam[k];
+                T.update(k);
+            }
+        }
+    };
+    while (T.node[1] >= 0) {
+        const int64_t i = T.node[1];
         st[i] = CPT;
+        T.update(i);
         for (int64_t q = ST.rp[i]; q < ST.rp[i + 1]; ++q)
             if (st[ST.ci[q]] == UND) make_f(ST.ci[q]);
         for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
             const int32_t k = S.ci[q];
             if (st[k] != UND) continue;
             if (--lam[k] == 0) make_f(k);
-            else heap.push({lam[k], -(int64_t)k});
+            else T.update(k);
         }
     }
     for (auto &s : st)
@@ -196,11 +233,18 @@ Pattern second_strength(const Pattern &S, const std::vector<int8_t> &cf, int pat
 }
 
 std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths) {
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double t0 = now();
     std::vector<int8_t> cf = rs_first_pass(S);
     if (!aggressive) return cf;
+    double t1 = now();
     std::vector<int32_t> cpts;
     const Pattern S2 = second_strength(S, cf, paths, cpts);
+    double t2 = now();
     const std::vector<int8_t> cf2 = rs_first_pass(S2);
+    if (std::getenv("PLS_AMG_TRACE"))
+        fprintf(stderr, "[boomeramg coarsen] n %lld S nnz %lld: RS %.2f s; S2 (%zu C1 points, nnz %lld) %.2f s; RS2 %.2f s\n",
+                (long long)S.n, (long long)S.ci.size(), t1 - t0, cpts.size(), (long long)S2.ci.size(), t2 - t1, now() - t2);
     std::vector<int8_t> out(S.n, FPT);
     for (size_t c = 0; c < cpts.size(); ++c)
         if (cf2[c] == CPT) out[cpts[c]] = CPT;
@@ -274,17 +318,22 @@ HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> 
         }
     const int T = setup_threads();
     for (int p = 1;; ++p) {
-        std::vector<int32_t> pts;
-        for (int64_t i = 0; i < n; ++i) {
-            if (pass[i] >= 0) continue;
-            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
-                const int32_t k = S.ci[q];
-                if (pass[k] >= 0 && pass[k] < p) {
-                    pts.push_back((int32_t)i);
-                    break;
+        // the points of pass p, decided from the passes before p (rows in parallel, kept in order)
+        std::vector<std::vector<int32_t>> found(T);
+        parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
+            for (int64_t i = i0; i < i1; ++i) {
+                if (pass[i] >= 0) continue;
+                for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+                    const int32_t k = S.ci[q];
+                    if (pass[k] >= 0 && pass[k] < p) {
+                        found[t].push_back((int32_t)i);
+                        break;
+                    }
                 }
             }
-        }
+        });
+        std::vector<int32_t> pts;
+        for (auto &f : found) pts.insert(pts.end(), f.begin(), f.end());
         if (pts.empty()) break;
         for (int32_t i : pts) pass[i] = p;
         parallel_rows((int64_t)pts.size(), T, [&](int, int64_t t0, int64_t t1) {
@@ -564,12 +613,28 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
     return A;
 }
 
+// level count of a triangular solve with T (lower: forward, else backward)
+int64_t tri_levels(const HostCSR &T, bool upper) {
+    const int64_t n = T.nrows;
+    std::vector<int64_t> lev(n, 0);
+    int64_t top = 0;
+    for (int64_t t = 0; t < n; ++t) {
+        const int64_t i = upper ? n - 1 - t : t;
+        int64_t l = 0;
+        for (int64_t k = T.rp[i]; k < T.rp[i + 1]; ++k)
+            if (T.ci[k] != i) l = std::max(l, lev[T.ci[k]] + 1);
+        lev[i] = l;
+        top = std::max(top, l + 1);
+    }
+    return top;
+}
+
 struct RelaxSet {  // the points one Gauss-Seidel pass visits (all, C or F)
     int64_t m = 0;
     bool all = true;
     DBuf<int64_t> idx;
     DevCSR lo, up;
-    std::unique_ptr<PCILU> fwd, bwd;
+    std::unique_ptr<PC> fwd, bwd;  // (D + L)_II^-1, (D + U)_II^-1
 };
 
 struct BLevel {
@@ -633,6 +698,8 @@ struct PCBoomer : PC {
         const bool view = o.flag("pls.amg_view", false);
         const bool allow_lds = o.flag("pls.ilu_lds", true);
         const int gmem = (int)o.integer("pls.ilu_gmem", 0), ring = (int)o.integer("pls.ilu_ring", 1);
+        const int64_t dense_min = o.integer("pls.amg_gs_dense_min", 2048);
+        const int64_t dense_max = o.integer("pls.lu_dense_max", 32768);
         double tm[7] = {0};
         auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         double t0 = now();
@@ -672,10 +739,25 @@ struct PCBoomer : PC {
                         rs->idx.alloc(gi.size());
                         HIPCHK(hipMemcpyAsync(rs->idx.p, gi.data(), sizeof(int64_t) * gi.size(), hipMemcpyHostToDevice, c.st));
                     }
-                    upload(triangle(Al, g, true), rs->lo, c);
-                    upload(triangle(Al, g, false), rs->up, c);
-                    rs->fwd = std::make_unique<PCILU>(rs->lo, 1, c, false, allow_lds, 0, gmem, ring);
-                    rs->bwd = std::make_unique<PCILU>(rs->up, 1, c, false, allow_lds, 0, gmem, ring);
+                    const HostCSR lo = triangle(Al, g, true), up = triangle(Al, g, false);
+                    upload(lo, rs->lo, c);
+                    upload(up, rs->up, c);
+                    for (int half = 0; half < 2; ++half) {
+                        const HostCSR &T = half ? up : lo;
+                        DevCSR &Td = half ? rs->up : rs->lo;
+                        std::unique_ptr<PC> &pc = half ? rs->bwd : rs->fwd;
+                        // a mostly sequential triangle (Galerkin operators below an
+                        // aggressive level are ~30 % dense: every row a level of its
+                        // own) small enough for a dense inverse: one GEMV per half-sweep
+                        const int64_t nlev = tri_levels(T, half == 1);
+                        if (T.nrows >= dense_min && T.nrows <= dense_max && nlev * 8 >= T.nrows) {
+                            pc = std::make_unique<PCDenseLU>(Td, c);
+                        } else {
+                            // wide levels: one grid-wide launch per level beats one workgroup
+                            const int gm = (nlev > 0 && T.nrows / nlev > 256) ? -1 : gmem;
+                            pc = std::make_unique<PCILU>(Td, 1, c, false, allow_lds, 0, gm, ring);
+                        }
+                    }
                 }
                 L->sets.push_back(std::move(rs));
             }
@@ -731,7 +813,7 @@ struct PCBoomer : PC {
     void half_sweep(BLevel &L, size_t l, RelaxSet &s, bool lower, BWork &W, const double *b, double *x, bool x_zero,
                     Ctx &c) {
         if (s.m == 0) return;
-        PCILU &T = lower ? *s.fwd : *s.bwd;
+        PC &T = lower ? *s.fwd : *s.bwd;
         const double *r = b;
         if (!x_zero) {
             spmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
@@ -825,6 +907,9 @@ void boomeramg_host_level(const HostCSR &A, const Options &o, const std::string 
         ++l;
     }, tm);
     nlevels = l + 1;
+    if (o.flag("pls.amg_view", false))
+        fprintf(stderr, "[boomeramg host] strength %.2f coarsen %.2f interp %.2f RAP %.2f s (%d threads)\n", tm[1], tm[2],
+                tm[3], tm[4], setup_threads());
     if (level == l) {  // the coarsest operator (P empty)
         n = coarse.nrows;
         P = coarse;

@@ -70,13 +70,16 @@ def _boomer_db(no_cf=True):
 
 @pytest.mark.parametrize("spec", [S.SynthSpec(2, 16), S.SynthSpec(3, 5)], ids=["2d16", "3d5"])
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
-@pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-inexact", "hypre-inexact-cf", "hypre-sa"])
+@pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-inexact", "hypre-inexact-cf", "hypre-inexact-dense", "hypre-sa"])
 def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
     """hypre: PETSc's defaults (HMIS / ext+i, no truncation, no aggressive
     level, C/F-ordered Gauss-Seidel); -inexact: petsc-options-inexact's
-    settings; -cf: the same with C/F relaxation; -sa: pls.hypre sa."""
+    settings; -cf: the same with C/F relaxation; -dense: every Gauss-Seidel
+    half-sweep through its dense triangular inverse (pls.amg_gs_dense_min 0,
+    the path of mostly sequential coarse levels); -sa: pls.hypre sa."""
     params = dict(BASE, **{"pc type": pc_type, "inner pc type": "lu"})
-    extra = {"hypre-inexact": _boomer_db(), "hypre-inexact-cf": _boomer_db(False), "hypre-sa": {"pls.hypre": "sa"}}
+    extra = {"hypre-inexact": _boomer_db(), "hypre-inexact-cf": _boomer_db(False), "hypre-sa": {"pls.hypre": "sa"},
+             "hypre-inexact-dense": dict(_boomer_db(), **{"pls.amg_gs_dense_min": "0"})}
     db = _amg_db(t.split("-")[0], extra.get(t))
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)

@@ -10,6 +10,7 @@
 #   bench                       the headline bench line (default flags)
 #   prof                        rocprofv3 --kernel-trace --stats of the headline
 #   prof_fe                     same for the assembled 3-D N=12 whole-block ILU solve
+#   prof_amg                    same for the classical AMG (-pc_type hypre) on the s block, 3-D N=27
 #   configs                     bench on every BASELINE config that fits one GPU
 #   fe                          bench on the assembled swelling systems
 #   pmc                         FETCH_SIZE / WRITE_SIZE passes (tools/pmc.sh)
@@ -38,6 +39,7 @@ prof() {  # prof <dir> <bench args...>
     (cd /tmp && export TMPDIR=/tmp &&
      run "$dir/stdout" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/gpurun_out/$dir" -o run -- \
          python3 "$REPO/bench.py" "$@") || exit $?
+    rm -f "$REPO/gpurun_out/$dir"/run_kernel_trace.csv  # per-launch rows: too large to copy back
 }
 
 for s in "$@"; do
@@ -48,6 +50,7 @@ for s in "$@"; do
       smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
       bench) run configs/headline 500 python -u bench.py ;;
       prof) prof prof --steps 2 --warmup 1 --no-cpu ;;
+      prof_amg) prof prof_amg --N 27 --inner hypre --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
       prof_fe) prof prof_fe --system fe --N 12 --inner ilu --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
       configs)
         run configs/swelling2d-exact 400 python -u bench.py --config swelling2d-exact --steps 3 --no-copy-probe
