@@ -55,12 +55,12 @@ class BlockPC:
 
         def inner(prefix, M, ksp_type, pc_type, fields, rows=None):
             # G ranks: BJACOBI blocks live inside each rank's [field slabs] rows
-            # (oracle/dist.py); other PC types are the same at any G
+            # (oracle/dist.py); every other PC type acts on the whole block --
+            # libpls gathers it and applies the PC redundantly (PETSc's
+            # PCREDUNDANT), so it is the same PC at any G
             pc = None
             if dist_size > 1:
                 ptype = opt(db, prefix, "pc_type", pc_type)
-                if ptype in ("ilu", "lu", "cholesky"):
-                    raise ValueError(f"{prefix}pc_type {ptype} is not distributable; use bjacobi")
                 if ptype == "bjacobi":
                     from .dist import PCBJacobiIndexed, bjacobi_blocks, bjacobi_blocks_owned
                     nbt = opt(db, prefix, "pc_bjacobi_blocks", dist_size, int)
@@ -92,8 +92,7 @@ class BlockPC:
                 if ptype == "fieldsplit":
                     # setFieldSplitIS((None, is_p)) then ((None, is_f)): split 0 = pressure
                     from .fieldsplit import PCFieldSplit
-                    if dist_size > 1:
-                        raise ValueError("fieldsplit is restated for one rank only")
+                    # G ranks: the gathered fp block, redundantly (same PC at any G)
                     fs = PCFieldSplit(Mfp_fp, self.is_p, self.is_f, db, "fp_")
                     self.ksp_fp = petsc.ksp_from_options("fp_", db, Mfp_fp, Mfp_fp, "gmres", "fieldsplit", pc=fs)
                 else:

@@ -388,6 +388,11 @@ static void make_dist(DevCSR &M, const Dist &D, int f0, int f1, Comm *comm, Ctx 
     }
     H->nlocal = nlocal;
     H->nghost = pos;
+    H->l2g.resize(nlocal + pos);
+    for (int f = f0; f <= f1; ++f)
+        for (int64_t i = 0; i < D.len[f]; ++i) H->l2g[l_off[f] + i] = cs_off[f] + D.lo[f] + i;
+    for (int q = 0, k = 0; q < D.size; ++q)
+        for (int64_t g : need[q]) H->l2g[nlocal + k++] = g;
     std::vector<std::vector<int64_t>> asked;
     comm->alltoallv_i64(need, asked);
     std::vector<int32_t> sidx;
@@ -442,6 +447,7 @@ struct Handle {
     std::vector<int64_t> perm;   // internal -> caller
     std::vector<int32_t> fp_is_f, fp_is_p;  // 2-way: f / p positions inside the sorted fp set (IndexSet.py:10-26)
     std::unique_ptr<PCFieldSplit> fs_fp;     // fp_ fieldsplit PC (2-way, inexact inner PC)
+    std::unique_ptr<PC> pc_red_fp;           // ... on a sharded fp block: gathered, redundant
     bool mixer_ready = false;
     DBuf<int64_t> dperm;
     DevCSR A, P, Pd;
@@ -740,7 +746,19 @@ static void do_setup(Handle &H) {
             if (pt == "fieldsplit") {
                 // setup_fieldsplit (Preconditioner.py:102-118): setFieldSplitIS((None, is_p)) then
                 // ((None, is_f)) -- split 0 = pressure, split 1 = fluid, fp-local positions
-                if (H.distributed) throw Error("fp_pc_type fieldsplit is not available with several ranks");
+                if (H.distributed) {
+                    // sharded fp block: the fieldsplit PC on the gathered block (field-major
+                    // global order: split 0 = p = [nf, nf + np), split 1 = f = [0, nf)), redundantly
+                    std::vector<int32_t> gf(H.dist.n[1]), gp(H.dist.n[2]);
+                    for (int64_t i = 0; i < H.dist.n[1]; ++i) gf[i] = (int32_t)i;
+                    for (int64_t i = 0; i < H.dist.n[2]; ++i) gp[i] = (int32_t)(H.dist.n[1] + i);
+                    H.pc_red_fp = make_redundant("fieldsplit", H.Kfp, c, [&](const DevCSR &Gm, Ctx &sc) -> std::unique_ptr<PC> {
+                        return std::make_unique<PCFieldSplit>(Gm, gp, gf, o, "fp_", sc);
+                    }, "fp_");
+                    H.ksp_fp = make_ksp("fp_", o, &H.Kfp, &H.Kfp, "gmres", "fieldsplit", c, 1e-5, 1e-50, 1e4, 10000, 30,
+                                        H.pc_red_fp.get());
+                    goto fp_done;
+                }
                 std::vector<int32_t> fpf = H.fp_is_f, fpp = H.fp_is_p;
                 if (fpf.empty() && fpp.empty()) {  // field-major fp block: [f | p]
                     for (int64_t i = 0; i < H.nf; ++i) fpf.push_back((int32_t)i);
@@ -754,6 +772,7 @@ static void do_setup(Handle &H) {
             }
         }
     }
+fp_done:
     // the inner Anderson history lives as long as the preconditioner object
     // (lib/Preconditioner.py: created in __init__, not in setUp)
     if (!H.mixer_ready) {

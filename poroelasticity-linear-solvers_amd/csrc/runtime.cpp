@@ -13,6 +13,7 @@
 #include <climits>
 
 #include <algorithm>
+#include <functional>
 #include <numeric>
 #include <cmath>
 #include <cstdio>
@@ -1236,14 +1237,150 @@ std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
                                    (int)o.integer("pls.ilu_ring", 1));
 }
 
+// PETSc PCREDUNDANT semantics for PCs that act on a whole parallel block
+// (ILU(0), LU, classical / smoothed-aggregation AMG) when the block is
+// sharded over G ranks: every rank gathers the block (its MPIAIJ rows with
+// block-global column indices, Halo::l2g) into the global matrix in the
+// block's global order, builds the PC on it with a single-rank context, and
+// per application allgathers x, applies the PC redundantly and keeps its own
+// rows.  The result is the one-rank PC's result on the same block, bitwise.
+struct PCRedundant : PC {
+    std::unique_ptr<Ctx> self;  // own stream, single-rank communicator
+    DevCSR Gm;                  // the gathered global block
+    std::unique_ptr<PC> inner;
+    int64_t nloc = 0, maxloc = 0, N = 0;
+    DBuf<int64_t> src, mine;    // xg[g] = gathered[src[g]];  y[i] = yg[mine[i]]
+    DBuf<double> sendbuf, gath, xg, yg;
+    hipEvent_t ev_a = nullptr, ev_b = nullptr;
+
+    PCRedundant(const std::string &t, const DevCSR &M, Ctx &c,
+                const std::function<std::unique_ptr<PC>(const DevCSR &, Ctx &)> &factory, const std::string &prefix) {
+        type = t;
+        n = nloc = M.nrows;
+        const Halo &H = *M.halo;
+        if ((int64_t)H.l2g.size() < M.ncols || H.nlocal != M.nrows)
+            throw Error("redundant PC (prefix " + prefix + "): block is not a diagonal block of the sharded system");
+        Comm &cm = *c.comm;
+        const int G = cm.size;
+        // host CSR of my rows, block-global rows / columns
+        const HostCSR L = download(M, c);
+        std::vector<int64_t> cnt{nloc, (int64_t)L.ci.size()}, all(2 * G);
+        cm.allgather_host(cnt.data(), sizeof(int64_t) * 2, all.data());
+        int64_t maxnnz = 0;
+        for (int q = 0; q < G; ++q) {
+            maxloc = std::max(maxloc, all[2 * q]);
+            maxnnz = std::max(maxnnz, all[2 * q + 1]);
+            N += all[2 * q];
+        }
+        // message: rows (global ids), row lengths, columns (global), values -- padded to the largest rank's
+        const int64_t words = 2 * maxloc + 2 * maxnnz;
+        std::vector<int64_t> msg(words, 0), recv((size_t)words * G);
+        for (int64_t i = 0; i < nloc; ++i) {
+            msg[i] = H.l2g[i];
+            msg[maxloc + i] = L.rp[i + 1] - L.rp[i];
+        }
+        for (size_t k = 0; k < L.ci.size(); ++k) {
+            msg[2 * maxloc + k] = H.l2g[L.ci[k]];
+            std::memcpy(&msg[2 * maxloc + maxnnz + k], &L.v[k], sizeof(double));
+        }
+        cm.allgather_host(msg.data(), sizeof(int64_t) * words, recv.data());
+        // global CSR: row g from its owner, columns sorted
+        std::vector<int64_t> rowlen(N, -1), srcslot(N, -1), rowpos(N);
+        for (int q = 0; q < G; ++q) {
+            const int64_t *m = recv.data() + (size_t)words * q;
+            for (int64_t i = 0; i < all[2 * q]; ++i) {
+                const int64_t g = m[i];
+                if (g < 0 || g >= N || rowlen[g] >= 0) throw Error("redundant PC: inconsistent row ownership");
+                rowlen[g] = m[maxloc + i];
+                srcslot[g] = q * maxloc + i;
+            }
+        }
+        HostCSR Gh;
+        Gh.nrows = Gh.ncols = N;
+        Gh.rp.assign(N + 1, 0);
+        for (int64_t g = 0; g < N; ++g) Gh.rp[g + 1] = Gh.rp[g] + rowlen[g];
+        Gh.ci.resize(Gh.rp[N]);
+        Gh.v.resize(Gh.rp[N]);
+        std::vector<std::pair<int64_t, double>> row;
+        for (int q = 0; q < G; ++q) {
+            const int64_t *m = recv.data() + (size_t)words * q;
+            int64_t k = 0;
+            for (int64_t i = 0; i < all[2 * q]; ++i) {
+                const int64_t g = m[i], len = m[maxloc + i];
+                row.resize(len);
+                for (int64_t e = 0; e < len; ++e, ++k) {
+                    double v;
+                    std::memcpy(&v, &m[2 * maxloc + maxnnz + k], sizeof(double));
+                    row[e] = {m[2 * maxloc + k], v};
+                }
+                std::sort(row.begin(), row.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+                for (int64_t e = 0; e < len; ++e) {
+                    Gh.ci[Gh.rp[g] + e] = (int32_t)row[e].first;
+                    Gh.v[Gh.rp[g] + e] = row[e].second;
+                }
+            }
+        }
+        self = std::make_unique<Ctx>();
+        self->sell_d16 = c.sell_d16;
+        self->d16_wide_lpr = c.d16_wide_lpr;
+        self->d16_unroll = c.d16_unroll;
+        self->d16_segs = c.d16_segs;
+        self->d16_sigma = c.d16_sigma;
+        self->d16_sigma_pad = c.d16_sigma_pad;
+        self->d16_sorted_lpr = c.d16_sorted_lpr;
+        self->spmv_b3 = c.spmv_b3;
+        upload(Gh, Gm, *self);
+        inner = factory(Gm, *self);
+        std::vector<int64_t> mg(H.l2g.begin(), H.l2g.begin() + nloc);
+        src.alloc(std::max<int64_t>(N, 1));
+        mine.alloc(std::max<int64_t>(nloc, 1));
+        HIPCHK(hipMemcpyAsync(src.p, srcslot.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, c.st));
+        if (nloc) HIPCHK(hipMemcpyAsync(mine.p, mg.data(), sizeof(int64_t) * nloc, hipMemcpyHostToDevice, c.st));
+        sendbuf.alloc(std::max<int64_t>(maxloc, 1));
+        HIPCHK(hipMemsetAsync(sendbuf.p, 0, sizeof(double) * std::max<int64_t>(maxloc, 1), c.st));
+        gath.alloc(std::max<int64_t>(maxloc * G, 1));
+        xg.alloc(std::max<int64_t>(N, 1));
+        yg.alloc(std::max<int64_t>(N, 1));
+        HIPCHK(hipEventCreateWithFlags(&ev_a, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_b, hipEventDisableTiming));
+        self->sync();
+        c.sync();
+    }
+    ~PCRedundant() override {
+        if (ev_a) (void)hipEventDestroy(ev_a);
+        if (ev_b) (void)hipEventDestroy(ev_b);
+    }
+    void apply(const double *x, double *y, Ctx &c) override {
+        if (nloc) launch_copy(nloc, x, sendbuf.p, c.st);
+        c.comm->allgather_dev(sendbuf.p, (int)std::max<int64_t>(maxloc, 1), gath.p, c.st);
+        launch_gather(N, src.p, gath.p, xg.p, c.st);
+        HIPCHK(hipEventRecord(ev_a, c.st));
+        HIPCHK(hipStreamWaitEvent(self->st, ev_a, 0));
+        inner->apply(xg.p, yg.p, *self);
+        HIPCHK(hipEventRecord(ev_b, self->st));
+        HIPCHK(hipStreamWaitEvent(c.st, ev_b, 0));
+        launch_gather(nloc, mine.p, yg.p, y, c.st);
+    }
+};
+
+std::unique_ptr<PC> make_redundant(const std::string &type, const DevCSR &M, Ctx &c,
+                                   const std::function<std::unique_ptr<PC>(const DevCSR &, Ctx &)> &factory,
+                                   const std::string &prefix) {
+    return std::make_unique<PCRedundant>(type, M, c, factory, prefix);
+}
+
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c) {
     if (type == "none") return std::make_unique<PCNone>(M.nrows);
     if (type == "jacobi") return std::make_unique<PCJacobi>(M, c);
     const bool dist = c.comm && c.comm->size > 1;
-    if (dist && (type == "ilu" || type == "lu" || type == "cholesky"))
-        throw Error("PC type '" + type + "' (prefix " + prefix +
-                    ") acts on the whole parallel matrix; with several ranks use bjacobi (ILU(0) per rank block)");
+    // whole-block PCs on a sharded block: gathered and applied redundantly (PCREDUNDANT)
+    if (M.halo && (type == "ilu" || type == "lu" || type == "cholesky" || type == "gamg" || type == "hypre")) {
+        if (o.flag("pls.redundant_error", false))
+            throw Error("PC type '" + type + "' (prefix " + prefix + ") acts on the whole parallel matrix (pls.redundant_error)");
+        return make_redundant(type, M, c, [&](const DevCSR &Gm, Ctx &sc) { return make_pc(type, Gm, o, prefix, sc); },
+                              prefix);
+    }
     if (type == "ilu") {
         if (o.integer(prefix + "pc_factor_levels", 0) != 0)
             throw Error(prefix + "pc_factor_levels > 0: only ILU(0) is implemented");

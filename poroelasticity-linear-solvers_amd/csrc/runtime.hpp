@@ -9,6 +9,7 @@
 
 #include <cstdint>
 #include <map>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -126,6 +127,9 @@ struct DevSELL {
 // other ranks need are packed and exchanged into `ghost`.
 struct Halo {
     int64_t nlocal = 0, nghost = 0, nsend = 0;
+    // block-global index of every local column (owned [0, nlocal), then the
+    // ghosts); for a diagonal block also of every local row (host, setup only)
+    std::vector<int64_t> l2g;
     DBuf<int32_t> send_idx;
     DBuf<double> sendbuf, ghost;
     std::vector<int64_t> scnt, soff, rcnt, roff;
@@ -390,6 +394,11 @@ struct PCFieldSplit : PC {
     void apply(const double *x, double *y, Ctx &c) override;
 };
 
+// PCREDUNDANT: a sharded diagonal block (Halo::l2g) gathered on every rank,
+// factory(global block, single-rank context) builds the PC applied redundantly.
+std::unique_ptr<PC> make_redundant(const std::string &type, const DevCSR &M, Ctx &c,
+                                   const std::function<std::unique_ptr<PC>(const DevCSR &, Ctx &)> &factory,
+                                   const std::string &prefix);
 // Configure a KSP from programmatic defaults + options (setFromOptions order).
 std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const DevCSR *Amat, const DevCSR *Pmat,
                               const std::string &default_ksp, const std::string &default_pc, Ctx &c,
