@@ -599,12 +599,12 @@ __global__ __launch_bounds__(TPB) void k_final(int nb, const double *partial, do
     if (threadIdx.x == 0) out[j] = sqrt_it ? sqrt(v) : v;
 }
 
-// mdot: blockIdx.x = chunk, blockIdx.y = group of 4 vectors
+// mdot: blockIdx.x = chunk, blockIdx.y = group of MDOT_NJ vectors
 // CGS dot block h_j = V_j . w, j in [0, k): blocks of MDOT_NJ columns per
 // grid row, 16-B loads (pairs of rows; chunks start on even rows, V columns
 // are 512-B aligned), one partial per (column, block) -> k_final in fixed order.
 typedef double cgs_d2 __attribute__((ext_vector_type(2)));
-static constexpr int MDOT_NJ = 8;
+static constexpr int MDOT_NJ = 16;
 __device__ __forceinline__ void chunk_even(int64_t n, int nb, int b, int64_t &s, int64_t &e) {
     int64_t c = (n + nb - 1) / nb;
     c = (c + 1) & ~(int64_t)1;
@@ -683,8 +683,8 @@ void launch_norm2(int64_t n, const double *x, double *partial, double *out, hipS
 }
 
 // w -= sum_j h[j] V[:, j] (j ascending, as VecMAXPY); partial ||w||^2.
-// Pairs of rows per thread (16-B loads), four basis columns loaded ahead of
-// their FMAs so every lane keeps 4-5 loads in flight.
+// Pairs of rows per thread (16-B loads), eight basis columns loaded ahead of
+// their FMAs so every lane keeps 8-9 loads in flight.
 __global__ __launch_bounds__(TPB) void k_maxpy_norm(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
                                                     const double *__restrict__ h, double *__restrict__ w,
                                                     double *partial) {
@@ -698,12 +698,12 @@ __global__ __launch_bounds__(TPB) void k_maxpy_norm(int64_t n, int k, const doub
     for (int64_t i = s + 2 * threadIdx.x; i + 1 < e; i += 2 * TPB) {
         cgs_d2 t = *reinterpret_cast<const cgs_d2 *>(w + i);
         int j = 0;
-        for (; j + 4 <= k; j += 4) {
-            cgs_d2 v[4];
+        for (; j + 8 <= k; j += 8) {
+            cgs_d2 v[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const cgs_d2 *>(V + (int64_t)(j + u) * ldv + i);
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const cgs_d2 *>(V + (int64_t)(j + u) * ldv + i);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < 8; ++u) {
                 const double hj = (j + u) < 512 ? hs[j + u] : h[j + u];
                 t.x -= hj * v[u].x;
                 t.y -= hj * v[u].y;
