@@ -122,12 +122,24 @@ static void spmv_rows(const int64_t *rp, const int32_t *ci, const double *v, int
     }
 }
 
+/* fixed-order dot: 64 contiguous chunks summed left to right, then the chunk
+ * sums in order -- the same value for any thread count and any run (an
+ * OpenMP reduction combines the threads' partials in completion order, which
+ * moved GMRES's crossing of rtol by several iterations between runs) */
 static double dot(int64_t n, const double *a, const double *b) {
-    double s = 0.0;
+    enum { NCH = 64 };
+    double part[NCH];
 #ifdef _OPENMP
-#pragma omp parallel for schedule(static) reduction(+ : s)
+#pragma omp parallel for schedule(static)
 #endif
-    for (int64_t i = 0; i < n; ++i) s += a[i] * b[i];
+    for (int c = 0; c < NCH; ++c) {
+        const int64_t lo = n * c / NCH, hi = n * (c + 1) / NCH;
+        double s = 0.0;
+        for (int64_t i = lo; i < hi; ++i) s += a[i] * b[i];
+        part[c] = s;
+    }
+    double s = 0.0;
+    for (int c = 0; c < NCH; ++c) s += part[c];
     return s;
 }
 

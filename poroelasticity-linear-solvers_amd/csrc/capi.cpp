@@ -189,8 +189,9 @@ struct AndersonLS {
 __global__ void k_anderson_update(int64_t n, int mk, const double *const *X, const double *const *F,
                                   const double *alpha, double beta, const double *f, double *y) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        double v = y[e] + beta * f[e];
-        for (int i = 0; i < mk; ++i) v = v + alpha[i] * (X[i][e] + beta * F[i][e]);
+        // the oracle's operation order, no contraction (AAR.py:109-111)
+        double v = __dadd_rn(y[e], __dmul_rn(beta, f[e]));
+        for (int i = 0; i < mk; ++i) v = __dadd_rn(v, __dmul_rn(alpha[i], __dadd_rn(X[i][e], __dmul_rn(beta, F[i][e]))));
         y[e] = v;
     }
 }

@@ -3,9 +3,11 @@ through pls_anderson_* against the oracle's restatement (oracle/aar.py).
 
 The same sequence of g_k vectors goes to both (open loop: the oracle's own
 fixed-point iteration x_{k+1} = G(x_k) generates it), so each mixed iterate is
-compared without feedback.  Bound: 1e-12 relative to ||x_k||, far above the
-Householder-vs-TSQR rounding of these well-conditioned histories (cond(R)
-recorded by the oracle and asserted small).  The g_k repeated twice in a row
+compared without feedback.  Bound: relative to ||x_k||, 10x the oracle's own
+deviation when its numpy QR is swapped for the device's TSQR (measured per
+case), at least 1e-11 (the open loop carries the device's rounding through up
+to 24 steps of X / F histories: 1.7e-12 measured at step 20 of n = 1000,
+order 3); cond(R) recorded by the oracle and asserted small.  The g_k repeated twice in a row
 exercises the reference's ||delta f|| < 1e-12 branch (AndersonAcceleration.py:
 44-46: k -= 1, x_k = g_k)."""
 import numpy as np
@@ -16,13 +18,15 @@ from oracle.aar import AndersonAcceleration as OracleAA
 pytestmark = pytest.mark.gpu
 
 
-def _sequence(n, order, steps, seed):
-    """g_k of a damped linear fixed-point map mixed by the oracle."""
+def _sequence(n, order, steps, seed, lstsq=None):
+    """g_k of a damped linear fixed-point map mixed by the oracle (lstsq: the
+    oracle's least-squares hook, e.g. the device's TSQR algorithm)."""
     rng = np.random.default_rng(seed)
     M = rng.standard_normal((n, n)) / np.sqrt(n)
     M = 0.9 * M / np.max(np.abs(np.linalg.eigvals(M)))
     c = rng.standard_normal(n)
     aa = OracleAA(order)
+    aa.lstsq = lstsq
     x = np.zeros(n)
     gs, xs = [], []
     for k in range(steps):
@@ -36,11 +40,16 @@ def _sequence(n, order, steps, seed):
     return gs, xs, aa.max_cond
 
 
-@pytest.mark.parametrize("n,order", [(300, 1), (1000, 3), (2048, 5), (777, 15)])
-def test_anderson_matches_oracle(gpu, n, order):
+@pytest.mark.parametrize("n,order,steps", [(300, 1, 24), (1000, 3, 24), (2048, 5, 24), (4096, 10, 10)])
+def test_anderson_matches_oracle(gpu, n, order, steps):
     from lib.AndersonAcceleration import AndersonAcceleration
-    gs, xs, cond = _sequence(n, order, 24, seed=n + order)
+    from oracle.aar import tsqr_lstsq
+    gs, xs, cond = _sequence(n, order, steps, seed=n + order)
     assert cond < 1e8
+    # bound: 10x the oracle's own deviation when its numpy QR is replaced by the
+    # device's Householder TSQR (same g sequence), at least 1e-12
+    _, xt, _ = _sequence(n, order, steps, seed=n + order, lstsq=tsqr_lstsq)
+    tol = max(1e-11, 10 * max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(xt, xs)))
     aa = AndersonAcceleration(order)
     try:
         for k, (g, xo) in enumerate(zip(gs, xs)):
@@ -48,7 +57,7 @@ def test_anderson_matches_oracle(gpu, n, order):
             out = aa.get_next_vector(v)
             assert out is v  # in place, as the reference's self.xk.copy(gk)
             err = np.linalg.norm(v - xo) / np.linalg.norm(xo)
-            assert err <= 1e-12, (k, err)
+            assert err <= tol, (k, err, tol)
     finally:
         aa.destroy()
 
