@@ -323,7 +323,7 @@ __global__ __launch_bounds__(SR * 256) void k_band_sweep(int64_t n, int64_t nb, 
                                                         const double *__restrict__ Gn, const double *__restrict__ b,
                                                         double *__restrict__ y, uint64_t *Gr, uint64_t *ticket,
                                                         uint64_t ticket_base, uint32_t epoch, int upper,
-                                                        int32_t *fail) {
+                                                        int32_t *fail, int64_t plen) {
     static_assert(SR == 2, "the chain below is written for two positions per workgroup");
     __shared__ int64_t sp;
     __shared__ double ys[BT];
@@ -334,6 +334,10 @@ __global__ __launch_bounds__(SR * 256) void k_band_sweep(int64_t n, int64_t nb, 
     const int64_t nsr = (nb + SR - 1) / SR;
     if (sp < 0 || sp >= nsr) return;  // uniform
     const int64_t p0 = sp * SR;
+    // SPIKE partitions (plen > 0, a multiple of SR): the chain restarts at the
+    // first position of every partition (couplings to the previous partition
+    // are applied afterwards through the spikes)
+    const int64_t ps = plen > 0 ? (p0 / plen) * plen : 0;
     const int g = threadIdx.x >> 8, lt = threadIdx.x & 255, row = lt >> 2, part = lt & 3;
     const int64_t W = bl + bu + 1, bw = upper ? bu : bl;  // tiles on the solved side
     const int64_t pI = p0 + g;
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(SR * 256) void k_band_sweep(int64_t n, int64_t nb, 
     auto tile_row = [&](int64_t pJ) { return upper ? nb - 1 - pJ : pJ; };
     auto tile = [&](int64_t pJ) { return T + (I * W + (tile_row(pJ) - I + bl)) * TILE + row * BT + part * 16; };
     // off the chain: b, Dinv and the near-tile product
-    const bool has_near = act && bw >= 1 && pI >= 1;
+    const bool has_near = act && bw >= 1 && pI >= 1 && pI - 1 >= ps;
     double bi = 0.0;
     bd_d2 dm[8], gm[8];
     if (act) {
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(SR * 256) void k_band_sweep(int64_t n, int64_t nb, 
     // far tiles preceding the super-row: positions [p0 - bw, p0 - 2]; group g
     // uses [pI - bw, pI - 2]
     double acc = 0.0;
-    for (int64_t pJ = (p0 - bw > 0 ? p0 - bw : 0); pJ <= p0 - 2; ++pJ) {
+    for (int64_t pJ = (p0 - bw > ps ? p0 - bw : ps); pJ <= p0 - 2; ++pJ) {
         const bool use = act && pJ >= pI - bw;
         bd_d2 m[8];
         if (use) band_load16(m, tile(pJ), true);
@@ -370,12 +374,12 @@ __global__ __launch_bounds__(SR * 256) void k_band_sweep(int64_t n, int64_t nb, 
         if (part == 0) rs[0][row] = bi - r;
     }
     bd_d2 m1[8];
-    const bool use1 = act && g == 1 && p0 >= 1 && p0 - 1 >= pI - bw;
+    const bool use1 = act && g == 1 && p0 > ps && p0 - 1 >= pI - bw;
     if (use1) band_load16(m1, tile(p0 - 1), true);
     __syncthreads();
     double c0 = 0.0;
     if (g == 0 && act) c0 = band_rowsum(band_dot16(dm, rs[0], part));
-    if (p0 >= 1 && bw >= 1) {
+    if (p0 > ps && bw >= 1) {
         band_stage(gr, tile_row(p0 - 1), epoch, ys, fail);  // the cross-workgroup hop
         if (g == 0 && act) {
             const double v = c0 - band_rowsum(band_dot16(gm, ys, part));
@@ -406,10 +410,166 @@ int64_t band_sweep_tickets(int64_t nb) { return (nb + SR - 1) / SR; }
 
 void launch_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu, const double *T, const double *Dinv,
                        const double *Gn, const double *b, double *y, uint64_t *Gr, uint64_t *ticket,
-                       uint64_t ticket_base, uint32_t epoch, int upper, int32_t *fail, hipStream_t st) {
+                       uint64_t ticket_base, uint32_t epoch, int upper, int32_t *fail, hipStream_t st, int64_t plen) {
     if (nb > 0)
         k_band_sweep<<<(unsigned)band_sweep_tickets(nb), SR * 256, 0, st>>>(n, nb, bl, bu, T, Dinv, Gn, b, y, Gr,
-                                                                            ticket, ticket_base, epoch, upper, fail);
+                                                                            ticket, ticket_base, epoch, upper, fail,
+                                                                            plen);
+}
+
+// ------------------------------------------------------------------ SPIKE --
+// Partitioned triangle solve.  Positions (as in the sweep) are cut into
+// partitions of plen positions (plen >= bw, a multiple of SR).  With t_k the
+// solution on the last bw positions of partition k - 1 (its "tail"), the
+// solution on partition k is  y = z - W t_k,  where z is the partition's own
+// chain (k_band_sweep with plen: couplings to earlier partitions dropped) and
+// the spikes  W[p][c] = Dinv_p (T(p, q_c) - sum_{p' in k, p - bw <= p' < p}
+// T(p, p') W[p'][c])  (q_c = first position of k - bw + c; T(p, q_c) = 0
+// outside the band) are formed once at setup, one tile GEMM chain per
+// (partition, c) in parallel.  Per sweep: the partitions' chains run
+// concurrently (plen / SR hops instead of nb / SR), then the tails are
+// corrected partition by partition (P - 2 small launches), then every other
+// position in one bandwidth-bound pass.  W takes nb x bw tiles.
+__device__ __forceinline__ void band_tile_mac(const double *A, const double *B, double (*at)[BT + 1],
+                                              double (*b)[BT + 1], double acc[4][4]) {
+    __syncthreads();  // the previous product is done with the staging tiles
+    for (int t = threadIdx.x; t < BT * BT; t += BTPB) {
+        const int r = t / BT, cc = t % BT;
+        at[cc][r] = A[t];
+        b[r][cc] = B[t];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    for (int kk = 0; kk < BT; ++kk) {
+        double av[4], bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) av[r] = at[kk][ty + 16 * r];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[q] = b[kk][tx + 16 * q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] += av[r] * bv[q];
+    }
+}
+
+// spikes of position offset t in every partition k >= 1: blockIdx.x = c, blockIdx.y = k - 1
+__global__ __launch_bounds__(BTPB) void k_spike_w(int64_t nb, int64_t bl, int64_t bu, int upper, int64_t plen,
+                                                  int64_t t, const double *__restrict__ T,
+                                                  const double *__restrict__ Dinv, double *__restrict__ Wt) {
+    __shared__ double at[BT][BT + 1];
+    __shared__ double bb[BT][BT + 1];
+    __shared__ double cs[BT][BT + 1];
+    const int64_t W = bl + bu + 1, bw = upper ? bu : bl;
+    const int64_t c = blockIdx.x, k = (int64_t)blockIdx.y + 1, k0 = k * plen;
+    const int64_t pI = k0 + t, kend = (k0 + plen < nb) ? k0 + plen : nb;
+    if (pI >= kend) return;
+    auto trow = [&](int64_t p) { return upper ? nb - 1 - p : p; };
+    auto tile = [&](int64_t pa, int64_t pb) { return T + (trow(pa) * W + (trow(pb) - trow(pa) + bl)) * TILE; };
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    double acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[r][q] = 0.0;
+    // sum_{p'} T(pI, p') W[p'][c], p' ascending
+    for (int64_t pJ = (pI - bw > k0 ? pI - bw : k0); pJ < pI; ++pJ)
+        band_tile_mac(tile(pI, pJ), Wt + (pJ * bw + c) * TILE, at, bb, acc);
+    // cs = T(pI, q_c) - sum
+    const int64_t qc = k0 - bw + c;
+    const bool in_band = qc >= 0 && qc >= pI - bw;
+    const double *Tq = in_band ? tile(pI, qc) : nullptr;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = ty + 16 * r, j = tx + 16 * q;
+            cs[i][j] = (in_band ? Tq[i * BT + j] : 0.0) - acc[r][q];
+        }
+    __syncthreads();
+    // W[pI][c] = Dinv(pI) cs
+    const double *D = Dinv + trow(pI) * TILE;
+    double o[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[r][q] = 0.0;
+    for (int kk = 0; kk < BT; ++kk) {
+        double dv[4], cv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dv[r] = D[(ty + 16 * r) * BT + kk];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cv[q] = cs[kk][tx + 16 * q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[r][q] += dv[r] * cv[q];
+    }
+    double *out = Wt + (pI * bw + c) * TILE;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(ty + 16 * r) * BT + tx + 16 * q] = o[r][q];
+}
+
+void launch_spike_setup(int64_t nb, int64_t bl, int64_t bu, int upper, int64_t plen, const double *T,
+                        const double *Dinv, double *Wt, hipStream_t st) {
+    const int64_t bw = upper ? bu : bl, P = (nb + plen - 1) / plen;
+    if (P < 2 || bw == 0) return;
+    for (int64_t t = 0; t < plen; ++t)
+        k_spike_w<<<dim3((unsigned)bw, (unsigned)(P - 1)), BTPB, 0, st>>>(nb, bl, bu, upper, plen, t, T, Dinv, Wt);
+}
+
+// y_p -= sum_c W[p][c] y_{q_c} for the positions p0 + blockIdx.x (one workgroup
+// each; thread t: row t / 4, columns 16 (t % 4) .. +16 of every tile; sums in
+// c, then column order, then the 4 parts).  mode 0: the tail positions of
+// partition k (p0 = its last bw positions); mode 1: every position of every
+// partition k >= 1 except the tails already corrected (p0 = 0, all nb).
+__global__ __launch_bounds__(BTPB) void k_spike_correct(int64_t n, int64_t nb, int64_t bw, int upper, int64_t plen,
+                                                        int64_t p0, int mode, const double *__restrict__ Wt,
+                                                        double *__restrict__ y) {
+    __shared__ double ts[BT];
+    const int64_t pI = p0 + blockIdx.x;
+    if (pI >= nb) return;
+    const int64_t k = pI / plen, k0 = k * plen, kend = (k0 + plen < nb) ? k0 + plen : nb;
+    const int64_t P = (nb + plen - 1) / plen;
+    if (k == 0) return;
+    if (mode == 1 && k < P - 1 && pI >= kend - bw) return;  // a tail: done by mode 0
+    auto trow = [&](int64_t p) { return upper ? nb - 1 - p : p; };
+    const int lt = threadIdx.x, row = lt >> 2, part = lt & 3;
+    double s = 0.0;
+    for (int64_t c = 0; c < bw; ++c) {
+        const int64_t qc = k0 - bw + c;
+        __syncthreads();
+        if (lt < BT) {
+            const int64_t gq = trow(qc) * BT + lt;
+            ts[lt] = (qc >= 0 && gq < n) ? y[gq] : 0.0;
+        }
+        __syncthreads();
+        const bd_d2 *w = reinterpret_cast<const bd_d2 *>(Wt + (pI * bw + c) * TILE + row * BT + part * 16);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bd_d2 m = __builtin_nontemporal_load(w + u);
+            s += m.x * ts[part * 16 + 2 * u];
+            s += m.y * ts[part * 16 + 2 * u + 1];
+        }
+    }
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    const int64_t gi = trow(pI) * BT + row;
+    if (part == 0 && gi < n) y[gi] = y[gi] - s;
+}
+
+void launch_spike_apply(int64_t n, int64_t nb, int64_t bw, int upper, int64_t plen, const double *Wt, double *y,
+                        hipStream_t st) {
+    const int64_t P = (nb + plen - 1) / plen;
+    if (P < 2 || bw == 0) return;
+    for (int64_t k = 1; k + 1 < P; ++k) {  // tails, in partition order (each needs the previous one final)
+        const int64_t kend = (k + 1) * plen;
+        k_spike_correct<<<(unsigned)bw, BTPB, 0, st>>>(n, nb, bw, upper, plen, kend - bw, 0, Wt, y);
+    }
+    k_spike_correct<<<(unsigned)nb, BTPB, 0, st>>>(n, nb, bw, upper, plen, 0, 1, Wt, y);
 }
 
 }  // namespace pls

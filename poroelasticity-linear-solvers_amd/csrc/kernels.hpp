@@ -242,6 +242,13 @@ void launch_band_factor(int64_t nb, int64_t bl, int64_t bu, double *T, double *D
 int64_t band_sweep_tickets(int64_t nb);
 void launch_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu, const double *T, const double *Dinv,
                        const double *Gn, const double *b, double *y, uint64_t *Gr, uint64_t *ticket,
-                       uint64_t ticket_base, uint32_t epoch, int upper, int32_t *fail, hipStream_t st);
+                       uint64_t ticket_base, uint32_t epoch, int upper, int32_t *fail, hipStream_t st, int64_t plen = 0);
+// SPIKE partitioned sweeps (band.hip): spikes W (nb x bw tiles) of a triangle
+// (upper = 0: L / Dl, bw = bl; 1: U / Du, bw = bu) for partitions of plen
+// positions; apply = the corrections after a launch_band_sweep(..., plen).
+void launch_spike_setup(int64_t nb, int64_t bl, int64_t bu, int upper, int64_t plen, const double *T,
+                        const double *Dinv, double *Wt, hipStream_t st);
+void launch_spike_apply(int64_t n, int64_t nb, int64_t bw, int upper, int64_t plen, const double *Wt, double *y,
+                        hipStream_t st);
 
 }  // namespace pls

@@ -1176,7 +1176,7 @@ void csr_bandwidths(const DevCSR &M, int64_t &kl, int64_t &ku, Ctx &c) {
     }
 }
 
-PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c) {
+PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c, int64_t spike_plen) {
     type = "lu";
     n = M.nrows;
     if (M.ncols != n) throw Error("lu: block is not square");
@@ -1200,6 +1200,26 @@ PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c) {
     launch_band_factor(nb, bl, bu, T.p, Dl.p, Du.p, Gl.p, Gu.p, fail.p, c.st);
     HIPCHK(hipGetLastError());
     if (check_fail(c)) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+    // SPIKE partitions (band.hip): ~16 concurrent chains per triangle
+    const int64_t bwmax = std::max<int64_t>(std::max(bl, bu), 1);
+    int64_t pl = spike_plen < 0 ? std::max(bwmax, (nb + 15) / 16) : spike_plen;
+    if (pl > 0) {
+        pl = std::max(pl, bwmax);
+        pl += pl & 1;  // whole super-rows
+    }
+    if (pl > 0 && pl < nb && (bl > 0 || bu > 0)) {
+        plen = pl;
+        if (bl > 0) {
+            Wl.alloc((size_t)(nb * bl) * 4096);
+            launch_spike_setup(nb, bl, bu, 0, plen, T.p, Dl.p, Wl.p, c.st);
+        }
+        if (bu > 0) {
+            Wu.alloc((size_t)(nb * bu) * 4096);
+            launch_spike_setup(nb, bl, bu, 1, plen, T.p, Du.p, Wu.p, c.st);
+        }
+        HIPCHK(hipGetLastError());
+        c.sync();
+    }
 }
 
 int32_t PCBandLU::check_fail(Ctx &c) {
@@ -1213,11 +1233,13 @@ void PCBandLU::apply(const double *x, double *y, Ctx &c) {
     // epochs 2s+1, 2s+2 (never 0); each sweep draws band_sweep_tickets(nb) tickets
     const uint64_t nt = (uint64_t)band_sweep_tickets(nb);
     launch_band_sweep(n, nb, bl, bu, T.p, Dl.p, Gl.p, x, t.p, G.p, ticket.p, sweeps * nt, (uint32_t)(sweeps + 1), 0,
-                      fail.p, c.st);
+                      fail.p, c.st, plen);
     ++sweeps;
+    if (plen > 0 && bl > 0) launch_spike_apply(n, nb, bl, 0, plen, Wl.p, t.p, c.st);
     launch_band_sweep(n, nb, bl, bu, T.p, Du.p, Gu.p, t.p, y, G.p, ticket.p, sweeps * nt, (uint32_t)(sweeps + 1), 1,
-                      fail.p, c.st);
+                      fail.p, c.st, plen);
     ++sweeps;
+    if (plen > 0 && bu > 0) launch_spike_apply(n, nb, bu, 1, plen, Wu.p, y, c.st);
 }
 
 std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
@@ -1231,7 +1253,8 @@ std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
         csr_bandwidths(M, kl, ku, c);
         const double nbt = (double)((M.nrows + 63) / 64), w = (double)((kl + 63) / 64 + (ku + 63) / 64 + 1);
         const double gb = nbt * w * 4096.0 * 8.0 / 1e9;
-        if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 64.0)) return std::make_unique<PCBandLU>(M, kl, ku, c);
+        if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 64.0))
+            return std::make_unique<PCBandLU>(M, kl, ku, c, o.integer("pls.band_spike_plen", -1));
     }
     return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true), 0, (int)o.integer("pls.ilu_gmem", 0),
                                    (int)o.integer("pls.ilu_ring", 1));

@@ -316,7 +316,10 @@ struct PCBandLU : PC {
     DBuf<int32_t> fail;
     DBuf<uint64_t> G, ticket;  // G: 128 tagged granules per tile row (the sweeps' hand-off)
     uint64_t sweeps = 0;  // launched sweeps (ticket base = sweeps * band_sweep_tickets(nb))
-    PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c);
+    int64_t plen = 0;     // SPIKE partition length in tile rows (0: one chain per triangle)
+    DBuf<double> Wl, Wu;  // SPIKE spikes of L and U (nb x bl, nb x bu tiles)
+    // spike_plen: -1 auto (~16 partitions), 0 off, > 0 partition length in tile rows
+    PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c, int64_t spike_plen = -1);
     void apply(const double *x, double *y, Ctx &c) override;
     int32_t check_fail(Ctx &c);  // synchronising: the fail word (2: a sweep spin gave up)
 };

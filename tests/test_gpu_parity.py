@@ -323,7 +323,12 @@ def test_facade_end_to_end(gpu):
 # exact LU on the device: the dense Gauss-Jordan inverse (blocks up to
 # pls.lu_dense_max rows, default), the 64 x 64-tile band LU with flag-chained
 # sweeps, and the envelope-pattern sparse LU
-LU_PATHS = {"dense": {}, "band": {"pls.lu_path": "band"}, "envelope": {"pls.lu_path": "envelope"}}
+# band: SPIKE partitions chosen automatically (~16 per triangle, at least the
+# bandwidth); band_chain: one flag-chained sweep per triangle (no partitions);
+# band_spike2: the shortest partitions the bandwidth allows (most spikes)
+LU_PATHS = {"dense": {}, "band": {"pls.lu_path": "band"}, "envelope": {"pls.lu_path": "envelope"},
+            "band_chain": {"pls.lu_path": "band", "pls.band_spike_plen": "0"},
+            "band_spike2": {"pls.lu_path": "band", "pls.band_spike_plen": "2"}}
 
 
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
@@ -339,7 +344,9 @@ def test_exact_lu_inner_blocks(gpu, pc_type, lu_path):
 
 
 @pytest.mark.parametrize("lu_path,dim,N", [("dense", 3, 2), ("envelope", 3, 2), ("dense", 3, 3), ("dense", 2, 16),
-                                           ("band", 3, 2), ("band", 2, 16), ("band", 2, 48), ("band", 3, 5)])
+                                           ("band", 3, 2), ("band", 2, 16), ("band", 2, 48), ("band", 3, 5),
+                                           ("band_chain", 2, 48), ("band_spike2", 2, 16), ("band_spike2", 2, 48),
+                                           ("band_spike2", 3, 5)])
 def test_exact_lu_pc_apply_is_exact(gpu, lu_path, dim, N):
     """||P_lower y - x|| at rounding level: multi-block Gauss-Jordan (n not a
     multiple of 64), the band LU (2-D N=48: 295 / 343 tile rows, more than

@@ -10,6 +10,7 @@
 #   bench                       the headline bench line (default flags)
 #   prof                        rocprofv3 --kernel-trace --stats of the headline
 #   prof_fe                     same for the assembled 3-D N=12 whole-block ILU solve
+#   prof_footing                same for configs[2] (footing-inexact-ilu, band-LU Schur block)
 #   prof_amg                    same for the classical AMG (-pc_type hypre) on the s block, 3-D N=27
 #   configs                     bench on every BASELINE config that fits one GPU
 #   fe                          bench on the assembled swelling systems
@@ -50,6 +51,7 @@ for s in "$@"; do
       smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
       bench) run configs/headline 500 python -u bench.py ;;
       prof) prof prof --steps 2 --warmup 1 --no-cpu ;;
+      prof_footing) prof prof_footing --config footing-inexact-ilu --steps 3 --warmup 1 --no-cpu --no-copy-probe ;;
       prof_amg) prof prof_amg --N 27 --inner hypre --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
       prof_fe) prof prof_fe --system fe --N 12 --inner ilu --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
       configs)
