@@ -561,13 +561,61 @@ __global__ __launch_bounds__(BTPB) void k_spike_correct(int64_t n, int64_t nb, i
     if (part == 0 && gi < n) y[gi] = y[gi] - s;
 }
 
+// The tails are on the sequential path: their bw x bw tiles per position are
+// spread over SPIKE_G workgroups (SPIKE_CG spike tiles each) whose partial
+// row sums a second launch adds in group order.
+static constexpr int SPIKE_CG = 4;
+__global__ __launch_bounds__(BTPB) void k_spike_tail_part(int64_t n, int64_t nb, int64_t bw, int upper, int64_t plen,
+                                                          int64_t p0, const double *__restrict__ Wt,
+                                                          const double *__restrict__ y, double *__restrict__ part_out) {
+    __shared__ double ts[BT];
+    const int64_t pI = p0 + blockIdx.x, k0 = (pI / plen) * plen;
+    const int64_t c0 = (int64_t)blockIdx.y * SPIKE_CG, c1 = (c0 + SPIKE_CG < bw) ? c0 + SPIKE_CG : bw;
+    auto trow = [&](int64_t p) { return upper ? nb - 1 - p : p; };
+    const int lt = threadIdx.x, row = lt >> 2, part = lt & 3;
+    double s = 0.0;
+    for (int64_t c = c0; c < c1; ++c) {
+        const int64_t qc = k0 - bw + c;
+        __syncthreads();
+        if (lt < BT) {
+            const int64_t gq = trow(qc) * BT + lt;
+            ts[lt] = (qc >= 0 && gq < n) ? y[gq] : 0.0;
+        }
+        __syncthreads();
+        const bd_d2 *w = reinterpret_cast<const bd_d2 *>(Wt + (pI * bw + c) * TILE + row * BT + part * 16);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bd_d2 m = __builtin_nontemporal_load(w + u);
+            s += m.x * ts[part * 16 + 2 * u];
+            s += m.y * ts[part * 16 + 2 * u + 1];
+        }
+    }
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    if (part == 0) part_out[((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * BT + row] = s;
+}
+__global__ __launch_bounds__(BT) void k_spike_tail_fin(int64_t n, int64_t nb, int upper, int64_t p0, int G,
+                                                       const double *__restrict__ part_in, double *__restrict__ y) {
+    const int64_t pI = p0 + blockIdx.x;
+    const int row = threadIdx.x;
+    double s = 0.0;
+    for (int g = 0; g < G; ++g) s += part_in[((int64_t)blockIdx.x * G + g) * BT + row];
+    const int64_t gi = (upper ? nb - 1 - pI : pI) * BT + row;
+    if (gi < n) y[gi] = y[gi] - s;
+}
+
+int64_t spike_scratch_doubles(int64_t bw) { return bw * ((bw + SPIKE_CG - 1) / SPIKE_CG) * BT; }
+
 void launch_spike_apply(int64_t n, int64_t nb, int64_t bw, int upper, int64_t plen, const double *Wt, double *y,
-                        hipStream_t st) {
+                        double *scratch, hipStream_t st) {
     const int64_t P = (nb + plen - 1) / plen;
     if (P < 2 || bw == 0) return;
+    const int G = (int)((bw + SPIKE_CG - 1) / SPIKE_CG);
     for (int64_t k = 1; k + 1 < P; ++k) {  // tails, in partition order (each needs the previous one final)
-        const int64_t kend = (k + 1) * plen;
-        k_spike_correct<<<(unsigned)bw, BTPB, 0, st>>>(n, nb, bw, upper, plen, kend - bw, 0, Wt, y);
+        const int64_t p0 = (k + 1) * plen - bw;
+        k_spike_tail_part<<<dim3((unsigned)bw, (unsigned)G), BTPB, 0, st>>>(n, nb, bw, upper, plen, p0, Wt, y,
+                                                                            scratch);
+        k_spike_tail_fin<<<(unsigned)bw, BT, 0, st>>>(n, nb, upper, p0, G, scratch, y);
     }
     k_spike_correct<<<(unsigned)nb, BTPB, 0, st>>>(n, nb, bw, upper, plen, 0, 1, Wt, y);
 }

@@ -249,6 +249,7 @@ void launch_band_sweep(int64_t n, int64_t nb, int64_t bl, int64_t bu, const doub
 void launch_spike_setup(int64_t nb, int64_t bl, int64_t bu, int upper, int64_t plen, const double *T,
                         const double *Dinv, double *Wt, hipStream_t st);
 void launch_spike_apply(int64_t n, int64_t nb, int64_t bw, int upper, int64_t plen, const double *Wt, double *y,
-                        hipStream_t st);
+                        double *scratch, hipStream_t st);
+int64_t spike_scratch_doubles(int64_t bw);  // scratch of launch_spike_apply
 
 }  // namespace pls

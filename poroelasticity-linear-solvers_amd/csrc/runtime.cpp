@@ -1200,7 +1200,8 @@ PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c, int64_t spik
     launch_band_factor(nb, bl, bu, T.p, Dl.p, Du.p, Gl.p, Gu.p, fail.p, c.st);
     HIPCHK(hipGetLastError());
     if (check_fail(c)) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
-    // SPIKE partitions (band.hip): ~16 concurrent chains per triangle
+    // SPIKE partitions (band.hip): ~16 concurrent chains per triangle (footing
+    // N=128 Schur block, 2,064 tile rows: 16 -> 201 it/s, 32 -> 195, 64 -> 194)
     const int64_t bwmax = std::max<int64_t>(std::max(bl, bu), 1);
     int64_t pl = spike_plen < 0 ? std::max(bwmax, (nb + 15) / 16) : spike_plen;
     if (pl > 0) {
@@ -1209,6 +1210,7 @@ PCBandLU::PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c, int64_t spik
     }
     if (pl > 0 && pl < nb && (bl > 0 || bu > 0)) {
         plen = pl;
+        spike_tmp.alloc((size_t)std::max<int64_t>(spike_scratch_doubles(bwmax), 1));
         if (bl > 0) {
             Wl.alloc((size_t)(nb * bl) * 4096);
             launch_spike_setup(nb, bl, bu, 0, plen, T.p, Dl.p, Wl.p, c.st);
@@ -1235,11 +1237,11 @@ void PCBandLU::apply(const double *x, double *y, Ctx &c) {
     launch_band_sweep(n, nb, bl, bu, T.p, Dl.p, Gl.p, x, t.p, G.p, ticket.p, sweeps * nt, (uint32_t)(sweeps + 1), 0,
                       fail.p, c.st, plen);
     ++sweeps;
-    if (plen > 0 && bl > 0) launch_spike_apply(n, nb, bl, 0, plen, Wl.p, t.p, c.st);
+    if (plen > 0 && bl > 0) launch_spike_apply(n, nb, bl, 0, plen, Wl.p, t.p, spike_tmp.p, c.st);
     launch_band_sweep(n, nb, bl, bu, T.p, Du.p, Gu.p, t.p, y, G.p, ticket.p, sweeps * nt, (uint32_t)(sweeps + 1), 1,
                       fail.p, c.st, plen);
     ++sweeps;
-    if (plen > 0 && bu > 0) launch_spike_apply(n, nb, bu, 1, plen, Wu.p, y, c.st);
+    if (plen > 0 && bu > 0) launch_spike_apply(n, nb, bu, 1, plen, Wu.p, y, spike_tmp.p, c.st);
 }
 
 std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {

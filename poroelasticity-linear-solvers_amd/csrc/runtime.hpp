@@ -318,6 +318,7 @@ struct PCBandLU : PC {
     uint64_t sweeps = 0;  // launched sweeps (ticket base = sweeps * band_sweep_tickets(nb))
     int64_t plen = 0;     // SPIKE partition length in tile rows (0: one chain per triangle)
     DBuf<double> Wl, Wu;  // SPIKE spikes of L and U (nb x bl, nb x bu tiles)
+    DBuf<double> spike_tmp;  // tail partial sums
     // spike_plen: -1 auto (~16 partitions), 0 off, > 0 partition length in tile rows
     PCBandLU(const DevCSR &M, int64_t kl, int64_t ku, Ctx &c, int64_t spike_plen = -1);
     void apply(const double *x, double *y, Ctx &c) override;
