@@ -699,6 +699,7 @@ struct PCBoomer : PC {
         const bool allow_lds = o.flag("pls.ilu_lds", true);
         const int gmem = (int)o.integer("pls.ilu_gmem", 0), ring = (int)o.integer("pls.ilu_ring", 1);
         const int64_t dense_min = o.integer("pls.amg_gs_dense_min", 2048);
+        const int64_t wide_rows = o.integer("pls.amg_wide_rows", 256);  // rows per level above which: grid-wide sweeps
         const int64_t dense_max = o.integer("pls.lu_dense_max", 32768);
         double tm[7] = {0};
         auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -754,7 +755,7 @@ struct PCBoomer : PC {
                             pc = std::make_unique<PCDenseLU>(Td, c);
                         } else {
                             // wide levels: one grid-wide launch per level beats one workgroup
-                            const int gm = (nlev > 0 && T.nrows / nlev > 256) ? -1 : gmem;
+                            const int gm = (nlev > 0 && T.nrows / nlev > wide_rows) ? -1 : gmem;
                             pc = std::make_unique<PCILU>(Td, 1, c, false, allow_lds, 0, gm, ring);
                         }
                     }
