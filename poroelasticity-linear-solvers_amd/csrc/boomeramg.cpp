@@ -700,6 +700,7 @@ struct PCBoomer : PC {
         const int gmem = (int)o.integer("pls.ilu_gmem", 0), ring = (int)o.integer("pls.ilu_ring", 1);
         const int64_t dense_min = o.integer("pls.amg_gs_dense_min", 2048);
         const int64_t wide_rows = o.integer("pls.amg_wide_rows", 256);  // rows per level above which: grid-wide sweeps
+        const int wide_mode = (int)o.integer("pls.amg_wide_mode", -2);  // -2: CSR level kernels, -1: SELL level slices
         const int64_t dense_max = o.integer("pls.lu_dense_max", 32768);
         double tm[7] = {0};
         auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -755,7 +756,7 @@ struct PCBoomer : PC {
                             pc = std::make_unique<PCDenseLU>(Td, c);
                         } else {
                             // wide levels: one grid-wide launch per level beats one workgroup
-                            const int gm = (nlev > 0 && T.nrows / nlev > wide_rows) ? -1 : gmem;
+                            const int gm = (nlev > 0 && T.nrows / nlev > wide_rows) ? wide_mode : gmem;
                             pc = std::make_unique<PCILU>(Td, 1, c, false, allow_lds, 0, gm, ring);
                         }
                     }

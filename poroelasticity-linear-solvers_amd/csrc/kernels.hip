@@ -1709,6 +1709,38 @@ void launch_tri_blocks(int64_t nblocks, const int64_t *goff, const int64_t *gsli
     if (nblocks > 0)
         k_tri_blocks<<<(unsigned)nblocks, 1024, 0, st>>>(goff, gslice, sptr, slot_row, slot_len, col, val, sdinv, b, y);
 }
+// One level of a triangular sweep straight from the factored CSR: TRI_G lanes
+// per row (entries dealt round robin, partial sums combined by lane shuffles),
+// so a long row costs one or two dependent gather rounds instead of one per
+// entry as with a lane per row.  upper = 0: y_i = b_i - sum_{k < diag} l_ik y_k;
+// 1: y_i = dinv_i (b_i - sum_{k > diag} u_ik y_k) (b may alias y).
+static constexpr int TRI_G = 16;
+__global__ __launch_bounds__(TPB) void k_tri_csr_level(int64_t m, const int32_t *__restrict__ rows,
+                                                       const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                       const double *__restrict__ val, const int64_t *__restrict__ diag,
+                                                       const double *__restrict__ dinv, int upper, const double *b,
+                                                       double *y) {
+    const int64_t gid = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    const int64_t r = gid / TRI_G;
+    const int j = (int)(gid % TRI_G);
+    if (r >= m) return;  // whole groups of TRI_G lanes (m rows x TRI_G lanes, TRI_G divides 64)
+    const int64_t i = rows[r], d = diag[i];
+    const int64_t lo = upper ? d + 1 : rp[i], hi = upper ? rp[i + 1] : d;
+    double s = 0.0;
+    for (int64_t k = lo + j; k < hi; k += TRI_G) s += val[k] * y[ci[k]];
+#pragma unroll
+    for (int off = TRI_G / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off, TRI_G);
+    if (j == 0) {
+        const double v = b[i] - s;
+        y[i] = upper ? v * dinv[i] : v;
+    }
+}
+void launch_tri_csr_level(int64_t m, const int32_t *rows, const int64_t *rp, const int32_t *ci, const double *val,
+                          const int64_t *diag, const double *dinv, int upper, const double *b, double *y,
+                          hipStream_t st) {
+    if (m > 0)
+        k_tri_csr_level<<<grid_for(m * TRI_G, TPB), TPB, 0, st>>>(m, rows, rp, ci, val, diag, dinv, upper, b, y);
+}
 void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t *slot_row, const int32_t *slot_len,
                       const int32_t *col, const double *val, const double *sdinv, const double *b, double *y,
                       hipStream_t st) {

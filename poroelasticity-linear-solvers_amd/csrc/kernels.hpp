@@ -168,6 +168,10 @@ void launch_tri_fill(int64_t nslices, const int32_t *slot_row, const int32_t *sl
 void launch_tri_blocks(int64_t nblocks, const int64_t *goff, const int64_t *gslice, const int64_t *sptr,
                        const int32_t *slot_row, const int32_t *slot_len, const int32_t *col, const double *val,
                        const double *sdinv, const double *b, double *y, hipStream_t st);
+// one level of a triangular sweep from the factored CSR, 16 lanes per row (kernels.hip)
+void launch_tri_csr_level(int64_t m, const int32_t *rows, const int64_t *rp, const int32_t *ci, const double *val,
+                          const int64_t *diag, const double *dinv, int upper, const double *b, double *y,
+                          hipStream_t st);
 void launch_tri_group(int64_t s0, int64_t s1, const int64_t *sptr, const int32_t *slot_row, const int32_t *slot_len,
                       const int32_t *col, const double *val, const double *sdinv, const double *b, double *y,
                       hipStream_t st);

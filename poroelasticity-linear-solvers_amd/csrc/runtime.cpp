@@ -1084,8 +1084,19 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         std::vector<int32_t> ordU;
         std::vector<int64_t> Uptr;
         nlev_U = level_order(n, rp, ci, true, ordU, Uptr);
-        build_tri_sell(*this, rp, dg, ordL, Lptr, nullptr, false, Lf, c);
-        build_tri_sell(*this, rp, dg, ordU, Uptr, nullptr, true, Uf, c);
+        if (gmem_mode == -2 && !exact) {
+            csr_levels = true;
+            lrowsL.alloc(std::max<int64_t>(n, 1));
+            lrowsU.alloc(std::max<int64_t>(n, 1));
+            HIPCHK(hipMemcpyAsync(lrowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+            HIPCHK(hipMemcpyAsync(lrowsU.p, ordU.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+            lptrL = Lptr;
+            lptrU = Uptr;
+            c.sync();
+        } else {
+            build_tri_sell(*this, rp, dg, ordL, Lptr, nullptr, false, Lf, c);
+            build_tri_sell(*this, rp, dg, ordU, Uptr, nullptr, true, Uf, c);
+        }
     }
 }
 
@@ -1134,6 +1145,15 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
             }
             profile_tag.clear();
         }
+        return;
+    }
+    if (csr_levels) {
+        for (int64_t l = 0; l < nlev_L; ++l)
+            launch_tri_csr_level(lptrL[l + 1] - lptrL[l], lrowsL.p + lptrL[l], F.rp.p, F.ci.p, F.val.p, diag.p,
+                                 dinv.p, 0, x, y, c.st);
+        for (int64_t l = 0; l < nlev_U; ++l)
+            launch_tri_csr_level(lptrU[l + 1] - lptrU[l], lrowsU.p + lptrU[l], F.rp.p, F.ci.p, F.val.p, diag.p,
+                                 dinv.p, 1, y, y, c.st);
         return;
     }
     Lf.apply(x, y, c);

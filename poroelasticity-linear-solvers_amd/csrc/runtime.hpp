@@ -289,9 +289,15 @@ struct PCILU : PC {
     int64_t nlev_L = 0, nlev_U = 0;
     bool allow_lds = true;  // block solution resident in LDS when it fits
     bool exact = false;     // envelope pattern: exact LU (PCLU)
+    // gmem_mode -2: per-level launches straight from the factored CSR, 16 lanes
+    // per row (long rows, wide levels: the AMG's Gauss-Seidel triangles)
+    bool csr_levels = false;
+    DBuf<int32_t> lrowsL, lrowsU;
+    std::vector<int64_t> lptrL, lptrU;
     std::string profile_tag;  // non-empty: dump per-block sweep timings once (option pls.sweep_profile)
     // gmem_mode (option pls.ilu_gmem): 0 auto, 1 force the y-resident
-    // workgroup sweep (also on blocks that fit LDS), -1 never
+    // workgroup sweep (also on blocks that fit LDS), -1 never, -2 never and
+    // per-level CSR kernels instead of the SELL-64 level slices
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0,
           int gmem_mode = 0, int ring_mode = 1);
     bool reentrant() const override { return profile_tag.empty(); }

@@ -128,12 +128,15 @@ def test_hypre_error_option(gpu):
         h.setup()
 
 
-@pytest.mark.parametrize("t", ["gamg", "hypre"])
+@pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-csr-levels"])
 def test_amg_larger_hierarchy(gpu, t):
-    """Two or more coarse levels on the solid block (3-D, N = 12)."""
+    """Two or more coarse levels on the solid block (3-D, N = 12; 46,875 rows,
+    beyond LDS).  hypre-csr-levels: every Gauss-Seidel triangle through the
+    per-level CSR kernels (pls.amg_wide_rows 0), the path of the N=59 level 0."""
     spec = S.SynthSpec(3, 12)
     params = dict(BASE, **{"pc type": "diagonal 3-way", "inner pc type": "lu"})
-    db = _amg_db(t, _boomer_db() if t == "hypre" else None)
+    extra = dict(_boomer_db(), **({"pls.amg_wide_rows": "0"} if t == "hypre-csr-levels" else {}))
+    db = _amg_db(t.split("-")[0], extra if t.startswith("hypre") else None)
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)
     assert len(o.block_pc.ksp_s.pc.levels) >= 2

@@ -364,10 +364,11 @@ def test_exact_lu_pc_apply_is_exact(gpu, lu_path, dim, N):
     assert np.linalg.norm(M @ y - x) <= 1e-12 * np.linalg.norm(x)
 
 
-@pytest.mark.parametrize("inner", ["ilu", "lu"])
-def test_global_level_launch_path(gpu, inner):
-    """pls.ilu_lds 0 with one block: one launch per global level."""
-    db = dict(ILU_DB, **{"pls.ilu_lds": "0"})
+@pytest.mark.parametrize("inner,mode", [("ilu", "0"), ("lu", "0"), ("ilu", "-2")])
+def test_global_level_launch_path(gpu, inner, mode):
+    """pls.ilu_lds 0 with one block: one launch per global level (mode -2:
+    the CSR level kernel with 16 lanes per row instead of SELL level slices)."""
+    db = dict(ILU_DB, **{"pls.ilu_lds": "0", "pls.ilu_gmem": mode})
     for pre in ("s_", "fp_", "f_", "p_", "diff_"):
         db[pre + "pc_type"] = inner
     _compare_solve(S.SynthSpec(2, 6), {"inner pc type": inner}, db=db)
