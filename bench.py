@@ -449,7 +449,7 @@ def main():
 
     # HBM traffic of the same kernel from the committed PMC passes (tools/pmc.sh)
     traffic, traffic_src = None, None
-    kname = ("void pls::k_d16_spmv<4, 1, false>" if d16 else "void pls::k_sell_spmv<8, 1, false>")
+    kname = ("void pls::k_d16_spmv<4, 1, false" if d16 else "void pls::k_sell_spmv<8, 1, false")  # any unroll
     pmc = next((q for q in (os.path.join(ROOT, "profiles", f"r{r:02d}_pmc_N59_summary.json") for r in range(9, 0, -1))
                 if os.path.exists(q)), "")  # the latest round's committed PMC passes
     if os.path.exists(pmc) and n_global == 10326954 and world == 1 and fe is None:
