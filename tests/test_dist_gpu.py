@@ -106,6 +106,13 @@ FE_CASES = [
      "params": dict(FE_BASE, **{"pc type": "diagonal 3-way"}), "db": _fe_db(3)},
     {"name": "fe_facade_twoway_3d", "system": "fe", "facade": True, "dim": 3, "N": 3,
      "params": dict(FE_BASE, **{"pc type": "diagonal"}), "db": _fe_db(3)},
+    # the reference's exact option set under mpirun (MUMPS LU on every block ->
+    # each sharded block gathered and factored redundantly)
+    {"name": "fe_exact_lu_threeway_2d", "system": "fe", "dim": 2, "N": 8,
+     "params": dict(FE_BASE, **{"pc type": "diagonal 3-way", "inner pc type": "lu"}),
+     "db": dict({"global_ksp_type": "gmres", "global_ksp_pc_side": "right"},
+                **{pre + k: v for pre in ("s_", "f_", "p_", "diff_") for k, v in
+                   (("ksp_type", "preonly"), ("pc_type", "lu"))})},
 ]
 
 
