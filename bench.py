@@ -237,11 +237,16 @@ def _cpu_baseline_fe(args, params, db):
     """--system fe: the Python oracle (1 thread) on the assembled swelling
     system at N = cpu_N, iters/s scaled by DoF to the benched system."""
     from lib.fe_swelling import assemble_swelling
+    from lib.fe_footing import assemble_footing, footing_dofs
     from oracle.solver import OracleSolver
     t0 = time.perf_counter()
-    fe = assemble_swelling(args.dim, args.cpu_N, params["pc type"])
+    footing = args.config.startswith("footing")
+    if footing:
+        fe = assemble_footing(args.cpu_N, params["pc type"])
+    else:
+        fe = assemble_swelling(args.dim, args.cpu_N, params["pc type"])
     n_sample = fe.A.shape[0]
-    n_metric = n_sample if args.N == args.cpu_N else (
+    n_metric = n_sample if args.N == args.cpu_N else footing_dofs(args.N) if footing else (
         6 * (2 * args.N + 1) ** 3 + (args.N + 1) ** 3 if args.dim == 3 else 4 * (2 * args.N + 1) ** 2 + (args.N + 1) ** 2)
     p = dict(params)
     p["solver maxiter"] = args.cpu_maxit
@@ -256,7 +261,8 @@ def _cpu_baseline_fe(args, params, db):
             "cores": 1, "kind": "port",
             "sample": (f"oracle (numpy/scipy + C kernels, 1 thread) {params['pc type']} / {params['solver type']} "
                        f"solve of the assembled N={args.cpu_N} {args.dim}-D swelling system ({n_sample} DoF), {o.its} "
-                       f"outer iterations in {dt:.2f}s (second solve; assembly + setup + first solve {t_setup:.1f}s); iters/s x {n_sample}/{n_metric}"),
+                       f"outer iterations in {dt:.2f}s (second solve; assembly + setup + first solve {t_setup:.1f}s); iters/s x {n_sample}/{n_metric}")
+                       .replace("swelling system", "footing system" if footing else "swelling system"),
             "raw_iters_per_s": rate}
 
 
@@ -305,8 +311,9 @@ def main():
     ap.add_argument("--blocks-p", type=int, default=11, help="3-way p_ / diff_ blocks")
     ap.add_argument("--blocks-inner", type=int, default=64, help="footing preset: bjacobi blocks per inner PC")
     ap.add_argument("--maxit", type=int, default=100)
-    ap.add_argument("--pc-type", default="diagonal", choices=["diagonal", "diagonal 3-way", "3-way"],
-                    help="block preconditioner (the metric: 2-way 'diagonal')")
+    ap.add_argument("--pc-type", default=None, choices=["diagonal", "diagonal 3-way", "3-way", "undrained"],
+                    help="block preconditioner (the metric: 2-way 'diagonal'; --system fe with the footing "
+                         "config: footing.py's 'undrained')")
     ap.add_argument("--solver", default="gmres", choices=["gmres", "aar"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-copy-probe", action="store_true", help="skip the device-copy bandwidth probe")
@@ -320,17 +327,24 @@ def main():
                     help="G > 1: strong (same system, same total block counts), weak (G x the DoF), replicas")
     ap.add_argument("--replicas", action="store_true", help="alias of --scaling replicas")
     ap.add_argument("--system", default="synthetic", choices=["synthetic", "fe"],
-                    help="fe: the P2-P2-P1 swelling system (lib/fe_swelling.py, assembled on the host; one GPU)")
+                    help="fe: the P2-P2-P1 FE system assembled on the host, one GPU -- swelling "
+                         "(lib/fe_swelling.py), or with --config footing-inexact-ilu footing.py's locally refined "
+                         "system (lib/fe_footing.py)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="host: host-staged gloo communicator (ranks may share a GPU; rehearsal only)")
     pre, _ = ap.parse_known_args()
     preset = dict(CONFIGS[pre.config])
     ap.set_defaults(preset=preset.pop("preset"), **preset)
     args = ap.parse_args()
+    footing_fe = args.system == "fe" and args.config.startswith("footing")
+    if args.pc_type is None:
+        args.pc_type = "undrained" if footing_fe else "diagonal"  # footing.py:71
     if args.pc_type == "3-way":
         args.pc_type = "diagonal 3-way"
     if args.cpu_N is None:
         args.cpu_N = args.N
+    if footing_fe and "--cpu-N" not in sys.argv:
+        args.cpu_N = 12  # the oracle's inner CG + BJACOBI(ILU) on the refined footing system: ~1 min at N=12
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -364,9 +378,14 @@ def main():
         comm = Communicator.rccl() if args.comm == "rccl" else Communicator.gloo()
         h = Handle.synthetic_dist(args.dim, N_glob, SEED, DELTA, opts, comm)
     elif args.system == "fe":
-        from lib.fe_swelling import assemble_swelling
-        fe = assemble_swelling(args.dim, args.N, args.pc_type)
-        _progress(rank, f"assembled the {args.dim}-D N={args.N} swelling system in {time.perf_counter() - t0:.1f} s")
+        if footing_fe:
+            from lib.fe_footing import assemble_footing
+            fe = assemble_footing(args.N, args.pc_type)
+        else:
+            from lib.fe_swelling import assemble_swelling
+            fe = assemble_swelling(args.dim, args.N, args.pc_type)
+        _progress(rank, f"assembled the {args.dim}-D N={args.N} {'footing' if footing_fe else 'swelling'} system "
+                        f"in {time.perf_counter() - t0:.1f} s")
         h = Handle.from_csr(fe.A, fe.P, fe.P_diff, fe.is_s, fe.is_f, fe.is_p, fe.bcs_sub_pressure, opts)
     else:
         h = Handle.synthetic(args.dim, args.N, SEED + rank, DELTA, opts)
@@ -473,14 +492,18 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic (seeded SPD 3-field block system, SURVEY.md 8(d); generated in HBM)" if fe is None else
+                     "P2-P2-P1 footing FE system (lib/fe_footing.py: footing.py's twice locally refined mesh, "
+                     "traction and BCs; lib/Assembler.py's forms, first time step; assembled on the host, copied to "
+                     "HBM before timing)" if footing_fe else
                      "P2-P2-P1 swelling FE system (lib/fe_swelling.py: lib/Assembler.py's forms, first time step; "
                      "assembled on the host, copied to HBM before timing)"),
             "config": {
-                "workload": (f"{args.config}{' on the assembled swelling FE system' if fe is not None else ''}: "
+                "workload": (f"{args.config}"
+                             f"{(' on the assembled ' + ('footing' if footing_fe else 'swelling') + ' FE system') if fe is not None else ''}: "
                              f"{args.dim}-D N={N_glob} ({n_global} DoF): outer "
                              + ("GMRES right-PC" if args.solver == "gmres" else f"AAR({args.aar_order}, p=5)")
                              + f" rtol 1e-6 atol {args.atol:g} maxit={args.maxit}, "
-                             + ("2-way" if args.pc_type == "diagonal" else "3-way") + " block PC, "
+                             + ("3-way" if "3-way" in args.pc_type else "2-way") + f" '{args.pc_type}' block PC, "
                              + ("petsc-options-exact (PREONLY + LU blocks)" if args.preset == "exact" else
                                 "petsc-options-inexact with ILU(0) for BoomerAMG (CG blocks, Schur fieldsplit fp)"
                                 if args.preset == "inexact-ilu" else

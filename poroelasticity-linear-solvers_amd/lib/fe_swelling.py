@@ -273,20 +273,13 @@ def _dirichlet(M, rows):
     return M
 
 
-def assemble_swelling(dim: int, N: int, pc_type: str = "diagonal", params: dict | None = None,
-                      ordering: str = "field-major", t: float | None = None) -> SwellingSystem:
-    """The swelling (dim 2: swelling.py) / swelling-3d (dim 3) system at the
-    first time step: A, P, P_diff (None unless ``"3-way" in pc_type``), b,
-    index sets and pressure-BC positions, as the reference hands them to
-    ``Preconditioner`` / ``Solver`` (lib/Poromechanics.py:58-98)."""
-    if dim not in (2, 3):
-        raise ValueError("dim must be 2 or 3")
-    prm = dict(SWELLING_2D if dim == 2 else SWELLING_3D, **(params or {}))
-    t = prm["dt"] if t is None else t
-    coords, cells, pairs, cell_nodes, node2x, nv = _p2_nodes(dim, N)
-    nnodes = node2x.shape[0]
-    h = SIDE_LENGTH / N
-    M2, G, C, Mp, Kp = _element_blocks(dim, coords[cells].astype(np.float64) * h)
+def assemble_forms(dim, xcells, cells, cell_nodes, nv, nnodes, pc_type, prm, ordering):
+    """A, P, P_diff (None unless 3-way) of ``pc_type`` on a simplicial mesh
+    (physical vertex coordinates per cell ``xcells``; P2 nodes ``cell_nodes``:
+    the cell's vertices, then its edges in ``itertools.combinations`` order)
+    and the dof numbers (us, vf, p) -- shared by the swelling and footing
+    assemblers (lib/Assembler.py:66-221)."""
+    M2, G, C, Mp, Kp = _element_blocks(dim, xcells)
     Mv, E, Dd, Bt = _vector_blocks(dim, M2, G, C)
     elem = {"Mv": Mv, "E": E, "Dd": Dd, "Bt": Bt, "Bq": np.transpose(Bt, (0, 2, 1)), "Mp": Mp, "Kp": Kp}
 
@@ -316,6 +309,25 @@ def assemble_swelling(dim: int, N: int, pc_type: str = "diagonal", params: dict 
     fa, fp_, fd = _forms(pc_type, prm, dim)
     A, P = build(fa), build(fp_)
     Pd = build(fd) if fd is not None else None
+    return A, P, Pd, (us, vf, p)
+
+
+def assemble_swelling(dim: int, N: int, pc_type: str = "diagonal", params: dict | None = None,
+                      ordering: str = "field-major", t: float | None = None) -> SwellingSystem:
+    """The swelling (dim 2: swelling.py) / swelling-3d (dim 3) system at the
+    first time step: A, P, P_diff (None unless ``"3-way" in pc_type``), b,
+    index sets and pressure-BC positions, as the reference hands them to
+    ``Preconditioner`` / ``Solver`` (lib/Poromechanics.py:58-98)."""
+    if dim not in (2, 3):
+        raise ValueError("dim must be 2 or 3")
+    prm = dict(SWELLING_2D if dim == 2 else SWELLING_3D, **(params or {}))
+    t = prm["dt"] if t is None else t
+    coords, cells, pairs, cell_nodes, node2x, nv = _p2_nodes(dim, N)
+    nnodes = node2x.shape[0]
+    h = SIDE_LENGTH / N
+    A, P, Pd, (us, vf, p) = assemble_forms(dim, coords[cells].astype(np.float64) * h, cells, cell_nodes, nv, nnodes,
+                                           pc_type, prm, ordering)
+    n = A.shape[0]
 
     # ---- right-hand side: surface tractions at time t (Assembler.py:235-269)
     cs = -1e3 * 0.9 * (1 - np.exp(-t ** 2 / 0.25))
