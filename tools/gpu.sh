@@ -11,6 +11,8 @@
 #   prof                        rocprofv3 --kernel-trace --stats of the headline
 #   prof_fe                     same for the assembled 3-D N=12 whole-block ILU solve
 #   prof_footing                same for configs[2] (footing-inexact-ilu, band-LU Schur block)
+#   footing                     configs[2] bench on the assembled footing system (N=128)
+#   prof_footing_fe             rocprofv3 of that solve
 #   prof_amg                    same for the classical AMG (-pc_type hypre) on the s block, 3-D N=27
 #   configs                     bench on every BASELINE config that fits one GPU
 #   fe                          bench on the assembled swelling systems
@@ -64,6 +66,9 @@ for s in "$@"; do
         run fe/exact2d_3way 300 python -u bench.py --config swelling2d-exact --system fe --pc-type "diagonal 3-way" --steps 20 --warmup 2 --no-copy-probe
         run fe/ilu3d_N12 300 python -u bench.py --system fe --N 12 --inner ilu --steps 5 --warmup 1 --no-copy-probe --cpu-N 6
         run fe/ilu3d_N20 300 python -u bench.py --system fe --N 20 --inner ilu --steps 3 --warmup 1 --no-copy-probe --no-cpu ;;
+      footing)  # configs[2] on the assembled footing system (lib/fe_footing.py)
+        run fe/footing_N128 600 python -u bench.py --config footing-inexact-ilu --system fe --steps 2 --warmup 1 --no-copy-probe ;;
+      prof_footing_fe) prof prof_footing_fe --config footing-inexact-ilu --system fe --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
       pmc) run pmc 1300 bash tools/pmc.sh ;;
       custom:*) rest=${s#custom:}; name=${rest%%:*}; cmd=${rest#*:}; run "$name" 1100 bash -c "$cmd" ;;
       *) echo "unknown step $s"; exit 2 ;;
