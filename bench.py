@@ -87,6 +87,9 @@ CONFIGS = {
     # blocks, Schur lower/selfp fieldsplit on fp (Schur block: device LU).
     # footing.py:73-76 atol 1e-4 maxit 500.
     "footing-inexact-ilu": dict(dim=2, N=128, maxit=500, atol=1e-4, preset="inexact-ilu", cpu_N=48),
+    # footing.py's own inner PC ("inner pc type" hypre, footing.py:73) with
+    # petsc-options-inexact itself: BoomerAMG -> the classical AMG
+    "footing-inexact": dict(dim=2, N=128, maxit=500, atol=1e-4, preset=None, inexact=True, cpu_N=12),
     # configs[4]: AAR depth m=5 (sharded across ranks under torchrun)
     "aar-m5": dict(dim=3, N=59, maxit=100, atol=1e-8, preset=None, solver="aar", aar_order=5, cpu_N=20),
 }

@@ -44,8 +44,9 @@ DIVERGED_NULL = -2
 DIVERGED_ITS = -3
 DIVERGED_DTOL = -4
 DIVERGED_BREAKDOWN = -5
-DIVERGED_INDEFINITE_MAT = -8
+DIVERGED_INDEFINITE_PC = -8
 DIVERGED_NANORINF = -9
+DIVERGED_INDEFINITE_MAT = -10
 
 PETSC_DEFAULT_RTOL = 1e-5
 PETSC_DEFAULT_ATOL = 1e-50
@@ -394,6 +395,9 @@ def _cg(ksp: KSP, b):
         its = i + 1
         if beta == 0.0:
             reason = CONVERGED_ATOL
+            break
+        if i > 0 and beta * betaold < 0.0:  # cg.c: indefinite preconditioner
+            reason = DIVERGED_INDEFINITE_PC
             break
         if i == 0:
             p = z.copy()

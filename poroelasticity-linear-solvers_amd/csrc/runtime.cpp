@@ -1273,9 +1273,14 @@ std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
     if (path == "band" || path == "auto") {
         int64_t kl = 0, ku = 0;
         csr_bandwidths(M, kl, ku, c);
+        // band tiles + the SPIKE spikes (nb x (bl + bu) tiles): ~2x the band.  Default cap:
+        // 3/4 of the free HBM (288 GB per MI355X: the 2-D footing N=128 Schur block's
+        // 95 GB band fits), pls.lu_band_max_gb overrides
         const double nbt = (double)((M.nrows + 63) / 64), w = (double)((kl + 63) / 64 + (ku + 63) / 64 + 1);
-        const double gb = nbt * w * 4096.0 * 8.0 / 1e9;
-        if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 64.0))
+        const double gb = nbt * (2.0 * w - 1.0) * 4096.0 * 8.0 / 1e9;
+        size_t free_b = 0, total_b = 0;
+        HIPCHK(hipMemGetInfo(&free_b, &total_b));
+        if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 0.75 * (double)free_b / 1e9))
             return std::make_unique<PCBandLU>(M, kl, ku, c, o.integer("pls.band_spike_plen", -1));
     }
     return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true), 0, (int)o.integer("pls.ilu_gmem", 0),
@@ -1693,6 +1698,13 @@ void KSP::solve_cg(const double *b, double *x, Ctx &c) {
         its = (int)(i + 1);
         if (beta == 0.0) {
             reason = CONVERGED_ATOL;
+            break;
+        }
+        // cg.c: (z, r) changing sign means an indefinite PC (e.g. ILU(0) of an
+        // undrained solid block with negative pivots): stop with that reason
+        // instead of iterating to max_it
+        if (i > 0 && beta * betaold < 0.0) {
+            reason = DIVERGED_INDEFINITE_PC;
             break;
         }
         if (i == 0) launch_copy(n, z, p, c.st);

@@ -350,7 +350,7 @@ void boomeramg_host_level(const HostCSR &A, const Options &o, const std::string 
 enum Reason {
     CONVERGED_ITERATING = 0, CONVERGED_RTOL = 2, CONVERGED_ATOL = 3, CONVERGED_ITS = 4,
     DIVERGED_NULL = -2, DIVERGED_ITS = -3, DIVERGED_DTOL = -4, DIVERGED_BREAKDOWN = -5,
-    DIVERGED_INDEFINITE_MAT = -8, DIVERGED_NANORINF = -9
+    DIVERGED_INDEFINITE_PC = -8, DIVERGED_NANORINF = -9, DIVERGED_INDEFINITE_MAT = -10  // petscksp.h
 };
 
 struct KSP {

@@ -35,7 +35,7 @@ def _args(config, **over):
 
 
 def test_every_preset_names_a_known_configuration():
-    assert set(bench.CONFIGS) == {"swelling2d-exact", "swelling3d-bjacobi", "footing-inexact-ilu", "aar-m5"}
+    assert set(bench.CONFIGS) == {"swelling2d-exact", "swelling3d-bjacobi", "footing-inexact-ilu", "footing-inexact", "aar-m5"}
     assert bench.CONFIGS["swelling3d-bjacobi"]["N"] == 59  # the metric's 10.33M-DoF system
 
 

@@ -20,9 +20,9 @@ same CSR.
   that swap (148 vs 150-153), so neither is a parity case;
 * the committed footing fixtures (tests/golden/footing/) reproduced by the
   device -- its, reason, history and x;
-* configs[2]'s size, N = 128 (1,308,592 DoF): the full inexact-ILU solve
-  through properties (converged, bitwise reproducible, true residual of the
-  returned x consistent with the last history entry).
+* configs[2]'s size, N = 128 (1,308,592 DoF): the full solve with
+  footing.py's own inner PC (classical AMG) through properties (converged,
+  bitwise reproducible, true residual of the returned x).
 """
 import json
 import os
@@ -59,6 +59,31 @@ def test_footing_vs_oracle(gpu, N, pc, preset):
     assert r.reason > 0
 
 
+def test_inner_cg_indefinite_pc_abort(gpu):
+    """N = 12, configs[2]'s inexact-ILU set: ILU(0) blocks of the undrained
+    solid block are indefinite, and PETSc's CG (cg.c) stops the inner solve
+    with KSP_DIVERGED_INDEFINITE_PC after ~4 iterations instead of iterating
+    to max_it.  The device block PC (inner CG + BJACOBI(ILU(0)), Schur
+    fieldsplit on fp) against the oracle's on the same vectors."""
+    from lib.handle import Handle, params_to_options
+    from oracle.solver import OracleSolver
+    s = FF.assemble_footing(12, "undrained")
+    params, db = _options("inexact-ilu")
+    o = OracleSolver(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, params, db, s.bcs_sub_pressure)
+    opts = dict(db)
+    opts.update(params_to_options(params))
+    h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    rng = np.random.default_rng(4)
+    aborted = 0
+    for x in (s.b, rng.standard_normal(s.A.shape[0])):
+        yo = o.block_pc.apply(x)
+        aborted += o.block_pc.ksp_s.reason == -8
+        y = h.pc_apply(x)
+        assert np.max(np.abs(y - yo)) <= 1e-8 * np.max(np.abs(yo))
+    assert aborted >= 1
+    h.destroy()
+
+
 @pytest.mark.parametrize("name", ["footing_N8_undrained_exact", "footing_N8_undrained_inexact_ilu",
                                   "footing_N8_3way_exact"])
 def test_device_reproduces_footing_golden(gpu, name):
@@ -74,15 +99,19 @@ def test_device_reproduces_footing_golden(gpu, name):
 
 
 def test_footing_configs2_full_size(gpu):
-    """N = 128 (configs[2]'s size) with bench's footing-inexact-ilu option set:
-    converges, two fresh handles give bitwise equal histories and solutions.
+    """N = 128 (configs[2]'s size, 1,308,592 DoF) with footing.py's own inner
+    PC: petsc-options-inexact, BoomerAMG -> the classical AMG (the ILU(0)
+    variant's inner CG iterations grow ~N^2 on the undrained solid block: 19
+    at N=8, 43 at N=12 in the oracle, far beyond a test's budget at N=128).
+    The fp Schur block's LU (615,714 rows, 95 GB band) takes the band path.
+    Converges; two fresh handles give bitwise equal histories and solutions.
     The inner CG makes the PC nonlinear, so non-flexible GMRES's estimate is
     not the true residual (in the reference too): ||b - A x|| is only held to
     10x the convergence threshold."""
     from lib.handle import Handle, params_to_options
     s = FF.assemble_footing(128, "undrained")
     assert s.A.shape[0] == 1_308_592
-    params, db = _options("inexact-ilu")
+    params, db = _options("inexact")
     opts = dict(db)
     opts.update(params_to_options(params))
     runs = []

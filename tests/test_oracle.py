@@ -198,6 +198,45 @@ def test_cg_matches_textbook():
     assert np.allclose(x, xr, rtol=1e-9, atol=1e-12)
 
 
+def test_cg_indefinite_pc_stops_like_petsc():
+    """cg.c: when (z, r) changes sign between iterations the PC is indefinite
+    and KSPSolve_CG stops with KSP_DIVERGED_INDEFINITE_PC (-8) instead of
+    running to max_it (ILU(0) of footing's undrained solid block does this).
+    Against a textbook CG that records (z, r) per iteration."""
+    A = rand_spd(60, density=0.1, seed=5, shift=0.5)
+    d = np.ones(60)
+    d[::3] = -0.2  # an indefinite diagonal PC
+
+    class PCSigned:
+        type = "signed"
+
+        def apply(self, r):
+            return d * r
+
+    b = np.random.default_rng(6).standard_normal(60)
+    ksp = petsc.KSP(A, PCSigned(), "cg", rtol=1e-12, atol=0, maxit=500, norm_type="unpreconditioned")
+    ksp.solve(b)
+    assert petsc.DIVERGED_INDEFINITE_PC == -8 and petsc.DIVERGED_INDEFINITE_MAT == -10  # petscksp.h
+    # textbook CG: the first iteration whose beta = (z, r) has the other sign
+    x, r = np.zeros(60), b.copy()
+    z = d * r
+    beta, p, k = z @ r, None, 0
+    betas = [beta]
+    while True:
+        p = z.copy() if p is None else z + (beta / betas[-2]) * p
+        w = A @ p
+        a = beta / (p @ w)
+        x, r = x + a * p, r - a * w
+        z = d * r
+        beta = z @ r
+        betas.append(beta)
+        k += 1
+        if beta * betas[-2] < 0:
+            break
+    assert ksp.reason == petsc.DIVERGED_INDEFINITE_PC
+    assert ksp.its == k + 1
+
+
 def test_converged_default():
     c = petsc.ConvergedDefault(rtol=1e-2, atol=1e-5, dtol=10.0)
     assert c(0, 1.0) == 0
