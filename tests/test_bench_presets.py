@@ -65,6 +65,29 @@ def test_footing_preset_replaces_boomeramg_by_ilu_blocks():
     assert db["global_ksp_norm_type"] == "unpreconditioned"
 
 
+def test_footing_inexact_preset_is_the_reference_set():
+    """footing-inexact: footing.py's own inner PC (hypre) with
+    petsc-options-inexact unchanged (BoomerAMG settings on every block)."""
+    params, db = bench.solver_options(_args("footing-inexact"))
+    assert params["solver atol"] == 1e-4 and params["solver maxiter"] == 500
+    for pre in ("s_", "f_", "p_", "diff_", "fp_fieldsplit_0_"):
+        assert db[pre + "pc_type"] == "hypre"
+        assert db[pre + "pc_hypre_boomeramg_coarsen_type"] == "HMIS"
+        assert db[pre + "pc_hypre_boomeramg_interp_type"] == "ext+i"
+    assert db["fp_fieldsplit_1_pc_type"] == "lu"
+
+
+def test_fe_cpu_baseline_footing():
+    """--system fe with a footing config: the CPU baseline solves the assembled
+    footing system (lib/fe_footing.py) and scales by its DoF."""
+    from lib.fe_footing import footing_dofs
+    a = _args("footing-inexact", system="fe", N=8, cpu_N=4, pc_type="undrained")
+    params, db = bench.solver_options(a)
+    out = bench.cpu_baseline(a, params, db)
+    assert out["value"] > 0 and "footing system" in out["sample"]
+    assert abs(out["value"] - out["raw_iters_per_s"] * footing_dofs(4) / footing_dofs(8)) <= 1e-9 * out["value"]
+
+
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
 def test_headline_preset_block_counts(pc_type):
     _, db = bench.solver_options(_args("swelling3d-bjacobi", pc_type=pc_type))
