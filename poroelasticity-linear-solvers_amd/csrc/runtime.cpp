@@ -1274,13 +1274,14 @@ std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
         int64_t kl = 0, ku = 0;
         csr_bandwidths(M, kl, ku, c);
         // band tiles + the SPIKE spikes (nb x (bl + bu) tiles): ~2x the band.  Default cap:
-        // 3/4 of the free HBM (288 GB per MI355X: the 2-D footing N=128 Schur block's
-        // 95 GB band fits), pls.lu_band_max_gb overrides
+        // 3/4 of the card's HBM (288 GB per MI355X: the 2-D footing N=128 Schur block's
+        // 95 GB band + 95 GB of spikes fit; an allocation that then fails is reported),
+        // pls.lu_band_max_gb overrides
         const double nbt = (double)((M.nrows + 63) / 64), w = (double)((kl + 63) / 64 + (ku + 63) / 64 + 1);
         const double gb = nbt * (2.0 * w - 1.0) * 4096.0 * 8.0 / 1e9;
         size_t free_b = 0, total_b = 0;
         HIPCHK(hipMemGetInfo(&free_b, &total_b));
-        if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 0.75 * (double)free_b / 1e9))
+        if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 0.75 * (double)total_b / 1e9))
             return std::make_unique<PCBandLU>(M, kl, ku, c, o.integer("pls.band_spike_plen", -1));
     }
     return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true), 0, (int)o.integer("pls.ilu_gmem", 0),
