@@ -69,6 +69,7 @@ for s in "$@"; do
       footing)  # configs[2] on the assembled footing system (lib/fe_footing.py)
         run fe/footing_N128 600 python -u bench.py --config footing-inexact-ilu --system fe --steps 2 --warmup 1 --no-copy-probe ;;
       prof_footing_fe) prof prof_footing_fe --config footing-inexact-ilu --system fe --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
+      prof_footing_amg) prof prof_footing_amg --config footing-inexact --system fe --N 12 --steps 1 --warmup 0 --no-cpu --no-copy-probe ;;
       pmc) run pmc 1300 bash tools/pmc.sh ;;
       custom:*) rest=${s#custom:}; name=${rest%%:*}; cmd=${rest#*:}; run "$name" 1100 bash -c "$cmd" ;;
       *) echo "unknown step $s"; exit 2 ;;
