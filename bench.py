@@ -286,6 +286,52 @@ def shard_plan(args, world):
     return sharded, N_glob
 
 
+def launch_plan(gpus, env):
+    """How this process runs ``--gpus G`` (the reference's ``mpirun -np G``,
+    paper-scripts/robustness_2d.sh:29):
+
+    * ``("run", G)``: this process is a rank of a G-rank job (WORLD_SIZE = G is
+      set by torch.distributed.run) or G is 1;
+    * ``("spawn", G)``: WORLD_SIZE is unset and G > 1 -- the caller must start G
+      fresh rank processes (before any HIP call in this one) and exit with
+      their status;
+    * ``("error", msg)``: WORLD_SIZE disagrees with --gpus (a G-GPU line would
+      otherwise report the wrong rank count).
+
+    ``gpus`` None means "whatever WORLD_SIZE says" (1 outside a job)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        G = 1 if gpus is None else int(gpus)
+        if G < 1:
+            return "error", f"--gpus {G}: need at least one GPU"
+        return ("spawn", G) if G > 1 else ("run", 1)
+    W = int(ws)
+    if gpus is not None and int(gpus) != W:
+        return "error", f"--gpus {gpus} but WORLD_SIZE={W}: launch {gpus} ranks or pass --gpus {W}"
+    return "run", W
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(G, argv):
+    """Run this script as a G-rank torch.distributed job (one process per GPU,
+    LOCAL_RANK = GPU index) and return its exit status.  The parent imports
+    nothing that touches the GPU; the ranks are fresh child processes (no exec
+    of a process with an initialised GPU)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={G}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"[bench] --gpus {G}: launching {G} ranks (torch.distributed.run)", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def _progress(rank, msg):
     """Progress on stderr (rank 0): long configurations stay visibly alive;
     stdout carries only the JSON line."""
@@ -300,7 +346,8 @@ def main():
     ap.add_argument("--dim", type=int, default=3, choices=[2, 3])
     ap.add_argument("--atol", type=float, default=1e-8)
     ap.add_argument("--aar-order", type=int, default=10)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment, G > 1 launches G ranks itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--N", type=int, default=59)
@@ -339,6 +386,12 @@ def main():
     preset = dict(CONFIGS[pre.config])
     ap.set_defaults(preset=preset.pop("preset"), **preset)
     args = ap.parse_args()
+    mode, val = launch_plan(args.gpus, os.environ)
+    if mode == "error":
+        print(f"[bench] error: {val}", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    if mode == "spawn":
+        raise SystemExit(spawn_ranks(val, sys.argv[1:]))
     footing_fe = args.system == "fe" and args.config.startswith("footing")
     if args.pc_type is None:
         args.pc_type = "undrained" if footing_fe else "diagonal"  # footing.py:71
@@ -454,7 +507,9 @@ def main():
     achieved = alg_bytes / spmv_avg / 1e9 if spmv_avg > 0 else 0.0
     iso = h.bench_spmv(d_x.p, d_b.p, 10)
     # latency of the solve's global sums: a CGS step's k+1 dots (k ~ its/2) and a norm
-    gsum_us = {"dots_40": 1e6 * h.bench_global_sum(40, 50), "norm_1": 1e6 * h.bench_global_sum(1, 50)}
+    # (sharded runs only: a single rank's "global" sum is a local reduction)
+    gsum_us = ({"dots_40": 1e6 * h.bench_global_sum(40, 50), "norm_1": 1e6 * h.bench_global_sum(1, 50)}
+               if sharded else None)
     d16, mat_bytes = h.spmv_layout()
     fmt_bytes = mat_bytes + 8.0 * n + 8.0 * n  # + x once + y once
     load_rhs()
@@ -519,8 +574,9 @@ def main():
                                 f"replicas x{world}" if world > 1 else "single GPU"),
             },
             "its_per_solve": its / args.steps,
-            "comm": {"global_sum_latency_us": gsum_us, "spmv_gbs_rank0": achieved,
-                     "note": "per-rank SpMV includes the halo exchange it waits for"},
+            "comm": ({"global_sum_latency_us": gsum_us, "spmv_gbs_rank0": achieved,
+                      "note": "per-rank SpMV includes the halo exchange it waits for"} if sharded else
+                     {"global_sum_latency_us": None, "note": "one rank per solve: no communication"}),
             "reasons": sorted(set(reasons)),
             "setup_s": t_setup,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

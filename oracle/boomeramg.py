@@ -61,12 +61,27 @@ Setup, level l (A_l square CSR, sorted columns), single rank:
   reached, or when coarsening selects no or every point; the coarsest level is
   solved exactly (hypre's relax type 9, Gaussian elimination).
 V-cycle (one PC application, x = 0): per level, grid_sweeps_all sweeps of
-hybrid symmetric Gauss-Seidel (PETSc's PCHYPRE default relax type, hypre 6;
-one rank: forward then backward GS), lexicographic with no_CF, else over the
-C points then the F points going down and F then C going up (hypre's CF
-relaxation order); restricted to a point set I, forward is
-x_I += (D + L)_II^-1 (b - A x)_I and backward x_I += (D + U)_II^-1 (b - A x)_I;
-r = b - A x; recurse on R r from 0; x += P e; post-smooth.
+hybrid symmetric Gauss-Seidel (PETSc's PCHYPRE default relax type, hypre 6),
+lexicographic with no_CF, else over the C points then the F points going
+down and F then C going up (hypre's CF relaxation order); r = b - A x;
+recurse on R r from 0; x += P e; post-smooth.
+* hybrid symmetric Gauss-Seidel with K chunks (libpls option
+  ``pls.hypre_relax_chunks``, default 256 -- hypre's relax type 6 as its
+  OpenMP build runs it with K threads, par_relax.c): the level's n rows are
+  cut into K_l = min(K, n // R, n) contiguous chunks, at least 1, with R =
+  ``pls.hypre_relax_min_rows`` (default 1024; 0: no floor) -- undamped
+  hybrid sweeps over chunks of ~100 rows diverge on the undrained footing
+  solid block (footing N=12: 500 its at K_l = 64, 50 at one chunk, 53 with
+  R = 1024, measured with this oracle) -- (size n / K_l, the first n % K_l
+  chunks one row longer); u_old = u at the start of the sweep; within chunk c,
+  row by row forward and then backward over the chunk's points of the set,
+  u_i = (b_i - sum_{j != i} a_ij v_j) / a_ii with v_j = u_j for j in c and
+  v_j = u_old_j otherwise (``hybrid_sgs_literal`` is that loop).  In matrix
+  form, with A_c the chunk-block-diagonal part of A restricted to the set I
+  (D its diagonal, L / U its strict triangles): u_I += M^-1 (b - A u_old)_I,
+  M = (D + L) D^-1 (D + U) -- forward d1 = (D + L)^-1 r, the backward sweep's
+  right-hand side is r - A_c d1 = -U d1, d2 = (D + U)^-1 (-U d1), and
+  d1 + d2 = (D + U)^-1 D d1.  K = 1 is plain symmetric Gauss-Seidel.
 """
 from __future__ import annotations
 
@@ -349,8 +364,65 @@ def truncate(P, pmax):
     return _csr_from_rows(rows, P.shape[1])
 
 
-def _tri(A, lower):
-    return (sp.tril(A) if lower else sp.triu(A)).tocsr()
+def chunk_ids(n, K):
+    """Chunk of every row: hypre's OpenMP partition of n rows over K threads
+    (par_relax.c relax type 6: size = n / K, the first n % K chunks one row
+    longer; K_l = min(K, n) so no chunk is empty)."""
+    K = max(1, min(int(K), n))
+    q, r = divmod(n, K)
+    lens = np.full(K, q, dtype=np.int64)
+    lens[:r] += 1
+    return np.repeat(np.arange(K, dtype=np.int64), lens)
+
+
+def level_chunks(n, K, min_rows):
+    """Chunks of a level of n rows: K, fewer when a chunk would hold fewer than
+    min_rows rows (0: no floor)."""
+    if min_rows > 0:
+        K = min(K, max(1, n // min_rows))
+    return max(1, min(K, n))
+
+
+def hybrid_sgs_literal(A, b, u, K, points=None):
+    """hypre's relax type 6 with K threads, row by row (pure-Python loops: small
+    KAT cases only).  points: boolean mask of the rows this pass relaxes (the
+    C / F set), None = every row."""
+    A = A.tocsr()
+    n = A.shape[0]
+    cid = chunk_ids(n, K)
+    u = np.array(u, dtype=np.float64)
+    tmp = u.copy()
+    rp, ci, v = A.indptr, A.indices, A.data
+    starts = np.flatnonzero(np.r_[True, cid[1:] != cid[:-1]]) if n else []
+    for ns in list(starts):
+        ne = ns
+        while ne < n and cid[ne] == cid[ns]:
+            ne += 1
+        for rng in (range(ns, ne), range(ne - 1, ns - 1, -1)):
+            for i in rng:
+                if points is not None and not points[i]:
+                    continue
+                d, res = 0.0, b[i]
+                for k in range(rp[i], rp[i + 1]):
+                    j = ci[k]
+                    if j == i:
+                        d = v[k]
+                    else:
+                        res -= v[k] * (u[j] if ns <= j < ne else tmp[j])
+                if d != 0.0:
+                    u[i] = res / d
+    return u
+
+
+def _sgs_factors(A, cid, idx):
+    """(D + L, D + U, strict U) of the chunk-block-diagonal part of A restricted to idx."""
+    Asub = A if idx is None else A[idx][:, idx]
+    c = cid if idx is None else cid[idx]
+    Asub = Asub.tocoo()
+    keep = c[Asub.row] == c[Asub.col]
+    Abd = sp.csr_matrix((Asub.data[keep], (Asub.row[keep], Asub.col[keep])), shape=Asub.shape)
+    Abd.sort_indices()
+    return sp.tril(Abd).tocsr(), sp.triu(Abd).tocsr(), sp.triu(Abd, k=1).tocsr()
 
 
 class PCBoomerAMG:
@@ -373,6 +445,10 @@ class PCBoomerAMG:
             raise NotImplementedError(f"boomeramg coarsen_type {coarsen_t} / interp_type {interp_t}")
         if self.K < 1:
             raise ValueError("grid_sweeps_all must be >= 1")
+        self.chunks = int(db.get("pls.hypre_relax_chunks", 256))
+        self.chunk_rows = int(db.get("pls.hypre_relax_min_rows", 1024))
+        if self.chunks < 1 or self.chunk_rows < 0:
+            raise ValueError("pls.hypre_relax_chunks must be >= 1, pls.hypre_relax_min_rows >= 0")
         A = A.tocsr()
         A.sort_indices()
         self.levels = []
@@ -395,19 +471,33 @@ class PCBoomerAMG:
         self.coarse = A
         self.coarse_lu = spla.splu(sp.csc_matrix(A)) if A.shape[0] else None
 
+    def _smoother(self, L):
+        """Per relaxation set ("all", or "C" / "F"): its rows and the hybrid SGS factors."""
+        if "sgs" not in L:
+            A = L["A"]
+            cid = chunk_ids(A.shape[0], level_chunks(A.shape[0], self.chunks, self.chunk_rows))
+            sets = {"all": None} if self.no_cf else {o: np.flatnonzero(L["cf"] == (C if o == "C" else F)) for o in "CF"}
+            L["sgs"] = {k: (idx,) + _sgs_factors(A, cid, idx) for k, idx in sets.items()}
+        return L["sgs"]
+
     def _relax(self, L, b, x, order):
         A = L["A"]
-        sets = [None] if self.no_cf else [np.flatnonzero(L["cf"] == (C if o == "C" else F)) for o in order]
+        sm = self._smoother(L)
+        sets = [sm["all"]] if self.no_cf else [sm[o] for o in order]
         for _ in range(self.K):
-            for idx in sets:
-                for lower in (True, False):
-                    r = b - A @ x
-                    if idx is None:
-                        x = x + spla.spsolve_triangular(_tri(A, lower), r, lower=lower)
-                    elif len(idx):
-                        Asub = A[idx][:, idx]
-                        x = x.copy()
-                        x[idx] += spla.spsolve_triangular(_tri(Asub, lower), r[idx], lower=lower)
+            for idx, lo, up, us in sets:
+                if idx is not None and not len(idx):
+                    continue
+                r = b - A @ x
+                if idx is not None:
+                    r = r[idx]
+                d1 = spla.spsolve_triangular(lo, r, lower=True)
+                d2 = spla.spsolve_triangular(up, -(us @ d1), lower=False)
+                x = x.copy()
+                if idx is None:
+                    x += d1 + d2
+                else:
+                    x[idx] += d1 + d2
         return x
 
     def _vcycle(self, l, b):

@@ -14,10 +14,13 @@
 // the order the spec writes it, without contraction.  Row-local stages
 // (strength, S2, interpolation rows, truncation, Galerkin products) run on
 // host threads (row results do not depend on the thread count); the
-// coarsening pass is sequential by definition.  Each level's Gauss-Seidel
-// half-sweep is a device triangular solve: (D + L)^-1 r is the ILU(0) apply of
-// the lower triangle tril(A) (its ILU(0) factors are exact: I + L D^-1 and D),
-// (D + U)^-1 r that of triu(A), on libpls's level-scheduled sweeps.
+// coarsening pass is sequential by definition.  Smoothing is hypre's relax
+// type 6 as its OpenMP build runs it with K threads (pls.hypre_relax_chunks,
+// oracle "hybrid symmetric Gauss-Seidel with K chunks"): one symmetric sweep
+// is x_I += M^-1 (b - A x)_I with M = (D + L) D^-1 (D + U) of the
+// chunk-block-diagonal part, i.e. one ILU-style apply of the factors
+// I + L D^-1 and D + U (PCILU in sgs mode) -- the chunks are its blocks, so
+// one workgroup sweeps each chunk on libpls's level-scheduled LDS sweeps.
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -520,9 +523,27 @@ HostCSR truncate(const HostCSR &P, int64_t pmax) {
     return to_csr(R, P.ncols);
 }
 
-// rows / columns `idx` of A (idx ascending; empty: all), lower or upper triangle with the diagonal
-HostCSR triangle(const HostCSR &A, const std::vector<int32_t> &idx, bool lower) {
+// hypre's OpenMP partition of a level's n rows over its K_l threads (par_relax.c
+// relax type 6): chunk size n / K_l, the first n % K_l chunks one row longer;
+// K_l = K, fewer when a chunk would hold fewer than min_rows rows (0: no floor)
+int64_t level_chunks(int64_t n, int64_t K, int64_t min_rows) {
+    if (min_rows > 0) K = std::min<int64_t>(K, std::max<int64_t>(1, n / min_rows));
+    return std::max<int64_t>(1, std::min<int64_t>(K, n));
+}
+struct ChunkMap {
+    int64_t q = 1, r = 0;
+    ChunkMap(int64_t n, int64_t K) : q(n / K), r(n % K) {}
+    int64_t operator()(int64_t i) const { return i < r * (q + 1) ? i / (q + 1) : r + (i - r * (q + 1)) / q; }
+};
+
+// The chunk-block-diagonal part of A (entries whose row and column share a
+// chunk of the level's K_l chunks) restricted to rows / columns `idx` (idx
+// ascending; empty: all): part 0 all of it, 1 its lower triangle with the
+// diagonal (D + L), 2 the upper one (D + U).  A zero or missing diagonal entry
+// is refused (hypre would skip the row).
+HostCSR chunk_part(const HostCSR &A, const std::vector<int32_t> &idx, int64_t K, int part) {
     const int64_t n = A.nrows;
+    const ChunkMap chunk(n, K);
     std::vector<int32_t> loc;
     const bool all = idx.empty();
     if (!all) {
@@ -535,10 +556,11 @@ HostCSR triangle(const HostCSR &A, const std::vector<int32_t> &idx, bool lower) 
     T.rp.assign(1, 0);
     for (int64_t r = 0; r < m; ++r) {
         const int64_t i = all ? r : idx[r];
+        const int64_t ch = chunk(i);
         bool has_diag = false;
         for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
             const int32_t j = all ? A.ci[k] : loc[A.ci[k]];
-            if (j < 0 || (lower ? j > r : j < r)) continue;
+            if (j < 0 || (part == 1 && j > r) || (part == 2 && j < r) || chunk(A.ci[k]) != ch) continue;
             if (j == r) {
                 if (A.v[k] == 0.0) break;
                 has_diag = true;
@@ -555,6 +577,7 @@ HostCSR triangle(const HostCSR &A, const std::vector<int32_t> &idx, bool lower) 
 struct BParams {
     double theta = 0.25, mu = 0.9, rap_bytes = 16e9;
     int64_t pmax = 0, agg_nl = 0, max_levels = 25;
+    int64_t chunks = 256, chunk_rows = 1024;  // hybrid Gauss-Seidel partition (pls.hypre_relax_*)
     int paths = 1, K = 1;
     bool no_cf = false;
 };
@@ -571,6 +594,10 @@ BParams parse_params(const Options &o, const std::string &prefix) {
     p.K = (int)o.integer(pre + "grid_sweeps_all", 1);
     p.no_cf = o.flag(pre + "no_CF", false);
     p.rap_bytes = o.num("pls.amg_rap_dense_gb", 16.0) * 1e9;
+    p.chunks = o.integer("pls.hypre_relax_chunks", 256);
+    p.chunk_rows = o.integer("pls.hypre_relax_min_rows", 1024);
+    if (p.chunks < 1 || p.chunk_rows < 0)
+        throw Error("pls.hypre_relax_chunks must be >= 1 and pls.hypre_relax_min_rows >= 0");
     const std::string ct = o.str(pre + "coarsen_type", "HMIS"), it = o.str(pre + "interp_type", "ext+i");
     if (ct != "HMIS") throw Error(pre + "coarsen_type " + ct + ": only HMIS is implemented");
     if (it != "ext+i") throw Error(pre + "interp_type " + it + ": only ext+i is implemented");
@@ -629,12 +656,87 @@ int64_t tri_levels(const HostCSR &T, bool upper) {
     return top;
 }
 
+// Hybrid symmetric Gauss-Seidel through dense per-chunk inverses (mostly
+// sequential chunks, e.g. the ~30 % dense Galerkin operators below an
+// aggressive level, where every row is a level of its own): M_c^-1 =
+// (D + U)_c^-1 D_c (D + L)_c^-1 is formed once per chunk on the device (two
+// Gauss-Jordan inverses, a row scaling and a GEMM), and a sweep is one
+// block-diagonal GEMV (8 bytes per row per chunk column, HBM-bound).
+struct PCSGSDense : PC {
+    int64_t ld = 64, K = 1;
+    DBuf<double> Minv;
+    DBuf<int32_t> cof;
+    DBuf<int64_t> cptr;
+    static int64_t ld_for(const std::vector<int64_t> &cp) {
+        int64_t mx = 1;
+        for (size_t k = 0; k + 1 < cp.size(); ++k) mx = std::max(mx, cp[k + 1] - cp[k]);
+        return (mx + 63) / 64 * 64;
+    }
+    // rows [c0, c0 + m) of a block-diagonal T, columns shifted to the chunk
+    static HostCSR chunk_block(const HostCSR &T, int64_t c0, int64_t m) {
+        HostCSR B;
+        B.nrows = B.ncols = m;
+        B.rp.assign(1, 0);
+        for (int64_t i = c0; i < c0 + m; ++i) {
+            for (int64_t k = T.rp[i]; k < T.rp[i + 1]; ++k) {
+                if (T.ci[k] < c0 || T.ci[k] >= c0 + m) throw Error("boomeramg: chunk block leaves its chunk");
+                B.ci.push_back(T.ci[k] - (int32_t)c0);
+                B.v.push_back(T.v[k]);
+            }
+            B.rp.push_back((int64_t)B.ci.size());
+        }
+        return B;
+    }
+    PCSGSDense(const HostCSR &lo, const HostCSR &up, const std::vector<int64_t> &cp, Ctx &c) {
+        type = "sgs";
+        n = lo.nrows;
+        K = (int64_t)cp.size() - 1;
+        ld = ld_for(cp);
+        Minv.alloc(K * ld * ld);
+        DBuf<double> Li(ld * ld), Ui(ld * ld), D(64 * 64), dd(ld);
+        DBuf<int32_t> fail(1);
+        HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
+        std::vector<double> dh(ld, 1.0);
+        for (int64_t k = 0; k < K; ++k) {
+            const int64_t c0 = cp[k], m = cp[k + 1] - c0;
+            DevCSR Ld, Ud;
+            upload(chunk_block(lo, c0, m), Ld, c);
+            upload(chunk_block(up, c0, m), Ud, c);
+            for (int64_t i = 0; i < m; ++i) dh[i] = lo.v[lo.rp[c0 + i + 1] - 1];  // the diagonal closes a lower row
+            HIPCHK(hipMemcpyAsync(dd.p, dh.data(), sizeof(double) * ld, hipMemcpyHostToDevice, c.st));
+            launch_dense_from_csr(m, ld, Ld.rp.p, Ld.ci.p, Ld.val.p, Li.p, c.st);
+            launch_dense_invert(ld, Li.p, D.p, fail.p, c.st);
+            launch_dense_from_csr(m, ld, Ud.rp.p, Ud.ci.p, Ud.val.p, Ui.p, c.st);
+            launch_dense_invert(ld, Ui.p, D.p, fail.p, c.st);
+            launch_dense_rowscale(m, ld, dd.p, Li.p, c.st);
+            launch_dense_gemm(ld, Ui.p, Li.p, Minv.p + k * ld * ld, c.st);
+            HIPCHK(hipGetLastError());
+            c.sync();  // Ld / Ud / dh are reused or freed
+        }
+        int32_t hfail = 0;
+        HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+        std::vector<int32_t> of(n);
+        for (int64_t k = 0; k < K; ++k)
+            for (int64_t i = cp[k]; i < cp[k + 1]; ++i) of[i] = (int32_t)k;
+        cof.alloc(std::max<int64_t>(n, 1));
+        cptr.alloc(K + 1);
+        HIPCHK(hipMemcpyAsync(cof.p, of.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+        HIPCHK(hipMemcpyAsync(cptr.p, cp.data(), sizeof(int64_t) * (K + 1), hipMemcpyHostToDevice, c.st));
+        c.sync();
+        if (hfail) throw Error("boomeramg: zero pivot in a dense Gauss-Seidel chunk");
+    }
+    bool reentrant() const override { return true; }
+    void apply(const double *x, double *y, Ctx &c) override {
+        launch_bdense_gemv(n, ld, cof.p, cptr.p, Minv.p, x, y, c.st);
+    }
+};
+
 struct RelaxSet {  // the points one Gauss-Seidel pass visits (all, C or F)
-    int64_t m = 0;
+    int64_t m = 0, chunks = 1;
     bool all = true;
     DBuf<int64_t> idx;
-    DevCSR lo, up;
-    std::unique_ptr<PC> fwd, bwd;  // (D + L)_II^-1, (D + U)_II^-1
+    DevCSR sub;                // C / F sets: the chunk-block-diagonal part restricted to the set
+    std::unique_ptr<PC> sgs;   // r -> M^-1 r: one hybrid symmetric GS sweep from 0
 };
 
 struct BLevel {
@@ -698,7 +800,11 @@ struct PCBoomer : PC {
         const bool view = o.flag("pls.amg_view", false);
         const bool allow_lds = o.flag("pls.ilu_lds", true);
         const int gmem = (int)o.integer("pls.ilu_gmem", 0), ring = (int)o.integer("pls.ilu_ring", 1);
-        const int64_t dense_min = o.integer("pls.amg_gs_dense_min", 2048);
+        // Gauss-Seidel chunks through dense inverses: -1 by the cost model below, 1 whenever
+        // they fit (pls.amg_gs_dense_gb, chunks <= pls.lu_dense_max rows), 0 never
+        const int gs_dense = (int)o.integer("pls.amg_gs_dense", -1);
+        const double level_us = o.num("pls.amg_gs_level_us", 0.5);  // sweep cost per level (measured ~0.3-1 us)
+        const double dense_gb = o.num("pls.amg_gs_dense_gb", 2.0);
         const int64_t wide_rows = o.integer("pls.amg_wide_rows", 256);  // rows per level above which: grid-wide sweeps
         const int wide_mode = (int)o.integer("pls.amg_wide_mode", -2);  // -2: CSR level kernels, -1: SELL level slices
         const int64_t dense_max = o.integer("pls.lu_dense_max", 32768);
@@ -731,9 +837,11 @@ struct PCBoomer : PC {
                 groups.resize(2);
                 for (int64_t i = 0; i < Al.nrows; ++i) groups[cf[i] == CPT ? 0 : 1].push_back((int32_t)i);
             }
+            const int64_t Kl = level_chunks(Al.nrows, prm.chunks, prm.chunk_rows);
             for (auto &g : groups) {
                 auto rs = std::make_unique<RelaxSet>();
                 rs->all = no_cf;
+                rs->chunks = Kl;
                 rs->m = no_cf ? Al.nrows : (int64_t)g.size();
                 if (rs->m > 0) {
                     if (!no_cf) {
@@ -741,23 +849,36 @@ struct PCBoomer : PC {
                         rs->idx.alloc(gi.size());
                         HIPCHK(hipMemcpyAsync(rs->idx.p, gi.data(), sizeof(int64_t) * gi.size(), hipMemcpyHostToDevice, c.st));
                     }
-                    const HostCSR lo = triangle(Al, g, true), up = triangle(Al, g, false);
-                    upload(lo, rs->lo, c);
-                    upload(up, rs->up, c);
-                    for (int half = 0; half < 2; ++half) {
-                        const HostCSR &T = half ? up : lo;
-                        DevCSR &Td = half ? rs->up : rs->lo;
-                        std::unique_ptr<PC> &pc = half ? rs->bwd : rs->fwd;
-                        // a mostly sequential triangle (Galerkin operators below an
-                        // aggressive level are ~30 % dense: every row a level of its
-                        // own) small enough for a dense inverse: one GEMV per half-sweep
-                        const int64_t nlev = tri_levels(T, half == 1);
-                        if (T.nrows >= dense_min && T.nrows <= dense_max && nlev * 8 >= T.nrows) {
-                            pc = std::make_unique<PCDenseLU>(Td, c);
+                    const HostCSR lo = chunk_part(Al, g, Kl, 1), up = chunk_part(Al, g, Kl, 2);
+                    // the set's chunk boundaries in its own numbering (chunks without set points dropped)
+                    std::vector<int64_t> cp{0};
+                    {
+                        const ChunkMap chunk(Al.nrows, Kl);
+                        for (int64_t t = 1; t < rs->m; ++t)
+                            if (chunk(no_cf ? t : g[t]) != chunk(no_cf ? t - 1 : g[t - 1])) cp.push_back(t);
+                        cp.push_back(rs->m);
+                    }
+                    // a sweep's critical path (levels of both triangles, one chunk per
+                    // workgroup) against the bytes of the dense chunk inverses: mostly
+                    // sequential chunks (every row a level of its own) go dense
+                    const int64_t nlev = tri_levels(lo, false), nlev_u = tri_levels(up, true);
+                    const int64_t ldc = PCSGSDense::ld_for(cp);
+                    const double dense_bytes = (double)((int64_t)cp.size() - 1) * ldc * ldc * 8.0;
+                    const double t_dense = (double)rs->m * ldc * 8.0 / 5e12 + 5e-6;
+                    const double t_sweep = (double)(nlev + nlev_u) * level_us * 1e-6;
+                    const bool dense = gs_dense != 0 && ldc <= dense_max && dense_bytes <= dense_gb * 1e9 &&
+                                       (gs_dense == 1 || t_dense < t_sweep);
+                    if (dense) {
+                        rs->sgs = std::make_unique<PCSGSDense>(lo, up, cp, c);
+                    } else {
+                        // wide levels: one grid-wide launch per level beats one workgroup
+                        const int gm = (nlev > 0 && lo.nrows / nlev > wide_rows) ? wide_mode : gmem;
+                        if (no_cf) {
+                            // the chunks are PCILU's blocks (the same partition): one workgroup per chunk
+                            rs->sgs = std::make_unique<PCILU>(*L->A, Kl, c, false, allow_lds, 0, gm, ring, true);
                         } else {
-                            // wide levels: one grid-wide launch per level beats one workgroup
-                            const int gm = (nlev > 0 && T.nrows / nlev > wide_rows) ? wide_mode : gmem;
-                            pc = std::make_unique<PCILU>(Td, 1, c, false, allow_lds, 0, gm, ring);
+                            upload(chunk_part(Al, g, Kl, 0), rs->sub, c);
+                            rs->sgs = std::make_unique<PCILU>(rs->sub, 1, c, false, allow_lds, 0, gm, ring, true);
                         }
                     }
                 }
@@ -783,8 +904,9 @@ struct PCBoomer : PC {
             } else {
                 Cmat = std::move(cur);
                 const DevCSR &Cm = Cmat ? *Cmat : M;
-                if (nco <= o.integer("pls.lu_dense_max", 32768)) Clu = std::make_unique<PCDenseLU>(Cm, c);
-                else Clu = std::make_unique<PCILU>(Cm, 1, c, true, allow_lds);
+                // hypre's Gaussian elimination (relax type 9): the exact device LU
+                // (dense inverse, band or envelope LU by size; make_lu)
+                Clu = make_lu(Cm, o, c);
             }
         }
         c.sync();
@@ -797,11 +919,13 @@ struct PCBoomer : PC {
                 next != L.nc)
                 throw Error("boomeramg: inconsistent hierarchy at level " + std::to_string(l));
             for (const auto &s : L.sets)
-                if (s->m > 0 && (s->lo.nrows != s->m || s->up.nrows != s->m)) throw Error("boomeramg: smoother size mismatch");
+                if (s->m > 0 && (!s->sgs || s->sgs->n != s->m)) throw Error("boomeramg: smoother size mismatch");
         }
         if (view) {
             fprintf(stderr, "[boomeramg %s] levels %zu:", prefix.c_str(), lv.size() + 1);
-            for (auto &L : lv) fprintf(stderr, " %lld(P nnz %lld)", (long long)L->n, (long long)L->P.nnz);
+            for (auto &L : lv)
+                fprintf(stderr, " %lld(P nnz %lld, %lld GS chunks)", (long long)L->n, (long long)L->P.nnz,
+                        (long long)(L->sets.empty() ? 0 : L->sets[0]->chunks));
             fprintf(stderr, " coarse %lld\n", (long long)nco);
             fprintf(stderr,
                     "[boomeramg %s] setup s: download/other %.2f strength %.2f coarsen %.2f interp %.2f RAP %.2f "
@@ -810,12 +934,9 @@ struct PCBoomer : PC {
         }
     }
 
-    // one Gauss-Seidel half-sweep over set s: x_I += T_II^-1 (b - A x)_I
-    // (x_zero: x == 0 on entry, so the residual is b and x_I is written)
-    void half_sweep(BLevel &L, size_t l, RelaxSet &s, bool lower, BWork &W, const double *b, double *x, bool x_zero,
-                    Ctx &c) {
-        if (s.m == 0) return;
-        PC &T = lower ? *s.fwd : *s.bwd;
+    // one hybrid symmetric Gauss-Seidel sweep over set s (oracle _relax):
+    // x_I += M^-1 (b - A x)_I  (x_zero: x == 0 on entry, so the residual is b)
+    void sweep(BLevel &L, size_t l, RelaxSet &s, BWork &W, const double *b, double *x, bool x_zero, Ctx &c) {
         const double *r = b;
         if (!x_zero) {
             spmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
@@ -823,15 +944,15 @@ struct PCBoomer : PC {
         }
         if (s.all) {
             if (x_zero) {
-                T.apply(r, x, c);
+                s.sgs->apply(r, x, c);
             } else {
-                T.apply(r, W.t[l].p, c);
+                s.sgs->apply(r, W.t[l].p, c);
                 launch_axpby(L.n, 1.0, W.t[l].p, 1.0, x, c.st);
             }
             return;
         }
         launch_gather(s.m, s.idx.p, r, W.rs[l].p, c.st);
-        T.apply(W.rs[l].p, W.ts[l].p, c);
+        s.sgs->apply(W.rs[l].p, W.ts[l].p, c);
         launch_gather(s.m, s.idx.p, x, W.xs[l].p, c.st);
         launch_axpby(s.m, 1.0, W.ts[l].p, 1.0, W.xs[l].p, c.st);
         launch_scatter(s.m, s.idx.p, W.xs[l].p, x, c.st);
@@ -844,9 +965,9 @@ struct PCBoomer : PC {
         for (int k = 0; k < K; ++k)
             for (size_t g = 0; g < L.sets.size(); ++g) {
                 RelaxSet &s = *L.sets[down ? g : L.sets.size() - 1 - g];
-                half_sweep(L, l, s, true, W, b, x, x_zero && no_cf, c);
+                if (s.m == 0) continue;
+                sweep(L, l, s, W, b, x, x_zero, c);
                 x_zero = false;
-                half_sweep(L, l, s, false, W, b, x, false, c);
             }
     }
 

@@ -219,4 +219,75 @@ void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, 
     if (n > 0) k_dense_gemv<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(n, ld, M, x, y);
 }
 
+// Block-diagonal GEMV: one wave per row, the row of its chunk's block.
+__global__ __launch_bounds__(256) void k_bdense_gemv(int64_t n, int64_t ld, const int32_t *__restrict__ cof,
+                                                     const int64_t *__restrict__ cptr, const double *__restrict__ M,
+                                                     const double *__restrict__ x, double *__restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t c = cof[i], c0 = cptr[c], len = cptr[c + 1] - c0;
+    const double *row = M + c * ld * ld + (i - c0) * ld;
+    const double *xc = x + c0;
+    double acc = 0.0;
+    const int64_t n2 = len & ~(int64_t)1;
+    for (int64_t k = 2 * lane; k < n2; k += 128) {
+        const dn_d2 m = __builtin_nontemporal_load(reinterpret_cast<const dn_d2 *>(row + k));
+        acc += m.x * xc[k];
+        acc += m.y * xc[k + 1];
+    }
+    if ((len & 1) && lane == 0) acc += row[len - 1] * xc[len - 1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) y[i] = acc;
+}
+void launch_bdense_gemv(int64_t n, int64_t ld, const int32_t *cof, const int64_t *cptr, const double *M,
+                        const double *x, double *y, hipStream_t st) {
+    if (n > 0) k_bdense_gemv<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(n, ld, cof, cptr, M, x, y);
+}
+
+__global__ __launch_bounds__(256) void k_dense_rowscale(int64_t n, int64_t ld, const double *d, double *M) {
+    const int64_t r = blockIdx.y;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r < n && j < ld) M[r * ld + j] = M[r * ld + j] * d[r];
+}
+void launch_dense_rowscale(int64_t n, int64_t ld, const double *d, double *M, hipStream_t st) {
+    if (n > 0) k_dense_rowscale<<<dim3((unsigned)((ld + 255) / 256), (unsigned)n), 256, 0, st>>>(n, ld, d, M);
+}
+
+// C = A B on 64 x 64 tiles (blockIdx = (tile column, tile row)), 4 x 4 outputs per thread
+__global__ __launch_bounds__(DTPB) void k_dense_gemm(int64_t ld, const double *A, const double *B, double *C) {
+    __shared__ double at[DB][DB + 1];  // A_ik^T
+    __shared__ double b[DB][DB + 1];   // B_kj
+    const int64_t j = blockIdx.x, i = blockIdx.y, nb = ld / DB;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    double acc[4][4] = {};
+    for (int64_t k = 0; k < nb; ++k) {
+        __syncthreads();
+        tile_load(A + (i * DB) * ld + k * DB, ld, at, true);
+        tile_load(B + (k * DB) * ld + j * DB, ld, b, false);
+        __syncthreads();
+        for (int kk = 0; kk < DB; ++kk) {
+            double av[4], bv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) av[r] = at[kk][ty + 16 * r];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bv[q] = b[kk][tx + 16 * q];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[r][q] += av[r] * bv[q];
+        }
+    }
+    double *Ct = C + (i * DB) * ld + j * DB;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ct[(int64_t)(ty + 16 * r) * ld + tx + 16 * q] = acc[r][q];
+}
+void launch_dense_gemm(int64_t ld, const double *A, const double *B, double *C, hipStream_t st) {
+    const unsigned nb = (unsigned)(ld / DB);
+    if (nb) k_dense_gemm<<<dim3(nb, nb), DTPB, 0, st>>>(ld, A, B, C);
+}
+
 }  // namespace pls

@@ -885,6 +885,34 @@ void launch_find_diag(int64_t n, const int64_t *rp, const int32_t *ci, int64_t *
     if (n > 0) k_find_diag<<<grid_for(n, TPB), TPB, 0, st>>>(n, rp, ci, diag, fail);
 }
 
+// Symmetric Gauss-Seidel factors (see kernels.hpp): 1/a_ii first, then every
+// strict-lower entry a_ij -> a_ij * (1/a_jj), the multiplier the ILU(0) IKJ
+// loop forms (k_ilu0_level: mult = a_ij * dinv[j]).
+__global__ __launch_bounds__(TPB) void k_sgs_dinv(int64_t n, const double *lu, const int64_t *diag, double *dinv,
+                                                  int32_t *fail) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const double d = lu[diag[i]];
+    if (d == 0.0) {
+        atomicMax(fail, 2);
+        dinv[i] = 0.0;
+    } else {
+        dinv[i] = 1.0 / d;
+    }
+}
+__global__ __launch_bounds__(TPB) void k_sgs_scale(int64_t n, const int64_t *rp, const int32_t *ci, double *lu,
+                                                   const int64_t *diag, const double *dinv) {
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    for (int64_t k = rp[i]; k < diag[i]; ++k) lu[k] = lu[k] * dinv[ci[k]];
+}
+void launch_sgs_factor(int64_t n, const int64_t *rp, const int32_t *ci, double *lu, const int64_t *diag,
+                       double *dinv, int32_t *fail, hipStream_t st) {
+    if (n <= 0) return;
+    k_sgs_dinv<<<grid_for(n, TPB), TPB, 0, st>>>(n, lu, diag, dinv, fail);
+    k_sgs_scale<<<grid_for(n, TPB), TPB, 0, st>>>(n, rp, ci, lu, diag, dinv);
+}
+
 // One 64-lane wave per row; the row is staged in LDS (cols + values), the
 // IKJ elimination runs over its strict-lower entries in column order, each
 // step updating the row's pattern positions that match row r's upper part

@@ -99,6 +99,12 @@ void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *
                        int32_t *fail, int64_t max_row, hipStream_t st);
 void launch_find_diag(int64_t n, const int64_t *rp, const int32_t *ci, int64_t *diag, int32_t *fail,
                       hipStream_t st);
+// Symmetric Gauss-Seidel "factors" in ILU(0) storage (hypre relax type 6 as a
+// preconditioner M = (D + L) D^-1 (D + U)): strict-lower entries scaled by the
+// column's 1/a_jj (the unit lower factor I + L D^-1), diagonal and upper kept
+// (the upper factor D + U), dinv = 1/a_ii; fail |= 2 on a zero diagonal.
+void launch_sgs_factor(int64_t n, const int64_t *rp, const int32_t *ci, double *lu, const int64_t *diag,
+                       double *dinv, int32_t *fail, hipStream_t st);
 // Level-ordered triangular factor storage ("row r of level order"): build
 void launch_lvl_count(int64_t n, const int32_t *order, const int64_t *rp, const int64_t *diag,
                       int upper, int64_t *len, hipStream_t st);
@@ -228,6 +234,15 @@ void launch_dense_from_csr(int64_t n, int64_t ld, const int64_t *rp, const int32
 void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStream_t st);
 // y = M[:n, :n] x
 void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, double *y, hipStream_t st);
+// Block-diagonal dense operators (hybrid Gauss-Seidel chunks of the AMG): chunk
+// c holds rows [cptr[c], cptr[c+1]) and its ld x ld row-major block at
+// M + c ld^2; cof[i] = chunk of row i.  y = blockdiag(M_c) x.
+void launch_bdense_gemv(int64_t n, int64_t ld, const int32_t *cof, const int64_t *cptr, const double *M,
+                        const double *x, double *y, hipStream_t st);
+// rows r < n of the ld x ld block M scaled by d[r]
+void launch_dense_rowscale(int64_t n, int64_t ld, const double *d, double *M, hipStream_t st);
+// C = A B, all ld x ld row-major (ld a multiple of 64)
+void launch_dense_gemm(int64_t ld, const double *A, const double *B, double *C, hipStream_t st);
 
 // ------------------------------------------------- banded exact LU (band.hip) --
 // T: nb tile rows x (bl + bu + 1) tiles of 64 x 64 (see band.hip); padding

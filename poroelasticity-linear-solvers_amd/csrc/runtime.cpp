@@ -968,10 +968,11 @@ static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order
 }
 
 PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr, int gmem_mode,
-             int ring_mode) {
+             int ring_mode, bool sgs_factors) {
     exact = exact_lu;
+    sgs = sgs_factors && !exact_lu;
     allow_lds = lds;
-    type = exact ? "lu" : (nb > 1 ? "bjacobi" : "ilu");
+    type = exact ? "lu" : sgs ? "sgs" : (nb > 1 ? "bjacobi" : "ilu");
     n = M.nrows;
     nblocks = exact ? 1 : std::max<int64_t>(1, std::min<int64_t>(nb, n));
     WindowSpec w{};
@@ -1005,7 +1006,12 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
     std::vector<int32_t> ordL;
     std::vector<int64_t> Lptr;
     nlev_L = level_order(n, rp, ci, false, ordL, Lptr);
-    {
+    if (sgs) {
+        launch_sgs_factor(n, F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p, fail.p, c.st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+        c.sync();
+    } else {
         DBuf<int32_t> rowsL(std::max<int64_t>(n, 1));
         HIPCHK(hipMemcpyAsync(rowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
         for (int64_t l = 0; l < nlev_L; ++l)

@@ -298,8 +298,12 @@ struct PCILU : PC {
     // gmem_mode (option pls.ilu_gmem): 0 auto, 1 force the y-resident
     // workgroup sweep (also on blocks that fit LDS), -1 never, -2 never and
     // per-level CSR kernels instead of the SELL-64 level slices
+    // sgs: no ILU(0) -- the factors are symmetric Gauss-Seidel's (I + L D^-1, D + U;
+    // launch_sgs_factor), so apply() is one hybrid symmetric GS sweep from 0 with
+    // the blocks as hypre's thread chunks (boomeramg.cpp)
+    bool sgs = false;
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0,
-          int gmem_mode = 0, int ring_mode = 1);
+          int gmem_mode = 0, int ring_mode = 1, bool sgs_factors = false);
     bool reentrant() const override { return profile_tag.empty(); }
     void apply(const double *x, double *y, Ctx &c) override;
 };

@@ -136,3 +136,24 @@ def test_weak_scaling_plan(G, N):
 def test_replicas_plan():
     a = _args("swelling3d-bjacobi", scaling="strong", replicas=True)
     assert bench.shard_plan(a, 4) == (False, 59) and a.scaling == "replicas"
+
+
+def test_launch_plan_gpus_vs_world_size():
+    """--gpus G without WORLD_SIZE launches G ranks itself; inside a job the
+    rank count is WORLD_SIZE and a disagreeing --gpus is an error (the driver's
+    G-GPU line must never silently run one rank)."""
+    assert bench.launch_plan(None, {}) == ("run", 1)
+    assert bench.launch_plan(1, {}) == ("run", 1)
+    assert bench.launch_plan(8, {}) == ("spawn", 8)
+    assert bench.launch_plan(None, {"WORLD_SIZE": "4"}) == ("run", 4)
+    assert bench.launch_plan(4, {"WORLD_SIZE": "4"}) == ("run", 4)
+    assert bench.launch_plan(8, {"WORLD_SIZE": "1"})[0] == "error"
+    assert bench.launch_plan(0, {})[0] == "error"
+
+
+def test_bench_exits_nonzero_on_rank_count_mismatch():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr

@@ -52,6 +52,11 @@ for _pre in ("s_", "f_", "p_", "diff_", "fp_fieldsplit_0_"):  # petsc-options-in
 INEXACT_PARAMS = {"inner ksp type": "cg", "inner pc type": "hypre", "solver maxiter": 200}
 
 
+# hybrid Gauss-Seidel partitions (oracle/boomeramg.py "K chunks")
+K1 = {"pls.hypre_relax_chunks": "1"}
+K256 = {"pls.hypre_relax_chunks": "256", "pls.hypre_relax_min_rows": "0"}
+
+
 def _amg_db(t, extra=None):
     """AMG on the s/f/p/diff blocks; the coupled (indefinite) 2-way fp block keeps ILU(0)."""
     db = dict(ILU_DB)
@@ -70,16 +75,21 @@ def _boomer_db(no_cf=True):
 
 @pytest.mark.parametrize("spec", [S.SynthSpec(2, 16), S.SynthSpec(3, 5)], ids=["2d16", "3d5"])
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
-@pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-inexact", "hypre-inexact-cf", "hypre-inexact-dense", "hypre-sa"])
+@pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-inexact", "hypre-inexact-cf", "hypre-inexact-dense", "hypre-sa",
+                               "hypre-inexact-k1", "hypre-inexact-k256", "hypre-inexact-cf-k256"])
 def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
     """hypre: PETSc's defaults (HMIS / ext+i, no truncation, no aggressive
     level, C/F-ordered Gauss-Seidel); -inexact: petsc-options-inexact's
     settings; -cf: the same with C/F relaxation; -dense: every Gauss-Seidel
-    half-sweep through its dense triangular inverse (pls.amg_gs_dense_min 0,
-    the path of mostly sequential coarse levels); -sa: pls.hypre sa."""
+    sweep through its dense chunk inverses (pls.amg_gs_dense 1, the path of
+    mostly sequential coarse levels); -sa: pls.hypre sa; -k1 / -k256:
+    the hybrid Gauss-Seidel with one chunk (plain symmetric GS) / 256 chunks on
+    every level (no row floor)."""
     params = dict(BASE, **{"pc type": pc_type, "inner pc type": "lu"})
     extra = {"hypre-inexact": _boomer_db(), "hypre-inexact-cf": _boomer_db(False), "hypre-sa": {"pls.hypre": "sa"},
-             "hypre-inexact-dense": dict(_boomer_db(), **{"pls.amg_gs_dense_min": "0"})}
+             "hypre-inexact-dense": dict(_boomer_db(), **{"pls.amg_gs_dense": "1"}),
+             "hypre-inexact-k1": dict(_boomer_db(), **K1), "hypre-inexact-k256": dict(_boomer_db(), **K256),
+             "hypre-inexact-cf-k256": dict(_boomer_db(False), **K256)}
     db = _amg_db(t.split("-")[0], extra.get(t))
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)
@@ -94,6 +104,15 @@ def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
 def test_gmres_preonly_gamg(gpu, pc_type):
     """Linear inner solves: the strict 1e-10 history bound."""
     _compare_solve(S.SynthSpec(2, 16), {"pc type": pc_type, "inner pc type": "lu"}, db=_amg_db("gamg"))
+
+
+@pytest.mark.parametrize("chunks", ["k1", "default", "k256"])
+def test_gmres_preonly_hypre_hybrid_gs(gpu, chunks):
+    """Linear inner solves (PREONLY + classical AMG): iteration count exact and
+    the strict 1e-10 history bound for each hybrid Gauss-Seidel partition."""
+    extra = dict(_boomer_db(), **{"k1": K1, "default": {}, "k256": K256}[chunks])
+    _compare_solve(S.SynthSpec(2, 16), {"pc type": "diagonal 3-way", "inner pc type": "lu"},
+                   db=_amg_db("hypre", extra))
 
 
 def test_gmres_preonly_gamg_options(gpu):
@@ -128,14 +147,16 @@ def test_hypre_error_option(gpu):
         h.setup()
 
 
-@pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-csr-levels"])
+@pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-csr-levels", "hypre-k1", "hypre-k256"])
 def test_amg_larger_hierarchy(gpu, t):
     """Two or more coarse levels on the solid block (3-D, N = 12; 46,875 rows,
-    beyond LDS).  hypre-csr-levels: every Gauss-Seidel triangle through the
-    per-level CSR kernels (pls.amg_wide_rows 0), the path of the N=59 level 0."""
+    beyond LDS).  hypre-csr-levels: one chunk, every sweep through the
+    per-level CSR kernels (pls.amg_wide_rows 0); -k1: one chunk (one
+    workgroup or per-level launches); -k256: 256 chunks (LDS sweeps)."""
     spec = S.SynthSpec(3, 12)
     params = dict(BASE, **{"pc type": "diagonal 3-way", "inner pc type": "lu"})
-    extra = dict(_boomer_db(), **({"pls.amg_wide_rows": "0"} if t == "hypre-csr-levels" else {}))
+    extra = dict(_boomer_db(), **({"pls.amg_wide_rows": "0", **K1} if t == "hypre-csr-levels" else
+                                  K1 if t == "hypre-k1" else K256 if t == "hypre-k256" else {}))
     db = _amg_db(t.split("-")[0], extra if t.startswith("hypre") else None)
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)

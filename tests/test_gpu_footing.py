@@ -20,9 +20,10 @@ same CSR.
   that swap (148 vs 150-153), so neither is a parity case;
 * the committed footing fixtures (tests/golden/footing/) reproduced by the
   device -- its, reason, history and x;
-* a larger solve, N = 32, with the exact option set through properties
-  (converged, bitwise reproducible, true residual of the returned x);
-  configs[2]'s N = 128 is bench-only (setup 263 s).
+* larger solves, N = 32, through properties (converged, bitwise
+  reproducible, true residual of the returned x): the exact option set, and
+  footing.py's own (petsc-options-inexact, hypre -> the classical AMG with
+  hybrid Gauss-Seidel over 256-chunk partitions).
 """
 import json
 import os
@@ -51,6 +52,7 @@ def _options(preset, pc="undrained"):
     (8, "diagonal 3-way", "exact"),
     (8, "undrained", "inexact-ilu"),
     (8, "undrained", "inexact"),
+    (12, "undrained", "inexact"),
 ])
 def test_footing_vs_oracle(gpu, N, pc, preset):
     s = FF.assemble_footing(N, pc)
@@ -125,3 +127,32 @@ def test_footing_full_solve_properties(gpu):
     assert h1[-1] <= max(params["solver rtol"] * h1[0], params["solver atol"])
     true_r = np.linalg.norm(s.b - s.A @ x1)
     assert abs(true_r - h1[-1]) <= 1e-2 * h1[-1] + 1e-12 * np.linalg.norm(s.b)
+
+
+def test_footing_amg_solve_properties(gpu):
+    """footing.py's own option set (petsc-options-inexact, BoomerAMG -> the
+    classical AMG, hybrid Gauss-Seidel in chunks) on the N = 32 system: the
+    outer GMRES converges, two fresh handles give bitwise equal histories and
+    solutions, and the returned x's true residual is within 10x the
+    convergence threshold (inner CG makes the PC nonlinear, so the GMRES
+    estimate is not the true residual)."""
+    import time
+    from lib.handle import Handle, params_to_options
+    s = FF.assemble_footing(32, "undrained")
+    params, db = _options("inexact")
+    opts = dict(db)
+    opts.update(params_to_options(params))
+    runs = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+        x, r = h.solve(s.b)
+        runs.append((r, h.history(), x))
+        h.destroy()
+        print(f"footing N=32 AMG: {r.its} its, reason {r.reason}, {time.perf_counter() - t0:.1f} s (setup + solve)")
+    (r1, h1, x1), (r2, h2, x2) = runs
+    assert r1.reason > 0 and r1.its == r2.its
+    assert np.array_equal(h1, h2) and np.array_equal(x1, x2)
+    thr = max(params["solver rtol"] * h1[0], params["solver atol"])
+    assert h1[-1] <= thr
+    assert np.linalg.norm(s.b - s.A @ x1) <= 10 * thr

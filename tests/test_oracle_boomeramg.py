@@ -193,3 +193,51 @@ def test_libpls_host_setup_bitwise(db):
         nl, n, nc, cf, Ac = boomeramg_host_level(A, db, "x_", len(pc.levels))
         Co = pc.coarse.tocsr()
         assert np.array_equal(Ac.indptr, Co.indptr) and np.array_equal(Ac.data, Co.data), name
+
+
+# ------------------------------------------- hybrid Gauss-Seidel (K chunks) ----
+@pytest.mark.parametrize("K", [1, 3, 7, 64, 1000])
+@pytest.mark.parametrize("points", [None, "C", "F"])
+def test_hybrid_sgs_matrix_form_equals_hypre_loop(K, points):
+    """The spec's matrix form u_I += M^-1 (b - A u)_I, M = (D+L) D^-1 (D+U) of
+    the chunk-block-diagonal part, equals hypre's relax type 6 with K threads
+    row by row (par_relax.c: chunk rows read new values, the rest the values
+    before the sweep), on a nonsymmetric matrix, nonzero start, C/F subsets."""
+    from oracle.boomeramg import _sgs_factors, chunk_ids, hybrid_sgs_literal
+    import scipy.sparse.linalg as spla
+    rng = np.random.default_rng(K)
+    A = (lap2(9, eps=0.4) + sp.random(81, 81, density=0.03, random_state=1)).tocsr()
+    A.sort_indices()
+    n = A.shape[0]
+    b, u = rng.standard_normal((2, n))
+    mask = None if points is None else (rng.random(n) < 0.4) ^ (points == "F")
+    idx = None if mask is None else np.flatnonzero(mask)
+    ref = hybrid_sgs_literal(A, b, u, K, mask)
+    lo, up, us = _sgs_factors(A, chunk_ids(n, K), idx)
+    r = (b - A @ u) if idx is None else (b - A @ u)[idx]
+    d1 = spla.spsolve_triangular(lo, r, lower=True)
+    d = d1 + spla.spsolve_triangular(up, -(us @ d1), lower=False)
+    got = u.copy()
+    if idx is None:
+        got += d
+    else:
+        got[idx] += d
+    assert np.max(np.abs(got - ref)) <= 1e-13 * np.max(np.abs(ref))
+
+
+def test_chunk_partition_is_hypres():
+    from oracle.boomeramg import chunk_ids
+    c = chunk_ids(10, 4)  # size 2, rest 2: chunks of 3, 3, 2, 2
+    assert c.tolist() == [0, 0, 0, 1, 1, 1, 2, 2, 3, 3]
+    assert chunk_ids(3, 256).tolist() == [0, 1, 2]  # Jacobi when rows < K
+    from oracle.boomeramg import level_chunks
+    assert level_chunks(5_000_000, 256, 1024) == 256 and level_chunks(10_000, 256, 1024) == 9
+    assert level_chunks(500, 256, 1024) == 1 and level_chunks(500, 256, 0) == 256
+
+
+@pytest.mark.parametrize("K", [1, 8, 256])
+def test_hybrid_vcycle_pcg_converges(K):
+    A = lap2(40)
+    pc = PCBoomerAMG(A, dict(INEXACT, **{"pls.hypre_relax_chunks": str(K), "pls.hypre_relax_min_rows": "0"}), "x_")
+    b = np.random.default_rng(0).standard_normal(A.shape[0])
+    assert pcg(A, b, pc.apply) <= 14

@@ -14,6 +14,7 @@
 #   footing                     configs[2] bench on the assembled footing system (N=128)
 #   prof_footing_fe             rocprofv3 of that solve
 #   prof_amg                    same for the classical AMG (-pc_type hypre) on the s block, 3-D N=27
+#   prof_amg59                  same at the metric's N=59
 #   configs                     bench on every BASELINE config that fits one GPU
 #   fe                          bench on the assembled swelling systems
 #   pmc                         FETCH_SIZE / WRITE_SIZE passes (tools/pmc.sh)
@@ -55,6 +56,7 @@ for s in "$@"; do
       prof) prof prof --steps 2 --warmup 1 --no-cpu ;;
       prof_footing) prof prof_footing --config footing-inexact-ilu --steps 3 --warmup 1 --no-cpu --no-copy-probe ;;
       prof_amg) prof prof_amg --N 27 --inner hypre --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
+      prof_amg59) prof prof_amg59 --inner hypre --steps 1 --warmup 1 --no-cpu --no-copy-probe ;;
       prof_fe) prof prof_fe --system fe --N 12 --inner ilu --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
       configs)
         run configs/swelling2d-exact 400 python -u bench.py --config swelling2d-exact --steps 3 --no-copy-probe
