@@ -748,11 +748,36 @@ static void do_setup(Handle &H) {
                 // setup_fieldsplit (Preconditioner.py:102-118): setFieldSplitIS((None, is_p)) then
                 // ((None, is_f)) -- split 0 = pressure, split 1 = fluid, fp-local positions
                 if (H.distributed) {
-                    // sharded fp block: the fieldsplit PC on the gathered block (field-major
-                    // global order: split 0 = p = [nf, nf + np), split 1 = f = [0, nf)), redundantly
-                    std::vector<int32_t> gf(H.dist.n[1]), gp(H.dist.n[2]);
-                    for (int64_t i = 0; i < H.dist.n[1]; ++i) gf[i] = (int32_t)i;
-                    for (int64_t i = 0; i < H.dist.n[2]; ++i) gp[i] = (int32_t)(H.dist.n[1] + i);
+                    // sharded fp block: the fieldsplit PC on the gathered block, redundantly.
+                    // Gathered order = the block's global order: synthetic shards are
+                    // field-major (split 0 = p = [nf, nf + np), split 1 = f = [0, nf));
+                    // caller-assembled ones (pls_create_dist, 2-way: one fp field) are
+                    // rank-major, each rank's rows its sorted f U p (PETSc's is_fp), so the
+                    // splits are every rank's fp_is_p / fp_is_f offset by its first row
+                    std::vector<int32_t> gf, gp;
+                    const Dist &D = H.dist;
+                    if (D.n[2] == 0) {
+                        Comm *cm = c.comm;
+                        const int G = cm->size;
+                        int64_t mine[2] = {(int64_t)H.fp_is_f.size(), (int64_t)H.fp_is_p.size()};
+                        std::vector<int64_t> cnts((size_t)2 * G);
+                        cm->allgather_host(mine, sizeof(mine), cnts.data());
+                        int64_t mx = 1;
+                        for (int64_t v : cnts) mx = std::max(mx, v);
+                        std::vector<int32_t> sendf(mx, -1), sendp(mx, -1), allf((size_t)mx * G), allp((size_t)mx * G);
+                        std::copy(H.fp_is_f.begin(), H.fp_is_f.end(), sendf.begin());
+                        std::copy(H.fp_is_p.begin(), H.fp_is_p.end(), sendp.begin());
+                        cm->allgather_host(sendf.data(), sizeof(int32_t) * mx, allf.data());
+                        cm->allgather_host(sendp.data(), sizeof(int32_t) * mx, allp.data());
+                        for (int q = 0; q < G; ++q) {
+                            const int64_t base = D.start[1][q];
+                            for (int64_t k = 0; k < cnts[2 * q]; ++k) gf.push_back((int32_t)(base + allf[(size_t)q * mx + k]));
+                            for (int64_t k = 0; k < cnts[2 * q + 1]; ++k) gp.push_back((int32_t)(base + allp[(size_t)q * mx + k]));
+                        }
+                    } else {
+                        for (int64_t i = 0; i < D.n[1]; ++i) gf.push_back((int32_t)i);
+                        for (int64_t i = 0; i < D.n[2]; ++i) gp.push_back((int32_t)(D.n[1] + i));
+                    }
                     H.pc_red_fp = make_redundant("fieldsplit", H.Kfp, c, [&](const DevCSR &Gm, Ctx &sc) -> std::unique_ptr<PC> {
                         return std::make_unique<PCFieldSplit>(Gm, gp, gf, o, "fp_", sc);
                     }, "fp_");

@@ -290,4 +290,315 @@ void launch_dense_gemm(int64_t ld, const double *A, const double *B, double *C, 
     if (nb) k_dense_gemm<<<dim3(nb, nb), DTPB, 0, st>>>(ld, A, B, C);
 }
 
+// ============================================ multifrontal LU (sparse_lu.cpp) ==
+// A front's tile (I, J) (64 x 64, leading dimension ld = 64 ldt).
+__device__ __forceinline__ double *mf_tile(const MFront &f, double *W, int64_t I, int64_t J) {
+    const int64_t ld = (int64_t)f.ldt * DB;
+    return W + f.ws + (I * DB) * ld + J * DB;
+}
+
+__global__ __launch_bounds__(256) void k_mf_pad(const MFront *F, double *W) {
+    const MFront f = F[blockIdx.y];
+    const int64_t r = f.p + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r < (int64_t)f.pt * DB) W[f.ws + r * ((int64_t)f.ldt * DB) + r] = 1.0;
+}
+void launch_mf_pad(int nf, const MFront *F, int max_pad, double *W, hipStream_t st) {
+    if (nf > 0 && max_pad > 0) k_mf_pad<<<dim3((unsigned)((max_pad + 255) / 256), (unsigned)nf), 256, 0, st>>>(F, W);
+}
+
+__global__ __launch_bounds__(256) void k_mf_scatter(int64_t m, const int64_t *dst, const int64_t *src,
+                                                    const double *val, double *W) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k < m) W[dst[k]] = val[src[k]];
+}
+void launch_mf_scatter(int64_t m, const int64_t *dst, const int64_t *src, const double *val, double *W,
+                       hipStream_t st) {
+    if (m > 0) k_mf_scatter<<<(unsigned)((m + 255) / 256), 256, 0, st>>>(m, dst, src, val, W);
+}
+
+// blockIdx.x: child, blockIdx.y: update row of the child
+__global__ __launch_bounds__(256) void k_mf_extend(const MChild *C, const int32_t *maps, const double *Wprev,
+                                                   double *Wcur) {
+    const MChild c = C[blockIdx.x];
+    const int64_t r = blockIdx.y;
+    if (r >= c.q) return;
+    const int64_t pr = maps[c.map_off + r];
+    const double *src = Wprev + c.src_ws + ((int64_t)c.src_pp + r) * c.src_ld + c.src_pp;
+    double *dst = Wcur + c.dst_ws + pr * c.dst_ld;
+    for (int64_t s = threadIdx.x; s < c.q; s += 256) {
+        const int64_t ps = maps[c.map_off + s];
+        dst[ps] = dst[ps] + src[s];
+    }
+}
+void launch_mf_extend(int nc, const MChild *C, int max_q, const int32_t *maps, const double *Wprev, double *Wcur,
+                      hipStream_t st) {
+    if (nc > 0 && max_q > 0) k_mf_extend<<<dim3((unsigned)nc, (unsigned)max_q), 256, 0, st>>>(C, maps, Wprev, Wcur);
+}
+
+// Gauss-Jordan step k, as launch_dense_invert but over the front's pivot tiles
+// only and batched over fronts (blockIdx.z).  The diagonal tile's inverse is
+// formed with partial pivoting inside the tile (row swaps on [T | I]): the block
+// elimination only needs D = T_kk^-1, however it is computed, and saddle-point
+// blocks (the 2-way fp block: zero pressure diagonal) have zero scalar pivots
+// whose tile is still regular.
+#pragma clang fp contract(off)
+__global__ __launch_bounds__(DTPB) void k_mf_gj_diag(const MFront *F, int k, double *W, double *D, int32_t *fail) {
+    __shared__ double a[DB][DB + 1];
+    __shared__ double v[DB][DB + 1];
+    __shared__ int prow;
+    const MFront f = F[blockIdx.z];
+    if (k >= f.pt) return;
+    const int64_t ld = (int64_t)f.ldt * DB;
+    const double *src = mf_tile(f, W, k, k);
+    for (int t = threadIdx.x; t < DB * DB; t += DTPB) {
+        const int i = t / DB, j = t % DB;
+        a[i][j] = src[(int64_t)i * ld + j];
+        v[i][j] = i == j ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    for (int p = 0; p < DB; ++p) {
+        if (threadIdx.x < DB) {  // wave 0: argmax |a[i][p]|, i >= p (ties: the smaller row)
+            const int i = threadIdx.x;
+            double m = i >= p ? fabs(a[i][p]) : -1.0;
+            int r = i;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const double m2 = __shfl_xor(m, o);
+                const int r2 = __shfl_xor(r, o);
+                if (m2 > m || (m2 == m && r2 < r)) {
+                    m = m2;
+                    r = r2;
+                }
+            }
+            if (i == 0) prow = r;
+        }
+        __syncthreads();
+        const int r = prow;
+        if (r != p && threadIdx.x < 2 * DB) {  // swap rows p and r of [a | v]
+            const int j = threadIdx.x & (DB - 1);
+            double (*m)[DB + 1] = threadIdx.x < DB ? a : v;
+            const double t = m[p][j];
+            m[p][j] = m[r][j];
+            m[r][j] = t;
+        }
+        __syncthreads();
+        const double piv = a[p][p];
+        if (piv == 0.0) {
+            if (threadIdx.x == 0) atomicOr(fail, 1);
+            return;  // uniform across the workgroup
+        }
+        if (threadIdx.x < 2 * DB) {
+            const int j = threadIdx.x & (DB - 1);
+            double (*m)[DB + 1] = threadIdx.x < DB ? a : v;
+            m[p][j] = m[p][j] / piv;
+        }
+        __syncthreads();
+        double fv[DB * DB / DTPB];
+        for (int u = 0; u < DB * DB / DTPB; ++u) fv[u] = a[(threadIdx.x + u * DTPB) / DB][p];
+        __syncthreads();
+        for (int u = 0; u < DB * DB / DTPB; ++u) {
+            const int t = threadIdx.x + u * DTPB, i = t / DB, j = t % DB;
+            if (i == p) continue;
+            a[i][j] = a[i][j] - fv[u] * a[p][j];
+            v[i][j] = v[i][j] - fv[u] * v[p][j];
+        }
+        __syncthreads();
+    }
+    double *Dt = D + (int64_t)blockIdx.z * DB * DB;
+    for (int t = threadIdx.x; t < DB * DB; t += DTPB) Dt[t] = v[t / DB][t % DB];
+}
+#pragma clang fp contract(on)
+
+__device__ __forceinline__ void mf_mm(const double *A, int64_t lda, const double *B, int64_t ldb,
+                                      double (*at)[DB + 1], double (*b)[DB + 1], double acc[4][4]) {
+    tile_load(A, lda, at, true);
+    tile_load(B, ldb, b, false);
+    __syncthreads();
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    for (int kk = 0; kk < DB; ++kk) {
+        double av[4], bv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) av[r] = at[kk][ty + 16 * r];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[q] = b[kk][tx + 16 * q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[r][q] += av[r] * bv[q];
+    }
+}
+
+// row panel: F_kj := D F_kj (j != k), F_kk := D
+__global__ __launch_bounds__(DTPB) void k_mf_gj_rowpanel(const MFront *F, int k, double *W, const double *D) {
+    __shared__ double at[DB][DB + 1];
+    __shared__ double b[DB][DB + 1];
+    const MFront f = F[blockIdx.z];
+    const int64_t j = blockIdx.x;
+    if (k >= f.pt || j >= f.ldt) return;
+    const int64_t ld = (int64_t)f.ldt * DB;
+    const double *Dt = D + (int64_t)blockIdx.z * DB * DB;
+    double *C = mf_tile(f, W, k, j);
+    if (j == k) {
+        for (int t = threadIdx.x; t < DB * DB; t += DTPB) C[(int64_t)(t / DB) * ld + t % DB] = Dt[t];
+        return;
+    }
+    double acc[4][4] = {};
+    mf_mm(Dt, DB, C, ld, at, b, acc);
+    __syncthreads();
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) C[(int64_t)(ty + 16 * r) * ld + tx + 16 * q] = acc[r][q];
+}
+
+// update: F_ij -= F_ik F_kj (i, j != k)
+__global__ __launch_bounds__(DTPB) void k_mf_gj_update(const MFront *F, int k, double *W) {
+    __shared__ double at[DB][DB + 1];
+    __shared__ double b[DB][DB + 1];
+    const MFront f = F[blockIdx.z];
+    if (k >= f.pt || (int)blockIdx.x >= f.ldt - 1 || (int)blockIdx.y >= f.ldt - 1) return;
+    const int64_t j = blockIdx.x + (blockIdx.x >= (unsigned)k ? 1 : 0);
+    const int64_t i = blockIdx.y + (blockIdx.y >= (unsigned)k ? 1 : 0);
+    const int64_t ld = (int64_t)f.ldt * DB;
+    double acc[4][4] = {};
+    mf_mm(mf_tile(f, W, i, k), ld, mf_tile(f, W, k, j), ld, at, b, acc);
+    double *C = mf_tile(f, W, i, j);
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double *c = C + (int64_t)(ty + 16 * r) * ld + tx + 16 * q;
+            *c = *c - acc[r][q];
+        }
+}
+
+// column panel: F_ik := -F_ik D (i != k)
+__global__ __launch_bounds__(DTPB) void k_mf_gj_colpanel(const MFront *F, int k, double *W, const double *D) {
+    __shared__ double at[DB][DB + 1];
+    __shared__ double b[DB][DB + 1];
+    const MFront f = F[blockIdx.z];
+    if (k >= f.pt || (int)blockIdx.x >= f.ldt - 1) return;
+    const int64_t i = blockIdx.x + (blockIdx.x >= (unsigned)k ? 1 : 0);
+    const int64_t ld = (int64_t)f.ldt * DB;
+    double *C = mf_tile(f, W, i, k);
+    double acc[4][4] = {};
+    mf_mm(C, ld, D + (int64_t)blockIdx.z * DB * DB, DB, at, b, acc);
+    __syncthreads();
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) C[(int64_t)(ty + 16 * r) * ld + tx + 16 * q] = -acc[r][q];
+}
+
+void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, double *D, int32_t *fail,
+                       hipStream_t st) {
+    if (nf <= 0 || max_ldt <= 0) return;
+    k_mf_gj_diag<<<dim3(1, 1, (unsigned)nf), DTPB, 0, st>>>(F, k, W, D, fail);
+    k_mf_gj_rowpanel<<<dim3((unsigned)max_ldt, 1, (unsigned)nf), DTPB, 0, st>>>(F, k, W, D);
+    if (max_ldt > 1) {
+        k_mf_gj_update<<<dim3((unsigned)(max_ldt - 1), (unsigned)(max_ldt - 1), (unsigned)nf), DTPB, 0, st>>>(F, k, W);
+        k_mf_gj_colpanel<<<dim3((unsigned)(max_ldt - 1), 1, (unsigned)nf), DTPB, 0, st>>>(F, k, W, D);
+    }
+}
+
+// blockIdx.x: front row (U part rows [0, pp), then X part rows), blockIdx.y: front
+__global__ __launch_bounds__(256) void k_mf_store(const MFront *F, const MStore *S, const double *W, double *U,
+                                                  double *X) {
+    const MFront f = F[blockIdx.y];
+    const MStore s = S[blockIdx.y];
+    const int64_t r = blockIdx.x, ld = (int64_t)f.ldt * DB, pp = (int64_t)f.pt * DB;
+    const double *src = W + f.ws + r * ld;
+    if (r < pp) {
+        for (int64_t c = threadIdx.x; c < ld; c += 256) U[s.uoff + r * ld + c] = src[c];
+    } else if (r < pp + f.q) {
+        for (int64_t c = threadIdx.x; c < pp; c += 256) X[s.xoff + (r - pp) * pp + c] = src[c];
+    }
+}
+void launch_mf_store(int nf, const MFront *F, const MStore *S, int max_rows, const double *W, double *U, double *X,
+                     hipStream_t st) {
+    if (nf > 0 && max_rows > 0) k_mf_store<<<dim3((unsigned)max_rows, (unsigned)nf), 256, 0, st>>>(F, S, W, U, X);
+}
+
+// ---------------------------------------------------------------- solve --
+__global__ __launch_bounds__(256) void k_mf_fwd_gather(int64_t m, const int32_t *rf, const int32_t *rl,
+                                                       const MSolve *S, const int64_t *cptr, const int64_t *cidx,
+                                                       const double *b, const double *cu, double *z, double *acc) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= m) return;
+    const MSolve s = S[rf[k]];
+    const int64_t r = rl[k];
+    double v = r < s.p ? b[s.pstart + r] : 0.0;
+    for (int64_t t = cptr[k]; t < cptr[k + 1]; ++t) v += cu[cidx[t]];
+    if (r < s.p) z[s.pstart + r] = v;
+    else acc[s.qoff + r - s.p] = v;
+}
+void launch_mf_fwd_gather(int64_t m, const int32_t *rf, const int32_t *rl, const MSolve *S, const int64_t *cptr,
+                          const int64_t *cidx, const double *b, const double *cu, double *z, double *acc,
+                          hipStream_t st) {
+    if (m > 0) k_mf_fwd_gather<<<(unsigned)((m + 255) / 256), 256, 0, st>>>(m, rf, rl, S, cptr, cidx, b, cu, z, acc);
+}
+
+__global__ __launch_bounds__(256) void k_mf_fwd_gemv(int64_t m, const int32_t *rf, const int32_t *rl,
+                                                     const MSolve *S, const double *__restrict__ X,
+                                                     const double *__restrict__ z, const double *acc, double *cu) {
+    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= m) return;
+    const int lane = threadIdx.x & 63;
+    const MSolve s = S[rf[k]];
+    const int64_t i = rl[k];
+    const double *row = X + s.xoff + i * s.pp;
+    const double *zp = z + s.pstart;
+    double a = 0.0;
+    for (int64_t j = lane; j < s.p; j += 64) a += row[j] * zp[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    if (lane == 0) cu[s.qoff + i] = acc[s.qoff + i] + a;
+}
+void launch_mf_fwd_gemv(int64_t m, const int32_t *rf, const int32_t *rl, const MSolve *S, const double *X,
+                        const double *z, const double *acc, double *cu, hipStream_t st) {
+    if (m > 0) k_mf_fwd_gemv<<<(unsigned)((m + 3) / 4), 256, 0, st>>>(m, rf, rl, S, X, z, acc, cu);
+}
+
+__global__ __launch_bounds__(256) void k_mf_bwd(int64_t m, const int32_t *rf, const int32_t *rl, const MSolve *S,
+                                                const double *__restrict__ U, const int32_t *__restrict__ slist,
+                                                const double *__restrict__ z, double *x) {
+    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= m) return;
+    const int lane = threadIdx.x & 63;
+    const MSolve s = S[rf[k]];
+    const int64_t r = rl[k];
+    const double *row = U + s.uoff + r * s.ld;
+    const double *zp = z + s.pstart;
+    double a = 0.0;
+    for (int64_t j = lane; j < s.p; j += 64) a += row[j] * zp[j];
+    const double *g = row + s.pp;
+    const int32_t *sl = slist + s.soff;
+    for (int64_t j = lane; j < s.q; j += 64) a -= g[j] * x[sl[j]];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    if (lane == 0) x[s.pstart + r] = a;
+}
+void launch_mf_bwd(int64_t m, const int32_t *rf, const int32_t *rl, const MSolve *S, const double *U,
+                   const int32_t *slist, const double *z, double *x, hipStream_t st) {
+    if (m > 0) k_mf_bwd<<<(unsigned)((m + 3) / 4), 256, 0, st>>>(m, rf, rl, S, U, slist, z, x);
+}
+
+__global__ __launch_bounds__(256) void k_gather_i32(int64_t n, const int32_t *perm, const double *b, double *x) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) x[i] = b[perm[i]];
+}
+__global__ __launch_bounds__(256) void k_scatter_i32(int64_t n, const int32_t *perm, const double *x, double *y) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) y[perm[i]] = x[i];
+}
+void launch_gather_i32(int64_t n, const int32_t *perm, const double *b, double *x, hipStream_t st) {
+    if (n > 0) k_gather_i32<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, perm, b, x);
+}
+void launch_scatter_i32(int64_t n, const int32_t *perm, const double *x, double *y, hipStream_t st) {
+    if (n > 0) k_scatter_i32<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, perm, x, y);
+}
+
 }  // namespace pls

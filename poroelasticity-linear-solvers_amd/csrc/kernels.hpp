@@ -244,6 +244,59 @@ void launch_dense_rowscale(int64_t n, int64_t ld, const double *d, double *M, hi
 // C = A B, all ld x ld row-major (ld a multiple of 64)
 void launch_dense_gemm(int64_t ld, const double *A, const double *B, double *C, hipStream_t st);
 
+// ------------------------------------------- multifrontal LU (dense.hip) --
+// Frontal matrices of one level of the assembly tree (sparse_lu.cpp): front f
+// is a dense ld x ld row-major block (ld = 64 ldt) at W + ws; its first p rows /
+// columns are the pivots (padded to 64 pt), the rest the update rows (q real).
+struct MFront {
+    int64_t ws;
+    int32_t ldt, pt, p, q;
+};
+// identity on the padding pivots [p, 64 pt) of every front
+void launch_mf_pad(int nf, const MFront *F, int max_pad, double *W, hipStream_t st);
+// W[dst[k]] = val[src[k]] (original entries into their fronts)
+void launch_mf_scatter(int64_t m, const int64_t *dst, const int64_t *src, const double *val, double *W,
+                       hipStream_t st);
+// Extend-add of children's update blocks into their parents (one child per
+// parent per launch, so no two children of a parent race).
+struct MChild {
+    int64_t src_ws, dst_ws, map_off;
+    int32_t src_ld, src_pp, dst_ld, q;
+};
+void launch_mf_extend(int nc, const MChild *C, int max_q, const int32_t *maps, const double *Wprev, double *Wcur,
+                      hipStream_t st);
+// Step k of the partial Gauss-Jordan elimination of every front's pivot tiles
+// (front := [F11^-1, F11^-1 F12; -F21 F11^-1, F22 - F21 F11^-1 F12]); D: nf
+// 64 x 64 scratch tiles; fail |= 1 on a zero pivot.
+void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, double *D, int32_t *fail,
+                       hipStream_t st);
+// Persistent factors: rows [0, 64 pt) of the front (U part, ld wide) to U + uoff
+// and rows [64 pt, 64 pt + q) x columns [0, 64 pt) (X part) to X + xoff.
+struct MStore {
+    int64_t uoff, xoff;
+};
+void launch_mf_store(int nf, const MFront *F, const MStore *S, int max_rows, const double *W, double *U, double *X,
+                     hipStream_t st);
+// Solve (ND order).  Per front: pivots at z/x[pstart, +p), update rows = slist[soff, +q).
+struct MSolve {
+    int64_t pstart, qoff, uoff, xoff, soff;
+    int32_t p, q, pp, ld;
+};
+// forward, gather: level row k = (front rf[k], local row rl[k]); v = b (pivot rows) +
+// the children's contributions cu[cidx[cptr[k] ..]]; pivot rows -> z, update rows -> acc
+void launch_mf_fwd_gather(int64_t m, const int32_t *rf, const int32_t *rl, const MSolve *S, const int64_t *cptr,
+                          const int64_t *cidx, const double *b, const double *cu, double *z, double *acc,
+                          hipStream_t st);
+// forward, update rows: cu = acc + X z_p (one wave per row)
+void launch_mf_fwd_gemv(int64_t m, const int32_t *rf, const int32_t *rl, const MSolve *S, const double *X,
+                        const double *z, const double *acc, double *cu, hipStream_t st);
+// backward, pivot rows: x_p = F11^-1 z_p - G12 x(slist) (one wave per row)
+void launch_mf_bwd(int64_t m, const int32_t *rf, const int32_t *rl, const MSolve *S, const double *U,
+                   const int32_t *slist, const double *z, double *x, hipStream_t st);
+// y[perm[i]] = x[i] / x[i] = b[perm[i]]
+void launch_gather_i32(int64_t n, const int32_t *perm, const double *b, double *x, hipStream_t st);
+void launch_scatter_i32(int64_t n, const int32_t *perm, const double *x, double *y, hipStream_t st);
+
 // ------------------------------------------------- banded exact LU (band.hip) --
 // T: nb tile rows x (bl + bu + 1) tiles of 64 x 64 (see band.hip); padding
 // rows past n are identity rows.

@@ -1272,24 +1272,22 @@ void PCBandLU::apply(const double *x, double *y, Ctx &c) {
 
 std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
     const std::string path = o.str("pls.lu_path", "auto");
-    if (path != "auto" && path != "dense" && path != "band" && path != "envelope")
-        throw Error("pls.lu_path " + path + " (auto, dense, band, envelope)");
+    if (path != "auto" && path != "dense" && path != "sparse" && path != "band" && path != "envelope")
+        throw Error("pls.lu_path " + path + " (auto, dense, sparse, band, envelope)");
     if (path == "dense" || (path == "auto" && M.nrows <= o.integer("pls.lu_dense_max", 32768)))
         return std::make_unique<PCDenseLU>(M, c);
-    if (path == "band" || path == "auto") {
+    // larger blocks: nested dissection + multifrontal LU (the MUMPS stand-in)
+    if (path == "sparse" || path == "auto") return make_sparse_lu(M, o, c);
+    if (path == "band") {
         int64_t kl = 0, ku = 0;
         csr_bandwidths(M, kl, ku, c);
         // band tiles + the SPIKE spikes (nb x (bl + bu) tiles): ~2x the band.  Default cap:
         // 3/4 of the card's HBM (288 GB per MI355X: the 2-D footing N=128 Schur block's
         // 95 GB band + 95 GB of spikes fit; an allocation that then fails is reported),
         // pls.lu_band_max_gb overrides
-        const double nbt = (double)((M.nrows + 63) / 64), w = (double)((kl + 63) / 64 + (ku + 63) / 64 + 1);
-        const double gb = nbt * (2.0 * w - 1.0) * 4096.0 * 8.0 / 1e9;
-        size_t free_b = 0, total_b = 0;
-        HIPCHK(hipMemGetInfo(&free_b, &total_b));
-        if (path == "band" || gb <= o.num("pls.lu_band_max_gb", 0.75 * (double)total_b / 1e9))
-            return std::make_unique<PCBandLU>(M, kl, ku, c, o.integer("pls.band_spike_plen", -1));
+        return std::make_unique<PCBandLU>(M, kl, ku, c, o.integer("pls.band_spike_plen", -1));
     }
+    // the envelope (profile) LU: exact, level-scheduled
     return std::make_unique<PCILU>(M, 1, c, true, o.flag("pls.ilu_lds", true), 0, (int)o.integer("pls.ilu_gmem", 0),
                                    (int)o.integer("pls.ilu_ring", 1));
 }
@@ -1912,6 +1910,9 @@ PCFieldSplit::PCFieldSplit(const DevCSR &M, const std::vector<int32_t> &s0, cons
     if (M.halo) throw Error(prefix + "pc_type fieldsplit: not available with several ranks");
     n0 = (int64_t)s0.size();
     n1 = (int64_t)s1.size();
+    if (n0 == 0 || n1 == 0 || n0 + n1 != n)
+        throw Error(prefix + "pc_type fieldsplit: the two splits must be non-empty and cover the block (" +
+                    std::to_string(n0) + " + " + std::to_string(n1) + " of " + std::to_string(n) + " rows)");
     ftype = o.str(prefix + "pc_fieldsplit_type", "multiplicative");
     if (ftype != "additive" && ftype != "multiplicative" && ftype != "schur")
         throw Error(prefix + "pc_fieldsplit_type " + ftype + " is not available (additive, multiplicative, schur)");

@@ -337,10 +337,11 @@ struct PCBandLU : PC {
 // Lower / upper bandwidth of a square CSR matrix with sorted rows.
 void csr_bandwidths(const DevCSR &M, int64_t &kl, int64_t &ku, Ctx &c);
 // -pc_type lu / cholesky (MUMPS in the reference): dense inverse up to
-// pls.lu_dense_max rows, else the band LU while its tiles fit
-// pls.lu_band_max_gb, else the envelope LU; pls.lu_path dense|band|envelope
-// forces one.
+// pls.lu_dense_max rows, else the sparse (nested dissection, multifrontal) LU;
+// pls.lu_path dense|sparse|band|envelope forces one.
 std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c);
+// Sparse LU by nested dissection + multifrontal factorization (sparse_lu.cpp)
+std::unique_ptr<PC> make_sparse_lu(const DevCSR &M, const Options &o, Ctx &c);
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c);
 // Smoothed-aggregation AMG (amg.cpp; -pc_type gamg, and hypre with pls.hypre sa).

@@ -1,0 +1,511 @@
+// sparse_lu.cpp -- exact sparse LU (PCLU) of large blocks: nested dissection +
+// a multifrontal factorization on the device.  The MUMPS stand-in for blocks
+// too large for the dense inverse (dense.hip): the reference factors every
+// block with MUMPS in petsc-options-exact:11-35 and the Schur split of the fp
+// fieldsplit in petsc-options-inexact:98-106.
+//
+// Ordering.  Nested dissection of the symmetrized graph (George's automatic
+// nested dissection): a breadth-first level structure from a pseudo-peripheral
+// vertex; the separator is the smallest level set whose two sides each hold
+// 30-70 % of the vertices; recursion on both sides down to `leaf` vertices; a
+// set the search does not connect splits into its components (empty separator).
+// The dissection tree is the assembly tree: a node's pivots are its separator
+// (or leaf) vertices, numbered in postorder, so every subtree is contiguous and
+// a node's update rows (its "structure") are vertices of its ancestors.
+//
+// Factorization.  Level by level from the deepest: every front of a level is a
+// dense (p + q)^2 block (padded to 64) assembled from the original entries
+// whose earlier-eliminated index is one of its pivots and the extend-add of its
+// children's update blocks; a partial Gauss-Jordan elimination of the p pivot
+// columns (64 x 64 tiles, no pivoting, like the dense and band LU) leaves
+//     [ F11^-1       F11^-1 F12           ]
+//     [ -F21 F11^-1  F22 - F21 F11^-1 F12 ]
+// whose last block is the update passed to the parent.  The first two blocks
+// are kept (the "U part", p x (p + q)) and the bottom-left one (the "X part").
+// The LU is exact up to rounding (ordering-invariant in exact arithmetic, as
+// MUMPS reorders too).
+//
+// Solve.  Forward, deepest level first: z_p = b_p + the children's
+// contributions at the front's rows, the front's contribution to its update
+// rows cu = (children's) + X z_p; backward, root first: x_p = F11^-1 z_p -
+// (F11^-1 F12) x_q.  Every level is three batched launches (a gather and two
+// wave-per-row GEMVs over the stored factors), so one apply reads the factors
+// once at HBM rate with ~3 launches per tree level.  All sums run in a fixed
+// order (children in tree order): the result does not depend on timing.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <numeric>
+
+#include "runtime.hpp"
+
+namespace pls {
+namespace {
+
+struct NDTree {
+    std::vector<std::vector<int32_t>> piv;  // per node: its vertices
+    std::vector<std::vector<int32_t>> ch;   // children (tree order)
+    std::vector<int32_t> parent, depth;
+    int add(int par, int d) {
+        piv.emplace_back();
+        ch.emplace_back();
+        parent.push_back(par);
+        depth.push_back(d);
+        if (par >= 0) ch[par].push_back((int)piv.size() - 1);
+        return (int)piv.size() - 1;
+    }
+};
+
+// symmetrized adjacency of M's pattern without the diagonal
+void sym_graph(const HostCSR &A, std::vector<int64_t> &gp, std::vector<int32_t> &gi) {
+    const int64_t n = A.nrows;
+    std::vector<int64_t> deg(n + 1, 0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
+            if (A.ci[k] != i) {
+                ++deg[i + 1];
+                ++deg[A.ci[k] + 1];
+            }
+    for (int64_t i = 0; i < n; ++i) deg[i + 1] += deg[i];
+    std::vector<int32_t> tmp(deg[n]);
+    std::vector<int64_t> pos(deg.begin(), deg.end() - 1);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
+            if (A.ci[k] != i) {
+                tmp[pos[i]++] = A.ci[k];
+                tmp[pos[A.ci[k]]++] = (int32_t)i;
+            }
+    gp.assign(n + 1, 0);
+    gi.clear();
+    gi.reserve(tmp.size());
+    for (int64_t i = 0; i < n; ++i) {
+        std::sort(tmp.begin() + deg[i], tmp.begin() + deg[i + 1]);
+        int32_t last = -1;
+        for (int64_t k = deg[i]; k < deg[i + 1]; ++k)
+            if (tmp[k] != last) gi.push_back(last = tmp[k]);
+        gp[i + 1] = (int64_t)gi.size();
+    }
+}
+
+struct Dissector {
+    const std::vector<int64_t> &gp;
+    const std::vector<int32_t> &gi;
+    int64_t leaf;
+    std::vector<int32_t> stamp, lev;
+    int32_t cur = 0;
+    std::vector<int32_t> order;
+    Dissector(const std::vector<int64_t> &p, const std::vector<int32_t> &i, int64_t n, int64_t lf)
+        : gp(p), gi(i), leaf(lf), stamp(n, 0), lev(n, -1) {}
+
+    // BFS inside the stamped set from s: order (visit order), lev; returns the depth
+    int32_t bfs(int32_t s) {
+        order.clear();
+        order.push_back(s);
+        lev[s] = 0;
+        int32_t depth = 0;
+        for (size_t h = 0; h < order.size(); ++h) {
+            const int32_t u = order[h];
+            for (int64_t k = gp[u]; k < gp[u + 1]; ++k) {
+                const int32_t v = gi[k];
+                if (stamp[v] == cur && lev[v] < 0) {
+                    lev[v] = lev[u] + 1;
+                    depth = std::max(depth, lev[v]);
+                    order.push_back(v);
+                }
+            }
+        }
+        return depth;
+    }
+    void clear_lev(const std::vector<int32_t> &set) {
+        for (int32_t v : set) lev[v] = -1;
+    }
+
+    void run(NDTree &T, std::vector<int32_t> all) {
+        struct Work {
+            std::vector<int32_t> set;
+            int parent, depth;
+        };
+        std::vector<Work> stack;
+        stack.push_back({std::move(all), -1, 0});
+        while (!stack.empty()) {
+            Work w = std::move(stack.back());
+            stack.pop_back();
+            const int node = T.add(w.parent, w.depth);
+            if ((int64_t)w.set.size() <= leaf) {
+                T.piv[node] = std::move(w.set);
+                continue;
+            }
+            ++cur;
+            for (int32_t v : w.set) stamp[v] = cur;
+            // pseudo-peripheral start: two sweeps from the set's first vertex
+            int32_t s = w.set[0];
+            for (int sweep = 0; sweep < 2; ++sweep) {
+                bfs(s);
+                s = order.back();
+                clear_lev(order);
+            }
+            const int32_t depth = bfs(s);
+            if (order.size() < w.set.size()) {  // not connected: the component vs the rest
+                std::vector<int32_t> comp(order), rest;
+                for (int32_t v : w.set)
+                    if (lev[v] < 0) rest.push_back(v);
+                clear_lev(comp);
+                stack.push_back({std::move(rest), node, w.depth + 1});
+                stack.push_back({std::move(comp), node, w.depth + 1});
+                continue;
+            }
+            if (depth < 2) {  // no interior level to cut: a (dense) leaf
+                clear_lev(order);
+                T.piv[node] = std::move(w.set);
+                continue;
+            }
+            std::vector<int64_t> cnt(depth + 1, 0);
+            for (int32_t v : order) ++cnt[lev[v]];
+            const int64_t m = (int64_t)order.size();
+            int64_t below = 0, best = -1, best_sz = INT64_MAX, median = -1;
+            for (int32_t l = 0; l <= depth; ++l) {
+                const int64_t above = m - below - cnt[l];
+                if (l >= 1 && l < depth) {
+                    if (median < 0 && below + cnt[l] >= m / 2) median = l;
+                    if (below >= 3 * m / 10 && above >= 3 * m / 10 && cnt[l] < best_sz) {
+                        best = l;
+                        best_sz = cnt[l];
+                    }
+                }
+                below += cnt[l];
+            }
+            const int32_t L = (int32_t)(best >= 0 ? best : (median >= 0 ? median : 1));
+            std::vector<int32_t> a, b, sep;
+            for (int32_t v : order) (lev[v] < L ? a : lev[v] > L ? b : sep).push_back(v);
+            clear_lev(order);
+            T.piv[node] = std::move(sep);
+            if (!b.empty()) stack.push_back({std::move(b), node, w.depth + 1});
+            if (!a.empty()) stack.push_back({std::move(a), node, w.depth + 1});
+        }
+    }
+};
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct PCSparseLU : PC {
+    int64_t nfront = 0, nlevels = 0;
+    DBuf<int32_t> perm;  // ND position -> row of M
+    DBuf<double> U, X;   // factors (per front: U part pp x ld, X part q x pp)
+    DBuf<MSolve> S;
+    DBuf<int32_t> slist;
+    // per level: fronts' rows for the solve kernels (level offsets on the host)
+    DBuf<int32_t> rf, rl, qf, ql, pf, pl;
+    DBuf<int64_t> cptr, cidx;
+    std::vector<int64_t> lr_off, lq_off, lp_off;  // nlevels + 1
+    std::map<hipStream_t, std::unique_ptr<DBuf<double>>> work;  // per stream: bp, z, x, cu, acc
+    int64_t nq = 0;
+    double setup_s[4] = {0, 0, 0, 0};  // ordering, symbolic, factorization, total
+    double factor_gb = 0;
+
+    PCSparseLU(const DevCSR &M, const Options &o, Ctx &c) {
+        type = "lu";
+        n = M.nrows;
+        if (M.ncols != n) throw Error("lu: block is not square");
+        const double t0 = now_s();
+        const HostCSR A = download(M, c);
+        // ---- ordering
+        std::vector<int64_t> gp;
+        std::vector<int32_t> gi;
+        sym_graph(A, gp, gi);
+        NDTree T;
+        {
+            Dissector D(gp, gi, n, std::max<int64_t>(1, o.integer("pls.lu_nd_leaf", 64)));
+            std::vector<int32_t> all(n);
+            std::iota(all.begin(), all.end(), 0);
+            D.run(T, std::move(all));
+        }
+        nfront = (int64_t)T.piv.size();
+        // postorder: children before parents, subtrees contiguous
+        std::vector<int32_t> post;
+        post.reserve(nfront);
+        {
+            std::vector<std::pair<int32_t, int32_t>> st{{0, 0}};
+            while (!st.empty()) {
+                auto &[v, k] = st.back();
+                if (k < (int32_t)T.ch[v].size()) {
+                    const int32_t cch = T.ch[v][k++];
+                    st.push_back({cch, 0});
+                } else {
+                    post.push_back(v);
+                    st.pop_back();
+                }
+            }
+        }
+        std::vector<int32_t> pos(n), permh(n), front_of(n);
+        std::vector<int64_t> pstart(nfront);
+        {
+            int64_t k = 0;
+            for (int32_t f : post) {
+                pstart[f] = k;
+                for (int32_t v : T.piv[f]) {
+                    pos[v] = (int32_t)k;
+                    permh[k] = v;
+                    front_of[k] = f;
+                    ++k;
+                }
+            }
+        }
+        const double t1 = now_s();
+        // ---- symbolic: update rows (ND positions, ascending) of every front
+        std::vector<std::vector<int32_t>> st(nfront);
+        {
+            std::vector<int32_t> mark(n, -1);
+            for (int32_t f : post) {
+                const int64_t pend = pstart[f] + (int64_t)T.piv[f].size();
+                std::vector<int32_t> &s = st[f];
+                auto add = [&](int32_t p) {
+                    if (p >= pend && mark[p] != f) {
+                        mark[p] = f;
+                        s.push_back(p);
+                    }
+                };
+                for (int32_t cch : T.ch[f])
+                    for (int32_t p : st[cch]) add(p);
+                for (int32_t v : T.piv[f])
+                    for (int64_t k = gp[v]; k < gp[v + 1]; ++k) add(pos[gi[k]]);
+                std::sort(s.begin(), s.end());
+            }
+        }
+        // ---- sizes, levels
+        int32_t maxd = 0;
+        for (int32_t d : T.depth) maxd = std::max(maxd, d);
+        nlevels = maxd + 1;
+        std::vector<std::vector<int32_t>> bylev(nlevels);
+        for (int32_t f : post) bylev[T.depth[f]].push_back(f);
+        std::vector<int64_t> p(nfront), q(nfront), pp(nfront), ld(nfront), uoff(nfront), xoff(nfront), soff(nfront),
+            qoff(nfront);
+        int64_t usz = 0, xsz = 0, ssz = 0;
+        for (int32_t f : post) {
+            p[f] = (int64_t)T.piv[f].size();
+            q[f] = (int64_t)st[f].size();
+            pp[f] = (p[f] + 63) / 64 * 64;
+            ld[f] = pp[f] + (q[f] + 63) / 64 * 64;
+            uoff[f] = usz;
+            usz += pp[f] * ld[f];
+            xoff[f] = xsz;
+            xsz += q[f] * pp[f];
+            soff[f] = qoff[f] = ssz;
+            ssz += q[f];
+        }
+        nq = ssz;
+        factor_gb = (double)(usz + xsz) * 8e-9;
+        const double cap = o.num("pls.lu_sparse_max_gb", 1e9);
+        if (factor_gb > cap)
+            throw Error("lu: sparse factors need " + std::to_string(factor_gb) + " GB (pls.lu_sparse_max_gb)");
+        U.alloc(std::max<int64_t>(usz, 1));
+        X.alloc(std::max<int64_t>(xsz, 1));
+        // local row of an ND position inside front f's row list (pivots, then update rows)
+        auto local = [&](int32_t f, int32_t ppos) -> int64_t {
+            if (ppos >= pstart[f] && ppos < pstart[f] + p[f]) return ppos - pstart[f];
+            const auto &s = st[f];
+            const auto it = std::lower_bound(s.begin(), s.end(), ppos);
+            if (it == s.end() || *it != ppos) throw Error("lu: sparse symbolic structure is inconsistent");
+            return p[f] + (it - s.begin());
+        };
+        // extend-add maps: child's update rows -> parent's local rows
+        std::vector<int32_t> maps(std::max<int64_t>(ssz, 1));
+        for (int32_t f : post)
+            if (T.parent[f] >= 0)
+                for (int64_t k = 0; k < q[f]; ++k) maps[soff[f] + k] = (int32_t)local(T.parent[f], st[f][k]);
+        // original entries: owner = the front of the earlier-eliminated index
+        std::vector<std::vector<int64_t>> sc_dst(nlevels), sc_src(nlevels);
+        std::vector<int64_t> wsoff(nfront), lev_ws(nlevels, 0);
+        for (int64_t d = 0; d < nlevels; ++d)
+            for (int32_t f : bylev[d]) {
+                wsoff[f] = lev_ws[d];
+                lev_ws[d] += ld[f] * ld[f];
+            }
+        for (int64_t i = 0; i < n; ++i)
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                const int32_t pi = pos[i], pj = pos[A.ci[k]];
+                const int32_t f = front_of[std::min(pi, pj)];
+                const int64_t r = local(f, pi), cc = local(f, pj);
+                sc_dst[T.depth[f]].push_back(wsoff[f] + r * ld[f] + cc);
+                sc_src[T.depth[f]].push_back(k);
+            }
+        const double t2 = now_s();
+        // ---- numeric factorization, deepest level first
+        int64_t wsmax = 1;
+        for (int64_t d = 0; d < nlevels; ++d) wsmax = std::max(wsmax, lev_ws[d]);
+        DBuf<double> Wa(wsmax), Wb(wsmax), val(std::max<int64_t>(M.nnz, 1));
+        HIPCHK(hipMemcpyAsync(val.p, A.v.data(), sizeof(double) * A.v.size(), hipMemcpyHostToDevice, c.st));
+        DBuf<int32_t> dmaps(maps.size()), fail(1);
+        HIPCHK(hipMemcpyAsync(dmaps.p, maps.data(), sizeof(int32_t) * maps.size(), hipMemcpyHostToDevice, c.st));
+        HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
+        double *Wcur = Wa.p, *Wprev = Wb.p;
+        std::vector<int64_t> prev_ws;  // workspace offsets of the previous (deeper) level's fronts
+        constexpr int CH = 32768;      // fronts per batched launch (grid z / y limit)
+        for (int64_t d = nlevels - 1; d >= 0; --d) {
+            const auto &fl = bylev[d];
+            HIPCHK(hipMemsetAsync(Wcur, 0, sizeof(double) * lev_ws[d], c.st));
+            for (size_t c0 = 0; c0 < fl.size(); c0 += CH) {
+                const size_t c1 = std::min(fl.size(), c0 + CH);
+                std::vector<MFront> hf;
+                std::vector<MStore> hs;
+                int max_pad = 0, max_ldt = 0, max_rows = 0, max_pt = 0;
+                for (size_t t = c0; t < c1; ++t) {
+                    const int32_t f = fl[t];
+                    hf.push_back({wsoff[f], (int32_t)(ld[f] / 64), (int32_t)(pp[f] / 64), (int32_t)p[f], (int32_t)q[f]});
+                    hs.push_back({uoff[f], xoff[f]});
+                    max_pad = std::max(max_pad, (int)(pp[f] - p[f]));
+                    max_ldt = std::max(max_ldt, (int)(ld[f] / 64));
+                    max_pt = std::max(max_pt, (int)(pp[f] / 64));
+                    max_rows = std::max(max_rows, (int)(pp[f] + q[f]));
+                }
+                DBuf<MFront> dF(hf.size());
+                DBuf<MStore> dS(hs.size());
+                DBuf<double> Dt(hf.size() * 4096);
+                HIPCHK(hipMemcpyAsync(dF.p, hf.data(), sizeof(MFront) * hf.size(), hipMemcpyHostToDevice, c.st));
+                HIPCHK(hipMemcpyAsync(dS.p, hs.data(), sizeof(MStore) * hs.size(), hipMemcpyHostToDevice, c.st));
+                launch_mf_pad((int)hf.size(), dF.p, max_pad, Wcur, c.st);
+                if (c0 == 0) {  // the level's original entries (all of its fronts)
+                    DBuf<int64_t> dd(std::max<size_t>(sc_dst[d].size(), 1)), ds(std::max<size_t>(sc_src[d].size(), 1));
+                    HIPCHK(hipMemcpyAsync(dd.p, sc_dst[d].data(), sizeof(int64_t) * sc_dst[d].size(), hipMemcpyHostToDevice,
+                                          c.st));
+                    HIPCHK(hipMemcpyAsync(ds.p, sc_src[d].data(), sizeof(int64_t) * sc_src[d].size(), hipMemcpyHostToDevice,
+                                          c.st));
+                    launch_mf_scatter((int64_t)sc_dst[d].size(), dd.p, ds.p, val.p, Wcur, c.st);
+                    c.sync();  // dd / ds are freed below
+                    // extend-add, one child rank per launch (children of a parent never race)
+                    size_t maxch = 0;
+                    for (int32_t f : fl) maxch = std::max(maxch, T.ch[f].size());
+                    for (size_t r = 0; r < maxch; ++r) {
+                        std::vector<MChild> hc;
+                        int max_q = 0;
+                        for (int32_t f : fl)
+                            if (r < T.ch[f].size()) {
+                                const int32_t cf = T.ch[f][r];
+                                if (q[cf] == 0) continue;
+                                hc.push_back({prev_ws[cf], wsoff[f], soff[cf], (int32_t)ld[cf], (int32_t)pp[cf],
+                                              (int32_t)ld[f], (int32_t)q[cf]});
+                                max_q = std::max(max_q, (int)q[cf]);
+                            }
+                        for (size_t h0 = 0; h0 < hc.size(); h0 += CH) {
+                            const size_t h1 = std::min(hc.size(), h0 + CH);
+                            DBuf<MChild> dC(h1 - h0);
+                            HIPCHK(hipMemcpyAsync(dC.p, hc.data() + h0, sizeof(MChild) * (h1 - h0), hipMemcpyHostToDevice,
+                                                  c.st));
+                            launch_mf_extend((int)(h1 - h0), dC.p, max_q, dmaps.p, Wprev, Wcur, c.st);
+                            c.sync();
+                        }
+                    }
+                }
+                for (int k = 0; k < max_pt; ++k) launch_mf_gj_step((int)hf.size(), dF.p, max_ldt, k, Wcur, Dt.p, fail.p, c.st);
+                launch_mf_store((int)hf.size(), dF.p, dS.p, max_rows, Wcur, U.p, X.p, c.st);
+                HIPCHK(hipGetLastError());
+                c.sync();
+            }
+            prev_ws.assign(nfront, 0);
+            for (int32_t f : fl) prev_ws[f] = wsoff[f];
+            std::swap(Wcur, Wprev);
+        }
+        int32_t hfail = 0;
+        HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+        c.sync();
+        if (hfail) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+        const double t3 = now_s();
+        // ---- solve tables
+        std::vector<MSolve> hS(nfront);
+        std::vector<int32_t> hsl(std::max<int64_t>(ssz, 1));
+        for (int32_t f : post) {
+            hS[f] = {pstart[f], qoff[f], uoff[f], xoff[f], soff[f], (int32_t)p[f], (int32_t)q[f], (int32_t)pp[f],
+                     (int32_t)ld[f]};
+            std::copy(st[f].begin(), st[f].end(), hsl.begin() + soff[f]);
+        }
+        std::vector<int32_t> hrf, hrl, hqf, hql, hpf, hpl;
+        std::vector<int64_t> hcp{0}, hci;
+        lr_off.assign(1, 0);
+        lq_off.assign(1, 0);
+        lp_off.assign(1, 0);
+        for (int64_t d = 0; d < nlevels; ++d) {
+            for (int32_t f : bylev[d]) {
+                // children's contributions per local row, in child order
+                std::vector<std::vector<int64_t>> contrib(p[f] + q[f]);
+                for (int32_t cf : T.ch[f])
+                    for (int64_t k = 0; k < q[cf]; ++k) contrib[maps[soff[cf] + k]].push_back(qoff[cf] + k);
+                for (int64_t r = 0; r < p[f] + q[f]; ++r) {
+                    hrf.push_back(f);
+                    hrl.push_back((int32_t)r);
+                    hci.insert(hci.end(), contrib[r].begin(), contrib[r].end());
+                    hcp.push_back((int64_t)hci.size());
+                }
+                for (int64_t k = 0; k < q[f]; ++k) {
+                    hqf.push_back(f);
+                    hql.push_back((int32_t)k);
+                }
+                for (int64_t k = 0; k < p[f]; ++k) {
+                    hpf.push_back(f);
+                    hpl.push_back((int32_t)k);
+                }
+            }
+            lr_off.push_back((int64_t)hrf.size());
+            lq_off.push_back((int64_t)hqf.size());
+            lp_off.push_back((int64_t)hpf.size());
+        }
+        auto up = [&](auto &dst, const auto &v) {
+            dst.alloc(std::max<size_t>(v.size(), 1));
+            if (!v.empty())
+                HIPCHK(hipMemcpyAsync(dst.p, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, c.st));
+        };
+        up(S, hS);
+        up(slist, hsl);
+        up(perm, permh);
+        up(rf, hrf);
+        up(rl, hrl);
+        up(qf, hqf);
+        up(ql, hql);
+        up(pf, hpf);
+        up(pl, hpl);
+        up(cptr, hcp);
+        up(cidx, hci);
+        c.sync();
+        setup_s[0] = t1 - t0;
+        setup_s[1] = t2 - t1;
+        setup_s[2] = t3 - t2;
+        setup_s[3] = now_s() - t0;
+        if (o.flag("pls.lu_view", false)) {
+            int64_t maxf = 0;
+            for (int32_t f : post) maxf = std::max(maxf, p[f] + q[f]);
+            fprintf(stderr,
+                    "[sparse lu] n %lld: %lld fronts, %lld levels, largest front %lld, factors %.2f GB; setup: "
+                    "ordering %.2f s, symbolic %.2f s, factorization %.2f s, total %.2f s\n",
+                    (long long)n, (long long)nfront, (long long)nlevels, (long long)maxf, factor_gb, setup_s[0],
+                    setup_s[1], setup_s[2], setup_s[3]);
+        }
+    }
+
+    bool reentrant() const override { return true; }
+
+    void apply(const double *xin, double *y, Ctx &c) override {
+        if (n == 0) return;
+        auto &w = work[c.st];
+        if (!w) w = std::make_unique<DBuf<double>>((size_t)(3 * n + 2 * std::max<int64_t>(nq, 1)));
+        double *bp = w->p, *z = bp + n, *x = z + n, *cu = x + n, *acc = cu + std::max<int64_t>(nq, 1);
+        launch_gather_i32(n, perm.p, xin, bp, c.st);
+        for (int64_t d = nlevels - 1; d >= 0; --d) {
+            launch_mf_fwd_gather(lr_off[d + 1] - lr_off[d], rf.p + lr_off[d], rl.p + lr_off[d], S.p,
+                                 cptr.p + lr_off[d], cidx.p, bp, cu, z, acc, c.st);
+            launch_mf_fwd_gemv(lq_off[d + 1] - lq_off[d], qf.p + lq_off[d], ql.p + lq_off[d], S.p, X.p, z, acc, cu,
+                               c.st);
+        }
+        for (int64_t d = 0; d < nlevels; ++d)
+            launch_mf_bwd(lp_off[d + 1] - lp_off[d], pf.p + lp_off[d], pl.p + lp_off[d], S.p, U.p, slist.p, z, x,
+                          c.st);
+        launch_scatter_i32(n, perm.p, x, y, c.st);
+    }
+};
+
+std::unique_ptr<PC> make_sparse_lu(const DevCSR &M, const Options &o, Ctx &c) {
+    return std::make_unique<PCSparseLU>(M, o, c);
+}
+
+}  // namespace pls

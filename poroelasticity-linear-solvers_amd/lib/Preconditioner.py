@@ -63,8 +63,6 @@ class PreconditionerCC(object):
         yy = self.handle.pc_apply(vec_array(x))
         ya = vec_array(y)
         ya[...] = yy
-        if hasattr(y, "setArray") and ya is not yy:
-            pass
         return y
 
     def print_timings(self):

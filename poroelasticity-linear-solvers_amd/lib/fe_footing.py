@@ -103,7 +103,9 @@ def footing_mesh(N: int, length: float = LENGTH, refinements: int = 0):
     """generate_footing_square (MeshCreation.py:53-77): float vertex
     coordinates (nv x 2) and triangles (nc x 3)."""
     icoords, cells = F.unit_mesh(2, N)
-    coords = icoords.astype(np.float64) * (length / N)  # UnitSquareMesh, coordinates *= length
+    # UnitSquareMesh's vertices are i / N, then coordinates *= length (ADVICE r02:
+    # i * (length / N) misses the top edge by an ulp for some N, e.g. 49)
+    coords = (icoords.astype(np.float64) / N) * length
     for _ in range(2):
         x, y = coords[cells, 0], coords[cells, 1]
         mark = (y.min(1) > 2 * length / 3) & (x.min(1) > length / 8) & (x.max(1) < 7 / 8 * length)
@@ -169,6 +171,8 @@ def assemble_footing(N: int, pc_type: str = "undrained", params: dict | None = N
         return np.abs(a - b) < _EPS
 
     top = on_all(lambda x: near(x[:, 1], length))
+    if not top.any():
+        raise ValueError(f"footing mesh N={N}: no facet on the top edge (traction and foot BCs would be lost)")
     bottom = on_all(lambda x: near(x[:, 1], 0.0))
     foot = on_all(lambda x: near(x[:, 1], length) & (np.abs(x[:, 0] - length / 2) < length / 4))
     not_foot = on_all(lambda x: ~(near(x[:, 1], length) & (np.abs(x[:, 0] - length / 2) < length / 4)))

@@ -92,6 +92,16 @@ def _fe_db(G):
 # numbering) handed over rank by rank through pls_create_dist: every rank
 # passes its PETSc-split rows (global columns) and the index sets of the dofs
 # it owns -- the reference's mpirun path (paper-scripts/robustness_2d.sh:29)
+def _fs_db():
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "s_ksp_type": "preonly", "s_pc_type": "bjacobi",
+          "s_pc_bjacobi_blocks": "3", "fp_ksp_type": "preonly", "fp_pc_type": "fieldsplit",
+          "fp_pc_fieldsplit_type": "schur", "fp_pc_fieldsplit_schur_fact_type": "lower",
+          "fp_pc_fieldsplit_schur_precondition": "selfp"}
+    db.update({"fp_fieldsplit_0_ksp_type": "preonly", "fp_fieldsplit_0_pc_type": "ilu",
+               "fp_fieldsplit_1_ksp_type": "preonly", "fp_fieldsplit_1_pc_type": "lu"})
+    return db
+
+
 FE_BASE = dict(BASE, **{"solver atol": 1e-8, "solver rtol": 1e-6, "solver maxiter": 60, "inner pc type": "bjacobi"})
 FE_CASES = [
     {"name": "fe_threeway_2d", "system": "fe", "dim": 2, "N": 8,
@@ -106,6 +116,14 @@ FE_CASES = [
      "params": dict(FE_BASE, **{"pc type": "diagonal 3-way"}), "db": _fe_db(3)},
     {"name": "fe_facade_twoway_3d", "system": "fe", "facade": True, "dim": 3, "N": 3,
      "params": dict(FE_BASE, **{"pc type": "diagonal"}), "db": _fe_db(3)},
+    # 2-way with a Schur fieldsplit on the fp block (petsc-options-inexact's fp_
+    # structure, linear split solves): under pls_create_dist every rank's fp rows
+    # interleave f and p, so the gathered block's splits come from every rank's
+    # fp index sets (they were taken as field-major slabs)
+    {"name": "fe_fieldsplit_twoway_2d", "system": "fe", "dim": 2, "N": 8,
+     "params": dict(FE_BASE, **{"pc type": "diagonal", "solver maxiter": 200}), "db": _fs_db()},
+    {"name": "fe_facade_fieldsplit_twoway_2d", "system": "fe", "facade": True, "dim": 2, "N": 8,
+     "params": dict(FE_BASE, **{"pc type": "diagonal", "solver maxiter": 200}), "db": _fs_db()},
     # the reference's exact option set under mpirun (MUMPS LU on every block ->
     # each sharded block gathered and factored redundantly)
     {"name": "fe_exact_lu_threeway_2d", "system": "fe", "dim": 2, "N": 8,

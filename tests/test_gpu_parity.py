@@ -326,7 +326,10 @@ def test_facade_end_to_end(gpu):
 # band: SPIKE partitions chosen automatically (~16 per triangle, at least the
 # bandwidth); band_chain: one flag-chained sweep per triangle (no partitions);
 # band_spike2: the shortest partitions the bandwidth allows (most spikes)
+# sparse: nested dissection + multifrontal LU (the default past pls.lu_dense_max);
+# sparse_leaf8: 8-vertex dissection leaves (a deep assembly tree, many levels)
 LU_PATHS = {"dense": {}, "band": {"pls.lu_path": "band"}, "envelope": {"pls.lu_path": "envelope"},
+            "sparse": {"pls.lu_path": "sparse"}, "sparse_leaf8": {"pls.lu_path": "sparse", "pls.lu_nd_leaf": "8"},
             "band_chain": {"pls.lu_path": "band", "pls.band_spike_plen": "0"},
             "band_spike2": {"pls.lu_path": "band", "pls.band_spike_plen": "2"}}
 
@@ -346,7 +349,9 @@ def test_exact_lu_inner_blocks(gpu, pc_type, lu_path):
 @pytest.mark.parametrize("lu_path,dim,N", [("dense", 3, 2), ("envelope", 3, 2), ("dense", 3, 3), ("dense", 2, 16),
                                            ("band", 3, 2), ("band", 2, 16), ("band", 2, 48), ("band", 3, 5),
                                            ("band_chain", 2, 48), ("band_spike2", 2, 16), ("band_spike2", 2, 48),
-                                           ("band_spike2", 3, 5)])
+                                           ("band_spike2", 3, 5), ("sparse", 3, 2), ("sparse", 2, 16),
+                                           ("sparse", 2, 48), ("sparse", 3, 5), ("sparse_leaf8", 2, 16),
+                                           ("sparse_leaf8", 3, 5)])
 def test_exact_lu_pc_apply_is_exact(gpu, lu_path, dim, N):
     """||P_lower y - x|| at rounding level: multi-block Gauss-Jordan (n not a
     multiple of 64), the band LU (2-D N=48: 295 / 343 tile rows, more than
@@ -427,12 +432,14 @@ FS_INEXACT = {  # petsc-options-inexact:73-114 with BoomerAMG -> Jacobi / ILU(0)
 FS_PARAMS = {"inner ksp type": "cg", "inner pc type": "hypre"}
 
 
-@pytest.mark.parametrize("variant", ["inexact", "inexact_band_lu", "lower_ilu", "full_implicit", "upper", "diag",
+@pytest.mark.parametrize("variant", ["inexact", "inexact_band_lu", "inexact_sparse_lu", "lower_ilu", "full_implicit", "upper", "diag",
                                      "multiplicative", "additive", "default"])
 def test_fieldsplit_fp(gpu, variant):
     db = dict(FS_INEXACT)
-    if variant == "inexact_band_lu":  # the Schur block's LU on the band path (the footing configuration's)
+    if variant == "inexact_band_lu":  # the Schur block's LU on the band path
         db["pls.lu_path"] = "band"
+    if variant == "inexact_sparse_lu":  # ... on the sparse path (the footing configuration's)
+        db["pls.lu_path"] = "sparse"
     elif variant == "lower_ilu":
         db.update({"fp_fieldsplit_0_ksp_type": "preonly", "fp_fieldsplit_0_pc_type": "ilu",
                    "fp_fieldsplit_1_pc_type": "ilu"})
