@@ -1431,6 +1431,13 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
     const bool dist = c.comm && c.comm->size > 1;
     // whole-block PCs on a sharded block: gathered and applied redundantly (PCREDUNDANT)
     if (M.halo && (type == "ilu" || type == "lu" || type == "cholesky" || type == "gamg" || type == "hypre")) {
+        // PETSc's own ILU refuses a parallel (MPIAIJ) matrix; MUMPS LU and hypre run
+        // distributed.  Redundant ILU is an extension, on request only.
+        if (type == "ilu" && !o.flag("pls.redundant_ilu", false))
+            throw Error("PC type 'ilu' (prefix " + prefix + ") on a matrix sharded over " +
+                        std::to_string(c.comm ? c.comm->size : 1) +
+                        " ranks: PETSc's ILU does not run on MPIAIJ matrices (use bjacobi, or pls.redundant_ilu 1 "
+                        "for the one-rank ILU applied redundantly)");
         if (o.flag("pls.redundant_error", false))
             throw Error("PC type '" + type + "' (prefix " + prefix + ") acts on the whole parallel matrix (pls.redundant_error)");
         return make_redundant(type, M, c, [&](const DevCSR &Gm, Ctx &sc) { return make_pc(type, Gm, o, prefix, sc); },

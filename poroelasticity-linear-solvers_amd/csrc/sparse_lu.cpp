@@ -303,13 +303,14 @@ struct PCSparseLU : PC {
             throw Error("lu: sparse factors need " + std::to_string(factor_gb) + " GB (pls.lu_sparse_max_gb)");
         U.alloc(std::max<int64_t>(usz, 1));
         X.alloc(std::max<int64_t>(xsz, 1));
-        // local row of an ND position inside front f's row list (pivots, then update rows)
+        // row of an ND position inside front f's dense block: pivots [0, p), update
+        // rows from pp on (the pivot block is padded to whole tiles)
         auto local = [&](int32_t f, int32_t ppos) -> int64_t {
             if (ppos >= pstart[f] && ppos < pstart[f] + p[f]) return ppos - pstart[f];
             const auto &s = st[f];
             const auto it = std::lower_bound(s.begin(), s.end(), ppos);
             if (it == s.end() || *it != ppos) throw Error("lu: sparse symbolic structure is inconsistent");
-            return p[f] + (it - s.begin());
+            return pp[f] + (it - s.begin());
         };
         // extend-add maps: child's update rows -> parent's local rows
         std::vector<int32_t> maps(std::max<int64_t>(ssz, 1));
@@ -431,7 +432,10 @@ struct PCSparseLU : PC {
                 // children's contributions per local row, in child order
                 std::vector<std::vector<int64_t>> contrib(p[f] + q[f]);
                 for (int32_t cf : T.ch[f])
-                    for (int64_t k = 0; k < q[cf]; ++k) contrib[maps[soff[cf] + k]].push_back(qoff[cf] + k);
+                    for (int64_t k = 0; k < q[cf]; ++k) {
+                        const int64_t dr = maps[soff[cf] + k];  // dense row -> row list index
+                        contrib[dr < pp[f] ? dr : p[f] + (dr - pp[f])].push_back(qoff[cf] + k);
+                    }
                 for (int64_t r = 0; r < p[f] + q[f]; ++r) {
                     hrf.push_back(f);
                     hrl.push_back((int32_t)r);
@@ -468,6 +472,9 @@ struct PCSparseLU : PC {
         up(cptr, hcp);
         up(cidx, hci);
         c.sync();
+        Mref = &M;
+        refine = (int)o.integer("pls.lu_refine", 1);
+        if (refine > 0 && !M.sell) build_sell(const_cast<DevCSR &>(M), c);
         setup_s[0] = t1 - t0;
         setup_s[1] = t2 - t1;
         setup_s[2] = t3 - t2;
@@ -485,11 +492,27 @@ struct PCSparseLU : PC {
 
     bool reentrant() const override { return true; }
 
+    // y = M^-1 x with `refine` steps of iterative refinement (y += LU^-1 (x - M y)):
+    // the explicit front inverses lose ~cond(F11) eps on ill-conditioned blocks
+    // (footing's undrained solid block: 4e-7 relative residual unrefined,
+    // rounding level after one step); a fixed number of steps keeps the PC linear.
     void apply(const double *xin, double *y, Ctx &c) override {
         if (n == 0) return;
         auto &w = work[c.st];
-        if (!w) w = std::make_unique<DBuf<double>>((size_t)(3 * n + 2 * std::max<int64_t>(nq, 1)));
-        double *bp = w->p, *z = bp + n, *x = z + n, *cu = x + n, *acc = cu + std::max<int64_t>(nq, 1);
+        if (!w) w = std::make_unique<DBuf<double>>((size_t)(5 * n + 2 * std::max<int64_t>(nq, 1)));
+        double *r = w->p + 3 * n + 2 * std::max<int64_t>(nq, 1), *d = r + n;
+        solve(xin, y, *w, c);
+        for (int k = 0; k < refine; ++k) {
+            spmv(*Mref, y, r, c, -1.0, 1.0, xin);
+            solve(r, d, *w, c);
+            launch_axpby(n, 1.0, d, 1.0, y, c.st);
+        }
+    }
+    const DevCSR *Mref = nullptr;
+    int refine = 1;
+
+    void solve(const double *xin, double *y, DBuf<double> &w, Ctx &c) {
+        double *bp = w.p, *z = bp + n, *x = z + n, *cu = x + n, *acc = cu + std::max<int64_t>(nq, 1);
         launch_gather_i32(n, perm.p, xin, bp, c.st);
         for (int64_t d = nlevels - 1; d >= 0; --d) {
             launch_mf_fwd_gather(lr_off[d + 1] - lr_off[d], rf.p + lr_off[d], rl.p + lr_off[d], S.p,

@@ -61,7 +61,8 @@ CASES = [
     {"name": "redundant_ilu_lu_3way_2d", "dim": 2, "N": 10, "params": dict(BASE, **{"pc type": "diagonal 3-way"}),
      "db": {"global_ksp_type": "gmres", "global_ksp_pc_side": "right",
             "s_ksp_type": "preonly", "s_pc_type": "ilu", "f_ksp_type": "preonly", "f_pc_type": "lu",
-            "p_ksp_type": "preonly", "p_pc_type": "lu", "diff_ksp_type": "preonly", "diff_pc_type": "ilu"}},
+            "p_ksp_type": "preonly", "p_pc_type": "lu", "diff_ksp_type": "preonly", "diff_pc_type": "ilu",
+            "pls.redundant_ilu": "1"}},
     # ... the classical AMG with petsc-options-inexact's BoomerAMG settings ...
     {"name": "redundant_hypre_3way_3d", "dim": 3, "N": 4, "params": dict(BASE, **{"pc type": "diagonal 3-way"}),
      "pc_tol": 1e-12, "db": dict({"global_ksp_type": "gmres", "global_ksp_pc_side": "right"},
