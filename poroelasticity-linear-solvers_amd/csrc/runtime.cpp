@@ -1555,12 +1555,21 @@ void KSP::solve(const double *b, double *x, Ctx &c) {
         pc->apply(b, x, c);
         its = 1;
         reason = CONVERGED_ITS;
-        return;
+    } else {
+        ensure_work(c);
+        if (type == "gmres") solve_gmres(b, x, c);
+        else if (type == "cg") solve_cg(b, x, c);
+        else throw Error("KSP type " + type + " not available");
     }
-    ensure_work(c);
-    if (type == "gmres") return solve_gmres(b, x, c);
-    if (type == "cg") return solve_cg(b, x, c);
-    throw Error("KSP type " + type + " not available");
+    stat_its += its;
+    stat_max = std::max<int64_t>(stat_max, its);
+    ++stat_solves;
+}
+
+KSP::~KSP() {
+    if (stats && stat_solves)
+        fprintf(stderr, "[ksp %s%s] %lld solves, %lld its (mean %.1f, max %lld)\n", prefix.c_str(), type.c_str(),
+                (long long)stat_solves, (long long)stat_its, (double)stat_its / (double)stat_solves, (long long)stat_max);
 }
 
 void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
@@ -1766,6 +1775,7 @@ std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const
     k->maxit = o.integer(prefix + "ksp_max_it", maxit);
     k->restart = o.integer(prefix + "ksp_gmres_restart", restart);
     k->monitor = o.has(prefix + "ksp_monitor");
+    k->stats = o.flag("pls.ksp_stats", false);
     if (o.has(prefix + "ksp_gmres_modifiedgramschmidt") && k->type == "gmres")
         throw Error(prefix + "ksp_gmres_modifiedgramschmidt: only classical Gram-Schmidt is implemented");
     k->resolve_side_norm(o.str(prefix + "ksp_pc_side", ""), o.str(prefix + "ksp_norm_type", ""));

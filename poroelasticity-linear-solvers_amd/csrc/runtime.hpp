@@ -375,6 +375,12 @@ struct KSP {
     std::vector<double> history;
     bool keep_history = true;
     bool monitor = false;
+    // pls.ksp_stats: iteration totals printed when the KSP is destroyed (diagnostics)
+    bool stats = false;
+    int64_t stat_its = 0, stat_max = 0, stat_solves = 0;
+    KSP() = default;
+    KSP(const KSP &) = delete;
+    ~KSP();
     // work
     DBuf<double> V, w, t1, t2, t3, t4;
     int64_t ldv = 0;  // column stride of the Krylov basis V

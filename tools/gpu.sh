@@ -13,6 +13,7 @@
 #   prof_footing                same for configs[2] (footing-inexact-ilu, band-LU Schur block)
 #   footing                     configs[2] bench on the assembled footing system (N=128)
 #   prof_footing_fe             rocprofv3 of that solve
+#   footing128 / prof_footing128  configs[2] at N=128 with footing.py's own set (classical AMG, sparse LU)
 #   prof_amg                    same for the classical AMG (-pc_type hypre) on the s block, 3-D N=27
 #   prof_amg59                  same at the metric's N=59
 #   configs                     bench on every BASELINE config that fits one GPU
@@ -72,6 +73,8 @@ for s in "$@"; do
         run fe/footing_N128 600 python -u bench.py --config footing-inexact-ilu --system fe --steps 2 --warmup 1 --no-copy-probe ;;
       prof_footing_fe) prof prof_footing_fe --config footing-inexact-ilu --system fe --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
       prof_footing_amg) prof prof_footing_amg --config footing-inexact --system fe --N 12 --steps 1 --warmup 0 --no-cpu --no-copy-probe ;;
+      prof_footing128) prof prof_footing128 --config footing-inexact --system fe --N 128 --steps 1 --warmup 0 --no-cpu --no-copy-probe --maxit 40 ;;
+      footing128) run fe/footing_amg_N128 1000 python -u bench.py --config footing-inexact --system fe --N 128 --steps 1 --warmup 0 --no-copy-probe --opt pls.lu_view=1 --opt pls.amg_view=1 --opt pls.ksp_stats=1 ;;
       pmc) run pmc 1300 bash tools/pmc.sh ;;
       custom:*) rest=${s#custom:}; name=${rest%%:*}; cmd=${rest#*:}; run "$name" 1100 bash -c "$cmd" ;;
       *) echo "unknown step $s"; exit 2 ;;
