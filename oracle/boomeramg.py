@@ -203,11 +203,30 @@ def second_strength(S, cf, num_paths):
     return S2, cpts
 
 
-def coarsen(S, n, aggressive, num_paths):
-    cf = rs_first_pass(S, n)
+def rs_partitioned(S, n, part):
+    """The Ruge-Stueben first pass run independently inside every partition
+    (part[i]: the partition of point i, contiguous ranges) on the strong
+    connections inside it -- HMIS's per-process first pass."""
+    if part is None or n == 0 or part[-1] == part[0]:
+        return rs_first_pass(S, n)
+    cf = np.empty(n, dtype=np.int64)
+    starts = np.flatnonzero(np.r_[True, part[1:] != part[:-1]])
+    ends = np.r_[starts[1:], n]
+    for a, b in zip(starts.tolist(), ends.tolist()):
+        Sl = [row[(row >= a) & (row < b)] - a for row in S[a:b]]
+        cf[a:b] = rs_first_pass(Sl, b - a)
+    return cf
+
+
+def coarsen(S, n, aggressive, num_paths, part=None):
+    """C/F splitting (HMIS).  part: the level's partition (hypre's HMIS runs the
+    first pass inside each process; libpls cuts levels of >= 2 x 65,536 rows
+    into partitions of at least that size, pls.hypre_coarsen_*, so the pass
+    runs on host threads) -- None: one partition."""
+    cf = rs_partitioned(S, n, part)
     if aggressive:
         S2, cpts = second_strength(S, cf, num_paths)
-        cf2 = rs_first_pass(S2, len(cpts))
+        cf2 = rs_partitioned(S2, len(cpts), None if part is None else part[cpts])
         cf = np.full(n, F, dtype=np.int64)
         cf[cpts[cf2 == C]] = C
     return cf
@@ -447,6 +466,10 @@ class PCBoomerAMG:
             raise ValueError("grid_sweeps_all must be >= 1")
         self.chunks = int(db.get("pls.hypre_relax_chunks", 256))
         self.chunk_rows = int(db.get("pls.hypre_relax_min_rows", 1024))
+        # coarsening partition: 0 = up to pls.hypre_relax_chunks partitions of at least
+        # pls.hypre_coarsen_min_rows (65536) rows, 1 = none, K > 1 = K partitions
+        self.coarsen_chunks = int(db.get("pls.hypre_coarsen_chunks", 0))
+        self.coarsen_rows = int(db.get("pls.hypre_coarsen_min_rows", 65536))
         if self.chunks < 1 or self.chunk_rows < 0:
             raise ValueError("pls.hypre_relax_chunks must be >= 1, pls.hypre_relax_min_rows >= 0")
         A = A.tocsr()
@@ -456,7 +479,12 @@ class PCBoomerAMG:
             n = A.shape[0]
             S = strength(A, self.theta, self.mu)
             aggressive = len(self.levels) < self.agg_nl
-            cf = coarsen(S, n, aggressive, self.npaths)
+            part = None
+            if self.coarsen_chunks != 1:
+                Kc = self.coarsen_chunks if self.coarsen_chunks > 1 else level_chunks(n, self.chunks,
+                                                                                        self.coarsen_rows)
+                part = chunk_ids(n, Kc) if Kc > 1 else None
+            cf = coarsen(S, n, aggressive, self.npaths, part)
             nc = int((cf == C).sum())
             if nc == 0 or nc == n:
                 break

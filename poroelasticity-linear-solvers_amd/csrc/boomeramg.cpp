@@ -235,16 +235,63 @@ Pattern second_strength(const Pattern &S, const std::vector<int8_t> &cf, int pat
     return concat_pattern(m, part);
 }
 
-std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths) {
+// oracle rs_partitioned(): the first pass inside each of K contiguous
+// partitions (hypre's ChunkMap sizes over S.n; `pt` maps a point to its
+// position in the partitioned set when S is a subset, e.g. the C1 points) on
+// the strong connections inside it; partitions run on host threads.
+std::vector<int8_t> rs_partitioned(const Pattern &S, int64_t K, const std::vector<int64_t> &part_start) {
+    const int64_t n = S.n;
+    if (K <= 1 || n == 0) return rs_first_pass(S);
+    std::vector<int8_t> cf(n, FPT);
+    parallel_rows(K, setup_threads(), [&](int, int64_t k0, int64_t k1) {
+        for (int64_t k = k0; k < k1; ++k) {
+            const int64_t a = part_start[k], b = part_start[k + 1];
+            if (b <= a) continue;
+            Pattern L;
+            L.n = b - a;
+            L.rp.assign(1, 0);
+            for (int64_t i = a; i < b; ++i) {
+                for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q)
+                    if (S.ci[q] >= a && S.ci[q] < b) L.ci.push_back((int32_t)(S.ci[q] - a));
+                L.rp.push_back((int64_t)L.ci.size());
+            }
+            const std::vector<int8_t> lc = rs_first_pass(L);
+            std::copy(lc.begin(), lc.end(), cf.begin() + a);
+        }
+    });
+    return cf;
+}
+
+// partition starts of n points in K chunks (hypre's thread partition)
+std::vector<int64_t> chunk_starts(int64_t n, int64_t K) {
+    std::vector<int64_t> st(K + 1, 0);
+    const int64_t q = n / K, r = n % K;
+    for (int64_t k = 0; k < K; ++k) st[k + 1] = st[k] + q + (k < r ? 1 : 0);
+    return st;
+}
+
+std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths, int64_t K) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double t0 = now();
-    std::vector<int8_t> cf = rs_first_pass(S);
+    K = std::max<int64_t>(1, std::min<int64_t>(K, S.n));
+    const std::vector<int64_t> pst = chunk_starts(S.n, K);
+    std::vector<int8_t> cf = rs_partitioned(S, K, pst);
     if (!aggressive) return cf;
     double t1 = now();
     std::vector<int32_t> cpts;
     const Pattern S2 = second_strength(S, cf, paths, cpts);
     double t2 = now();
-    const std::vector<int8_t> cf2 = rs_first_pass(S2);
+    // the C1 points' partitions: positions in cpts where the original chunk changes
+    std::vector<int64_t> pst2(K + 1, 0);
+    {
+        size_t t = 0;
+        for (int64_t k = 0; k < K; ++k) {
+            pst2[k] = (int64_t)t;
+            while (t < cpts.size() && cpts[t] < pst[k + 1]) ++t;
+        }
+        pst2[K] = (int64_t)cpts.size();
+    }
+    const std::vector<int8_t> cf2 = rs_partitioned(S2, K, pst2);
     if (std::getenv("PLS_AMG_TRACE"))
         fprintf(stderr, "[boomeramg coarsen] n %lld S nnz %lld: RS %.2f s; S2 (%zu C1 points, nnz %lld) %.2f s; RS2 %.2f s\n",
                 (long long)S.n, (long long)S.ci.size(), t1 - t0, cpts.size(), (long long)S2.ci.size(), t2 - t1, now() - t2);
@@ -578,6 +625,7 @@ struct BParams {
     double theta = 0.25, mu = 0.9, rap_bytes = 16e9;
     int64_t pmax = 0, agg_nl = 0, max_levels = 25;
     int64_t chunks = 256, chunk_rows = 1024;  // hybrid Gauss-Seidel partition (pls.hypre_relax_*)
+    int64_t coarsen_chunks = 0, coarsen_rows = 65536;  // HMIS partitions (pls.hypre_coarsen_*): 0 = auto, 1 = none
     int paths = 1, K = 1;
     bool no_cf = false;
 };
@@ -596,6 +644,8 @@ BParams parse_params(const Options &o, const std::string &prefix) {
     p.rap_bytes = o.num("pls.amg_rap_dense_gb", 16.0) * 1e9;
     p.chunks = o.integer("pls.hypre_relax_chunks", 256);
     p.chunk_rows = o.integer("pls.hypre_relax_min_rows", 1024);
+    p.coarsen_chunks = o.integer("pls.hypre_coarsen_chunks", 0);
+    p.coarsen_rows = o.integer("pls.hypre_coarsen_min_rows", 65536);
     if (p.chunks < 1 || p.chunk_rows < 0)
         throw Error("pls.hypre_relax_chunks must be >= 1 and pls.hypre_relax_min_rows >= 0");
     const std::string ct = o.str(pre + "coarsen_type", "HMIS"), it = o.str(pre + "interp_type", "ext+i");
@@ -620,7 +670,10 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
         tm[1] += now() - t0;
         t0 = now();
         const bool aggressive = nlev < p.agg_nl;
-        const std::vector<int8_t> cf = coarsen(S, aggressive, p.paths);
+        const int64_t Kc = p.coarsen_chunks == 1 ? 1
+                           : p.coarsen_chunks > 1 ? p.coarsen_chunks
+                                                  : level_chunks(A.nrows, p.chunks, p.coarsen_rows);
+        const std::vector<int8_t> cf = coarsen(S, aggressive, p.paths, Kc);
         tm[2] += now() - t0;
         int64_t nc = 0;
         for (int8_t v : cf) nc += v == CPT;
@@ -875,7 +928,9 @@ struct PCBoomer : PC {
                         const int gm = (nlev > 0 && lo.nrows / nlev > wide_rows) ? wide_mode : gmem;
                         if (no_cf) {
                             // the chunks are PCILU's blocks (the same partition): one workgroup per chunk
-                            rs->sgs = std::make_unique<PCILU>(*L->A, Kl, c, false, allow_lds, 0, gm, ring, true);
+                            auto pc = std::make_unique<PCILU>(*L->A, Kl, c, false, allow_lds, 0, gm, ring, true);
+                            if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+                            rs->sgs = std::move(pc);
                         } else {
                             upload(chunk_part(Al, g, Kl, 0), rs->sub, c);
                             rs->sgs = std::make_unique<PCILU>(rs->sub, 1, c, false, allow_lds, 0, gm, ring, true);

@@ -2294,14 +2294,16 @@ void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, co
                             const int64_t *Lcp, const int64_t *Ucoff, const int64_t *Ucg, const int64_t *Ucp,
                             const int32_t *ordL, const int32_t *mapUL, const int32_t *ordU, const int64_t *Lfrp,
                             const int32_t *Lfcol, const double *Lfval, const int64_t *Ufrp, const int32_t *Ufcol,
-                            const double *Ufval, const double *x, double *y, double *yL, double *yU, hipStream_t st) {
+                            const double *Ufval, const double *x, double *y, double *yL, double *yU, hipStream_t st,
+                            int tpb) {
+    if (tpb < 64 || tpb > RING_TPB || (tpb & 63)) tpb = RING_TPB;
     static bool configured = false;
     const int bytes = RING_SLOTS * 8;
     if (!configured) {
         (void)hipFuncSetAttribute((const void *)k_ilu_blocks_ring, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         configured = true;
     }
-    k_ilu_blocks_ring<<<(unsigned)nblocks, RING_TPB, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
+    k_ilu_blocks_ring<<<(unsigned)nblocks, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
                                                                Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, Lcoff, Lcg, Lcp,
                                                                Ucoff, Ucg, Ucp, ordL, mapUL, ordU, Lfrp, Lfcol, Lfval,
                                                                Ufrp, Ufcol, Ufval, x, y, yL, yU);
@@ -2319,7 +2321,9 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
-                           int64_t *prof, bool gmem) {
+                           int64_t *prof, bool gmem, int tpb) {
+    // tpb: threads per workgroup, 64 .. 1024 (narrow levels: fewer waves, cheaper barriers)
+    if (tpb < 64 || tpb > 1024 || (tpb & 63)) tpb = 1024;
     static bool configured = false;
     if (!configured) {
         (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2327,12 +2331,12 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
         configured = true;
     }
     if (gmem) {
-        k_ilu_blocks_lds<true><<<(unsigned)nblocks, 1024, 0, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
-                                                                   Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof);
+        k_ilu_blocks_lds<true><<<(unsigned)nblocks, tpb, 0, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
+                                                                  Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof);
         return;
     }
     const size_t bytes = (size_t)(n / nblocks + 1) * 8;
-    k_ilu_blocks_lds<false><<<(unsigned)nblocks, 1024, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval,
+    k_ilu_blocks_lds<false><<<(unsigned)nblocks, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval,
                                                                      Llpr, Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y,
                                                                      prof);
 }

@@ -192,7 +192,7 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
-                           int64_t *prof = nullptr, bool gmem = false);
+                           int64_t *prof = nullptr, bool gmem = false, int tpb = 1024);
 int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in registers
 // The ring sweep (kernels.hip, k_ilu_blocks_ring): blocks of narrow levels whose
 // every level has <= ilu_ring_chunk() rows; per triangle chunk tables (coff per
@@ -209,7 +209,7 @@ void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, co
                             const int64_t *Lcp, const int64_t *Ucoff, const int64_t *Ucg, const int64_t *Ucp,
                             const int32_t *ordL, const int32_t *mapUL, const int32_t *ordU, const int64_t *Lfrp,
                             const int32_t *Lfcol, const double *Lfval, const int64_t *Ufrp, const int32_t *Ufcol,
-                            const double *Ufval, const double *x, double *y, double *yL, double *yU, hipStream_t st);
+                            const double *Ufval, const double *x, double *y, double *yL, double *yU, hipStream_t st, int tpb = 1024);
 // LDS-kernel stream layout (header entry per lane, lanes-per-row slices, block-local columns)
 void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,
                      const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu, const int64_t *diag,

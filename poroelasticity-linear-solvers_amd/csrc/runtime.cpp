@@ -1085,6 +1085,23 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                           ring ? &loL : nullptr, ring ? &nlL : nullptr);
             build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oU, gU, fU, true, Us, c, ring ? &pU : nullptr,
                           ring ? &loU : nullptr, ring ? &nlU : nullptr);
+            // threads per workgroup: as few waves as the widest level's slices need
+            // (narrow, deep levels -- FE rows in their natural order, nearly one
+            // level per row -- pay a workgroup barrier per level: 16 waves cost
+            // ~0.6 us per level, one wave far less).  pls.sweep_tpb overrides.
+            int64_t wmax = 1;
+            for (const auto *g : {&gL, &gU})
+                for (size_t k = 0; k + 1 < g->size(); ++k) wmax = std::max<int64_t>(wmax, (*g)[k + 1] - (*g)[k]);
+            int lmax = 1;
+            {
+                std::vector<int32_t> hl(nblocks), hu(nblocks);
+                HIPCHK(hipMemcpyAsync(hl.data(), Ls.lpr.p, sizeof(int32_t) * nblocks, hipMemcpyDeviceToHost, c.st));
+                HIPCHK(hipMemcpyAsync(hu.data(), Us.lpr.p, sizeof(int32_t) * nblocks, hipMemcpyDeviceToHost, c.st));
+                c.sync();
+                for (int64_t b = 0; b < nblocks; ++b) lmax = std::max(lmax, std::max(hl[b], hu[b]));
+            }
+            const int64_t slices = (wmax * lmax + 63) / 64;
+            lds_tpb = slices <= 1 ? 64 : slices <= 4 ? 256 : 1024;
         }
     } else {
         std::vector<int32_t> ordU;
@@ -1116,14 +1133,16 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
         launch_ilu_blocks_ring(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
                                Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, Lr.coff.p, Lr.cg.p, Lr.cp.p,
                                Ur.coff.p, Ur.cg.p, Ur.cp.p, Lr.ord.p, mapUL.p, Ur.ord.p, Lr.frp.p, Lr.fcol.p,
-                               Lr.fval.p, Ur.frp.p, Ur.fcol.p, Ur.fval.p, x, y, sc.first.p, sc.second.p, c.st);
+                               Lr.fval.p, Ur.frp.p, Ur.fcol.p, Ur.fval.p, x, y, sc.first.p, sc.second.p, c.st,
+                               lds_tpb);
         return;
     }
     if (use_lds) {
         DBuf<int64_t> prof;
         if (!profile_tag.empty()) prof.alloc(nblocks * 8);
         launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
-                              Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof.p, lds_gmem);
+                              Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof.p, lds_gmem,
+                              lds_tpb);
         if (!profile_tag.empty()) {
             // diagnostics: per-block sweep times (100 MHz wall clock), slowest first
             std::vector<int64_t> h(nblocks * 8);
@@ -1446,8 +1465,10 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
     if (type == "ilu") {
         if (o.integer(prefix + "pc_factor_levels", 0) != 0)
             throw Error(prefix + "pc_factor_levels > 0: only ILU(0) is implemented");
-        return std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true), 0,
-                                       (int)o.integer("pls.ilu_gmem", 0), (int)o.integer("pls.ilu_ring", 1));
+        auto pc = std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true), 0,
+                                          (int)o.integer("pls.ilu_gmem", 0), (int)o.integer("pls.ilu_ring", 1));
+        if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+        return pc;
     }
     if (type == "lu" || type == "cholesky") return make_lu(M, o, c);
     if (type == "bjacobi") {
@@ -1464,6 +1485,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
                                               (int)o.integer("pls.sweep_lpr", 0), (int)o.integer("pls.ilu_gmem", 0),
                                               (int)o.integer("pls.ilu_ring", 1));
             if (o.flag("pls.sweep_profile", false)) pc->profile_tag = prefix;
+            if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
             return pc;
         }
         if (sub == "jacobi") return std::make_unique<PCJacobi>(M, c);

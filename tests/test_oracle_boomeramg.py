@@ -176,7 +176,9 @@ def _blocks():
     return out
 
 
-@pytest.mark.parametrize("db", [{}, INEXACT], ids=["defaults", "inexact"])
+@pytest.mark.parametrize("db", [{}, INEXACT, dict(INEXACT, **{"pls.hypre_coarsen_chunks": "7"}),
+                                dict(INEXACT, **{"pls.hypre_relax_min_rows": "64", "pls.hypre_coarsen_min_rows": "200"})],
+                         ids=["defaults", "inexact", "inexact-7-partitions", "inexact-chunked"])
 def test_libpls_host_setup_bitwise(db):
     from lib.handle import boomeramg_host_level
     for name, A in _blocks():
@@ -241,3 +243,20 @@ def test_hybrid_vcycle_pcg_converges(K):
     pc = PCBoomerAMG(A, dict(INEXACT, **{"pls.hypre_relax_chunks": str(K), "pls.hypre_relax_min_rows": "0"}), "x_")
     b = np.random.default_rng(0).standard_normal(A.shape[0])
     assert pcg(A, b, pc.apply) <= 14
+
+
+def test_partitioned_first_pass_is_per_partition():
+    """HMIS's first pass inside each partition: the C/F splitting of a
+    partitioned level equals the splittings of its partitions' own blocks."""
+    from oracle.boomeramg import chunk_ids, rs_first_pass, rs_partitioned
+    A = lap2(20)
+    n = A.shape[0]
+    S = strength(A)
+    part = chunk_ids(n, 3)
+    cf = rs_partitioned(S, n, part)
+    for k in range(3):
+        idx = np.flatnonzero(part == k)
+        a, b = idx[0], idx[-1] + 1
+        Sl = [row[(row >= a) & (row < b)] - a for row in S[a:b]]
+        assert np.array_equal(cf[a:b], rs_first_pass(Sl, b - a))
+    assert not np.array_equal(cf, rs_first_pass(S, n))  # the partition boundary changes the splitting
