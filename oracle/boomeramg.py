@@ -218,11 +218,29 @@ def rs_partitioned(S, n, part):
     return cf
 
 
+def coarsen_partition(S, n, K, max_cut=0.02):
+    """Automatic HMIS partition: the most partitions (<= K, halving) whose
+    boundaries cut at most max_cut of the strong connections (a partition
+    narrower than the matrix's coupling range would coarsen the boundary
+    layers independently); None when even two partitions cut more."""
+    if n == 0:
+        return None
+    rows = np.repeat(np.arange(n), [len(r) for r in S])
+    cols = np.concatenate(S) if len(S) else np.zeros(0, dtype=np.int64)
+    while K > 1:
+        part = chunk_ids(n, K)
+        if cols.size == 0 or np.count_nonzero(part[rows] != part[cols]) <= max_cut * cols.size:
+            return part
+        K //= 2
+    return None
+
+
 def coarsen(S, n, aggressive, num_paths, part=None):
     """C/F splitting (HMIS).  part: the level's partition (hypre's HMIS runs the
     first pass inside each process; libpls cuts levels of >= 2 x 65,536 rows
-    into partitions of at least that size, pls.hypre_coarsen_*, so the pass
-    runs on host threads) -- None: one partition."""
+    into partitions of at least that size whose boundaries cut <= 2 % of the
+    strong connections, pls.hypre_coarsen_*, so the pass runs on host
+    threads) -- None: one partition."""
     cf = rs_partitioned(S, n, part)
     if aggressive:
         S2, cpts = second_strength(S, cf, num_paths)
@@ -480,10 +498,10 @@ class PCBoomerAMG:
             S = strength(A, self.theta, self.mu)
             aggressive = len(self.levels) < self.agg_nl
             part = None
-            if self.coarsen_chunks != 1:
-                Kc = self.coarsen_chunks if self.coarsen_chunks > 1 else level_chunks(n, self.chunks,
-                                                                                        self.coarsen_rows)
-                part = chunk_ids(n, Kc) if Kc > 1 else None
+            if self.coarsen_chunks > 1:
+                part = chunk_ids(n, self.coarsen_chunks)
+            elif self.coarsen_chunks == 0:
+                part = coarsen_partition(S, n, level_chunks(n, self.chunks, self.coarsen_rows))
             cf = coarsen(S, n, aggressive, self.npaths, part)
             nc = int((cf == C).sum())
             if nc == 0 or nc == n:

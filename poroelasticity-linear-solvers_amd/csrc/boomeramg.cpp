@@ -262,6 +262,31 @@ std::vector<int8_t> rs_partitioned(const Pattern &S, int64_t K, const std::vecto
     return cf;
 }
 
+// oracle coarsen_partition(): the most partitions (<= K, halving) whose
+// boundaries cut at most 2 % of the strong connections; 1 if none does
+int64_t coarsen_partitions(const Pattern &S, int64_t K) {
+    const int64_t n = S.n, nnz = (int64_t)S.ci.size();
+    while (K > 1) {
+        const int64_t q = n / K, r = n % K;
+        auto part = [&](int64_t i) { return i < r * (q + 1) ? i / (q + 1) : r + (i - r * (q + 1)) / q; };
+        const int T = setup_threads();
+        std::vector<int64_t> cuts(T, 0);
+        parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
+            int64_t c = 0;
+            for (int64_t i = i0; i < i1; ++i) {
+                const int64_t pi = part(i);
+                for (int64_t k = S.rp[i]; k < S.rp[i + 1]; ++k) c += pi != part(S.ci[k]);
+            }
+            cuts[t] = c;
+        });
+        int64_t cut = 0;
+        for (int64_t c : cuts) cut += c;
+        if (nnz == 0 || cut <= 0.02 * (double)nnz) return K;
+        K /= 2;
+    }
+    return 1;
+}
+
 // partition starts of n points in K chunks (hypre's thread partition)
 std::vector<int64_t> chunk_starts(int64_t n, int64_t K) {
     std::vector<int64_t> st(K + 1, 0);
@@ -672,7 +697,7 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
         const bool aggressive = nlev < p.agg_nl;
         const int64_t Kc = p.coarsen_chunks == 1 ? 1
                            : p.coarsen_chunks > 1 ? p.coarsen_chunks
-                                                  : level_chunks(A.nrows, p.chunks, p.coarsen_rows);
+                                                  : coarsen_partitions(S, level_chunks(A.nrows, p.chunks, p.coarsen_rows));
         const std::vector<int8_t> cf = coarsen(S, aggressive, p.paths, Kc);
         tm[2] += now() - t0;
         int64_t nc = 0;
@@ -930,6 +955,8 @@ struct PCBoomer : PC {
                             // the chunks are PCILU's blocks (the same partition): one workgroup per chunk
                             auto pc = std::make_unique<PCILU>(*L->A, Kl, c, false, allow_lds, 0, gm, ring, true);
                             if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+                            if (o.flag("pls.sweep_profile", false))
+                                pc->profile_tag = prefix + "sgs L" + std::to_string(lv.size());
                             rs->sgs = std::move(pc);
                         } else {
                             upload(chunk_part(Al, g, Kl, 0), rs->sub, c);
