@@ -955,6 +955,7 @@ struct PCBoomer : PC {
                             // the chunks are PCILU's blocks (the same partition): one workgroup per chunk
                             auto pc = std::make_unique<PCILU>(*L->A, Kl, c, false, allow_lds, 0, gm, ring, true);
                             if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+            if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
                             if (o.flag("pls.sweep_profile", false))
                                 pc->profile_tag = prefix + "sgs L" + std::to_string(lv.size());
                             rs->sgs = std::move(pc);

@@ -2070,7 +2070,7 @@ __device__ __forceinline__ void sw2_slice_inline(const Sw2Ctx &x, int64_t sl) {
         const int64_t pos = sw2_at<R>(base, L, x.lane, k);
         const int32_t cc = x.col[pos];
         const double vv = x.val[pos];
-        if (W || k <= len) acc += vv * sw2_dep<R>(x, cc);
+        if (W || k <= len) acc += __dmul_rn(vv, sw2_dep<R>(x, cc));
     }
     sw2_finish<LPR, W, R>(x, h, dv, acc, R ? (int)(enc & 7) : 0);
 }
@@ -2123,7 +2123,7 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
             for (int u = 1; u <= P; ++u) d[u] = sw2_dep<R>(x, u <= len ? cur.c[u] : 0);
 #pragma unroll
             for (int u = 1; u <= P; ++u) {
-                const double t = cur.v[u] * d[u];
+                const double t = __dmul_rn(cur.v[u], d[u]);
                 acc += (u <= len) ? t : 0.0;
             }
         }
@@ -2138,7 +2138,7 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const double t = vv[u] * sw2_dep<R>(x, k0 + u <= len ? cc[u] : 0);
+                const double t = __dmul_rn(vv[u], sw2_dep<R>(x, k0 + u <= len ? cc[u] : 0));
                 acc += (k0 + u <= len) ? t : 0.0;
             }
         }
@@ -2167,15 +2167,130 @@ __device__ __forceinline__ void sweep2(Sw2Ctx &x, int64_t g0) {
     }
 }
 
+// Round-robin sweep for deep, narrow level DAGs (about one slice per level:
+// FE rows in their natural order, e.g. the classical AMG's hybrid Gauss-Seidel
+// chunks).  sweep2 gives every level to all waves and keeps two levels of
+// factor data in flight, so with one slice per level one wave works, the rest
+// idle at the barrier, and memory latency is exposed (footing N=128 smoother:
+// ~0.77 us per level, 970 levels per 2,405-row chunk).  Here wave w owns the
+// levels g0 + w, g0 + w + nw, ... and loads its next level's slice before
+// computing the current one, so its data has nw levels' time to arrive.  A
+// level's extra slices (rare) run inline.  Per-row sums are sweep2's (same
+// entries, same order): results are bitwise those of sweep2.
+template <int P, int LPR, bool W>
+__device__ __forceinline__ void sweep_rr(Sw2Ctx &x, int64_t g0) {
+    const int64_t g1 = x.g1;
+    const int nw = x.nw, w = x.wave;
+    const int64_t nown = g1 - g0 > w ? (g1 - g0 - w + nw - 1) / nw : 0;  // own levels of this wave
+    int64_t jb = 0, ms0 = 0, ms1 = 0, mb = -1, me = -1;  // lane l: own level jb + l (first slice, end, entry range)
+    auto refill = [&](int64_t j0) {
+        jb = j0;
+        const int64_t g = g0 + w + (j0 + x.lane) * nw;
+        if (j0 + x.lane < nown) {
+            ms0 = x.gslice[g];
+            ms1 = x.gslice[g + 1];
+            mb = ms1 > ms0 ? x.sptr[ms0] : -1;
+            me = ms1 > ms0 ? x.sptr[ms0 + 1] : -1;
+        } else {
+            ms0 = ms1 = 0;
+            mb = me = -1;
+        }
+        asm volatile("" : "+v"(ms0), "+v"(ms1), "+v"(mb), "+v"(me));
+    };
+    auto issue = [&](int64_t j, Sw2Slot<P> &sl) {
+        const int l = (int)(j - jb);
+        const int64_t base = j < nown ? readlane64(mb, l) : -1;
+        const int64_t next = base >= 0 ? readlane64(me, l) : 0;
+        sl.base = base;
+        sl.L = base >= 0 ? (next - base) >> 6 : 0;
+        sl.l2 = 0;
+#pragma unroll
+        for (int u = 0; u <= P; ++u) {
+            const int64_t pos = (base >= 0 ? base : 0) + (u < sl.L ? u : 0) * 64 + x.lane;
+            sl.c[u] = base >= 0 ? __builtin_nontemporal_load(x.col + pos) : 0;
+            sl.v[u] = base >= 0 ? __builtin_nontemporal_load(x.val + pos) : 0.0;
+        }
+    };
+    auto compute = [&](int64_t j, const Sw2Slot<P> &cur) {
+        if (cur.base < 0) return;
+        const int32_t h = cur.c[0];
+        const int32_t len = W ? (int32_t)cur.L - 1 : (int32_t)((uint32_t)h >> SW_ROW_BITS);
+        double acc = 0.0, d[P + 1];
+#pragma unroll
+        for (int u = 1; u <= P; ++u) d[u] = sw2_dep<false>(x, u <= len ? cur.c[u] : 0);
+#pragma unroll
+        for (int u = 1; u <= P; ++u) {
+            const double t = __dmul_rn(cur.v[u], d[u]);  // sweep2's rounding (no contraction)
+            acc += (u <= len) ? t : 0.0;
+        }
+        for (int64_t k0 = P + 1; k0 < cur.L; k0 += 8) {
+            int32_t cc[8];
+            double vv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t k = k0 + u < cur.L ? k0 + u : cur.L - 1;
+                cc[u] = __builtin_nontemporal_load(x.col + cur.base + k * 64 + x.lane);
+                vv[u] = __builtin_nontemporal_load(x.val + cur.base + k * 64 + x.lane);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const double t = __dmul_rn(vv[u], sw2_dep<false>(x, k0 + u <= len ? cc[u] : 0));
+                acc += (k0 + u <= len) ? t : 0.0;
+            }
+        }
+        sw2_finish<LPR, W, false>(x, h, cur.v[0], acc);
+        const int l = (int)(j - jb);
+        const int64_t s0 = readlane64(ms0, l), s1 = readlane64(ms1, l);
+        for (int64_t sl = s0 + 1; sl < s1; ++sl) sw2_slice_inline<LPR, W, false>(x, sl);
+    };
+    Sw2Slot<P> A, B;
+    refill(0);
+    issue(0, A);
+    int64_t j = 0;
+    for (int64_t g = g0; g < g1; ++g) {
+        if ((g - g0) % nw == w) {
+            if (j + 1 - jb >= 64) {  // keep the current level's metadata: refill from j
+                refill(j);
+            }
+            // compute first: its wait covers only the slot loaded nw levels ago, not
+            // the loads issued now for the next own level
+            if ((j & 1) == 0) {
+                compute(j, A);
+                issue(j + 1, B);
+            } else {
+                compute(j, B);
+                issue(j + 1, A);
+            }
+            ++j;
+        }
+        __syncthreads();
+    }
+}
+
 template <int P, bool W, bool R = false>
 __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int lane, int wave, int nw, bool upper,
                                             const int64_t *__restrict__ gslice, const int64_t *__restrict__ sptr,
                                             const int32_t *__restrict__ col, const double *__restrict__ val,
                                             double *ys, double *ring = nullptr, double *ypos = nullptr,
-                                            int64_t b0 = 0, int64_t ck0 = 0, int64_t ck1 = 0, RingIn rin = {}) {
+                                            int64_t b0 = 0, int64_t ck0 = 0, int64_t ck1 = 0, RingIn rin = {},
+                                            bool rr = false) {
     if (g0 >= g1) return;
     Sw2Ctx x{gslice, sptr, col, val, ys, g1, 0, 0, 0, 0, lane, wave, nw, upper,
              ring, ypos, 0, ck0, ck1, ck0 < ck1 ? rin.cg[ck0] : INT64_MAX, b0, ck0, rin};
+    if (!R && rr) {  // deep, narrow levels: round-robin over the waves
+        if (W) {
+            if (lpr == 16) sweep_rr<P, 16, W>(x, g0);
+            else if (lpr == 8) sweep_rr<P, 8, W>(x, g0);
+            else if (lpr == 4) sweep_rr<P, 4, W>(x, g0);
+            else if (lpr == 2) sweep_rr<P, 2, W>(x, g0);
+            else sweep_rr<P, 1, W>(x, g0);
+        } else {
+            if (lpr == 4) sweep_rr<P, 4, W>(x, g0);
+            else if (lpr == 2) sweep_rr<P, 2, W>(x, g0);
+            else sweep_rr<P, 1, W>(x, g0);
+        }
+        return;
+    }
     if (R) {  // ring sweep: lanes per row per slice
         sweep2<P, 0, true, true>(x, g0);
         if (ck1 > ck0) ring_flush(x, rin.cp[2 * ck1 - 2], rin.cp[2 * ck1 - 1]);  // the last chunk
@@ -2217,7 +2332,7 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
                                                          const int32_t *__restrict__ Ucol,
                                                          const double *__restrict__ Uval,
                                                          const int32_t *__restrict__ Ulpr, const double *x,
-                                                         double *y, int64_t *__restrict__ prof) {
+                                                         double *y, int64_t *__restrict__ prof, int rr) {
     extern __shared__ __attribute__((aligned(16))) double lds_y[];
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
     const int64_t q = n / nblocks, r = n % nblocks;
@@ -2232,9 +2347,11 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
     if (!GMEM || x != y)
         for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
     __syncthreads();
-    sweep_block<SW_P, GMEM>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol, Lval, ys);
+    sweep_block<SW_P, GMEM>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol, Lval, ys,
+                            nullptr, nullptr, 0, 0, 0, {}, rr != 0);
     if (prof) t1 = wall_clock64();
-    sweep_block<SW_P, GMEM>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol, Uval, ys);
+    sweep_block<SW_P, GMEM>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol, Uval, ys,
+                            nullptr, nullptr, 0, 0, 0, {}, rr != 0);
     if (!GMEM)
         for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
     if (prof && threadIdx.x == 0) {  // diagnostics (option pls.sweep_profile): 100 MHz wall clock
@@ -2321,7 +2438,7 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
-                           int64_t *prof, bool gmem, int tpb) {
+                           int64_t *prof, bool gmem, int tpb, int rr) {
     // tpb: threads per workgroup, 64 .. 1024 (narrow levels: fewer waves, cheaper barriers)
     if (tpb < 64 || tpb > 1024 || (tpb & 63)) tpb = 1024;
     static bool configured = false;
@@ -2332,13 +2449,13 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
     }
     if (gmem) {
         k_ilu_blocks_lds<true><<<(unsigned)nblocks, tpb, 0, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
-                                                                  Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof);
+                                                                  Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof, rr);
         return;
     }
     const size_t bytes = (size_t)(n / nblocks + 1) * 8;
     k_ilu_blocks_lds<false><<<(unsigned)nblocks, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval,
                                                                      Llpr, Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y,
-                                                                     prof);
+                                                                     prof, rr);
 }
 
 // =========================================================== distribution ====

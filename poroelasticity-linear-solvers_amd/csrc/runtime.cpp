@@ -1102,6 +1102,9 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             }
             const int64_t slices = (wmax * lmax + 63) / 64;
             lds_tpb = slices <= 1 ? 64 : slices <= 4 ? 256 : 1024;
+            // (the round-robin level sweep, pls.sweep_rr 1, is bitwise the same and was
+            // measured slower on the footing N=128 smoother chunks: 0.83 vs 0.77 us per
+            // level -- the per-level cost there is not memory latency)
         }
     } else {
         std::vector<int32_t> ordU;
@@ -1142,7 +1145,7 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
         if (!profile_tag.empty()) prof.alloc(nblocks * 8);
         launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
                               Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof.p, lds_gmem,
-                              lds_tpb);
+                              lds_tpb, lds_rr ? 1 : 0);
         if (!profile_tag.empty()) {
             // diagnostics: per-block sweep times (100 MHz wall clock), slowest first
             std::vector<int64_t> h(nblocks * 8);
@@ -1468,6 +1471,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         auto pc = std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true), 0,
                                           (int)o.integer("pls.ilu_gmem", 0), (int)o.integer("pls.ilu_ring", 1));
         if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+            if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
         return pc;
     }
     if (type == "lu" || type == "cholesky") return make_lu(M, o, c);
@@ -1486,6 +1490,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
                                               (int)o.integer("pls.ilu_ring", 1));
             if (o.flag("pls.sweep_profile", false)) pc->profile_tag = prefix;
             if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+            if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
             return pc;
         }
         if (sub == "jacobi") return std::make_unique<PCJacobi>(M, c);

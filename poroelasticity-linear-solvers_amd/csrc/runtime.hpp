@@ -287,6 +287,7 @@ struct PCILU : PC {
     bool use_lds = false;  // one workgroup per block sweeps (k_ilu_blocks_lds)
     bool lds_gmem = false;  // ... with the block solution kept in y (blocks too long for LDS)
     int lds_tpb = 1024;     // threads per workgroup of the LDS sweep (set from the widest level; pls.sweep_tpb)
+    bool lds_rr = false;    // round-robin level sweep (deep DAGs of ~one slice per level; pls.sweep_rr)
     int64_t nlev_L = 0, nlev_U = 0;
     bool allow_lds = true;  // block solution resident in LDS when it fits
     bool exact = false;     // envelope pattern: exact LU (PCLU)

@@ -223,3 +223,26 @@ def test_boomeramg_on_assembled_swelling_inexact(gpu):
     assert r.reason == 3 and lo - slack <= r.its <= hi + slack, (r.its, its)
     assert np.linalg.norm(s.b - s.A @ x) <= 10 * max(true_o), (np.linalg.norm(s.b - s.A @ x), true_o)
     h.destroy()
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_round_robin_sweep_is_bitwise(gpu, N):
+    """The round-robin level sweep (deep DAGs of about one slice per level --
+    the classical AMG's Gauss-Seidel chunks on the footing solid block) gives
+    bitwise the all-waves sweep's result: same entries, same order per row."""
+    from lib import fe_footing as FF
+    from lib.handle import Handle, params_to_options
+    s = FF.assemble_footing(N, "undrained")
+    params = dict(BASE, **{"pc type": "undrained", "inner pc type": "hypre"})
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "s_ksp_type": "preonly", "s_pc_type": "hypre",
+          "fp_ksp_type": "preonly", "fp_pc_type": "lu", "pls.amg_gs_dense": "0"}
+    db.update({"s_" + k: v for k, v in BOOMER.items()})
+    v = np.random.default_rng(2).standard_normal(s.A.shape[0])
+    out = []
+    for rr in ("0", "1"):
+        opts = dict(db, **{"pls.sweep_rr": rr})
+        opts.update(params_to_options(params))
+        h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+        out.append(h.pc_apply(v))
+        h.destroy()
+    assert np.array_equal(out[0], out[1])

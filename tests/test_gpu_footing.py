@@ -162,3 +162,34 @@ def test_footing_amg_solve_properties(gpu):
     assert np.array_equal(h1, h2) and np.array_equal(x1, x2)
     assert np.all(np.isfinite(h1)) and h1[-1] < h1[0]
     assert dt < 240
+
+
+def test_footing_N128_configs2_setup_and_iterations(gpu):
+    """configs[2] at its named size on its true matrices (1,308,592 DoF) with
+    footing.py's own option set: the whole setup (five classical-AMG
+    hierarchies, the sparse LU of the 615,714-row Schur split) within 60 s,
+    10 outer GMRES iterations whose estimates never increase, and the block
+    PC bitwise repeatable (two applications of the same vector).  A full
+    solve is dominated by inner CG solves of the undrained solid block that
+    stall at max_it."""
+    import time
+    from lib.handle import Handle, params_to_options
+    s = FF.assemble_footing(128, "undrained")
+    assert s.A.shape[0] == 1_308_592
+    params, db = _options("inexact")
+    params = dict(params, **{"solver maxiter": 10})
+    opts = dict(db)
+    opts.update(params_to_options(params))
+    t0 = time.perf_counter()
+    h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    h.setup()
+    h.create_solver()
+    t_setup = time.perf_counter() - t0
+    print(f"footing N=128 setup {t_setup:.1f} s")
+    assert t_setup < 60
+    x, r = h.solve(s.b)
+    hist = h.history()
+    assert r.its == 10 and np.all(np.isfinite(hist)) and np.all(np.diff(hist) <= 0)
+    v = np.random.default_rng(0).standard_normal(s.A.shape[0])
+    assert np.array_equal(h.pc_apply(v), h.pc_apply(v))
+    h.destroy()

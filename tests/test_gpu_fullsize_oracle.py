@@ -1,8 +1,8 @@
 """Headline configuration (BASELINE.json configs[1]) against the oracle at its
 full size.
 
-The metric point (3-D N=59, 10.33M DoF, 1.88 G nnz) and the "~1M DoF" point
-(N=27) are solved twice on the same system -- by libpls on the GPU and by the
+The metric point (3-D N=59, 10.33M DoF, 1.88 G nnz), the size configs[1]
+names (N=64, 13.15M DoF) and the "~1M DoF" point (N=27) are solved twice on the same system -- by libpls on the GPU and by the
 oracle's C/OpenMP restatement of the identical algorithm
 (``oracle/csrc/cpu_solver.c``: right-PC GMRES, CGS, Givens, BuildSoln with the
 extra PC apply, the 2-way PC of reference ``lib/Preconditioner.py:219-246``,
@@ -36,7 +36,9 @@ def _threads():
     return max(1, min(16, n))  # the GPU box's CPU share
 
 
-@pytest.mark.parametrize("N,nb_s,nb_fp", [(27, 64, 64), (59, 256, 264)])
+# N=64 is configs[1]'s named size (13.15M DoF; 320 / 330 blocks keep every
+# block solution in one CU's LDS); host A + P ~ 58 GB, inside the box's cap
+@pytest.mark.parametrize("N,nb_s,nb_fp", [(27, 64, 64), (59, 256, 264), (64, 320, 330)])
 def test_headline_vs_oracle_full_size(gpu, N, nb_s, nb_fp):
     import lib._native as Nt
     from lib.handle import Handle
