@@ -311,8 +311,116 @@ static bool build_b3(const DevCSR &M, DevSELL &S, std::vector<int32_t> &singles,
     return true;
 }
 
+// Reverse Cuthill-McKee order of a square pattern (host): per component, BFS
+// from a pseudo-peripheral vertex visiting neighbours by increasing degree,
+// then reversed.  order[new] = old.
+static std::vector<int32_t> rcm_order(const std::vector<int64_t> &rp, const std::vector<int32_t> &ci, int64_t n) {
+    std::vector<int32_t> order, lev(n, -1);
+    order.reserve(n);
+    std::vector<char> done(n, 0);
+    auto deg = [&](int32_t v) { return rp[v + 1] - rp[v]; };
+    std::vector<int32_t> q, nb;
+    auto bfs_last = [&](int32_t s) {  // last vertex of a plain BFS (pseudo-peripheral sweep)
+        q.assign(1, s);
+        lev[s] = 0;
+        for (size_t h = 0; h < q.size(); ++h)
+            for (int64_t k = rp[q[h]]; k < rp[q[h] + 1]; ++k)
+                if (lev[ci[k]] < 0 && !done[ci[k]]) {
+                    lev[ci[k]] = lev[q[h]] + 1;
+                    q.push_back(ci[k]);
+                }
+        const int32_t last = q.back();
+        for (int32_t v : q) lev[v] = -1;
+        return last;
+    };
+    for (int64_t s0 = 0; s0 < n; ++s0) {
+        if (done[s0]) continue;
+        int32_t s = bfs_last(bfs_last((int32_t)s0));
+        size_t h = order.size();
+        order.push_back(s);
+        done[s] = 1;
+        for (; h < order.size(); ++h) {
+            const int32_t u = order[h];
+            nb.clear();
+            for (int64_t k = rp[u]; k < rp[u + 1]; ++k)
+                if (!done[ci[k]]) {
+                    done[ci[k]] = 1;
+                    nb.push_back(ci[k]);
+                }
+            std::stable_sort(nb.begin(), nb.end(), [&](int32_t a, int32_t b) { return deg(a) < deg(b); });
+            order.insert(order.end(), nb.begin(), nb.end());
+        }
+    }
+    std::reverse(order.begin(), order.end());
+    return order;
+}
+
+// The D16 layout of M with rows and columns relabelled by RCM (FE matrices:
+// the caller's order interleaves P2 vertex, P2 edge and P1 dofs, so a slice's
+// rows gather x from several far-apart ranges); the slices map back to M's
+// rows through rowmap, and x is gathered into the RCM order before each product.
+static bool build_sell_rcm(DevCSR &M, Ctx &c) {
+    const int64_t n = M.nrows;
+    const HostCSR H = download(M, c);
+    const std::vector<int32_t> ord = rcm_order(H.rp, H.ci, n);
+    std::vector<int32_t> inv(n);
+    for (int64_t i = 0; i < n; ++i) inv[ord[i]] = (int32_t)i;
+    HostCSR P;
+    P.nrows = P.ncols = n;
+    P.rp.assign(n + 1, 0);
+    P.ci.resize(H.ci.size());
+    P.v.resize(H.v.size());
+    std::vector<std::pair<int32_t, double>> row;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t o = ord[i];
+        row.clear();
+        for (int64_t k = H.rp[o]; k < H.rp[o + 1]; ++k) row.emplace_back(inv[H.ci[k]], H.v[k]);
+        std::sort(row.begin(), row.end(), [](auto &a, auto &b) { return a.first < b.first; });
+        for (size_t t = 0; t < row.size(); ++t) {
+            P.ci[P.rp[i] + t] = row[t].first;
+            P.v[P.rp[i] + t] = row[t].second;
+        }
+        P.rp[i + 1] = P.rp[i] + (int64_t)row.size();
+    }
+    DevCSR Mp;
+    upload(P, Mp, c);
+    const int keep = c.spmv_rcm;
+    c.spmv_rcm = 0;
+    build_sell(Mp, c);
+    c.spmv_rcm = keep;
+    if (!Mp.sell || !Mp.sell->d16 || Mp.sell->b3_nslices) return false;
+    DevSELL &S = *Mp.sell;
+    std::vector<int32_t> rm(n);
+    if (S.nrows_mapped) {
+        HIPCHK(hipMemcpyAsync(rm.data(), S.rowmap.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c.st));
+        c.sync();
+        for (auto &r : rm) r = ord[r];
+    } else {
+        rm = ord;
+    }
+    S.rowmap.alloc(n);
+    S.nrows_mapped = n;
+    HIPCHK(hipMemcpyAsync(S.rowmap.p, rm.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+    S.xperm.alloc(n);
+    HIPCHK(hipMemcpyAsync(S.xperm.p, ord.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+    S.nperm = n;
+    c.sync();
+    M.sell = std::move(Mp.sell);
+    return true;
+}
+
 void build_sell(DevCSR &M, Ctx &c) {
     if (M.sell || M.nrows == 0) return;
+    if (c.spmv_rcm != 0 && c.sell_d16 && !c.spmv_b3 && !M.halo && M.nrows == M.ncols && M.nrows >= 16384) {
+        bool pads = c.spmv_rcm == 1;
+        if (!pads) {  // only where the plain plan pads (FE): the synthetic blocks keep their layout
+            std::vector<int64_t> sf;
+            std::vector<int32_t> lp, rm;
+            d16_plan(M, sf, lp, rm, c);
+            pads = !rm.empty();
+        }
+        if (pads && build_sell_rcm(M, c)) return;
+    }
     auto S = std::make_unique<DevSELL>();
     if (c.sell_d16 && M.nnz > 0) {
         std::vector<int64_t> sf;
@@ -456,7 +564,13 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
         if (!M.sell) throw Error("distributed matrix without SELL layout");
     }
     if (M.sell && M.sell->d16) {
-        const DevSELL &S = *M.sell;
+        DevSELL &S = *M.sell;
+        if (S.nperm) {  // RCM-relabelled columns: x in that order first
+            auto &xb = S.xbuf[c.st];
+            if (xb.n < (size_t)S.nperm) xb.alloc(S.nperm);
+            launch_gather_i32(S.nperm, S.xperm.p, x, xb.p, c.st);
+            x = xb.p;
+        }
         if (S.b3_nslices)
             launch_b3_spmv(S.b3_nslices, S.b3_ntrip, S.b3ptr.p, S.b3map.p, S.b3col.p, S.b3val.p, x, y, alpha, beta, z,
                            M.tag, c.st);

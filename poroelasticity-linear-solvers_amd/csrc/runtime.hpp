@@ -75,6 +75,7 @@ struct Ctx {
     double d16_sigma_pad = 0.15;  // ... used when the plain plan pads more than this fraction (pls.d16_sigma_pad)
     int d16_sorted_lpr = 2;       // lanes per row of sorted slices with 32+ entries per row (pls.d16_sorted_lpr)
     bool spmv_b3 = false;         // row-triple layout for FE vector fields (pls.spmv_b3; measured slower)
+    int spmv_rcm = -1;            // RCM-relabelled SpMV layout: -1 where the plain plan pads (FE), 0 never, 1 always
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
@@ -115,10 +116,15 @@ struct DevSELL {
     // run while the halo exchange is in flight)
     DBuf<int32_t> s_in, s_halo;
     int64_t n_in = 0, n_halo = 0;
+    // RCM-relabelled columns (FE matrices, pls.spmv_rcm): the product reads
+    // xp = x[xperm] (per-stream scratch) so a slice's gathers stay local
+    int64_t nperm = 0;
+    DBuf<int32_t> xperm;
+    std::map<hipStream_t, DBuf<double>> xbuf;
     int64_t bytes() const {  // bytes one product streams from the matrix
         return (d16 ? stored * 10 + nslices * (64 * 4 * nsegs + 20) + 8 + nrows_mapped * 4
                     : stored * 12 + (nslices + 1) * 8) +
-               b3_stored * 28 + b3_ntrip * 4 + (b3_nslices + 1) * 8;
+               b3_stored * 28 + b3_ntrip * 4 + (b3_nslices + 1) * 8 + nperm * 20;
     }
 };
 
