@@ -61,6 +61,21 @@ class BlockPC:
             pc = None
             if dist_size > 1:
                 ptype = opt(db, prefix, "pc_type", pc_type)
+                if ptype == "hypre" and str(db.get("pls.hypre", "boomeramg")) == "boomeramg":
+                    # BoomerAMG under mpirun -np G: the block's rank partition when every
+                    # rank's rows are one contiguous range (single-field slabs, or
+                    # caller-assembled ownership), as libpls's PCRedundant passes it on
+                    sizes_r = None
+                    if dist_owner is not None:
+                        own = dist_owner[rows]
+                        if np.all(np.diff(own) >= 0):
+                            sizes_r = np.bincount(own, minlength=dist_size).tolist()
+                    elif len(fields) == 1:
+                        from .dist import slab
+                        sizes_r = [slab(sizes[fields[0]], dist_size, q)[1] for q in range(dist_size)]
+                    if sizes_r is not None and "pls.hypre_ranks" not in db:
+                        db_r = dict(db, **{"pls.hypre_ranks": ",".join(str(v) for v in sizes_r)})
+                        pc = petsc.make_pc_of_type("hypre", M, db_r, prefix)
                 if ptype == "bjacobi":
                     from .dist import PCBJacobiIndexed, bjacobi_blocks, bjacobi_blocks_owned
                     nbt = opt(db, prefix, "pc_bjacobi_blocks", dist_size, int)

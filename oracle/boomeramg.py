@@ -412,6 +412,27 @@ def chunk_ids(n, K):
     return np.repeat(np.arange(K, dtype=np.int64), lens)
 
 
+def rank_sizes(spec, n):
+    """Level-0 rank sizes of ``pls.hypre_ranks`` ("G": PETSc's split of n rows over
+    G ranks, or "n0,n1,..."): BoomerAMG as it runs under mpirun -np G -- the
+    HMIS first pass inside every rank (the cross-rank PMIS stage is not
+    restated: boundary decisions are the ranks' own), a coarse level's rank
+    owns the C points of its rows, and each rank's rows are cut into its
+    threads' chunks (pls.hypre_relax_chunks / G threads per rank).  None: one rank."""
+    if spec is None or str(spec) == "":
+        return None
+    spec = str(spec)
+    if "," not in spec:
+        G = int(spec)
+        if G <= 1:
+            return None
+        return [n // G + (1 if q < n % G else 0) for q in range(G)]
+    sizes = [int(v) for v in spec.split(",")]
+    if sum(sizes) != n:
+        raise ValueError("pls.hypre_ranks: the rank sizes do not add up to the block's rows")
+    return sizes
+
+
 def level_chunks(n, K, min_rows):
     """Chunks of a level of n rows: K, fewer when a chunk would hold fewer than
     min_rows rows (0: no floor)."""
@@ -493,12 +514,15 @@ class PCBoomerAMG:
         A = A.tocsr()
         A.sort_indices()
         self.levels = []
+        parts = rank_sizes(db.get("pls.hypre_ranks"), A.shape[0])
         while A.shape[0] > 9 and len(self.levels) < self.max_levels - 1:
             n = A.shape[0]
             S = strength(A, self.theta, self.mu)
             aggressive = len(self.levels) < self.agg_nl
             part = None
-            if self.coarsen_chunks > 1:
+            if parts is not None:
+                part = np.repeat(np.arange(len(parts)), parts)
+            elif self.coarsen_chunks > 1:
                 part = chunk_ids(n, self.coarsen_chunks)
             elif self.coarsen_chunks == 0:
                 part = coarsen_partition(S, n, level_chunks(n, self.chunks, self.coarsen_rows))
@@ -512,7 +536,9 @@ class PCBoomerAMG:
             R.sort_indices()
             Ac = (R @ (A @ P)).tocsr()
             Ac.sort_indices()
-            self.levels.append({"A": A, "P": P, "R": R, "cf": cf})
+            self.levels.append({"A": A, "P": P, "R": R, "cf": cf, "parts": parts})
+            if parts is not None:  # the coarse level's ranks: their C points
+                parts = [int(np.count_nonzero(cf[part == q] == C)) for q in range(len(parts))]
             A = Ac
         self.coarse = A
         self.coarse_lu = spla.splu(sp.csc_matrix(A)) if A.shape[0] else None
@@ -521,7 +547,16 @@ class PCBoomerAMG:
         """Per relaxation set ("all", or "C" / "F"): its rows and the hybrid SGS factors."""
         if "sgs" not in L:
             A = L["A"]
-            cid = chunk_ids(A.shape[0], level_chunks(A.shape[0], self.chunks, self.chunk_rows))
+            if L.get("parts") is None:
+                cid = chunk_ids(A.shape[0], level_chunks(A.shape[0], self.chunks, self.chunk_rows))
+            else:  # ranks: each rank's rows in its threads' chunks
+                T = max(1, self.chunks // len(L["parts"]))
+                cid, base = [], 0
+                for sz in L["parts"]:
+                    if sz:
+                        cid.append(base + chunk_ids(sz, level_chunks(sz, T, self.chunk_rows)))
+                        base = int(cid[-1][-1]) + 1
+                cid = np.concatenate(cid)
             sets = {"all": None} if self.no_cf else {o: np.flatnonzero(L["cf"] == (C if o == "C" else F)) for o in "CF"}
             L["sgs"] = {k: (idx,) + _sgs_factors(A, cid, idx) for k, idx in sets.items()}
         return L["sgs"]

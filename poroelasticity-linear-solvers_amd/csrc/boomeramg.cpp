@@ -295,11 +295,10 @@ std::vector<int64_t> chunk_starts(int64_t n, int64_t K) {
     return st;
 }
 
-std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths, int64_t K) {
+std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths, const std::vector<int64_t> &pst) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double t0 = now();
-    K = std::max<int64_t>(1, std::min<int64_t>(K, S.n));
-    const std::vector<int64_t> pst = chunk_starts(S.n, K);
+    const int64_t K = (int64_t)pst.size() - 1;
     std::vector<int8_t> cf = rs_partitioned(S, K, pst);
     if (!aggressive) return cf;
     double t1 = now();
@@ -316,7 +315,7 @@ std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths, int64_
         }
         pst2[K] = (int64_t)cpts.size();
     }
-    const std::vector<int8_t> cf2 = rs_partitioned(S2, K, pst2);
+    const std::vector<int8_t> cf2 = rs_partitioned(S2, K, pst2);  // (K: partitions, some possibly empty)
     if (std::getenv("PLS_AMG_TRACE"))
         fprintf(stderr, "[boomeramg coarsen] n %lld S nnz %lld: RS %.2f s; S2 (%zu C1 points, nnz %lld) %.2f s; RS2 %.2f s\n",
                 (long long)S.n, (long long)S.ci.size(), t1 - t0, cpts.size(), (long long)S2.ci.size(), t2 - t1, now() - t2);
@@ -613,9 +612,12 @@ struct ChunkMap {
 // ascending; empty: all): part 0 all of it, 1 its lower triangle with the
 // diagonal (D + L), 2 the upper one (D + U).  A zero or missing diagonal entry
 // is refused (hypre would skip the row).
-HostCSR chunk_part(const HostCSR &A, const std::vector<int32_t> &idx, int64_t K, int part) {
+HostCSR chunk_part(const HostCSR &A, const std::vector<int32_t> &idx, const std::vector<int64_t> &cst, int part) {
     const int64_t n = A.nrows;
-    const ChunkMap chunk(n, K);
+    std::vector<int32_t> cid(n);
+    for (size_t k = 0; k + 1 < cst.size(); ++k)
+        for (int64_t i = cst[k]; i < cst[k + 1]; ++i) cid[i] = (int32_t)k;
+    auto chunk = [&](int64_t i) { return cid[i]; };
     std::vector<int32_t> loc;
     const bool all = idx.empty();
     if (!all) {
@@ -653,7 +655,38 @@ struct BParams {
     int64_t coarsen_chunks = 0, coarsen_rows = 65536;  // HMIS partitions (pls.hypre_coarsen_*): 0 = auto, 1 = none
     int paths = 1, K = 1;
     bool no_cf = false;
+    std::string ranks;  // pls.hypre_ranks: the level-0 rank partition ("G" or "n0,n1,..."), hypre under mpirun -np G
 };
+
+// level-0 rank sizes of pls.hypre_ranks (empty: one rank)
+std::vector<int64_t> rank_sizes(const std::string &spec, int64_t n) {
+    std::vector<int64_t> out;
+    if (spec.empty()) return out;
+    if (spec.find(',') == std::string::npos) {
+        const int64_t G = std::stoll(spec);
+        if (G <= 1) return out;
+        for (int64_t q = 0; q < G; ++q) out.push_back(n / G + (q < n % G ? 1 : 0));
+        return out;
+    }
+    int64_t tot = 0;
+    size_t a = 0;
+    while (a <= spec.size()) {
+        const size_t b = spec.find(',', a);
+        out.push_back(std::stoll(spec.substr(a, b == std::string::npos ? std::string::npos : b - a)));
+        tot += out.back();
+        if (b == std::string::npos) break;
+        a = b + 1;
+    }
+    if (tot != n) throw Error("pls.hypre_ranks: the rank sizes do not add up to the block's rows");
+    return out;
+}
+
+// starts of the level's parts (sizes; zero-sized parts kept)
+std::vector<int64_t> part_starts(const std::vector<int64_t> &sizes) {
+    std::vector<int64_t> st(1, 0);
+    for (int64_t v : sizes) st.push_back(st.back() + v);
+    return st;
+}
 
 BParams parse_params(const Options &o, const std::string &prefix) {
     const std::string pre = prefix + "pc_hypre_boomeramg_";
@@ -671,6 +704,7 @@ BParams parse_params(const Options &o, const std::string &prefix) {
     p.chunk_rows = o.integer("pls.hypre_relax_min_rows", 1024);
     p.coarsen_chunks = o.integer("pls.hypre_coarsen_chunks", 0);
     p.coarsen_rows = o.integer("pls.hypre_coarsen_min_rows", 65536);
+    p.ranks = o.str("pls.hypre_ranks", "");
     if (p.chunks < 1 || p.chunk_rows < 0)
         throw Error("pls.hypre_relax_chunks must be >= 1 and pls.hypre_relax_min_rows >= 0");
     const std::string ct = o.str(pre + "coarsen_type", "HMIS"), it = o.str(pre + "interp_type", "ext+i");
@@ -689,16 +723,26 @@ template <class F>
 HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     int64_t nlev = 0;
+    // ranks (hypre under mpirun -np G): the HMIS first pass inside every rank, a
+    // coarse level's rank owns the C points of its rows
+    std::vector<int64_t> parts = rank_sizes(p.ranks, A.nrows);
     while (A.nrows > 9 && nlev < p.max_levels - 1) {
         double t0 = now();
         const Pattern S = strength(A, p.theta, p.mu);
         tm[1] += now() - t0;
         t0 = now();
         const bool aggressive = nlev < p.agg_nl;
-        const int64_t Kc = p.coarsen_chunks == 1 ? 1
-                           : p.coarsen_chunks > 1 ? p.coarsen_chunks
-                                                  : coarsen_partitions(S, level_chunks(A.nrows, p.chunks, p.coarsen_rows));
-        const std::vector<int8_t> cf = coarsen(S, aggressive, p.paths, Kc);
+        std::vector<int64_t> pst;
+        if (!parts.empty()) {
+            pst = part_starts(parts);
+        } else {
+            int64_t Kc = p.coarsen_chunks == 1 ? 1
+                         : p.coarsen_chunks > 1 ? p.coarsen_chunks
+                                                : coarsen_partitions(S, level_chunks(A.nrows, p.chunks, p.coarsen_rows));
+            Kc = std::max<int64_t>(1, std::min<int64_t>(Kc, A.nrows));
+            pst = chunk_starts(A.nrows, Kc);
+        }
+        const std::vector<int8_t> cf = coarsen(S, aggressive, p.paths, pst);
         tm[2] += now() - t0;
         int64_t nc = 0;
         for (int8_t v : cf) nc += v == CPT;
@@ -711,7 +755,13 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
         HostCSR Ac;
         if (!galerkin_fused(A, P, nc, p.rap_bytes, Ac)) Ac = spgemm(R, spgemm(A, P));
         tm[4] += now() - t0;
-        on_level(A, cf, P, R, nc);
+        on_level(A, cf, P, R, nc, parts);
+        if (!parts.empty()) {  // the coarse level's rank sizes: C points per rank
+            std::vector<int64_t> np(parts.size(), 0);
+            for (size_t q = 0; q < parts.size(); ++q)
+                for (int64_t i = pst[q]; i < pst[q + 1]; ++i) np[q] += cf[i] == CPT;
+            parts.swap(np);
+        }
         A = std::move(Ac);
         ++nlev;
     }
@@ -871,7 +921,13 @@ struct PCBoomer : PC {
     PCBoomer(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c) {
         type = "hypre";
         n = M.nrows;
-        const BParams prm = parse_params(o, prefix);
+        BParams prm = parse_params(o, prefix);
+        int64_t rsum = 0;
+        for (int64_t v : c.rank_rows) rsum += v;
+        if (prm.ranks.empty() && c.rank_rows.size() > 1 && rsum == M.nrows) {  // gathered from G ranks (PCRedundant)
+            for (size_t q = 0; q < c.rank_rows.size(); ++q)
+                prm.ranks += (q ? "," : "") + std::to_string(c.rank_rows[q]);
+        }
         K = prm.K;
         no_cf = prm.no_cf;
         if (!M.sell) build_sell(const_cast<DevCSR &>(M), c);
@@ -891,7 +947,7 @@ struct PCBoomer : PC {
         double t0 = now();
         std::unique_ptr<DevCSR> cur;
         HostCSR A = host_setup(download(M, c), prm, [&](const HostCSR &Al, const std::vector<int8_t> &cf, const HostCSR &P,
-                                                        const HostCSR &R, int64_t nc) {
+                                                        const HostCSR &R, int64_t nc, const std::vector<int64_t> &parts) {
             const double t1 = now();
             auto L = std::make_unique<BLevel>();
             L->n = Al.nrows;
@@ -915,7 +971,22 @@ struct PCBoomer : PC {
                 groups.resize(2);
                 for (int64_t i = 0; i < Al.nrows; ++i) groups[cf[i] == CPT ? 0 : 1].push_back((int32_t)i);
             }
-            const int64_t Kl = level_chunks(Al.nrows, prm.chunks, prm.chunk_rows);
+            // smoother chunks: K_l uniform chunks, or with ranks each rank's rows cut into its
+            // threads' chunks (pls.hypre_relax_chunks / ranks threads per rank)
+            std::vector<int64_t> cst;
+            if (parts.empty()) {
+                cst = chunk_starts(Al.nrows, level_chunks(Al.nrows, prm.chunks, prm.chunk_rows));
+            } else {
+                cst.assign(1, 0);
+                const int64_t T = std::max<int64_t>(1, prm.chunks / (int64_t)parts.size());
+                for (int64_t sz : parts) {
+                    if (sz == 0) continue;
+                    const std::vector<int64_t> loc = chunk_starts(sz, level_chunks(sz, T, prm.chunk_rows));
+                    const int64_t base = cst.back();
+                    for (size_t k = 1; k < loc.size(); ++k) cst.push_back(base + loc[k]);
+                }
+            }
+            const int64_t Kl = (int64_t)cst.size() - 1;
             for (auto &g : groups) {
                 auto rs = std::make_unique<RelaxSet>();
                 rs->all = no_cf;
@@ -927,13 +998,15 @@ struct PCBoomer : PC {
                         rs->idx.alloc(gi.size());
                         HIPCHK(hipMemcpyAsync(rs->idx.p, gi.data(), sizeof(int64_t) * gi.size(), hipMemcpyHostToDevice, c.st));
                     }
-                    const HostCSR lo = chunk_part(Al, g, Kl, 1), up = chunk_part(Al, g, Kl, 2);
+                    const HostCSR lo = chunk_part(Al, g, cst, 1), up = chunk_part(Al, g, cst, 2);
                     // the set's chunk boundaries in its own numbering (chunks without set points dropped)
                     std::vector<int64_t> cp{0};
                     {
-                        const ChunkMap chunk(Al.nrows, Kl);
+                        std::vector<int32_t> cid(Al.nrows);
+                        for (size_t k = 0; k + 1 < cst.size(); ++k)
+                            for (int64_t i = cst[k]; i < cst[k + 1]; ++i) cid[i] = (int32_t)k;
                         for (int64_t t = 1; t < rs->m; ++t)
-                            if (chunk(no_cf ? t : g[t]) != chunk(no_cf ? t - 1 : g[t - 1])) cp.push_back(t);
+                            if (cid[no_cf ? t : g[t]] != cid[no_cf ? t - 1 : g[t - 1]]) cp.push_back(t);
                         cp.push_back(rs->m);
                     }
                     // a sweep's critical path (levels of both triangles, one chunk per
@@ -953,14 +1026,15 @@ struct PCBoomer : PC {
                         const int gm = (nlev > 0 && lo.nrows / nlev > wide_rows) ? wide_mode : gmem;
                         if (no_cf) {
                             // the chunks are PCILU's blocks (the same partition): one workgroup per chunk
-                            auto pc = std::make_unique<PCILU>(*L->A, Kl, c, false, allow_lds, 0, gm, ring, true);
+                            auto pc = std::make_unique<PCILU>(*L->A, Kl, c, false, allow_lds, 0, gm, ring, true,
+                                                              parts.empty() ? nullptr : &cst);
                             if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
             if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
                             if (o.flag("pls.sweep_profile", false))
                                 pc->profile_tag = prefix + "sgs L" + std::to_string(lv.size());
                             rs->sgs = std::move(pc);
                         } else {
-                            upload(chunk_part(Al, g, Kl, 0), rs->sub, c);
+                            upload(chunk_part(Al, g, cst, 0), rs->sub, c);
                             rs->sgs = std::make_unique<PCILU>(rs->sub, 1, c, false, allow_lds, 0, gm, ring, true);
                         }
                     }
@@ -1090,7 +1164,7 @@ struct PCBoomer : PC {
 }  // namespace
 
 std::unique_ptr<PC> make_boomeramg(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c) {
-    if (M.halo) throw Error("PC type hypre (prefix " + prefix + "): multigrid is single-rank in this build");
+    if (M.halo) throw Error("PC type hypre (prefix " + prefix + "): a sharded block reaches the AMG through PCRedundant");
     return std::make_unique<PCBoomer>(M, o, prefix, c);
 }
 
@@ -1103,7 +1177,7 @@ void boomeramg_host_level(const HostCSR &A, const Options &o, const std::string 
     int64_t l = 0;
     n = nc = 0;
     HostCSR coarse = host_setup(A, prm, [&](const HostCSR &Al, const std::vector<int8_t> &cfl, const HostCSR &Pl,
-                                            const HostCSR &, int64_t ncl) {
+                                            const HostCSR &, int64_t ncl, const std::vector<int64_t> &) {
         if (l == level) {
             n = Al.nrows;
             nc = ncl;

@@ -216,6 +216,38 @@ void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, void *tmp, s
 }
 
 // ========================================================== extraction =====
+// Block of a row: explicit starts (binary search; nb + 1 entries) or PETSc's
+// sizes (n / nb, the first n % nb blocks one longer).  b0 / len of the block.
+__device__ __forceinline__ int64_t block_of(int64_t i, int64_t n, int64_t nb, const int64_t *bstart, int64_t &b0,
+                                            int64_t &len) {
+    if (bstart) {
+        int64_t lo = 0, hi = nb;  // largest b with bstart[b] <= i
+        while (hi - lo > 1) {
+            const int64_t m = (lo + hi) >> 1;
+            if (bstart[m] <= i) lo = m; else hi = m;
+        }
+        b0 = bstart[lo];
+        len = bstart[lo + 1] - b0;
+        return lo;
+    }
+    const int64_t q = n / nb, r = n % nb;
+    const int64_t b = i < r * (q + 1) ? i / (q + 1) : r + (i - r * (q + 1)) / q;
+    b0 = b * q + (b < r ? b : r);
+    len = q + (b < r ? 1 : 0);
+    return b;
+}
+__device__ __forceinline__ void block_range(int64_t b, int64_t n, int64_t nb, const int64_t *bstart, int64_t &b0,
+                                            int64_t &len) {
+    if (bstart) {
+        b0 = bstart[b];
+        len = bstart[b + 1] - b0;
+        return;
+    }
+    const int64_t q = n / nb, r = n % nb;
+    b0 = b * q + (b < r ? b : r);
+    len = q + (b < r ? 1 : 0);
+}
+
 __device__ __forceinline__ void window_of(const WindowSpec &w, int64_t lr, int64_t nloc, int64_t r0,
                                           int64_t &lo, int64_t &hi) {
     if (w.mode == 0) {
@@ -223,18 +255,8 @@ __device__ __forceinline__ void window_of(const WindowSpec &w, int64_t lr, int64
         hi = w.c1;
         return;
     }
-    const int64_t nb = w.nblocks;
-    const int64_t q = nloc / nb, r = nloc % nb;
     int64_t b0, len;
-    if (lr < r * (q + 1)) {
-        const int64_t b = lr / (q + 1);
-        b0 = b * (q + 1);
-        len = q + 1;
-    } else {
-        const int64_t b = r + (lr - r * (q + 1)) / q;
-        b0 = r * (q + 1) + (b - r) * q;
-        len = q;
-    }
+    block_of(lr, nloc, w.nblocks, w.bstart, b0, len);
     lo = r0 + b0;
     hi = r0 + b0 + len;
 }
@@ -1803,7 +1825,7 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
                                                   const int32_t *ci, const double *lu, const int64_t *diag,
                                                   const double *dinv, int upper, int64_t n, int64_t nb,
                                                   const int64_t *sptr2, int32_t *ocol, double *oval, int wide,
-                                                  const int32_t *posof, const int32_t *row_lo) {
+                                                  const int32_t *posof, const int32_t *row_lo, const int64_t *bstart) {
     const int64_t sl = ((int64_t)blockIdx.x * TPB + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     if (sl >= nslices) return;
@@ -1813,9 +1835,8 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
     const int64_t base = sptr2[sl], L = (sptr2[sl + 1] - base) >> 6;
     int64_t b0 = 0, src = 0, len = 0;
     if (i >= 0) {
-        const int64_t q = n / nb, rr = n % nb;
-        const int64_t blk = i < rr * (q + 1) ? i / (q + 1) : rr + (i - rr * (q + 1)) / q;
-        b0 = blk * q + (blk < rr ? blk : rr);
+        int64_t blen;
+        block_of(i, n, nb, bstart, b0, blen);
         src = upper ? diag[i] + 1 : rp[i];
         len = upper ? rp[i + 1] - diag[i] - 1 : diag[i] - rp[i];
     }
@@ -1861,11 +1882,12 @@ __global__ __launch_bounds__(TPB) void k_lds_fill(int64_t nslices, const int32_t
 void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,
                      const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu, const int64_t *diag,
                      const double *dinv, int upper, int64_t n, int64_t nb, const int64_t *sptr2, int32_t *ocol,
-                     double *oval, hipStream_t st, bool wide, const int32_t *posof, const int32_t *row_lo) {
+                     double *oval, hipStream_t st, bool wide, const int32_t *posof, const int32_t *row_lo,
+                     const int64_t *bstart) {
     if (nslices > 0)
         k_lds_fill<<<grid_for(nslices * 64, TPB), TPB, 0, st>>>(nslices, s_start, s_n, s_lpr, order, rp, ci, lu, diag,
                                                                 dinv, upper, n, nb, sptr2, ocol, oval, wide ? 1 : 0,
-                                                                posof, row_lo);
+                                                                posof, row_lo, bstart);
 }
 
 // One sweep over a block's levels.  Pipeline: the loads of level g+2 are
@@ -2332,13 +2354,13 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
                                                          const int32_t *__restrict__ Ucol,
                                                          const double *__restrict__ Uval,
                                                          const int32_t *__restrict__ Ulpr, const double *x,
-                                                         double *y, int64_t *__restrict__ prof, int rr) {
+                                                         double *y, int64_t *__restrict__ prof, int rr,
+                                                         const int64_t *__restrict__ bstart) {
     extern __shared__ __attribute__((aligned(16))) double lds_y[];
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
-    const int64_t q = n / nblocks, r = n % nblocks;
-    const int64_t b0 = blk * q + (blk < r ? blk : r);
+    int64_t b0, len;
+    block_range(blk, n, nblocks, bstart, b0, len);
     double *ys = GMEM ? y + b0 : lds_y;
-    const int64_t len = q + (blk < r ? 1 : 0);
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int nw = blockDim.x >> 6;
@@ -2386,12 +2408,12 @@ __global__ __launch_bounds__(RING_TPB) void k_ilu_blocks_ring(
     const int64_t *__restrict__ Ucp, const int32_t *__restrict__ ordL, const int32_t *__restrict__ mapUL,
     const int32_t *__restrict__ ordU, const int64_t *__restrict__ Lfrp, const int32_t *__restrict__ Lfcol,
     const double *__restrict__ Lfval, const int64_t *__restrict__ Ufrp, const int32_t *__restrict__ Ufcol,
-    const double *__restrict__ Ufval, const double *x, double *y, double *yL, double *yU) {
+    const double *__restrict__ Ufval, const double *x, double *y, double *yL, double *yU,
+    const int64_t *__restrict__ bstart) {
     extern __shared__ __attribute__((aligned(16))) double ring[];
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
-    const int64_t q = n / nblocks, r = n % nblocks;
-    const int64_t b0 = blk * q + (blk < r ? blk : r);
-    const int64_t len = q + (blk < r ? 1 : 0);
+    int64_t b0, len;
+    block_range(blk, n, nblocks, bstart, b0, len);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     sweep_block<RING_P, true, true>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol,
                                   Lval, nullptr, ring, yL + b0, b0, Lcoff[blk], Lcoff[blk + 1],
@@ -2412,7 +2434,7 @@ void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, co
                             const int32_t *ordL, const int32_t *mapUL, const int32_t *ordU, const int64_t *Lfrp,
                             const int32_t *Lfcol, const double *Lfval, const int64_t *Ufrp, const int32_t *Ufcol,
                             const double *Ufval, const double *x, double *y, double *yL, double *yU, hipStream_t st,
-                            int tpb) {
+                            int tpb, const int64_t *bstart) {
     if (tpb < 64 || tpb > RING_TPB || (tpb & 63)) tpb = RING_TPB;
     static bool configured = false;
     const int bytes = RING_SLOTS * 8;
@@ -2423,7 +2445,7 @@ void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, co
     k_ilu_blocks_ring<<<(unsigned)nblocks, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
                                                                Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, Lcoff, Lcg, Lcp,
                                                                Ucoff, Ucg, Ucp, ordL, mapUL, ordU, Lfrp, Lfcol, Lfval,
-                                                               Ufrp, Ufcol, Ufval, x, y, yL, yU);
+                                                               Ufrp, Ufcol, Ufval, x, y, yL, yU, bstart);
 }
 void set_ring_probe(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(ring_probe), &v, sizeof(int)); }
 int ilu_ring_slots() { return RING_SLOTS; }
@@ -2438,7 +2460,7 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
-                           int64_t *prof, bool gmem, int tpb, int rr) {
+                           int64_t *prof, bool gmem, int tpb, int rr, const int64_t *bstart, int64_t max_len) {
     // tpb: threads per workgroup, 64 .. 1024 (narrow levels: fewer waves, cheaper barriers)
     if (tpb < 64 || tpb > 1024 || (tpb & 63)) tpb = 1024;
     static bool configured = false;
@@ -2449,13 +2471,13 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
     }
     if (gmem) {
         k_ilu_blocks_lds<true><<<(unsigned)nblocks, tpb, 0, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
-                                                                  Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof, rr);
+                                                                  Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof, rr, bstart);
         return;
     }
-    const size_t bytes = (size_t)(n / nblocks + 1) * 8;
+    const size_t bytes = (size_t)(max_len > 0 ? max_len : n / nblocks + 1) * 8;
     k_ilu_blocks_lds<false><<<(unsigned)nblocks, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval,
                                                                      Llpr, Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y,
-                                                                     prof, rr);
+                                                                     prof, rr, bstart);
 }
 
 // =========================================================== distribution ====

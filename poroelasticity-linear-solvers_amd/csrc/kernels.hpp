@@ -38,7 +38,8 @@ size_t exclusive_scan_tmp_bytes(int64_t n);
 struct WindowSpec {
     int mode;
     int64_t c0, c1;
-    int64_t nblocks;  // mode 1
+    int64_t nblocks;                  // mode 1
+    const int64_t *bstart = nullptr;  // mode 1: explicit block starts (nblocks + 1, device), else PETSc sizes
 };
 void launch_extract_count(const int64_t *rp, const int32_t *ci, int64_t r0, int64_t r1,
                           WindowSpec w, int64_t *row_len, hipStream_t st);
@@ -192,7 +193,8 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
-                           int64_t *prof = nullptr, bool gmem = false, int tpb = 1024, int rr = 0);
+                           int64_t *prof = nullptr, bool gmem = false, int tpb = 1024, int rr = 0,
+                           const int64_t *bstart = nullptr, int64_t max_len = 0);
 int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in registers
 // The ring sweep (kernels.hip, k_ilu_blocks_ring): blocks of narrow levels whose
 // every level has <= ilu_ring_chunk() rows; per triangle chunk tables (coff per
@@ -209,14 +211,14 @@ void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, co
                             const int64_t *Lcp, const int64_t *Ucoff, const int64_t *Ucg, const int64_t *Ucp,
                             const int32_t *ordL, const int32_t *mapUL, const int32_t *ordU, const int64_t *Lfrp,
                             const int32_t *Lfcol, const double *Lfval, const int64_t *Ufrp, const int32_t *Ufcol,
-                            const double *Ufval, const double *x, double *y, double *yL, double *yU, hipStream_t st, int tpb = 1024);
+                            const double *Ufval, const double *x, double *y, double *yL, double *yU, hipStream_t st, int tpb = 1024, const int64_t *bstart = nullptr);
 // LDS-kernel stream layout (header entry per lane, lanes-per-row slices, block-local columns)
 void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n, const int32_t *s_lpr,
                      const int32_t *order, const int64_t *rp, const int32_t *ci, const double *lu, const int64_t *diag,
                      const double *dinv, int upper, int64_t n, int64_t nb, const int64_t *sptr2, int32_t *ocol,
                      double *oval, hipStream_t st, bool wide = false,
                      const int32_t *posof = nullptr /* ring sweep: row -> block-local level-order position */,
-                     const int32_t *row_lo = nullptr /* ring sweep: entries with position < row_lo[row] are far */);
+                     const int32_t *row_lo = nullptr /* ring sweep: entries with position < row_lo[row] are far */, const int64_t *bstart = nullptr);
 
 // distribution helpers
 void launch_flag_ghosts(int64_t nnz, const int32_t *ci, const int32_t *own, uint8_t *flag, hipStream_t st);

@@ -741,9 +741,18 @@ static int64_t level_order(int64_t n, const std::vector<int64_t> &rp, const std:
 
 // Block-major level groups: rows sorted by (block, level); grp[g] = first row
 // of group g, off[b] = first group of block b (PETSc bjacobi block sizes).
+// block starts: explicit (bounds) or PETSc's bjacobi sizes
+static std::vector<int64_t> block_starts(int64_t n, int64_t nb, const std::vector<int64_t> *bounds) {
+    if (bounds) return *bounds;
+    std::vector<int64_t> st(nb + 1, 0);
+    const int64_t q = n / nb, r = n % nb;
+    for (int64_t b = 0; b < nb; ++b) st[b + 1] = st[b] + q + (b < r ? 1 : 0);
+    return st;
+}
+
 static void block_level_groups(int64_t n, int64_t nb, const std::vector<int64_t> &rp, const std::vector<int32_t> &ci,
                                bool upper, std::vector<int32_t> &order, std::vector<int64_t> &grp,
-                               std::vector<int64_t> &off) {
+                               std::vector<int64_t> &off, const std::vector<int64_t> *bounds = nullptr) {
     std::vector<int32_t> lvl(n, 0);
     if (!upper) {
         for (int64_t i = 0; i < n; ++i) {
@@ -758,7 +767,7 @@ static void block_level_groups(int64_t n, int64_t nb, const std::vector<int64_t>
             lvl[i] = L;
         }
     }
-    const int64_t q = n / nb, r = n % nb;
+    const std::vector<int64_t> bst = block_starts(n, nb, bounds);
     order.clear();
     order.reserve(n);
     grp.clear();
@@ -766,7 +775,7 @@ static void block_level_groups(int64_t n, int64_t nb, const std::vector<int64_t>
     int64_t b0 = 0;
     std::vector<int64_t> cnt;
     for (int64_t b = 0; b < nb; ++b) {
-        const int64_t len = q + (b < r ? 1 : 0);
+        const int64_t len = bst[b + 1] - bst[b];
         int32_t nl = 0;
         for (int64_t i = b0; i < b0 + len; ++i) nl = std::max(nl, lvl[i] + 1);
         cnt.assign(nl + 1, 0);
@@ -951,7 +960,7 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
     if (row_lo) up(d_lo, *row_lo);
     launch_lds_fill(ns, d_start.p, d_n.p, d_lpr.p, d_order.p, P.F.rp.p, P.F.ci.p, P.F.val.p, P.diag.p, P.dinv.p,
                     upper ? 1 : 0, n, nb, D.sptr.p, D.col.p, D.val.p, c.st, /*wide headers: y-resident sweep*/ max_lpr > 4,
-                    posof ? d_posof.p : nullptr, row_lo ? d_lo.p : nullptr);
+                    posof ? d_posof.p : nullptr, row_lo ? d_lo.p : nullptr, P.bstart_h.empty() ? nullptr : P.bstart.p);
     HIPCHK(hipGetLastError());
     c.sync();
     if (posof) {  // ring sweep: slice starts carry log2(lanes per row) in bits 0-2
@@ -1022,15 +1031,16 @@ static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order
                         const std::vector<int64_t> &goff, const std::vector<int64_t> &rp, const std::vector<int32_t> &ci,
                         const std::vector<int64_t> &dg, const std::vector<double> &fv, bool upper,
                         std::vector<int32_t> &posof, std::vector<int32_t> &row_lo, std::vector<int32_t> &near_len,
-                        RingTri &T, Ctx &c) {
-    const int64_t q = n / nb, r = n % nb, C = ilu_ring_chunk(), R = ilu_ring_slots();
+                        RingTri &T, Ctx &c, const std::vector<int64_t> *bounds = nullptr) {
+    const std::vector<int64_t> bst = block_starts(n, nb, bounds);
+    const int64_t C = ilu_ring_chunk(), R = ilu_ring_slots();
     posof.assign(n, 0);
     row_lo.assign(n, 0);
     near_len.assign(n, 0);
     std::vector<int64_t> coff(nb + 1, 0), cg, cp;
     int64_t b0 = 0;
     for (int64_t b = 0; b < nb; ++b) {
-        const int64_t len = q + (b < r ? 1 : 0);
+        const int64_t len = bst[b + 1] - bst[b];
         for (int64_t k = b0; k < b0 + len; ++k) posof[order[k]] = (int32_t)(k - b0);
         coff[b] = (int64_t)cg.size();
         for (int64_t g = goff[b]; g < goff[b + 1];) {
@@ -1082,17 +1092,30 @@ static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order
 }
 
 PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr, int gmem_mode,
-             int ring_mode, bool sgs_factors) {
+             int ring_mode, bool sgs_factors, const std::vector<int64_t> *bounds) {
     exact = exact_lu;
     sgs = sgs_factors && !exact_lu;
     allow_lds = lds;
     type = exact ? "lu" : sgs ? "sgs" : (nb > 1 ? "bjacobi" : "ilu");
     n = M.nrows;
     nblocks = exact ? 1 : std::max<int64_t>(1, std::min<int64_t>(nb, n));
+    const std::vector<int64_t> *bnd = nullptr;
+    if (bounds && !exact) {  // explicit block starts (nb + 1, from 0 to n, nondecreasing)
+        if (bounds->size() < 2 || bounds->front() != 0 || bounds->back() != n)
+            throw Error("PCILU: block bounds must run from 0 to n");
+        for (size_t k = 0; k + 1 < bounds->size(); ++k)
+            if ((*bounds)[k + 1] <= (*bounds)[k]) throw Error("PCILU: empty or decreasing block");
+        bstart_h = *bounds;
+        nblocks = (int64_t)bounds->size() - 1;
+        bstart.alloc(bstart_h.size());
+        HIPCHK(hipMemcpyAsync(bstart.p, bstart_h.data(), sizeof(int64_t) * bstart_h.size(), hipMemcpyHostToDevice, c.st));
+        bnd = &bstart_h;
+    }
     WindowSpec w{};
     if (nblocks > 1) {
         w.mode = 1;
         w.nblocks = nblocks;
+        w.bstart = bnd ? bstart.p : nullptr;
     } else {
         w.mode = 0;
         w.c0 = 0;
@@ -1136,7 +1159,10 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         c.sync();
     }
     if (hfail) throw Error("ILU(0): zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
-    const int64_t blen = n / nblocks + 1;
+    int64_t blen = n / nblocks + 1;
+    if (bnd)
+        for (size_t k = 0; k + 1 < bnd->size(); ++k) blen = std::max<int64_t>(blen, (*bnd)[k + 1] - (*bnd)[k]);
+    max_len = blen;
     const bool fits_lds = blen <= ilu_lds_max_rows() && gmem_mode != 1;
     // Blocks too long for LDS: one workgroup per block with y itself as the
     // block solution when levels are narrow -- FE blocks in a bandwidth-
@@ -1149,8 +1175,8 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
     if (nblocks >= 64 || (fits_lds && allow_lds) || gmem) {
         std::vector<int32_t> oL, oU;
         std::vector<int64_t> gL, gU, fL, fU;
-        block_level_groups(n, nblocks, rp, ci, false, oL, gL, fL);
-        block_level_groups(n, nblocks, rp, ci, true, oU, gU, fU);
+        block_level_groups(n, nblocks, rp, ci, false, oL, gL, fL, bnd);
+        block_level_groups(n, nblocks, rp, ci, true, oU, gU, fU, bnd);
         build_tri_sell(*this, rp, dg, oL, gL, &fL, false, Lf, c);
         build_tri_sell(*this, rp, dg, oU, gU, &fU, true, Uf, c);
         nlev_U = (int64_t)gU.size() - 1;
@@ -1180,14 +1206,14 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                 std::vector<double> fv(F.nnz);
                 if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
                 c.sync();
-                ring_tables(n, nblocks, oL, gL, fL, rp, ci, dg, fv, false, pL, loL, nlL, Lr, c);
-                ring_tables(n, nblocks, oU, gU, fU, rp, ci, dg, fv, true, pU, loU, nlU, Ur, c);
+                ring_tables(n, nblocks, oL, gL, fL, rp, ci, dg, fv, false, pL, loL, nlL, Lr, c, bnd);
+                ring_tables(n, nblocks, oU, gU, fU, rp, ci, dg, fv, true, pU, loU, nlU, Ur, c, bnd);
                 // mapUL[b0 + t] = b0 + (L position of the row at U position t)
                 std::vector<int32_t> m(n);
-                const int64_t q = n / nblocks, r = n % nblocks;
+                const std::vector<int64_t> bst = block_starts(n, nblocks, bnd);
                 int64_t b0 = 0;
                 for (int64_t b = 0; b < nblocks; ++b) {
-                    const int64_t len = q + (b < r ? 1 : 0);
+                    const int64_t len = bst[b + 1] - bst[b];
                     for (int64_t t = b0; t < b0 + len; ++t) m[t] = (int32_t)(b0 + pL[oU[t]]);
                     b0 += len;
                 }
@@ -1251,7 +1277,7 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
                                Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, Lr.coff.p, Lr.cg.p, Lr.cp.p,
                                Ur.coff.p, Ur.cg.p, Ur.cp.p, Lr.ord.p, mapUL.p, Ur.ord.p, Lr.frp.p, Lr.fcol.p,
                                Lr.fval.p, Ur.frp.p, Ur.fcol.p, Ur.fval.p, x, y, sc.first.p, sc.second.p, c.st,
-                               lds_tpb);
+                               lds_tpb, bstart_h.empty() ? nullptr : bstart.p);
         return;
     }
     if (use_lds) {
@@ -1259,7 +1285,7 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
         if (!profile_tag.empty()) prof.alloc(nblocks * 8);
         launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
                               Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof.p, lds_gmem,
-                              lds_tpb, lds_rr ? 1 : 0);
+                              lds_tpb, lds_rr ? 1 : 0, bstart_h.empty() ? nullptr : bstart.p, max_len);
         if (!profile_tag.empty()) {
             // diagnostics: per-block sweep times (100 MHz wall clock), slowest first
             std::vector<int64_t> h(nblocks * 8);
@@ -1520,6 +1546,22 @@ struct PCRedundant : PC {
         self->d16_sigma_pad = c.d16_sigma_pad;
         self->d16_sorted_lpr = c.d16_sorted_lpr;
         self->spmv_b3 = c.spmv_b3;
+        self->spmv_rcm = c.spmv_rcm;
+        // the ranks' rows: contiguous ranges in rank order (every single-field block,
+        // every caller-assembled one) -> the inner PC may restate how the reference's
+        // PC runs over G ranks (classical AMG: hypre's per-rank HMIS and smoother)
+        {
+            bool contiguous = true;
+            int64_t start = 0;
+            for (int q = 0; q < G && contiguous; ++q) {
+                const int64_t *m = recv.data() + (size_t)words * q;
+                for (int64_t i = 0; i < all[2 * q]; ++i)
+                    if (m[i] != start + i) contiguous = false;
+                start += all[2 * q];
+            }
+            if (contiguous)
+                for (int q = 0; q < G; ++q) self->rank_rows.push_back(all[2 * q]);
+        }
         upload(Gh, Gm, *self);
         inner = factory(Gm, *self);
         std::vector<int64_t> mg(H.l2g.begin(), H.l2g.begin() + nloc);

@@ -81,6 +81,9 @@ struct Ctx {
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
     DBuf<char> scan_tmp;
     size_t scan_tmp_bytes = 0;
+    // a redundant PC's gathered block: the rows each rank owns (contiguous, rank
+    // order; empty when not) -- the classical AMG builds hypre's np = G hierarchy
+    std::vector<int64_t> rank_rows;
     Ctx();
     ~Ctx();
     void sync() { HIPCHK(hipStreamSynchronize(st)); }
@@ -310,8 +313,12 @@ struct PCILU : PC {
     // launch_sgs_factor), so apply() is one hybrid symmetric GS sweep from 0 with
     // the blocks as hypre's thread chunks (boomeramg.cpp)
     bool sgs = false;
+    // explicit block starts (bounds: nblocks + 1 entries from 0 to n) instead of PETSc's bjacobi sizes
+    std::vector<int64_t> bstart_h;
+    DBuf<int64_t> bstart;
+    int64_t max_len = 0;  // longest block
     PCILU(const DevCSR &M, int64_t nblocks, Ctx &c, bool exact_lu = false, bool allow_lds = true, int force_lpr = 0,
-          int gmem_mode = 0, int ring_mode = 1, bool sgs_factors = false);
+          int gmem_mode = 0, int ring_mode = 1, bool sgs_factors = false, const std::vector<int64_t> *bounds = nullptr);
     bool reentrant() const override { return profile_tag.empty(); }
     void apply(const double *x, double *y, Ctx &c) override;
 };

@@ -55,6 +55,9 @@ INEXACT_PARAMS = {"inner ksp type": "cg", "inner pc type": "hypre", "solver maxi
 # hybrid Gauss-Seidel partitions (oracle/boomeramg.py "K chunks")
 K1 = {"pls.hypre_relax_chunks": "1"}
 K256 = {"pls.hypre_relax_chunks": "256", "pls.hypre_relax_min_rows": "0"}
+# BoomerAMG as under mpirun -np 3 (per-rank HMIS first pass, 4 smoother chunks per
+# rank: explicit, non-uniform chunk bounds on the device)
+RANKS3 = {"pls.hypre_ranks": "3", "pls.hypre_relax_chunks": "12", "pls.hypre_relax_min_rows": "0"}
 
 
 def _amg_db(t, extra=None):
@@ -76,7 +79,8 @@ def _boomer_db(no_cf=True):
 @pytest.mark.parametrize("spec", [S.SynthSpec(2, 16), S.SynthSpec(3, 5)], ids=["2d16", "3d5"])
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
 @pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-inexact", "hypre-inexact-cf", "hypre-inexact-dense", "hypre-sa",
-                               "hypre-inexact-k1", "hypre-inexact-k256", "hypre-inexact-cf-k256"])
+                               "hypre-inexact-k1", "hypre-inexact-k256", "hypre-inexact-cf-k256",
+                               "hypre-inexact-ranks3", "hypre-inexact-cf-ranks3"])
 def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
     """hypre: PETSc's defaults (HMIS / ext+i, no truncation, no aggressive
     level, C/F-ordered Gauss-Seidel); -inexact: petsc-options-inexact's
@@ -84,12 +88,14 @@ def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
     sweep through its dense chunk inverses (pls.amg_gs_dense 1, the path of
     mostly sequential coarse levels); -sa: pls.hypre sa; -k1 / -k256:
     the hybrid Gauss-Seidel with one chunk (plain symmetric GS) / 256 chunks on
-    every level (no row floor)."""
+    every level (no row floor); -ranks3: hypre under mpirun -np 3."""
     params = dict(BASE, **{"pc type": pc_type, "inner pc type": "lu"})
     extra = {"hypre-inexact": _boomer_db(), "hypre-inexact-cf": _boomer_db(False), "hypre-sa": {"pls.hypre": "sa"},
              "hypre-inexact-dense": dict(_boomer_db(), **{"pls.amg_gs_dense": "1"}),
              "hypre-inexact-k1": dict(_boomer_db(), **K1), "hypre-inexact-k256": dict(_boomer_db(), **K256),
-             "hypre-inexact-cf-k256": dict(_boomer_db(False), **K256)}
+             "hypre-inexact-cf-k256": dict(_boomer_db(False), **K256),
+             "hypre-inexact-ranks3": dict(_boomer_db(), **RANKS3),
+             "hypre-inexact-cf-ranks3": dict(_boomer_db(False), **RANKS3)}
     db = _amg_db(t.split("-")[0], extra.get(t))
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)

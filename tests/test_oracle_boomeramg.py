@@ -260,3 +260,33 @@ def test_partitioned_first_pass_is_per_partition():
         Sl = [row[(row >= a) & (row < b)] - a for row in S[a:b]]
         assert np.array_equal(cf[a:b], rs_first_pass(Sl, b - a))
     assert not np.array_equal(cf, rs_first_pass(S, n))  # the partition boundary changes the splitting
+
+
+@pytest.mark.parametrize("ranks", ["3", "2"])
+def test_libpls_host_setup_bitwise_ranks(ranks):
+    """hypre under mpirun -np G (pls.hypre_ranks): libpls's host setup equals
+    the spec bit for bit with the per-rank HMIS first pass and inherited
+    coarse ranks."""
+    from lib.handle import boomeramg_host_level
+    db = dict(INEXACT, **{"pls.hypre_ranks": ranks})
+    for name, A in _blocks():
+        A = A.tocsr()
+        A.sort_indices()
+        pc = PCBoomerAMG(A, db, "x_")
+        for l, L in enumerate(pc.levels):
+            nl, n, nc, cf, P = boomeramg_host_level(A, db, "x_", l)
+            assert np.array_equal(cf, L["cf"].astype(np.int8)), (name, l)
+            assert np.array_equal(P.data, L["P"].data), (name, l)
+        assert not pc.levels or pc.levels[0]["parts"] is not None
+
+
+def test_rank_partition_is_inherited():
+    """Level 0 split as PETSc splits rows over 3 ranks; a coarse level's ranks own
+    their C points; V-cycle PCG still converges."""
+    A = lap2(24)
+    three = PCBoomerAMG(A, dict(INEXACT, **{"pls.hypre_ranks": "3"}), "x_")
+    assert three.levels[0]["parts"] == [192, 192, 192]
+    for L, Ln in zip(three.levels, three.levels[1:]):
+        assert sum(Ln["parts"]) == Ln["A"].shape[0] == int((L["cf"] == C).sum())
+    b = np.random.default_rng(0).standard_normal(A.shape[0])
+    assert pcg(A, b, three.apply) <= 14
