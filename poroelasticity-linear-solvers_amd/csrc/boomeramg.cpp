@@ -147,11 +147,75 @@ struct Tournament {
     }
 };
 
+// The same argmax (lambda, -i) by lambda buckets (round 3): per bucket a
+// three-level bitmap over the points, the smallest index its first set bit --
+// a lambda change is O(1) word updates and a selection a few word scans,
+// where the tournament compares O(log n) siblings (random reads of lambda).
+// lambda <= 2 max |S^T_i| (it starts at |S^T_i| and grows once per point of
+// S^T_i that becomes F).
+struct LamBuckets {
+    int64_t w0 = 0, w1 = 0, w2 = 0, top = -1;
+    std::vector<std::vector<uint64_t>> b0, b1, b2;
+    std::vector<int64_t> cnt;
+    LamBuckets(int64_t n, int64_t maxlam) {
+        w0 = (n + 63) / 64;
+        w1 = (w0 + 63) / 64;
+        w2 = (w1 + 63) / 64;
+        b0.resize(maxlam + 1);
+        b1.resize(maxlam + 1);
+        b2.resize(maxlam + 1);
+        cnt.assign(maxlam + 1, 0);
+    }
+    void insert(int64_t b, int64_t i) {
+        if (b0[b].empty()) {
+            b0[b].assign(w0, 0);
+            b1[b].assign(w1, 0);
+            b2[b].assign(w2, 0);
+        }
+        uint64_t &x0 = b0[b][i >> 6];
+        if (!x0) {
+            uint64_t &x1 = b1[b][i >> 12];
+            if (!x1) b2[b][i >> 18] |= 1ull << ((i >> 12) & 63);
+            x1 |= 1ull << ((i >> 6) & 63);
+        }
+        x0 |= 1ull << (i & 63);
+        ++cnt[b];
+        if (b > top) top = b;
+    }
+    void erase(int64_t b, int64_t i) {
+        uint64_t &x0 = b0[b][i >> 6];
+        x0 &= ~(1ull << (i & 63));
+        if (!x0) {
+            uint64_t &x1 = b1[b][i >> 12];
+            x1 &= ~(1ull << ((i >> 6) & 63));
+            if (!x1) b2[b][i >> 18] &= ~(1ull << ((i >> 12) & 63));
+        }
+        --cnt[b];
+    }
+    int64_t best() {  // the largest lambda's smallest point, -1: none left
+        while (top >= 0 && cnt[top] == 0) --top;
+        if (top < 0) return -1;
+        const std::vector<uint64_t> &B2 = b2[top];
+        int64_t k2 = 0;
+        while (!B2[k2]) ++k2;
+        const int64_t k1 = (k2 << 6) | __builtin_ctzll(B2[k2]);
+        const int64_t k0 = (k1 << 6) | __builtin_ctzll(b1[top][k1]);
+        return (k0 << 6) | __builtin_ctzll(b0[top][k0]);
+    }
+};
+
 std::vector<int8_t> rs_first_pass(const Pattern &S) {
     const int64_t n = S.n;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = now();
     const Pattern ST = transpose(S);
+    const double t1 = now();
     std::vector<int64_t> lam(n);
-    for (int64_t i = 0; i < n; ++i) lam[i] = ST.len(i);
+    int64_t maxst = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        lam[i] = ST.len(i);
+        maxst = std::max(maxst, lam[i]);
+    }
     std::vector<int8_t> st(n, UND);
     for (int64_t i = 0; i < n; ++i)
         if (S.len(i) == 0 && lam[i] == 0) st[i] = FPT;
@@ -163,33 +227,65 @@ std::vector<int8_t> rs_first_pass(const Pattern &S) {
         for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q)
             if (st[S.ci[q]] == UND) ++lam[S.ci[q]];
     }
-    Tournament T(n, lam, st);
-    auto make_f = [&](int64_t j) {
-        st[j] = FPT;
-        T.update(j);
-        for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q) {
-            const int32_t k = S.ci[q];
-            if (st[k] == UND) {
-                ++lam[k];
-                T.update(k);
+    if (std::getenv("PLS_RS_TOURNAMENT")) {  // (the round-2 selection structure; same result)
+        Tournament T(n, lam, st);
+        auto make_f = [&](int64_t j) {
+            st[j] = FPT;
+            T.update(j);
+            for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q) {
+                const int32_t k = S.ci[q];
+                if (st[k] == UND) {
+                    ++lam[k];
+                    T.update(k);
+                }
+            }
+        };
+        while (T.node[1] >= 0) {
+            const int64_t i = T.node[1];
+            st[i] = CPT;
+            T.update(i);
+            for (int64_t q = ST.rp[i]; q < ST.rp[i + 1]; ++q)
+                if (st[ST.ci[q]] == UND) make_f(ST.ci[q]);
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+                const int32_t k = S.ci[q];
+                if (st[k] != UND) continue;
+                if (--lam[k] == 0) make_f(k);
+                else T.update(k);
             }
         }
-    };
-    while (T.node[1] >= 0) {
-        const int64_t i = T.node[1];
-        st[i] = CPT;
-        T.update(i);
-        for (int64_t q = ST.rp[i]; q < ST.rp[i + 1]; ++q)
-            if (st[ST.ci[q]] == UND) make_f(ST.ci[q]);
-        for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
-            const int32_t k = S.ci[q];
-            if (st[k] != UND) continue;
-            if (--lam[k] == 0) make_f(k);
-            else T.update(k);
+    } else {
+        LamBuckets B(n, 2 * maxst + 1);
+        for (int64_t i = 0; i < n; ++i)
+            if (st[i] == UND) B.insert(lam[i], i);
+        auto make_f = [&](int64_t j) {  // j undecided, in bucket lam[j]
+            st[j] = FPT;
+            B.erase(lam[j], j);
+            for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q) {
+                const int32_t k = S.ci[q];
+                if (st[k] == UND) {
+                    B.erase(lam[k], k);
+                    B.insert(++lam[k], k);
+                }
+            }
+        };
+        for (int64_t i; (i = B.best()) >= 0;) {
+            st[i] = CPT;
+            B.erase(lam[i], i);
+            for (int64_t q = ST.rp[i]; q < ST.rp[i + 1]; ++q)
+                if (st[ST.ci[q]] == UND) make_f(ST.ci[q]);
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
+                const int32_t k = S.ci[q];
+                if (st[k] != UND) continue;
+                B.erase(lam[k], k);
+                B.insert(--lam[k], k);
+                if (lam[k] == 0) make_f(k);
+            }
         }
     }
     for (auto &s : st)
         if (s == UND) s = FPT;
+    if (std::getenv("PLS_AMG_TRACE") && n > 100000)
+        fprintf(stderr, "[rs_first_pass] n %lld: transpose %.2f s, pass %.2f s\n", (long long)n, t1 - t0, now() - t1);
     return st;
 }
 
@@ -873,18 +969,26 @@ struct BLevel {
     DevCSR P, R;
     int64_t n = 0, nc = 0;
     std::vector<std::unique_ptr<RelaxSet>> sets;  // no_CF: {all}; else {C, F}
+    // sharded (PCBoomer::dist): n / nc are this rank's rows; gn the level's global
+    // rows, set_global the sets' sizes over all ranks
+    int64_t gn = 0;
+    std::vector<int64_t> set_global;
 };
 
 struct BWork {
     std::vector<DBuf<double>> r, t, x, b, xs, rs, ts;
     DBuf<double> cx, cb;
+    DBuf<double> csend, cgath, cbg, cxg;  // sharded: the coarsest level's gather
 };
 
 struct PCBoomer : PC {
     std::vector<std::unique_ptr<BLevel>> lv;
     int K = 1;
     bool no_cf = false;
-    int64_t nco = 0;
+    bool dist = false;             // this rank's rows of hypre's np = G hierarchy (sharded block)
+    int64_t nco = 0;               // coarsest level rows (all ranks)
+    int64_t nco_mine = 0, coarse_a = 0, maxc = 1;  // sharded: my coarsest rows [coarse_a, + nco_mine)
+    DBuf<int64_t> coarse_src;      // global coarse row -> slot in the padded allgather
     DevCSR Cinv;
     std::unique_ptr<PC> Clu;
     std::unique_ptr<DevCSR> Cmat;
@@ -912,26 +1016,25 @@ struct PCBoomer : PC {
                     w->ts[l].alloc(m);
                 }
             }
-            w->cx.alloc(std::max<int64_t>(nco, 1));
-            w->cb.alloc(std::max<int64_t>(nco, 1));
+            w->cx.alloc(std::max<int64_t>(nco_mine, 1));
+            w->cb.alloc(std::max<int64_t>(nco_mine, 1));
+            if (dist) {
+                w->csend.alloc(maxc);
+                HIPCHK(hipMemsetAsync(w->csend.p, 0, sizeof(double) * maxc, c.st));
+                w->cgath.alloc(maxc * c.comm->size);
+                w->cbg.alloc(std::max<int64_t>(nco, 1));
+                w->cxg.alloc(std::max<int64_t>(nco, 1));
+            }
         }
         return *w;
     }
 
-    PCBoomer(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c) {
-        type = "hypre";
-        n = M.nrows;
-        BParams prm = parse_params(o, prefix);
-        int64_t rsum = 0;
-        for (int64_t v : c.rank_rows) rsum += v;
-        if (prm.ranks.empty() && c.rank_rows.size() > 1 && rsum == M.nrows) {  // gathered from G ranks (PCRedundant)
-            for (size_t q = 0; q < c.rank_rows.size(); ++q)
-                prm.ranks += (q ? "," : "") + std::to_string(c.rank_rows[q]);
-        }
-        K = prm.K;
-        no_cf = prm.no_cf;
-        if (!M.sell) build_sell(const_cast<DevCSR &>(M), c);
-        const bool view = o.flag("pls.amg_view", false);
+    // the smoother of one level: hybrid symmetric Gauss-Seidel sets (no_CF: all
+    // rows; else C then F) over the chunks cst of Al's rows (bounds: explicit
+    // chunk starts on the device); Adev: the level's device matrix (PCILU
+    // extracts each chunk's block from it; a sharded one drops its ghost columns)
+    void build_sets(BLevel &L, const HostCSR &Al, const std::vector<int8_t> &cf, const std::vector<int64_t> &cst,
+                    bool bounds, const DevCSR &Adev, const Options &o, const std::string &prefix, Ctx &c) {
         const bool allow_lds = o.flag("pls.ilu_lds", true);
         const int gmem = (int)o.integer("pls.ilu_gmem", 0), ring = (int)o.integer("pls.ilu_ring", 1);
         // Gauss-Seidel chunks through dense inverses: -1 by the cost model below, 1 whenever
@@ -942,104 +1045,202 @@ struct PCBoomer : PC {
         const int64_t wide_rows = o.integer("pls.amg_wide_rows", 256);  // rows per level above which: grid-wide sweeps
         const int wide_mode = (int)o.integer("pls.amg_wide_mode", -2);  // -2: CSR level kernels, -1: SELL level slices
         const int64_t dense_max = o.integer("pls.lu_dense_max", 32768);
+        std::vector<std::vector<int32_t>> groups;
+        if (no_cf) {
+            groups.emplace_back();
+        } else {
+            groups.resize(2);
+            for (int64_t i = 0; i < Al.nrows; ++i) groups[cf[i] == CPT ? 0 : 1].push_back((int32_t)i);
+        }
+        const int64_t Kl = (int64_t)cst.size() - 1;
+        for (auto &g : groups) {
+            auto rs = std::make_unique<RelaxSet>();
+            rs->all = no_cf;
+            rs->chunks = Kl;
+            rs->m = no_cf ? Al.nrows : (int64_t)g.size();
+            if (rs->m > 0) {
+                if (!no_cf) {
+                    std::vector<int64_t> gi(g.begin(), g.end());
+                    rs->idx.alloc(gi.size());
+                    HIPCHK(hipMemcpyAsync(rs->idx.p, gi.data(), sizeof(int64_t) * gi.size(), hipMemcpyHostToDevice, c.st));
+                }
+                const HostCSR lo = chunk_part(Al, g, cst, 1), up = chunk_part(Al, g, cst, 2);
+                // the set's chunk boundaries in its own numbering (chunks without set points dropped)
+                std::vector<int64_t> cp{0};
+                {
+                    std::vector<int32_t> cid(Al.nrows);
+                    for (size_t k = 0; k + 1 < cst.size(); ++k)
+                        for (int64_t i = cst[k]; i < cst[k + 1]; ++i) cid[i] = (int32_t)k;
+                    for (int64_t t = 1; t < rs->m; ++t)
+                        if (cid[no_cf ? t : g[t]] != cid[no_cf ? t - 1 : g[t - 1]]) cp.push_back(t);
+                    cp.push_back(rs->m);
+                }
+                // a sweep's critical path (levels of both triangles, one chunk per
+                // workgroup) against the bytes of the dense chunk inverses: mostly
+                // sequential chunks (every row a level of its own) go dense
+                const int64_t nlev = tri_levels(lo, false), nlev_u = tri_levels(up, true);
+                const int64_t ldc = PCSGSDense::ld_for(cp);
+                const double dense_bytes = (double)((int64_t)cp.size() - 1) * ldc * ldc * 8.0;
+                const double t_dense = (double)rs->m * ldc * 8.0 / 5e12 + 5e-6;
+                const double t_sweep = (double)(nlev + nlev_u) * level_us * 1e-6;
+                const bool dense = gs_dense != 0 && ldc <= dense_max && dense_bytes <= dense_gb * 1e9 &&
+                                   (gs_dense == 1 || t_dense < t_sweep);
+                if (dense) {
+                    rs->sgs = std::make_unique<PCSGSDense>(lo, up, cp, c);
+                } else {
+                    // wide levels: one grid-wide launch per level beats one workgroup
+                    const int gm = (nlev > 0 && lo.nrows / nlev > wide_rows) ? wide_mode : gmem;
+                    if (no_cf) {
+                        // the chunks are PCILU's blocks (the same partition): one workgroup per chunk
+                        auto pc = std::make_unique<PCILU>(Adev, Kl, c, false, allow_lds, 0, gm, ring, true,
+                                                          bounds ? &cst : nullptr);
+                        if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+                        if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
+                        if (o.flag("pls.sweep_profile", false))
+                            pc->profile_tag = prefix + "sgs L" + std::to_string(lv.size());
+                        rs->sgs = std::move(pc);
+                    } else {
+                        upload(chunk_part(Al, g, cst, 0), rs->sub, c);
+                        rs->sgs = std::make_unique<PCILU>(rs->sub, 1, c, false, allow_lds, 0, gm, ring, true);
+                    }
+                }
+            }
+            L.sets.push_back(std::move(rs));
+        }
+    }
+
+    // rows [a, a + m) of T (columns unchanged)
+    static HostCSR row_range(const HostCSR &T, int64_t a, int64_t m) {
+        HostCSR B;
+        B.nrows = m;
+        B.ncols = T.ncols;
+        B.rp.assign(1, 0);
+        for (int64_t i = a; i < a + m; ++i) {
+            B.ci.insert(B.ci.end(), T.ci.begin() + T.rp[i], T.ci.begin() + T.rp[i + 1]);
+            B.v.insert(B.v.end(), T.v.begin() + T.rp[i], T.v.begin() + T.rp[i + 1]);
+            B.rp.push_back((int64_t)B.ci.size());
+        }
+        return B;
+    }
+    // rows and columns [a, a + m) of T, shifted to 0 (a rank's diagonal block)
+    static HostCSR diag_block(const HostCSR &T, int64_t a, int64_t m) {
+        HostCSR B;
+        B.nrows = B.ncols = m;
+        B.rp.assign(1, 0);
+        for (int64_t i = a; i < a + m; ++i) {
+            for (int64_t k = T.rp[i]; k < T.rp[i + 1]; ++k)
+                if (T.ci[k] >= a && T.ci[k] < a + m) {
+                    B.ci.push_back(T.ci[k] - (int32_t)a);
+                    B.v.push_back(T.v[k]);
+                }
+            B.rp.push_back((int64_t)B.ci.size());
+        }
+        return B;
+    }
+
+    // M: the block (one rank), or this rank's rows of a sharded block (M.halo)
+    // with `global` the gathered block and rank_rows the ranks' contiguous row
+    // counts: hypre under mpirun -np G -- the hierarchy of the G-rank setup
+    // (identical on every rank), each rank holding and smoothing only its rows of
+    // every level (A_l, P_l with halos; R_l = its coarse rows of P_l^T), Jacobi
+    // across ranks through the halo values of the residual, the coarsest level
+    // gathered and solved redundantly.
+    PCBoomer(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c, const HostCSR *global = nullptr,
+             const std::vector<int64_t> *rank_rows = nullptr) {
+        type = "hypre";
+        n = M.nrows;
+        dist = global != nullptr;
+        BParams prm = parse_params(o, prefix);
+        const std::vector<int64_t> &rr = rank_rows ? *rank_rows : c.rank_rows;
+        int64_t rsum = 0;
+        for (int64_t v : rr) rsum += v;
+        const int64_t nglob = dist ? global->nrows : M.nrows;
+        if (prm.ranks.empty() && rr.size() > 1 && rsum == nglob) {  // the G ranks' partition (hypre's np = G setup)
+            for (size_t q = 0; q < rr.size(); ++q) prm.ranks += (q ? "," : "") + std::to_string(rr[q]);
+        }
+        if (dist && (!c.comm || (int64_t)rr.size() != c.comm->size || rsum != nglob || rr[c.comm->rank] != M.nrows))
+            throw Error("boomeramg (prefix " + prefix + "): the sharded block's ranks must own contiguous rows");
+        K = prm.K;
+        no_cf = prm.no_cf;
+        if (!M.sell) build_sell(const_cast<DevCSR &>(M), c);
+        const bool view = o.flag("pls.amg_view", false);
         double tm[7] = {0};
         auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
         double t0 = now();
         std::unique_ptr<DevCSR> cur;
-        HostCSR A = host_setup(download(M, c), prm, [&](const HostCSR &Al, const std::vector<int8_t> &cf, const HostCSR &P,
-                                                        const HostCSR &R, int64_t nc, const std::vector<int64_t> &parts) {
+        const int me = dist ? c.comm->rank : 0;
+        std::vector<int64_t> cps_last;  // dist: the coarsest level's rank starts
+        HostCSR A = host_setup(dist ? *global : download(M, c), prm,
+                               [&](const HostCSR &Al, const std::vector<int8_t> &cf, const HostCSR &P, const HostCSR &R,
+                                   int64_t nc, const std::vector<int64_t> &parts) {
             const double t1 = now();
             auto L = std::make_unique<BLevel>();
-            L->n = Al.nrows;
-            L->nc = nc;
-            if (lv.empty()) {
-                L->A = &M;
-            } else {  // the level's Galerkin operator
-                L->Aown = std::make_unique<DevCSR>();
-                upload(Al, *L->Aown, c);
-                amg_layout(*L->Aown, c);
-                L->A = L->Aown.get();
-            }
-            upload(P, L->P, c);
-            upload(R, L->R, c);
-            amg_layout(L->P, c);
-            amg_layout(L->R, c);
-            std::vector<std::vector<int32_t>> groups;
-            if (no_cf) {
-                groups.emplace_back();
+            if (!dist) {
+                L->n = Al.nrows;
+                L->nc = nc;
+                if (lv.empty()) {
+                    L->A = &M;
+                } else {  // the level's Galerkin operator
+                    L->Aown = std::make_unique<DevCSR>();
+                    upload(Al, *L->Aown, c);
+                    amg_layout(*L->Aown, c);
+                    L->A = L->Aown.get();
+                }
+                upload(P, L->P, c);
+                upload(R, L->R, c);
+                amg_layout(L->P, c);
+                amg_layout(L->R, c);
+                std::vector<int64_t> cst;
+                if (parts.empty()) {
+                    cst = chunk_starts(Al.nrows, level_chunks(Al.nrows, prm.chunks, prm.chunk_rows));
+                } else {
+                    // each rank's rows cut into its threads' chunks (pls.hypre_relax_chunks / ranks threads per rank)
+                    cst.assign(1, 0);
+                    const int64_t T = std::max<int64_t>(1, prm.chunks / (int64_t)parts.size());
+                    for (int64_t sz : parts) {
+                        if (sz == 0) continue;
+                        const std::vector<int64_t> loc = chunk_starts(sz, level_chunks(sz, T, prm.chunk_rows));
+                        const int64_t base = cst.back();
+                        for (size_t k = 1; k < loc.size(); ++k) cst.push_back(base + loc[k]);
+                    }
+                }
+                build_sets(*L, Al, cf, cst, !parts.empty(), *L->A, o, prefix, c);
             } else {
-                groups.resize(2);
-                for (int64_t i = 0; i < Al.nrows; ++i) groups[cf[i] == CPT ? 0 : 1].push_back((int32_t)i);
-            }
-            // smoother chunks: K_l uniform chunks, or with ranks each rank's rows cut into its
-            // threads' chunks (pls.hypre_relax_chunks / ranks threads per rank)
-            std::vector<int64_t> cst;
-            if (parts.empty()) {
-                cst = chunk_starts(Al.nrows, level_chunks(Al.nrows, prm.chunks, prm.chunk_rows));
-            } else {
-                cst.assign(1, 0);
+                // this rank's rows of the level (parts: the level's rank sizes) and of its coarse level
+                const std::vector<int64_t> pst = part_starts(parts);
+                std::vector<int64_t> cnt(parts.size(), 0);
+                for (size_t q = 0; q < parts.size(); ++q)
+                    for (int64_t i = pst[q]; i < pst[q + 1]; ++i) cnt[q] += cf[i] == CPT;
+                const std::vector<int64_t> cps = part_starts(cnt);
+                const int64_t a = pst[me], m = pst[me + 1] - a, ca = cps[me], mc = cps[me + 1] - ca;
+                L->n = m;
+                L->nc = mc;
+                L->gn = Al.nrows;
+                if (lv.empty()) {
+                    L->A = &M;
+                } else {
+                    L->Aown = std::make_unique<DevCSR>();
+                    upload_dist(row_range(Al, a, m), pst, *L->Aown, c);
+                    L->A = L->Aown.get();
+                }
+                upload_dist(row_range(P, a, m), cps, L->P, c);
+                upload_dist(row_range(R, ca, mc), pst, L->R, c);
+                // the C / F set sizes over all ranks (a set is visited when any rank has points in it)
+                int64_t nC = 0;
+                for (int8_t v : cf) nC += v == CPT;
+                L->set_global = no_cf ? std::vector<int64_t>{Al.nrows} : std::vector<int64_t>{nC, Al.nrows - nC};
                 const int64_t T = std::max<int64_t>(1, prm.chunks / (int64_t)parts.size());
-                for (int64_t sz : parts) {
-                    if (sz == 0) continue;
-                    const std::vector<int64_t> loc = chunk_starts(sz, level_chunks(sz, T, prm.chunk_rows));
-                    const int64_t base = cst.back();
-                    for (size_t k = 1; k < loc.size(); ++k) cst.push_back(base + loc[k]);
-                }
-            }
-            const int64_t Kl = (int64_t)cst.size() - 1;
-            for (auto &g : groups) {
-                auto rs = std::make_unique<RelaxSet>();
-                rs->all = no_cf;
-                rs->chunks = Kl;
-                rs->m = no_cf ? Al.nrows : (int64_t)g.size();
-                if (rs->m > 0) {
-                    if (!no_cf) {
-                        std::vector<int64_t> gi(g.begin(), g.end());
-                        rs->idx.alloc(gi.size());
-                        HIPCHK(hipMemcpyAsync(rs->idx.p, gi.data(), sizeof(int64_t) * gi.size(), hipMemcpyHostToDevice, c.st));
-                    }
-                    const HostCSR lo = chunk_part(Al, g, cst, 1), up = chunk_part(Al, g, cst, 2);
-                    // the set's chunk boundaries in its own numbering (chunks without set points dropped)
-                    std::vector<int64_t> cp{0};
-                    {
-                        std::vector<int32_t> cid(Al.nrows);
-                        for (size_t k = 0; k + 1 < cst.size(); ++k)
-                            for (int64_t i = cst[k]; i < cst[k + 1]; ++i) cid[i] = (int32_t)k;
-                        for (int64_t t = 1; t < rs->m; ++t)
-                            if (cid[no_cf ? t : g[t]] != cid[no_cf ? t - 1 : g[t - 1]]) cp.push_back(t);
-                        cp.push_back(rs->m);
-                    }
-                    // a sweep's critical path (levels of both triangles, one chunk per
-                    // workgroup) against the bytes of the dense chunk inverses: mostly
-                    // sequential chunks (every row a level of its own) go dense
-                    const int64_t nlev = tri_levels(lo, false), nlev_u = tri_levels(up, true);
-                    const int64_t ldc = PCSGSDense::ld_for(cp);
-                    const double dense_bytes = (double)((int64_t)cp.size() - 1) * ldc * ldc * 8.0;
-                    const double t_dense = (double)rs->m * ldc * 8.0 / 5e12 + 5e-6;
-                    const double t_sweep = (double)(nlev + nlev_u) * level_us * 1e-6;
-                    const bool dense = gs_dense != 0 && ldc <= dense_max && dense_bytes <= dense_gb * 1e9 &&
-                                       (gs_dense == 1 || t_dense < t_sweep);
-                    if (dense) {
-                        rs->sgs = std::make_unique<PCSGSDense>(lo, up, cp, c);
-                    } else {
-                        // wide levels: one grid-wide launch per level beats one workgroup
-                        const int gm = (nlev > 0 && lo.nrows / nlev > wide_rows) ? wide_mode : gmem;
-                        if (no_cf) {
-                            // the chunks are PCILU's blocks (the same partition): one workgroup per chunk
-                            auto pc = std::make_unique<PCILU>(*L->A, Kl, c, false, allow_lds, 0, gm, ring, true,
-                                                              parts.empty() ? nullptr : &cst);
-                            if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
-            if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
-                            if (o.flag("pls.sweep_profile", false))
-                                pc->profile_tag = prefix + "sgs L" + std::to_string(lv.size());
-                            rs->sgs = std::move(pc);
-                        } else {
-                            upload(chunk_part(Al, g, cst, 0), rs->sub, c);
-                            rs->sgs = std::make_unique<PCILU>(rs->sub, 1, c, false, allow_lds, 0, gm, ring, true);
-                        }
+                const std::vector<int64_t> cst = chunk_starts(m, m > 0 ? level_chunks(m, T, prm.chunk_rows) : 1);
+                const std::vector<int8_t> cfm(cf.begin() + a, cf.begin() + a + m);
+                if (m > 0) {
+                    build_sets(*L, diag_block(Al, a, m), cfm, cst, true, *L->A, o, prefix, c);
+                } else {
+                    for (size_t g = 0; g < L->set_global.size(); ++g) {
+                        L->sets.push_back(std::make_unique<RelaxSet>());
+                        L->sets.back()->all = no_cf;
                     }
                 }
-                L->sets.push_back(std::move(rs));
+                cps_last = cps;
             }
             lv.push_back(std::move(L));
             c.sync();
@@ -1053,6 +1254,21 @@ struct PCBoomer : PC {
         }
         t0 = now();
         nco = A.nrows;
+        nco_mine = nco;
+        if (dist) {
+            if (lv.empty()) throw Error("boomeramg (prefix " + prefix + "): a sharded block needs at least one level");
+            // the coarsest level is solved redundantly: gather b_c (padded allgather), keep my rows of x_c
+            const int G = c.comm->size;
+            nco_mine = cps_last[me + 1] - cps_last[me];
+            coarse_a = cps_last[me];
+            maxc = 1;
+            for (int q = 0; q < G; ++q) maxc = std::max(maxc, cps_last[q + 1] - cps_last[q]);
+            std::vector<int64_t> src(std::max<int64_t>(nco, 1), 0);
+            for (int q = 0; q < G; ++q)
+                for (int64_t i = cps_last[q]; i < cps_last[q + 1]; ++i) src[i] = q * maxc + (i - cps_last[q]);
+            coarse_src.alloc(src.size());
+            HIPCHK(hipMemcpyAsync(coarse_src.p, src.data(), sizeof(int64_t) * src.size(), hipMemcpyHostToDevice, c.st));
+        }
         work_for(c);
         if (nco > 0) {
             if (nco <= 1024) {
@@ -1071,15 +1287,15 @@ struct PCBoomer : PC {
         // the V-cycle's vectors are sized from these: check the chain before any launch
         for (size_t l = 0; l < lv.size(); ++l) {
             const BLevel &L = *lv[l];
-            const int64_t next = l + 1 < lv.size() ? lv[l + 1]->n : nco;
-            if (L.A->nrows != L.n || L.P.nrows != L.n || L.P.ncols != L.nc || L.R.nrows != L.nc || L.R.ncols != L.n ||
-                next != L.nc)
+            const int64_t next = l + 1 < lv.size() ? lv[l + 1]->n : nco_mine;
+            const bool cols_ok = dist ? true : (L.P.ncols == L.nc && L.R.ncols == L.n);
+            if (L.A->nrows != L.n || L.P.nrows != L.n || !cols_ok || L.R.nrows != L.nc || next != L.nc)
                 throw Error("boomeramg: inconsistent hierarchy at level " + std::to_string(l));
             for (const auto &s : L.sets)
                 if (s->m > 0 && (!s->sgs || s->sgs->n != s->m)) throw Error("boomeramg: smoother size mismatch");
         }
         if (view) {
-            fprintf(stderr, "[boomeramg %s] levels %zu:", prefix.c_str(), lv.size() + 1);
+            fprintf(stderr, "[boomeramg %s] levels %zu%s:", prefix.c_str(), lv.size() + 1, dist ? " (this rank's rows)" : "");
             for (auto &L : lv)
                 fprintf(stderr, " %lld(P nnz %lld, %lld GS chunks)", (long long)L->n, (long long)L->P.nnz,
                         (long long)(L->sets.empty() ? 0 : L->sets[0]->chunks));
@@ -1091,14 +1307,28 @@ struct PCBoomer : PC {
         }
     }
 
+    // y = alpha M x + beta z on a level matrix; a sharded one with no local rows
+    // still takes part in the halo exchange (the exchange is collective)
+    void lspmv(const DevCSR &Mx, const double *x, double *y, Ctx &c, double alpha = 1.0, double beta = 0.0,
+               const double *z = nullptr) {
+        if (Mx.halo && Mx.nrows == 0) {
+            Halo &H = *Mx.halo;
+            launch_pack(H.nsend, H.send_idx.p, x, H.sendbuf.p, c.st);
+            c.comm->exchange_dev(H.sendbuf.p, H.scnt, H.soff, H.ghost.p, H.rcnt, H.roff, c.st);
+            return;
+        }
+        spmv(Mx, x, y, c, alpha, beta, z);
+    }
+
     // one hybrid symmetric Gauss-Seidel sweep over set s (oracle _relax):
     // x_I += M^-1 (b - A x)_I  (x_zero: x == 0 on entry, so the residual is b)
     void sweep(BLevel &L, size_t l, RelaxSet &s, BWork &W, const double *b, double *x, bool x_zero, Ctx &c) {
         const double *r = b;
         if (!x_zero) {
-            spmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
+            lspmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
             r = W.r[l].p;
         }
+        if (s.m == 0) return;  // (sharded: no points of this set on this rank)
         if (s.all) {
             if (x_zero) {
                 s.sgs->apply(r, x, c);
@@ -1121,8 +1351,9 @@ struct PCBoomer : PC {
         if (x_zero && !no_cf) launch_set(L.n, 0.0, x, c.st);
         for (int k = 0; k < K; ++k)
             for (size_t g = 0; g < L.sets.size(); ++g) {
-                RelaxSet &s = *L.sets[down ? g : L.sets.size() - 1 - g];
-                if (s.m == 0) continue;
+                const size_t gi = down ? g : L.sets.size() - 1 - g;
+                RelaxSet &s = *L.sets[gi];
+                if ((dist ? L.set_global[gi] : s.m) == 0) continue;
                 sweep(L, l, s, W, b, x, x_zero, c);
                 x_zero = false;
             }
@@ -1133,10 +1364,20 @@ struct PCBoomer : PC {
         if (Clu) Clu->apply(b, x, c);
         else spmv(Cinv, b, x, c);
     }
+    // sharded: my rows of b_c -> the whole coarse b (allgather), solved redundantly, my rows of x_c kept
+    void coarse_solve_dist(const double *b, double *x, BWork &W, Ctx &c) {
+        if (nco == 0) return;
+        if (nco_mine) launch_copy(nco_mine, b, W.csend.p, c.st);
+        c.comm->allgather_dev(W.csend.p, (int)maxc, W.cgath.p, c.st);
+        launch_gather(nco, coarse_src.p, W.cgath.p, W.cbg.p, c.st);
+        coarse_solve(W.cbg.p, W.cxg.p, c);
+        if (nco_mine) launch_copy(nco_mine, W.cxg.p + coarse_a, x, c.st);
+    }
 
     void vcycle(size_t l, BWork &W, const double *b, double *x, Ctx &c) {
         if (l == lv.size()) {
-            coarse_solve(b, x, c);
+            if (dist) coarse_solve_dist(b, x, W, c);
+            else coarse_solve(b, x, c);
             return;
         }
         BLevel &L = *lv[l];
@@ -1144,15 +1385,15 @@ struct PCBoomer : PC {
         double *bc = last ? W.cb.p : W.b[l + 1].p;
         double *xc = last ? W.cx.p : W.x[l + 1].p;
         relax(l, W, b, x, true, true, c);
-        spmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
-        spmv(L.R, W.r[l].p, bc, c);
+        lspmv(*L.A, x, W.r[l].p, c, -1.0, 1.0, b);
+        lspmv(L.R, W.r[l].p, bc, c);
         vcycle(l + 1, W, bc, xc, c);
-        spmv(L.P, xc, x, c, 1.0, 1.0, x);
+        lspmv(L.P, xc, x, c, 1.0, 1.0, x);
         relax(l, W, b, x, false, false, c);
     }
 
     void apply(const double *x, double *y, Ctx &c) override {
-        if (n == 0) return;
+        if (n == 0 && !dist) return;
         if (lv.empty()) {
             coarse_solve(x, y, c);
             return;
@@ -1162,6 +1403,13 @@ struct PCBoomer : PC {
 };
 
 }  // namespace
+
+// hypre on a sharded block (BoomerAMG under mpirun -np G): the gathered block
+// sets up hypre's np = G hierarchy on every rank, each rank keeps its rows
+std::unique_ptr<PC> make_boomeramg_dist(const DevCSR &M, const HostCSR &global, const std::vector<int64_t> &rank_rows,
+                                        const Options &o, const std::string &prefix, Ctx &c) {
+    return std::make_unique<PCBoomer>(M, o, prefix, c, &global, &rank_rows);
+}
 
 std::unique_ptr<PC> make_boomeramg(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c) {
     if (M.halo) throw Error("PC type hypre (prefix " + prefix + "): a sharded block reaches the AMG through PCRedundant");

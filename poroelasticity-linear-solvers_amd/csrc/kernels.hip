@@ -2480,6 +2480,159 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                                                                      prof, rr, bstart);
 }
 
+// ======================================================= chain sweep ====
+// Blocks whose level DAG is deep and narrow -- FE rows in their natural
+// order, ~2-3 rows per level: the classical AMG's hybrid Gauss-Seidel chunks
+// (footing's solid block, the synthetic N=59 s block) -- spend their time in
+// the per-level hand-off, not in bytes: the workgroup sweep above pays a
+// barrier and a two-level-deep prefetch per level (~0.77 us per level on the
+// footing N=128 chunks).  Here ONE wave walks a block's slices in order
+// (a level's rows are independent, so a level cut into several slices is
+// still a valid order): no barrier (LDS accesses of one wave complete in
+// order), and the factor data of NW_D slices in flight, which the in-order
+// vmcnt covers with 7 loads per slice (<= 63 outstanding).
+//
+// Stream layout (per triangle, runtime.cpp build_chain_tri): a slice is 4 +
+// nl * L entries (nl active lanes = rows x lanes per row, L = 4 or 8 entries
+// per lane, lane-major): entries [0, 4) the descriptor -- col[0] = size | (L
+// == 8) of the slice NW_D positions later in the same block (0: none) -- then
+// lane l's header (col = local row | count << SW_ROW_BITS, val = 1 / U_ii for
+// the upper triangle) and its factor entries at 4 + l * L.  A row's entries
+// are dealt round robin over its LPR lanes and the partial sums combined by
+// the DPP tree of sw2_finish, exactly as in the LDS sweep: with the same
+// lanes per row the results are bitwise those of k_ilu_blocks_lds.
+static constexpr int NW_D = 8;  // slices in flight per wave
+struct NwSlot {
+    int32_t c[8];
+    double v[8];
+    int32_t desc;  // size | flag of the slice NW_D later
+    int nl;        // active lanes of this slice
+};
+
+__device__ __forceinline__ void nw_issue(const int32_t *col, const double *val, int64_t base, int32_t szf, int lane,
+                                         NwSlot &s) {
+    const int sz = szf & ~3;
+    const int L = (szf & 1) ? 8 : 4;
+    s.nl = sz > 4 ? (sz - 4) / L : 0;
+    // range-checked to the slice: lanes past nl and slices past the block's
+    // end (size 0) read zeros without traffic; every path issues the same
+    // 7 loads, so the compiler's vmcnt bookkeeping stays exact
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void *)(col + base), (short)0, sz * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void *)(val + base), (short)0, sz * 8, 0x00020000);
+    const int off = 4 + lane * L;
+    const auto d4 = __builtin_amdgcn_raw_buffer_load_b128(rc, 0, 0, 0);
+    s.desc = (int32_t)d4[0];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(rc, (off + 4 * q) * 4, 0, 0);
+        s.c[4 * q + 0] = (int32_t)c4[0];
+        s.c[4 * q + 1] = (int32_t)c4[1];
+        s.c[4 * q + 2] = (int32_t)c4[2];
+        s.c[4 * q + 3] = (int32_t)c4[3];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rv, (off + 2 * q) * 8, 0, 0);
+        s.v[2 * q + 0] = __builtin_bit_cast(double, ((uint64_t)v4[1] << 32) | v4[0]);
+        s.v[2 * q + 1] = __builtin_bit_cast(double, ((uint64_t)v4[3] << 32) | v4[2]);
+    }
+}
+
+template <int LPR>
+__device__ __forceinline__ void nw_compute(const NwSlot &s, double *ys, int lane, bool upper) {
+    const int32_t h = s.c[0];
+    const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
+    double acc = 0.0, d[8];
+    // every dependency read issued before the first is consumed
+#pragma unroll
+    for (int u = 1; u < 8; ++u) d[u] = ys[u <= len ? s.c[u] : 0];
+#pragma unroll
+    for (int u = 1; u < 8; ++u) {
+        const double t = __dmul_rn(s.v[u], d[u]);  // the LDS sweep's rounding (no contraction)
+        acc += (u <= len) ? t : 0.0;
+    }
+    constexpr int lg = LPR >= 16 ? 4 : LPR >= 8 ? 3 : LPR >= 4 ? 2 : LPR >= 2 ? 1 : 0;
+    if (lg >= 1) acc += dpp_d<0xB1>(acc);
+    if (lg >= 2) acc += dpp_d<0x4E>(acc);
+    if (lg >= 3) acc += dpp_d<0x141>(acc);
+    if (lg >= 4) acc += dpp_d<0x140>(acc);
+    const int32_t li = h & SW_ROW_PAD;
+    if ((lane & (LPR - 1)) == 0 && lane < s.nl && li != SW_ROW_PAD) ys[li] = upper ? (ys[li] - acc) * s.v[0] : ys[li] - acc;
+}
+
+template <int LPR>
+__device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *first, int64_t nsl, const int32_t *col,
+                                         const double *val, double *ys, int lane, bool upper) {
+    if (nsl <= 0) return;
+    NwSlot s[NW_D];
+    int64_t ib = base;  // where the next issued slice starts
+#pragma unroll
+    for (int k = 0; k < NW_D; ++k) {
+        const int32_t f = __builtin_amdgcn_readfirstlane(first[k]);
+        nw_issue(col, val, ib, f, lane, s[k]);
+        ib += f & ~3;
+    }
+    for (int64_t j = 0;;) {
+#pragma unroll
+        for (int k = 0; k < NW_D; ++k) {
+            nw_compute<LPR>(s[k], ys, lane, upper);
+            const int32_t f = __builtin_amdgcn_readfirstlane(s[k].desc);
+            nw_issue(col, val, ib, f, lane, s[k]);
+            ib += f & ~3;
+            if (++j >= nsl) return;
+        }
+    }
+}
+
+__device__ __forceinline__ void nw_dispatch(int lpr, int64_t base, const int32_t *first, int64_t nsl,
+                                            const int32_t *col, const double *val, double *ys, int lane, bool upper) {
+    switch (lpr) {
+        case 16: nw_sweep<16>(base, first, nsl, col, val, ys, lane, upper); break;
+        case 8: nw_sweep<8>(base, first, nsl, col, val, ys, lane, upper); break;
+        case 4: nw_sweep<4>(base, first, nsl, col, val, ys, lane, upper); break;
+        case 2: nw_sweep<2>(base, first, nsl, col, val, ys, lane, upper); break;
+        default: nw_sweep<1>(base, first, nsl, col, val, ys, lane, upper); break;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_ilu_blocks_chain(
+    int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart, const int64_t *__restrict__ Lbase,
+    const int32_t *__restrict__ Lfirst, const int64_t *__restrict__ Lnsl, const int32_t *__restrict__ Llpr,
+    const int32_t *__restrict__ Lcol, const double *__restrict__ Lval, const int64_t *__restrict__ Ubase,
+    const int32_t *__restrict__ Ufirst, const int64_t *__restrict__ Unsl, const int32_t *__restrict__ Ulpr,
+    const int32_t *__restrict__ Ucol, const double *__restrict__ Uval, const double *x, double *y) {
+    extern __shared__ __attribute__((aligned(16))) double ys[];
+    const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;  // heaviest (last) blocks first
+    int64_t b0, len;
+    block_range(blk, n, nblocks, bstart, b0, len);
+    const int lane = threadIdx.x;
+    for (int64_t t = lane; t < len; t += 64) ys[t] = x[b0 + t];
+    __syncthreads();
+    nw_dispatch(Llpr[blk], Lbase[blk], Lfirst + blk * NW_D, Lnsl[blk], Lcol, Lval, ys, lane, false);
+    nw_dispatch(Ulpr[blk], Ubase[blk], Ufirst + blk * NW_D, Unsl[blk], Ucol, Uval, ys, lane, true);
+    __syncthreads();
+    for (int64_t t = lane; t < len; t += 64) y[b0 + t] = ys[t];
+}
+
+int ilu_chain_depth() { return NW_D; }
+int ilu_chain_max_lpr() { return 16; }
+
+void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *Lbase,
+                             const int32_t *Lfirst, const int64_t *Lnsl, const int32_t *Llpr, const int32_t *Lcol,
+                             const double *Lval, const int64_t *Ubase, const int32_t *Ufirst, const int64_t *Unsl,
+                             const int32_t *Ulpr, const int32_t *Ucol, const double *Uval, const double *x, double *y,
+                             int64_t max_len, hipStream_t st) {
+    static bool configured = false;
+    if (!configured) {
+        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)163840);
+        configured = true;
+    }
+    const size_t bytes = (size_t)std::max<int64_t>(max_len, 1) * 8;
+    k_ilu_blocks_chain<<<(unsigned)nblocks, 64, bytes, st>>>(n, nblocks, bstart, Lbase, Lfirst, Lnsl, Llpr, Lcol, Lval,
+                                                             Ubase, Ufirst, Unsl, Ulpr, Ucol, Uval, x, y);
+}
+
 // =========================================================== distribution ====
 // flag[c] = 1 for every column c (relative to the column space) of the matrix
 // that this rank does not own (own[c] < 0)

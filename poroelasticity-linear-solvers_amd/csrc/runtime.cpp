@@ -1091,6 +1091,90 @@ static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order
     c.sync();
 }
 
+// Chain-sweep stream of one triangle (kernels.hip, "chain sweep"): per block
+// the fewest lanes per row (1..ilu_chain_max_lpr(), powers of two) that keep
+// every lane's share of the block's longest row within 7 entries -- the LDS
+// sweep's rule, so blocks whose rows fit 4 lanes get the LDS sweep's lanes and
+// sums -- then per level slices of 64 / lpr rows in the level's row order.
+// Returns the slice count, or -1 when a row does not fit (fv / dinv empty: a
+// dry run that only counts).
+static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
+                               const std::vector<int32_t> &ci, const std::vector<int64_t> &dg,
+                               const std::vector<double> &fv, const std::vector<double> &dinv,
+                               const std::vector<int32_t> &order, const std::vector<int64_t> &grp,
+                               const std::vector<int64_t> &goff, bool upper, ChainTri *D, Ctx &c) {
+    const int W = ilu_lds_lane_entries(), ND = ilu_chain_depth(), LMAX = ilu_chain_max_lpr();
+    auto rlen = [&](int64_t i) -> int64_t { return upper ? rp[i + 1] - dg[i] - 1 : dg[i] - rp[i]; };
+    const bool dry = D == nullptr;
+    std::vector<int64_t> base(nblk, 0), nsl(nblk, 0);
+    std::vector<int32_t> first((size_t)nblk * ND, 0), lpr(nblk, 1), col;
+    std::vector<double> val;
+    int64_t total = 0;
+    for (int64_t b = 0; b < nblk; ++b) {
+        const int64_t b0 = bst[b];
+        int64_t mx = 0;
+        for (int64_t r = grp[goff[b]]; r < grp[goff[b + 1]]; ++r) mx = std::max(mx, rlen(order[r]));
+        int l = 1;
+        while (l < LMAX && (mx + l - 1) / l > W) l *= 2;
+        if ((mx + l - 1) / l > W) return -1;
+        lpr[b] = l;
+        const int64_t per = 64 / l;
+        std::vector<int32_t> sizes;
+        base[b] = (int64_t)col.size();
+        for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {
+            for (int64_t r0 = grp[g]; r0 < grp[g + 1]; r0 += per) {
+                const int64_t r1 = std::min(grp[g + 1], r0 + per);
+                ++total;
+                if (dry) continue;
+                int64_t mm = 0;
+                for (int64_t r = r0; r < r1; ++r) mm = std::max(mm, (rlen(order[r]) + l - 1) / l);
+                const int L = mm + 1 <= 4 ? 4 : 8;
+                const int64_t nl = (r1 - r0) * l, sz = 4 + nl * L;
+                sizes.push_back((int32_t)(sz | (L == 8 ? 1 : 0)));
+                const int64_t at = (int64_t)col.size();
+                col.resize(at + sz, 0);
+                val.resize(at + sz, 0.0);
+                for (int64_t rr = 0; rr < r1 - r0; ++rr) {
+                    const int64_t i = order[r0 + rr];
+                    const int64_t src = upper ? dg[i] + 1 : rp[i], len = rlen(i);
+                    for (int sub = 0; sub < l; ++sub) {
+                        const int64_t mine = len > sub ? (len - sub + l - 1) / l : 0;
+                        const int64_t e = at + 4 + (rr * l + sub) * L;
+                        col[e] = (int32_t)(i - b0) | (int32_t)(mine << 18);
+                        val[e] = upper ? dinv[i] : 0.0;
+                        for (int64_t k = 1; k <= mine; ++k) {
+                            const int64_t j = (k - 1) * l + sub;
+                            col[e + k] = ci[src + j] - (int32_t)b0;
+                            val[e + k] = fv[src + j];
+                        }
+                    }
+                }
+            }
+        }
+        if (dry) continue;
+        nsl[b] = (int64_t)sizes.size();
+        int64_t at = base[b];
+        for (size_t k = 0; k < sizes.size(); ++k) {  // slice k's descriptor: the size of slice k + ND
+            col[at] = k + ND < sizes.size() ? sizes[k + ND] : 0;
+            at += sizes[k] & ~3;
+        }
+        for (int k = 0; k < ND && k < (int)sizes.size(); ++k) first[(size_t)b * ND + k] = sizes[k];
+    }
+    if (dry) return total;
+    auto up = [&](auto &d, const auto &v) {
+        d.alloc(std::max<size_t>(v.size(), 1));
+        if (!v.empty()) HIPCHK(hipMemcpyAsync(d.p, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, c.st));
+    };
+    up(D->base, base);
+    up(D->nsl, nsl);
+    up(D->first, first);
+    up(D->lpr, lpr);
+    up(D->col, col);
+    up(D->val, val);
+    c.sync();
+    return total;
+}
+
 PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr, int gmem_mode,
              int ring_mode, bool sgs_factors, const std::vector<int64_t> *bounds) {
     exact = exact_lu;
@@ -1189,7 +1273,27 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                 for (size_t k = 0; k + 1 < g->size(); ++k) wmax = std::max<int64_t>(wmax, (*g)[k + 1] - (*g)[k]);
             ring = wmax <= ilu_ring_chunk();
         }
-        if (use_lds) {
+        if (use_lds && !gmem && c.sweep_chain != 0 && force_lpr == 0) {
+            // the chain sweep (one wave per block, slices in order, 8 in flight) for
+            // deep, narrow level DAGs: measured ~0.77 us per level for the workgroup
+            // sweep on the footing smoother chunks; a chain slice costs a fraction of
+            // that, so chain when slices <= 3.5 x levels (both triangles)
+            const std::vector<int64_t> bst = block_starts(n, nblocks, bnd);
+            const std::vector<double> none;
+            const int64_t sL = build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oL, gL, fL, false, nullptr, c);
+            const int64_t sU = sL < 0 ? -1 : build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oU, gU, fU, true, nullptr, c);
+            const int64_t lev = (int64_t)gL.size() - 1 + (int64_t)gU.size() - 1;
+            chain = sL >= 0 && sU >= 0 && (c.sweep_chain == 1 || 2 * (sL + sU) <= 7 * lev);
+            if (chain) {
+                std::vector<double> fv(F.nnz), dv(n);
+                if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
+                if (n) HIPCHK(hipMemcpyAsync(dv.data(), dinv.p, sizeof(double) * n, hipMemcpyDeviceToHost, c.st));
+                c.sync();
+                build_chain_tri(nblocks, bst, rp, ci, dg, fv, dv, oL, gL, fL, false, &Lc, c);
+                build_chain_tri(nblocks, bst, rp, ci, dg, fv, dv, oU, gU, fU, true, &Uc, c);
+            }
+        }
+        if (use_lds && !chain) {
             const int max_lpr = gmem ? (ring ? 32 : 16) : 4;
             std::vector<int32_t> pL, pU, loL, loU, nlL, nlU;
             if (ring) {
@@ -1278,6 +1382,12 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
                                Ur.coff.p, Ur.cg.p, Ur.cp.p, Lr.ord.p, mapUL.p, Ur.ord.p, Lr.frp.p, Lr.fcol.p,
                                Lr.fval.p, Ur.frp.p, Ur.fcol.p, Ur.fval.p, x, y, sc.first.p, sc.second.p, c.st,
                                lds_tpb, bstart_h.empty() ? nullptr : bstart.p);
+        return;
+    }
+    if (use_lds && chain) {
+        launch_ilu_blocks_chain(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, Lc.base.p, Lc.first.p, Lc.nsl.p,
+                                Lc.lpr.p, Lc.col.p, Lc.val.p, Uc.base.p, Uc.first.p, Uc.nsl.p, Uc.lpr.p, Uc.col.p,
+                                Uc.val.p, x, y, max_len, c.st);
         return;
     }
     if (use_lds) {
@@ -1454,6 +1564,187 @@ std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
                                    (int)o.integer("pls.ilu_ring", 1));
 }
 
+// Gather a sharded diagonal block -- every rank's MPIAIJ rows with
+// block-global columns (Halo::l2g) -- into the global host CSR, in the block's
+// global order, on every rank (host allgather, setup only).  srcslot[g]: where
+// global row g sits in a padded allgather of the ranks' rows (q * maxloc + i);
+// rank_rows: the ranks' row counts when they own contiguous ranges in rank
+// order (every single-field block, every caller-assembled one), else empty.
+HostCSR gather_block(const DevCSR &M, Ctx &c, const std::string &prefix, std::vector<int64_t> &srcslot,
+                     int64_t &maxloc, std::vector<int64_t> &rank_rows) {
+    const int64_t nloc = M.nrows;
+    const Halo &H = *M.halo;
+    if ((int64_t)H.l2g.size() < M.ncols || H.nlocal != M.nrows)
+        throw Error("redundant PC (prefix " + prefix + "): block is not a diagonal block of the sharded system");
+    Comm &cm = *c.comm;
+    const int G = cm.size;
+    const HostCSR L = download(M, c);
+    std::vector<int64_t> cnt{nloc, (int64_t)L.ci.size()}, all(2 * G);
+    cm.allgather_host(cnt.data(), sizeof(int64_t) * 2, all.data());
+    int64_t maxnnz = 0, N = 0;
+    maxloc = 0;
+    for (int q = 0; q < G; ++q) {
+        maxloc = std::max(maxloc, all[2 * q]);
+        maxnnz = std::max(maxnnz, all[2 * q + 1]);
+        N += all[2 * q];
+    }
+    // message: rows (global ids), row lengths, columns (global), values -- padded to the largest rank's
+    const int64_t words = 2 * maxloc + 2 * maxnnz;
+    std::vector<int64_t> msg(words, 0), recv((size_t)words * G);
+    for (int64_t i = 0; i < nloc; ++i) {
+        msg[i] = H.l2g[i];
+        msg[maxloc + i] = L.rp[i + 1] - L.rp[i];
+    }
+    for (size_t k = 0; k < L.ci.size(); ++k) {
+        msg[2 * maxloc + k] = H.l2g[L.ci[k]];
+        std::memcpy(&msg[2 * maxloc + maxnnz + k], &L.v[k], sizeof(double));
+    }
+    cm.allgather_host(msg.data(), sizeof(int64_t) * words, recv.data());
+    // global CSR: row g from its owner, columns sorted
+    std::vector<int64_t> rowlen(N, -1);
+    srcslot.assign(N, -1);
+    for (int q = 0; q < G; ++q) {
+        const int64_t *m = recv.data() + (size_t)words * q;
+        for (int64_t i = 0; i < all[2 * q]; ++i) {
+            const int64_t g = m[i];
+            if (g < 0 || g >= N || rowlen[g] >= 0) throw Error("redundant PC: inconsistent row ownership");
+            rowlen[g] = m[maxloc + i];
+            srcslot[g] = q * maxloc + i;
+        }
+    }
+    HostCSR Gh;
+    Gh.nrows = Gh.ncols = N;
+    Gh.rp.assign(N + 1, 0);
+    for (int64_t g = 0; g < N; ++g) Gh.rp[g + 1] = Gh.rp[g] + rowlen[g];
+    Gh.ci.resize(Gh.rp[N]);
+    Gh.v.resize(Gh.rp[N]);
+    std::vector<std::pair<int64_t, double>> row;
+    for (int q = 0; q < G; ++q) {
+        const int64_t *m = recv.data() + (size_t)words * q;
+        int64_t k = 0;
+        for (int64_t i = 0; i < all[2 * q]; ++i) {
+            const int64_t g = m[i], len = m[maxloc + i];
+            row.resize(len);
+            for (int64_t e = 0; e < len; ++e, ++k) {
+                double v;
+                std::memcpy(&v, &m[2 * maxloc + maxnnz + k], sizeof(double));
+                row[e] = {m[2 * maxloc + k], v};
+            }
+            std::sort(row.begin(), row.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+            for (int64_t e = 0; e < len; ++e) {
+                Gh.ci[Gh.rp[g] + e] = (int32_t)row[e].first;
+                Gh.v[Gh.rp[g] + e] = row[e].second;
+            }
+        }
+    }
+    rank_rows.clear();
+    bool contiguous = true;
+    int64_t start = 0;
+    for (int q = 0; q < G && contiguous; ++q) {
+        const int64_t *m = recv.data() + (size_t)words * q;
+        for (int64_t i = 0; i < all[2 * q]; ++i)
+            if (m[i] != start + i) contiguous = false;
+        start += all[2 * q];
+    }
+    if (contiguous)
+        for (int q = 0; q < G; ++q) rank_rows.push_back(all[2 * q]);
+    return Gh;
+}
+
+// Local rows L (columns: global indices of a column space owned in contiguous
+// rank ranges cst[q] .. cst[q + 1]) -> a distributed DevCSR: owned columns ->
+// local [0, nlocal), referenced others -> ghosts nlocal + k in global order
+// (= owner-major), the halo plan by one alltoallv of index lists, entries of a
+// row sorted by local column, the SpMV layout built.  Every rank calls it.
+void upload_dist(const HostCSR &L, const std::vector<int64_t> &cst, DevCSR &M, Ctx &c) {
+    Comm &cm = *c.comm;
+    const int G = cm.size, r = cm.rank;
+    if ((int)cst.size() != G + 1) throw Error("upload_dist: one column range per rank expected");
+    const int64_t c0 = cst[r], nlocal = cst[r + 1] - cst[r];
+    std::vector<int64_t> gh;
+    for (int32_t j : L.ci)
+        if (j < c0 || j >= c0 + nlocal) gh.push_back(j);
+    std::sort(gh.begin(), gh.end());
+    gh.erase(std::unique(gh.begin(), gh.end()), gh.end());
+    auto H = std::make_shared<Halo>();
+    H->nlocal = nlocal;
+    H->nghost = (int64_t)gh.size();
+    std::vector<std::vector<int64_t>> need(G), asked;
+    H->rcnt.assign(G, 0);
+    H->roff.assign(G, 0);
+    {
+        size_t k = 0;
+        for (int q = 0; q < G; ++q) {
+            H->roff[q] = (int64_t)k;
+            while (k < gh.size() && gh[k] < cst[q + 1]) need[q].push_back(gh[k++]);
+            H->rcnt[q] = (int64_t)need[q].size();
+        }
+    }
+    cm.alltoallv_i64(need, asked);
+    std::vector<int32_t> sidx;
+    H->scnt.assign(G, 0);
+    H->soff.assign(G, 0);
+    for (int q = 0; q < G; ++q) {
+        H->soff[q] = (int64_t)sidx.size();
+        for (int64_t g : asked[q]) {
+            if (g < c0 || g >= c0 + nlocal) throw Error("halo plan: peer asked for a column this rank does not own");
+            sidx.push_back((int32_t)(g - c0));
+        }
+        H->scnt[q] = (int64_t)asked[q].size();
+    }
+    H->nsend = (int64_t)sidx.size();
+    H->send_idx.alloc(std::max<int64_t>(H->nsend, 1));
+    if (H->nsend) HIPCHK(hipMemcpyAsync(H->send_idx.p, sidx.data(), sizeof(int32_t) * H->nsend, hipMemcpyHostToDevice, c.st));
+    H->sendbuf.alloc(std::max<int64_t>(H->nsend, 1));
+    H->ghost.alloc(std::max<int64_t>(H->nghost, 1));
+    H->l2g.resize(nlocal + gh.size());
+    for (int64_t i = 0; i < nlocal; ++i) H->l2g[i] = c0 + i;
+    for (size_t k = 0; k < gh.size(); ++k) H->l2g[nlocal + k] = gh[k];
+    HostCSR T;
+    T.nrows = L.nrows;
+    T.ncols = nlocal + (int64_t)gh.size();
+    T.rp.assign(1, 0);
+    std::vector<std::pair<int32_t, double>> row;
+    for (int64_t i = 0; i < L.nrows; ++i) {
+        row.clear();
+        for (int64_t k = L.rp[i]; k < L.rp[i + 1]; ++k) {
+            const int64_t j = L.ci[k];
+            const int32_t lj = (j >= c0 && j < c0 + nlocal)
+                                   ? (int32_t)(j - c0)
+                                   : (int32_t)(nlocal + (std::lower_bound(gh.begin(), gh.end(), j) - gh.begin()));
+            row.push_back({lj, L.v[k]});
+        }
+        std::sort(row.begin(), row.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+        for (auto &e : row) {
+            T.ci.push_back(e.first);
+            T.v.push_back(e.second);
+        }
+        T.rp.push_back((int64_t)T.ci.size());
+    }
+    upload(T, M, c);
+    M.ncols = T.ncols;
+    M.halo = H;
+    M.sell.reset();
+    build_sell(M, c);
+    c.sync();
+}
+
+// a single-rank context carrying c's layout options
+std::unique_ptr<Ctx> layout_ctx(const Ctx &c) {
+    auto self = std::make_unique<Ctx>();
+    self->sell_d16 = c.sell_d16;
+    self->d16_wide_lpr = c.d16_wide_lpr;
+    self->d16_unroll = c.d16_unroll;
+    self->d16_segs = c.d16_segs;
+    self->d16_sigma = c.d16_sigma;
+    self->d16_sigma_pad = c.d16_sigma_pad;
+    self->d16_sorted_lpr = c.d16_sorted_lpr;
+    self->spmv_b3 = c.spmv_b3;
+    self->spmv_rcm = c.spmv_rcm;
+    self->sweep_chain = c.sweep_chain;
+    return self;
+}
+
 // PETSc PCREDUNDANT semantics for PCs that act on a whole parallel block
 // (ILU(0), LU, classical / smoothed-aggregation AMG) when the block is
 // sharded over G ranks: every rank gathers the block (its MPIAIJ rows with
@@ -1475,93 +1766,15 @@ struct PCRedundant : PC {
         type = t;
         n = nloc = M.nrows;
         const Halo &H = *M.halo;
-        if ((int64_t)H.l2g.size() < M.ncols || H.nlocal != M.nrows)
-            throw Error("redundant PC (prefix " + prefix + "): block is not a diagonal block of the sharded system");
-        Comm &cm = *c.comm;
-        const int G = cm.size;
-        // host CSR of my rows, block-global rows / columns
-        const HostCSR L = download(M, c);
-        std::vector<int64_t> cnt{nloc, (int64_t)L.ci.size()}, all(2 * G);
-        cm.allgather_host(cnt.data(), sizeof(int64_t) * 2, all.data());
-        int64_t maxnnz = 0;
-        for (int q = 0; q < G; ++q) {
-            maxloc = std::max(maxloc, all[2 * q]);
-            maxnnz = std::max(maxnnz, all[2 * q + 1]);
-            N += all[2 * q];
-        }
-        // message: rows (global ids), row lengths, columns (global), values -- padded to the largest rank's
-        const int64_t words = 2 * maxloc + 2 * maxnnz;
-        std::vector<int64_t> msg(words, 0), recv((size_t)words * G);
-        for (int64_t i = 0; i < nloc; ++i) {
-            msg[i] = H.l2g[i];
-            msg[maxloc + i] = L.rp[i + 1] - L.rp[i];
-        }
-        for (size_t k = 0; k < L.ci.size(); ++k) {
-            msg[2 * maxloc + k] = H.l2g[L.ci[k]];
-            std::memcpy(&msg[2 * maxloc + maxnnz + k], &L.v[k], sizeof(double));
-        }
-        cm.allgather_host(msg.data(), sizeof(int64_t) * words, recv.data());
-        // global CSR: row g from its owner, columns sorted
-        std::vector<int64_t> rowlen(N, -1), srcslot(N, -1), rowpos(N);
-        for (int q = 0; q < G; ++q) {
-            const int64_t *m = recv.data() + (size_t)words * q;
-            for (int64_t i = 0; i < all[2 * q]; ++i) {
-                const int64_t g = m[i];
-                if (g < 0 || g >= N || rowlen[g] >= 0) throw Error("redundant PC: inconsistent row ownership");
-                rowlen[g] = m[maxloc + i];
-                srcslot[g] = q * maxloc + i;
-            }
-        }
-        HostCSR Gh;
-        Gh.nrows = Gh.ncols = N;
-        Gh.rp.assign(N + 1, 0);
-        for (int64_t g = 0; g < N; ++g) Gh.rp[g + 1] = Gh.rp[g] + rowlen[g];
-        Gh.ci.resize(Gh.rp[N]);
-        Gh.v.resize(Gh.rp[N]);
-        std::vector<std::pair<int64_t, double>> row;
-        for (int q = 0; q < G; ++q) {
-            const int64_t *m = recv.data() + (size_t)words * q;
-            int64_t k = 0;
-            for (int64_t i = 0; i < all[2 * q]; ++i) {
-                const int64_t g = m[i], len = m[maxloc + i];
-                row.resize(len);
-                for (int64_t e = 0; e < len; ++e, ++k) {
-                    double v;
-                    std::memcpy(&v, &m[2 * maxloc + maxnnz + k], sizeof(double));
-                    row[e] = {m[2 * maxloc + k], v};
-                }
-                std::sort(row.begin(), row.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
-                for (int64_t e = 0; e < len; ++e) {
-                    Gh.ci[Gh.rp[g] + e] = (int32_t)row[e].first;
-                    Gh.v[Gh.rp[g] + e] = row[e].second;
-                }
-            }
-        }
-        self = std::make_unique<Ctx>();
-        self->sell_d16 = c.sell_d16;
-        self->d16_wide_lpr = c.d16_wide_lpr;
-        self->d16_unroll = c.d16_unroll;
-        self->d16_segs = c.d16_segs;
-        self->d16_sigma = c.d16_sigma;
-        self->d16_sigma_pad = c.d16_sigma_pad;
-        self->d16_sorted_lpr = c.d16_sorted_lpr;
-        self->spmv_b3 = c.spmv_b3;
-        self->spmv_rcm = c.spmv_rcm;
-        // the ranks' rows: contiguous ranges in rank order (every single-field block,
-        // every caller-assembled one) -> the inner PC may restate how the reference's
-        // PC runs over G ranks (classical AMG: hypre's per-rank HMIS and smoother)
-        {
-            bool contiguous = true;
-            int64_t start = 0;
-            for (int q = 0; q < G && contiguous; ++q) {
-                const int64_t *m = recv.data() + (size_t)words * q;
-                for (int64_t i = 0; i < all[2 * q]; ++i)
-                    if (m[i] != start + i) contiguous = false;
-                start += all[2 * q];
-            }
-            if (contiguous)
-                for (int q = 0; q < G; ++q) self->rank_rows.push_back(all[2 * q]);
-        }
+        const int G = c.comm->size;
+        std::vector<int64_t> srcslot, rank_rows;
+        const HostCSR Gh = gather_block(M, c, prefix, srcslot, maxloc, rank_rows);
+        N = Gh.nrows;
+        self = layout_ctx(c);
+        // the ranks' rows: contiguous ranges in rank order -> the inner PC may restate
+        // how the reference's PC runs over G ranks (classical AMG: hypre's per-rank
+        // HMIS and smoother)
+        self->rank_rows = rank_rows;
         upload(Gh, Gm, *self);
         inner = factory(Gm, *self);
         std::vector<int64_t> mg(H.l2g.begin(), H.l2g.begin() + nloc);
@@ -1616,6 +1829,14 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
                         std::to_string(c.comm ? c.comm->size : 1) +
                         " ranks: PETSc's ILU does not run on MPIAIJ matrices (use bjacobi, or pls.redundant_ilu 1 "
                         "for the one-rank ILU applied redundantly)");
+        if (type == "hypre" && o.str("pls.hypre", "boomeramg") == "boomeramg" && o.flag("pls.hypre_dist", true)) {
+            // BoomerAMG as under mpirun -np G: the np = G hierarchy, each rank smoothing its
+            // own rows (Jacobi across ranks); needs ranks owning contiguous rows in rank order
+            std::vector<int64_t> srcslot, rank_rows;
+            int64_t maxloc = 0;
+            const HostCSR Gh = gather_block(M, c, prefix, srcslot, maxloc, rank_rows);
+            if (!rank_rows.empty()) return make_boomeramg_dist(M, Gh, rank_rows, o, prefix, c);
+        }
         if (o.flag("pls.redundant_error", false))
             throw Error("PC type '" + type + "' (prefix " + prefix + ") acts on the whole parallel matrix (pls.redundant_error)");
         return make_redundant(type, M, c, [&](const DevCSR &Gm, Ctx &sc) { return make_pc(type, Gm, o, prefix, sc); },

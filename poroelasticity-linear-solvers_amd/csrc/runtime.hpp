@@ -76,6 +76,8 @@ struct Ctx {
     int d16_sorted_lpr = 2;       // lanes per row of sorted slices with 32+ entries per row (pls.d16_sorted_lpr)
     bool spmv_b3 = false;         // row-triple layout for FE vector fields (pls.spmv_b3; measured slower)
     int spmv_rcm = -1;            // RCM-relabelled SpMV layout: -1 where the plain plan pads (FE), 0 never, 1 always
+    int sweep_chain = -1;         // LDS-resident ILU / Gauss-Seidel blocks swept by one wave (k_ilu_blocks_chain):
+                                  // -1 where the level DAG is deep and narrow, 0 never, 1 whenever rows fit
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
@@ -280,8 +282,18 @@ struct RingTri {
     DBuf<double> fval;           // ... factor values
     int64_t nfar = 0;
 };
+// Chain-sweep stream of one triangle (kernels.hip, k_ilu_blocks_chain)
+struct ChainTri {
+    DBuf<int64_t> base, nsl;      // per block: first entry, slice count
+    DBuf<int32_t> first, lpr;     // per block: sizes of the first ilu_chain_depth() slices, lanes per row
+    DBuf<int32_t> col;
+    DBuf<double> val;
+};
 struct PCILU : PC {
     int64_t nblocks = 1;
+    // chain sweep (Ctx::sweep_chain): LDS-resident blocks of deep, narrow level DAGs
+    bool chain = false;
+    ChainTri Lc, Uc;
     // ring sweep (pls.ilu_ring, default on): y-resident blocks whose levels are
     // narrow sweep in level-order position space with an LDS ring of recent values
     bool ring = false;
@@ -363,6 +375,9 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
 std::unique_ptr<PC> make_amg(const DevCSR &M, const Options &o, const std::string &prefix, bool hypre, Ctx &c);
 // Classical AMG as the reference configures BoomerAMG (boomeramg.cpp; -pc_type hypre).
 std::unique_ptr<PC> make_boomeramg(const DevCSR &M, const Options &o, const std::string &prefix, Ctx &c);
+// hypre's np = G hierarchy on a sharded block (M: this rank's rows; global: the gathered block)
+std::unique_ptr<PC> make_boomeramg_dist(const DevCSR &M, const HostCSR &global, const std::vector<int64_t> &rank_rows,
+                                        const Options &o, const std::string &prefix, Ctx &c);
 void boomeramg_host_level(const HostCSR &A, const Options &o, const std::string &prefix, int64_t level,
                           int64_t &nlevels, int64_t &n, int64_t &nc, std::vector<int8_t> &cf, HostCSR &P);
 
@@ -432,6 +447,14 @@ struct PCFieldSplit : PC {
 
 // PCREDUNDANT: a sharded diagonal block (Halo::l2g) gathered on every rank,
 // factory(global block, single-rank context) builds the PC applied redundantly.
+// Sharded diagonal block -> the global host CSR on every rank (PCRedundant's
+// gather; rank_rows: the ranks' row counts when contiguous in rank order)
+HostCSR gather_block(const DevCSR &M, Ctx &c, const std::string &prefix, std::vector<int64_t> &srcslot,
+                     int64_t &maxloc, std::vector<int64_t> &rank_rows);
+// a single-rank context with c's layout options (own stream)
+std::unique_ptr<Ctx> layout_ctx(const Ctx &c);
+// local rows with global columns owned in contiguous rank ranges cst -> distributed DevCSR with halo
+void upload_dist(const HostCSR &L, const std::vector<int64_t> &cst, DevCSR &M, Ctx &c);
 std::unique_ptr<PC> make_redundant(const std::string &type, const DevCSR &M, Ctx &c,
                                    const std::function<std::unique_ptr<PC>(const DevCSR &, Ctx &)> &factory,
                                    const std::string &prefix);

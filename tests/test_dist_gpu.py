@@ -70,6 +70,21 @@ CASES = [
                                      "ksp_type": "preonly", "pc_type": "hypre", "pc_hypre_boomeramg_P_max": "4",
                                      "pc_hypre_boomeramg_agg_nl": "1", "pc_hypre_boomeramg_agg_num_paths": "2",
                                      "pc_hypre_boomeramg_no_CF": "true"}.items()})},
+    # (round 3: hypre on a sharded block runs BoomerAMG's np = G hierarchy with
+    # every rank smoothing only its own rows -- the case above -- and with C/F
+    # relaxation; the gathered, redundantly applied one stays on request)
+    {"name": "dist_hypre_cf_3way_3d", "dim": 3, "N": 4, "params": dict(BASE, **{"pc type": "diagonal 3-way"}),
+     "pc_tol": 1e-12, "db": dict({"global_ksp_type": "gmres", "global_ksp_pc_side": "right"},
+                                 **{pre + k: v for pre in ("s_", "f_", "p_", "diff_") for k, v in {
+                                     "ksp_type": "preonly", "pc_type": "hypre", "pc_hypre_boomeramg_P_max": "4",
+                                     "pc_hypre_boomeramg_agg_nl": "1", "pc_hypre_boomeramg_agg_num_paths": "2",
+                                     }.items()})},
+    {"name": "redundant_hypre_forced_3way_3d", "dim": 3, "N": 4, "params": dict(BASE, **{"pc type": "diagonal 3-way"}),
+     "pc_tol": 1e-12, "db": dict({"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "pls.hypre_dist": "0"},
+                                 **{pre + k: v for pre in ("s_", "f_", "p_", "diff_") for k, v in {
+                                     "ksp_type": "preonly", "pc_type": "hypre", "pc_hypre_boomeramg_P_max": "4",
+                                     "pc_hypre_boomeramg_agg_nl": "1", "pc_hypre_boomeramg_agg_num_paths": "2",
+                                     "pc_hypre_boomeramg_no_CF": "true"}.items()})},
     # ... and the fp block's Schur fieldsplit (petsc-options-inexact:73-114 with LU splits)
     {"name": "redundant_fieldsplit_2d", "dim": 2, "N": 10, "params": BASE,
      "db": dict(_db({"s_": 5}), **{"fp_ksp_type": "preonly", "fp_pc_type": "fieldsplit",
@@ -125,6 +140,15 @@ FE_CASES = [
      "params": dict(FE_BASE, **{"pc type": "diagonal", "solver maxiter": 200}), "db": _fs_db()},
     {"name": "fe_facade_fieldsplit_twoway_2d", "system": "fe", "facade": True, "dim": 2, "N": 8,
      "params": dict(FE_BASE, **{"pc type": "diagonal", "solver maxiter": 200}), "db": _fs_db()},
+    # petsc-options-inexact's BoomerAMG on every block of a caller-assembled
+    # system under mpirun: hypre's np = G hierarchy, each rank its own rows
+    {"name": "fe_hypre_threeway_2d", "system": "fe", "dim": 2, "N": 8,
+     "params": dict(FE_BASE, **{"pc type": "diagonal 3-way", "inner pc type": "hypre", "solver maxiter": 200}),
+     "db": dict({"global_ksp_type": "gmres", "global_ksp_pc_side": "right"},
+                **{pre + k: v for pre in ("s_", "f_", "p_", "diff_") for k, v in {
+                    "ksp_type": "preonly", "pc_type": "hypre", "pc_hypre_boomeramg_P_max": "4",
+                    "pc_hypre_boomeramg_agg_nl": "1", "pc_hypre_boomeramg_agg_num_paths": "2",
+                    "pc_hypre_boomeramg_no_CF": "true"}.items()})},
     # the reference's exact option set under mpirun (MUMPS LU on every block ->
     # each sharded block gathered and factored redundantly)
     {"name": "fe_exact_lu_threeway_2d", "system": "fe", "dim": 2, "N": 8,

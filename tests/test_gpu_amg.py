@@ -80,7 +80,8 @@ def _boomer_db(no_cf=True):
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
 @pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-inexact", "hypre-inexact-cf", "hypre-inexact-dense", "hypre-sa",
                                "hypre-inexact-k1", "hypre-inexact-k256", "hypre-inexact-cf-k256",
-                               "hypre-inexact-ranks3", "hypre-inexact-cf-ranks3"])
+                               "hypre-inexact-ranks3", "hypre-inexact-cf-ranks3", "hypre-inexact-k256-chain",
+                               "hypre-inexact-cf-chain"])
 def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
     """hypre: PETSc's defaults (HMIS / ext+i, no truncation, no aggressive
     level, C/F-ordered Gauss-Seidel); -inexact: petsc-options-inexact's
@@ -88,14 +89,17 @@ def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
     sweep through its dense chunk inverses (pls.amg_gs_dense 1, the path of
     mostly sequential coarse levels); -sa: pls.hypre sa; -k1 / -k256:
     the hybrid Gauss-Seidel with one chunk (plain symmetric GS) / 256 chunks on
-    every level (no row floor); -ranks3: hypre under mpirun -np 3."""
+    every level (no row floor); -ranks3: hypre under mpirun -np 3; -chain:
+    every LDS-resident smoother chunk on the chain sweep (pls.sweep_chain 1)."""
     params = dict(BASE, **{"pc type": pc_type, "inner pc type": "lu"})
     extra = {"hypre-inexact": _boomer_db(), "hypre-inexact-cf": _boomer_db(False), "hypre-sa": {"pls.hypre": "sa"},
              "hypre-inexact-dense": dict(_boomer_db(), **{"pls.amg_gs_dense": "1"}),
              "hypre-inexact-k1": dict(_boomer_db(), **K1), "hypre-inexact-k256": dict(_boomer_db(), **K256),
              "hypre-inexact-cf-k256": dict(_boomer_db(False), **K256),
              "hypre-inexact-ranks3": dict(_boomer_db(), **RANKS3),
-             "hypre-inexact-cf-ranks3": dict(_boomer_db(False), **RANKS3)}
+             "hypre-inexact-cf-ranks3": dict(_boomer_db(False), **RANKS3),
+             "hypre-inexact-k256-chain": dict(_boomer_db(), **K256, **{"pls.sweep_chain": "1"}),
+             "hypre-inexact-cf-chain": dict(_boomer_db(False), **{"pls.sweep_chain": "1"})}
     db = _amg_db(t.split("-")[0], extra.get(t))
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)
@@ -246,9 +250,40 @@ def test_round_robin_sweep_is_bitwise(gpu, N):
     v = np.random.default_rng(2).standard_normal(s.A.shape[0])
     out = []
     for rr in ("0", "1"):
-        opts = dict(db, **{"pls.sweep_rr": rr})
+        opts = dict(db, **{"pls.sweep_rr": rr, "pls.sweep_chain": "0"})
         opts.update(params_to_options(params))
         h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
         out.append(h.pc_apply(v))
         h.destroy()
     assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_chain_sweep_matches_workgroup_sweep(gpu, N):
+    """The chain sweep (one wave per Gauss-Seidel chunk walking its slices in
+    order, 8 slices of factor data in flight, no barrier) against the
+    workgroup LDS sweep on the same classical-AMG hierarchy of footing's solid
+    block: equal to rounding (bitwise where both take the same lanes per row;
+    the chain sweep deals rows of more than 28 entries per triangle over 8 or
+    16 lanes, the LDS sweep reloads them inside the level -- the Galerkin
+    levels' rows), and repeatable bitwise.  (A GMRES solve with this PREONLY
+    set stalls on the undrained N = 32 block, where 1e-13 differences grow to
+    O(1e-1) in the history -- the solve parity of the chain path is covered by
+    test_footing_vs_oracle, which runs it by default.)"""
+    from lib import fe_footing as FF
+    from lib.handle import Handle, params_to_options
+    s = FF.assemble_footing(N, "undrained")
+    params = dict(BASE, **{"pc type": "undrained", "inner pc type": "hypre"})
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "s_ksp_type": "preonly", "s_pc_type": "hypre",
+          "fp_ksp_type": "preonly", "fp_pc_type": "lu", "pls.amg_gs_dense": "0"}
+    db.update({"s_" + k: v for k, v in BOOMER.items()})
+    v = np.random.default_rng(2).standard_normal(s.A.shape[0])
+    out = []
+    for ch in ("0", "1"):
+        opts = dict(db, **{"pls.sweep_chain": ch})
+        opts.update(params_to_options(params))
+        h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+        out.append(h.pc_apply(v))
+        assert np.array_equal(h.pc_apply(v), out[-1])
+        h.destroy()
+    assert np.max(np.abs(out[0] - out[1])) <= 1e-13 * np.max(np.abs(out[0]))

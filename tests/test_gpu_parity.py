@@ -161,15 +161,20 @@ def test_spmv_matches_scipy(gpu, dim, N, segs):
 
 
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
-@pytest.mark.parametrize("inner", ["ilu", "jacobi", "bjacobi"])
+@pytest.mark.parametrize("inner", ["ilu", "jacobi", "bjacobi", "ilu-chain", "bjacobi-chain"])
 def test_pc_apply_matches_oracle(gpu, pc_type, inner):
+    """-chain: the LDS-resident ILU(0) sweeps forced onto the chain sweep (one
+    wave per block walking its slices in order, pls.sweep_chain 1)."""
     spec = S.SynthSpec(2, 10)
     params = dict(BASE, **{"pc type": pc_type})
     db = dict(ILU_DB)
+    kind = inner.split("-")[0]
     for pre in ("s_", "f_", "p_", "diff_", "fp_"):
-        db[pre + "pc_type"] = inner
-        if inner == "bjacobi":
+        db[pre + "pc_type"] = kind
+        if kind == "bjacobi":
             db[pre + "pc_bjacobi_blocks"] = "3"
+    if inner.endswith("-chain"):
+        db["pls.sweep_chain"] = "1"
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)
     rng = np.random.default_rng(2)
