@@ -64,7 +64,9 @@ class BlockPC:
                 if ptype == "hypre" and str(db.get("pls.hypre", "boomeramg")) == "boomeramg":
                     # BoomerAMG under mpirun -np G: the block's rank partition when every
                     # rank's rows are one contiguous range (single-field slabs, or
-                    # caller-assembled ownership), as libpls's PCRedundant passes it on
+                    # caller-assembled ownership) -- libpls runs that np = G hierarchy
+                    # with each rank smoothing its own rows (or, pls.hypre_dist 0,
+                    # gathered and applied redundantly): the same operator either way
                     sizes_r = None
                     if dist_owner is not None:
                         own = dist_owner[rows]

@@ -1247,7 +1247,7 @@ struct PCBoomer : PC {
             tm[5] += now() - t1;
         }, tm);
         tm[0] = now() - t0 - (tm[1] + tm[2] + tm[3] + tm[4] + tm[5]);
-        if (!lv.empty()) {
+        if (!lv.empty() || dist) {  // (sharded: the coarsest operator is the gathered global one)
             cur = std::make_unique<DevCSR>();
             upload(A, *cur, c);
             amg_layout(*cur, c);
@@ -1256,7 +1256,7 @@ struct PCBoomer : PC {
         nco = A.nrows;
         nco_mine = nco;
         if (dist) {
-            if (lv.empty()) throw Error("boomeramg (prefix " + prefix + "): a sharded block needs at least one level");
+            if (lv.empty()) cps_last = part_starts(rr);  // the block is the coarsest level (<= 9 rows, or no coarsening)
             // the coarsest level is solved redundantly: gather b_c (padded allgather), keep my rows of x_c
             const int G = c.comm->size;
             nco_mine = cps_last[me + 1] - cps_last[me];
@@ -1395,7 +1395,8 @@ struct PCBoomer : PC {
     void apply(const double *x, double *y, Ctx &c) override {
         if (n == 0 && !dist) return;
         if (lv.empty()) {
-            coarse_solve(x, y, c);
+            if (dist) coarse_solve_dist(x, y, work_for(c), c);
+            else coarse_solve(x, y, c);
             return;
         }
         vcycle(0, work_for(c), x, y, c);

@@ -2486,42 +2486,42 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
 // (footing's solid block, the synthetic N=59 s block) -- spend their time in
 // the per-level hand-off, not in bytes: the workgroup sweep above pays a
 // barrier and a two-level-deep prefetch per level (~0.77 us per level on the
-// footing N=128 chunks).  Here ONE wave walks a block's slices in order
-// (a level's rows are independent, so a level cut into several slices is
-// still a valid order): no barrier (LDS accesses of one wave complete in
-// order), and the factor data of NW_D slices in flight, which the in-order
-// vmcnt covers with 7 loads per slice (<= 63 outstanding).
+// footing N=128 chunks).  Here ONE wave walks a block's rows in STEPS of one
+// 16-lane DPP row each -- the rows of a step belong to one level, so they are
+// independent; a level with more rows takes several steps, one after the
+// other -- with no barrier (the LDS accesses of one wave complete in order).
+// A slice packs up to 4 consecutive steps (lanes 16q .. 16q + 15: step q),
+// and NW_D slices of factor data are in flight (6 loads each: the in-order
+// vmcnt covers <= 63 outstanding), i.e. up to 32 steps of look-ahead.
 //
-// Stream layout (per triangle, runtime.cpp build_chain_tri): a slice is 4 +
-// nl * L entries (nl active lanes = rows x lanes per row, L = 4 or 8 entries
-// per lane, lane-major): entries [0, 4) the descriptor -- col[0] = size | (L
-// == 8) of the slice NW_D positions later in the same block (0: none) -- then
-// lane l's header (col = local row | count << SW_ROW_BITS, val = 1 / U_ii for
-// the upper triangle) and its factor entries at 4 + l * L.  A row's entries
-// are dealt round robin over its LPR lanes and the partial sums combined by
-// the DPP tree of sw2_finish, exactly as in the LDS sweep: with the same
-// lanes per row the results are bitwise those of k_ilu_blocks_lds.
+// Stream layout (per triangle, runtime.cpp build_chain_tri): a slice is nl *
+// L entries (nl = 16 x its steps, L = 4 or 8 entries per lane, lane-major),
+// lane l's header (col = local row | count << SW_ROW_BITS, SW_ROW_PAD: no
+// row; val = 1 / U_ii for the upper triangle) then its factor entries at l *
+// L; slices follow one another, and a separate array holds every slice's size
+// | (L == 8), read 64 slices at a time into a vector register (lane l: slice
+// w0 + l) and picked with v_readlane.  A row's entries are dealt round robin
+// over its LPR lanes and the partial sums combined by the DPP tree of
+// sw2_finish, as in the LDS sweep: with the same lanes per row the results are
+// bitwise those of k_ilu_blocks_lds.
 static constexpr int NW_D = 8;  // slices in flight per wave
 struct NwSlot {
     int32_t c[8];
     double v[8];
-    int32_t desc;  // size | flag of the slice NW_D later
-    int nl;        // active lanes of this slice
+    int nl;  // active lanes of this slice (16 per step)
 };
 
 __device__ __forceinline__ void nw_issue(const int32_t *col, const double *val, int64_t base, int32_t szf, int lane,
                                          NwSlot &s) {
     const int sz = szf & ~3;
     const int L = (szf & 1) ? 8 : 4;
-    s.nl = sz > 4 ? (sz - 4) / L : 0;
+    s.nl = sz / L;
     // range-checked to the slice: lanes past nl and slices past the block's
     // end (size 0) read zeros without traffic; every path issues the same
-    // 7 loads, so the compiler's vmcnt bookkeeping stays exact
+    // 6 loads, so the compiler's vmcnt bookkeeping stays exact
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void *)(col + base), (short)0, sz * 4, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void *)(val + base), (short)0, sz * 8, 0x00020000);
-    const int off = 4 + lane * L;
-    const auto d4 = __builtin_amdgcn_raw_buffer_load_b128(rc, 0, 0, 0);
-    s.desc = (int32_t)d4[0];
+    const int off = lane * L;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
         const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(rc, (off + 4 * q) * 4, 0, 0);
@@ -2540,66 +2540,98 @@ __device__ __forceinline__ void nw_issue(const int32_t *col, const double *val, 
 
 template <int LPR>
 __device__ __forceinline__ void nw_compute(const NwSlot &s, double *ys, int lane, bool upper) {
-    const int32_t h = s.c[0];
-    const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
-    double acc = 0.0, d[8];
-    // every dependency read issued before the first is consumed
+    const int nsteps = s.nl >> 4;
 #pragma unroll
-    for (int u = 1; u < 8; ++u) d[u] = ys[u <= len ? s.c[u] : 0];
+    for (int q = 0; q < 4; ++q) {  // the slice's steps in order: step q is lanes 16q .. 16q + 15
+        if (q < nsteps && (lane >> 4) == q) {
+            const int32_t h = s.c[0];
+            const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
+            const int32_t li = h & SW_ROW_PAD;
+            // the row's own input first, then every dependency read before the first is consumed
+            const double yi = ys[li != SW_ROW_PAD ? li : 0];
+            double acc = 0.0, d[8];
 #pragma unroll
-    for (int u = 1; u < 8; ++u) {
-        const double t = __dmul_rn(s.v[u], d[u]);  // the LDS sweep's rounding (no contraction)
-        acc += (u <= len) ? t : 0.0;
-    }
-    constexpr int lg = LPR >= 16 ? 4 : LPR >= 8 ? 3 : LPR >= 4 ? 2 : LPR >= 2 ? 1 : 0;
-    if (lg >= 1) acc += dpp_d<0xB1>(acc);
-    if (lg >= 2) acc += dpp_d<0x4E>(acc);
-    if (lg >= 3) acc += dpp_d<0x141>(acc);
-    if (lg >= 4) acc += dpp_d<0x140>(acc);
-    const int32_t li = h & SW_ROW_PAD;
-    if ((lane & (LPR - 1)) == 0 && lane < s.nl && li != SW_ROW_PAD) ys[li] = upper ? (ys[li] - acc) * s.v[0] : ys[li] - acc;
-}
-
-template <int LPR>
-__device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *first, int64_t nsl, const int32_t *col,
-                                         const double *val, double *ys, int lane, bool upper) {
-    if (nsl <= 0) return;
-    NwSlot s[NW_D];
-    int64_t ib = base;  // where the next issued slice starts
+            for (int u = 1; u < 8; ++u) d[u] = ys[u <= len ? s.c[u] : 0];
 #pragma unroll
-    for (int k = 0; k < NW_D; ++k) {
-        const int32_t f = __builtin_amdgcn_readfirstlane(first[k]);
-        nw_issue(col, val, ib, f, lane, s[k]);
-        ib += f & ~3;
-    }
-    for (int64_t j = 0;;) {
-#pragma unroll
-        for (int k = 0; k < NW_D; ++k) {
-            nw_compute<LPR>(s[k], ys, lane, upper);
-            const int32_t f = __builtin_amdgcn_readfirstlane(s[k].desc);
-            nw_issue(col, val, ib, f, lane, s[k]);
-            ib += f & ~3;
-            if (++j >= nsl) return;
+            for (int u = 1; u < 8; ++u) {
+                const double t = __dmul_rn(s.v[u], d[u]);  // the LDS sweep's rounding (no contraction)
+                acc += (u <= len) ? t : 0.0;
+            }
+            constexpr int lg = LPR >= 16 ? 4 : LPR >= 8 ? 3 : LPR >= 4 ? 2 : LPR >= 2 ? 1 : 0;
+            if (lg >= 1) acc += dpp_d<0xB1>(acc);
+            if (lg >= 2) acc += dpp_d<0x4E>(acc);
+            if (lg >= 3) acc += dpp_d<0x141>(acc);
+            if (lg >= 4) acc += dpp_d<0x140>(acc);
+            if ((lane & (LPR - 1)) == 0 && li != SW_ROW_PAD) ys[li] = upper ? (yi - acc) * s.v[0] : yi - acc;
         }
     }
 }
 
-__device__ __forceinline__ void nw_dispatch(int lpr, int64_t base, const int32_t *first, int64_t nsl,
+template <int LPR>
+__device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *sz, int64_t nsl, const int32_t *col,
+                                         const double *val, double *ys, int lane, bool upper) {
+    if (nsl <= 0) return;
+    // slice sizes: lane l of `win` holds slice w0 + l, of `nxt` slice w0 + 64 + l
+    // (loaded a window ahead, so picking from it never waits on a fresh load)
+    int64_t w0 = 0;
+    int32_t win = lane < nsl ? sz[lane] : 0;
+    int32_t nxt = 64 + lane < nsl ? sz[64 + lane] : 0;
+    auto size_of = [&](int64_t t) -> int32_t {
+        if (t >= nsl) return 0;
+        const int d = (int)(t - w0);
+        return d < 64 ? __builtin_amdgcn_readlane(win, d) : __builtin_amdgcn_readlane(nxt, d - 64);
+    };
+    NwSlot s[NW_D];
+    int64_t ib = base;  // where the next issued slice starts
+#pragma unroll
+    for (int k = 0; k < NW_D; ++k) {
+        const int32_t f = size_of(k);
+        nw_issue(col, val, ib, f, lane, s[k]);
+        ib += f & ~3;
+    }
+    // whole rounds of NW_D slices without an exit inside (a loop exit between the
+    // slots makes the compiler's vmcnt bookkeeping give up at the loop header and
+    // drain every load in flight), then the last nsl % NW_D slices
+    const int64_t rounds = nsl / NW_D;
+    for (int64_t j = 0; j < rounds; ++j) {
+        const int64_t t0 = (j + 1) * NW_D;  // first slice issued this round
+        if (t0 >= w0 + 64) {  // move the window (the next one is loaded now, needed >= 7 rounds later)
+            w0 += 64;
+            win = nxt;
+            nxt = w0 + 64 + lane < nsl ? sz[w0 + 64 + lane] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < NW_D; ++k) {
+            nw_compute<LPR>(s[k], ys, lane, upper);
+            const int32_t f = size_of(t0 + k);
+            nw_issue(col, val, ib, f, lane, s[k]);
+            ib += f & ~3;
+        }
+    }
+    const int rem = (int)(nsl - rounds * NW_D);
+#pragma unroll
+    for (int k = 0; k < NW_D; ++k)
+        if (k < rem) nw_compute<LPR>(s[k], ys, lane, upper);
+}
+
+__device__ __forceinline__ void nw_dispatch(int lpr, int64_t base, const int32_t *sz, int64_t nsl,
                                             const int32_t *col, const double *val, double *ys, int lane, bool upper) {
     switch (lpr) {
-        case 16: nw_sweep<16>(base, first, nsl, col, val, ys, lane, upper); break;
-        case 8: nw_sweep<8>(base, first, nsl, col, val, ys, lane, upper); break;
-        case 4: nw_sweep<4>(base, first, nsl, col, val, ys, lane, upper); break;
-        case 2: nw_sweep<2>(base, first, nsl, col, val, ys, lane, upper); break;
-        default: nw_sweep<1>(base, first, nsl, col, val, ys, lane, upper); break;
+        case 16: nw_sweep<16>(base, sz, nsl, col, val, ys, lane, upper); break;
+        case 8: nw_sweep<8>(base, sz, nsl, col, val, ys, lane, upper); break;
+        case 4: nw_sweep<4>(base, sz, nsl, col, val, ys, lane, upper); break;
+        case 2: nw_sweep<2>(base, sz, nsl, col, val, ys, lane, upper); break;
+        default: nw_sweep<1>(base, sz, nsl, col, val, ys, lane, upper); break;
     }
 }
 
 __global__ __launch_bounds__(64) void k_ilu_blocks_chain(
     int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart, const int64_t *__restrict__ Lbase,
-    const int32_t *__restrict__ Lfirst, const int64_t *__restrict__ Lnsl, const int32_t *__restrict__ Llpr,
+    const int64_t *__restrict__ Lsoff, const int32_t *__restrict__ Lsz, const int64_t *__restrict__ Lnsl,
+    const int32_t *__restrict__ Llpr,
     const int32_t *__restrict__ Lcol, const double *__restrict__ Lval, const int64_t *__restrict__ Ubase,
-    const int32_t *__restrict__ Ufirst, const int64_t *__restrict__ Unsl, const int32_t *__restrict__ Ulpr,
+    const int64_t *__restrict__ Usoff, const int32_t *__restrict__ Usz, const int64_t *__restrict__ Unsl,
+    const int32_t *__restrict__ Ulpr,
     const int32_t *__restrict__ Ucol, const double *__restrict__ Uval, const double *x, double *y) {
     extern __shared__ __attribute__((aligned(16))) double ys[];
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;  // heaviest (last) blocks first
@@ -2608,8 +2640,8 @@ __global__ __launch_bounds__(64) void k_ilu_blocks_chain(
     const int lane = threadIdx.x;
     for (int64_t t = lane; t < len; t += 64) ys[t] = x[b0 + t];
     __syncthreads();
-    nw_dispatch(Llpr[blk], Lbase[blk], Lfirst + blk * NW_D, Lnsl[blk], Lcol, Lval, ys, lane, false);
-    nw_dispatch(Ulpr[blk], Ubase[blk], Ufirst + blk * NW_D, Unsl[blk], Ucol, Uval, ys, lane, true);
+    nw_dispatch(Llpr[blk], Lbase[blk], Lsz + Lsoff[blk], Lnsl[blk], Lcol, Lval, ys, lane, false);
+    nw_dispatch(Ulpr[blk], Ubase[blk], Usz + Usoff[blk], Unsl[blk], Ucol, Uval, ys, lane, true);
     __syncthreads();
     for (int64_t t = lane; t < len; t += 64) y[b0 + t] = ys[t];
 }
@@ -2618,10 +2650,10 @@ int ilu_chain_depth() { return NW_D; }
 int ilu_chain_max_lpr() { return 16; }
 
 void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *Lbase,
-                             const int32_t *Lfirst, const int64_t *Lnsl, const int32_t *Llpr, const int32_t *Lcol,
-                             const double *Lval, const int64_t *Ubase, const int32_t *Ufirst, const int64_t *Unsl,
-                             const int32_t *Ulpr, const int32_t *Ucol, const double *Uval, const double *x, double *y,
-                             int64_t max_len, hipStream_t st) {
+                             const int64_t *Lsoff, const int32_t *Lsz, const int64_t *Lnsl, const int32_t *Llpr,
+                             const int32_t *Lcol, const double *Lval, const int64_t *Ubase, const int64_t *Usoff,
+                             const int32_t *Usz, const int64_t *Unsl, const int32_t *Ulpr, const int32_t *Ucol,
+                             const double *Uval, const double *x, double *y, int64_t max_len, hipStream_t st) {
     static bool configured = false;
     if (!configured) {
         (void)hipFuncSetAttribute((const void *)k_ilu_blocks_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2629,8 +2661,8 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
         configured = true;
     }
     const size_t bytes = (size_t)std::max<int64_t>(max_len, 1) * 8;
-    k_ilu_blocks_chain<<<(unsigned)nblocks, 64, bytes, st>>>(n, nblocks, bstart, Lbase, Lfirst, Lnsl, Llpr, Lcol, Lval,
-                                                             Ubase, Ufirst, Unsl, Ulpr, Ucol, Uval, x, y);
+    k_ilu_blocks_chain<<<(unsigned)nblocks, 64, bytes, st>>>(n, nblocks, bstart, Lbase, Lsoff, Lsz, Lnsl, Llpr, Lcol,
+                                                             Lval, Ubase, Usoff, Usz, Unsl, Ulpr, Ucol, Uval, x, y);
 }
 
 // =========================================================== distribution ====

@@ -199,15 +199,15 @@ int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in r
 // The chain sweep (kernels.hip, k_ilu_blocks_chain): one wave per LDS-resident
 // block walks its slices in order with ilu_chain_depth() slices in flight
 // (deep, narrow level DAGs).  Per triangle and block: first slice's entry
-// (base), the sizes of its first ilu_chain_depth() slices (first), the slice
-// count (nsl), lanes per row (lpr, 1..ilu_chain_max_lpr()).
+// (base), its first slice in the size array sz (soff), the slice count (nsl),
+// lanes per row (lpr, 1..ilu_chain_max_lpr()).
 int ilu_chain_depth();
 int ilu_chain_max_lpr();
 void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *Lbase,
-                             const int32_t *Lfirst, const int64_t *Lnsl, const int32_t *Llpr, const int32_t *Lcol,
-                             const double *Lval, const int64_t *Ubase, const int32_t *Ufirst, const int64_t *Unsl,
-                             const int32_t *Ulpr, const int32_t *Ucol, const double *Uval, const double *x, double *y,
-                             int64_t max_len, hipStream_t st);
+                             const int64_t *Lsoff, const int32_t *Lsz, const int64_t *Lnsl, const int32_t *Llpr,
+                             const int32_t *Lcol, const double *Lval, const int64_t *Ubase, const int64_t *Usoff,
+                             const int32_t *Usz, const int64_t *Unsl, const int32_t *Ulpr, const int32_t *Ucol,
+                             const double *Uval, const double *x, double *y, int64_t max_len, hipStream_t st);
 // The ring sweep (kernels.hip, k_ilu_blocks_ring): blocks of narrow levels whose
 // every level has <= ilu_ring_chunk() rows; per triangle chunk tables (coff per
 // block, cg first level, cp [start, end) positions), level orders ordL / ordU

@@ -1095,19 +1095,21 @@ static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order
 // the fewest lanes per row (1..ilu_chain_max_lpr(), powers of two) that keep
 // every lane's share of the block's longest row within 7 entries -- the LDS
 // sweep's rule, so blocks whose rows fit 4 lanes get the LDS sweep's lanes and
-// sums -- then per level slices of 64 / lpr rows in the level's row order.
-// Returns the slice count, or -1 when a row does not fit (fv / dinv empty: a
+// sums -- then per level steps of 16 / lpr rows in the level's row order, and
+// slices of up to 4 consecutive steps (step q on lanes 16q .. 16q + 15).
+// Returns the step count, or -1 when a row does not fit (fv / dinv empty: a
 // dry run that only counts).
 static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
                                const std::vector<int32_t> &ci, const std::vector<int64_t> &dg,
                                const std::vector<double> &fv, const std::vector<double> &dinv,
                                const std::vector<int32_t> &order, const std::vector<int64_t> &grp,
                                const std::vector<int64_t> &goff, bool upper, ChainTri *D, Ctx &c) {
-    const int W = ilu_lds_lane_entries(), ND = ilu_chain_depth(), LMAX = ilu_chain_max_lpr();
+    const int W = ilu_lds_lane_entries(), LMAX = ilu_chain_max_lpr();
+    const int32_t PAD = (1 << 18) - 1;  // kernels.hip SW_ROW_PAD
     auto rlen = [&](int64_t i) -> int64_t { return upper ? rp[i + 1] - dg[i] - 1 : dg[i] - rp[i]; };
     const bool dry = D == nullptr;
-    std::vector<int64_t> base(nblk, 0), nsl(nblk, 0);
-    std::vector<int32_t> first((size_t)nblk * ND, 0), lpr(nblk, 1), col;
+    std::vector<int64_t> base(nblk, 0), nsl(nblk, 0), soff(nblk, 0);
+    std::vector<int32_t> szs, lpr(nblk, 1), col;
     std::vector<double> val;
     int64_t total = 0;
     for (int64_t b = 0; b < nblk; ++b) {
@@ -1118,28 +1120,36 @@ static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, co
         while (l < LMAX && (mx + l - 1) / l > W) l *= 2;
         if ((mx + l - 1) / l > W) return -1;
         lpr[b] = l;
-        const int64_t per = 64 / l;
+        const int64_t per = 16 / l;
+        // steps: [first row, end row) in `order` positions, a level's rows cut every `per`
+        std::vector<std::pair<int64_t, int64_t>> steps;
+        for (int64_t g = goff[b]; g < goff[b + 1]; ++g)
+            for (int64_t r0 = grp[g]; r0 < grp[g + 1]; r0 += per) steps.push_back({r0, std::min(grp[g + 1], r0 + per)});
+        total += (int64_t)steps.size();
+        if (dry) continue;
         std::vector<int32_t> sizes;
         base[b] = (int64_t)col.size();
-        for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {
-            for (int64_t r0 = grp[g]; r0 < grp[g + 1]; r0 += per) {
-                const int64_t r1 = std::min(grp[g + 1], r0 + per);
-                ++total;
-                if (dry) continue;
-                int64_t mm = 0;
-                for (int64_t r = r0; r < r1; ++r) mm = std::max(mm, (rlen(order[r]) + l - 1) / l);
-                const int L = mm + 1 <= 4 ? 4 : 8;
-                const int64_t nl = (r1 - r0) * l, sz = 4 + nl * L;
-                sizes.push_back((int32_t)(sz | (L == 8 ? 1 : 0)));
-                const int64_t at = (int64_t)col.size();
-                col.resize(at + sz, 0);
-                val.resize(at + sz, 0.0);
-                for (int64_t rr = 0; rr < r1 - r0; ++rr) {
-                    const int64_t i = order[r0 + rr];
+        for (size_t s0 = 0; s0 < steps.size(); s0 += 4) {
+            const size_t ns = std::min<size_t>(4, steps.size() - s0);
+            int64_t mm = 0;
+            for (size_t q = 0; q < ns; ++q)
+                for (int64_t r = steps[s0 + q].first; r < steps[s0 + q].second; ++r)
+                    mm = std::max(mm, (rlen(order[r]) + l - 1) / l);
+            const int L = mm + 1 <= 4 ? 4 : 8;
+            const int64_t nl = 16 * (int64_t)ns, sz = nl * L;
+            sizes.push_back((int32_t)(sz | (L == 8 ? 1 : 0)));
+            const int64_t at = (int64_t)col.size();
+            col.resize(at + sz, 0);
+            val.resize(at + sz, 0.0);
+            for (int64_t lane = 0; lane < nl; ++lane) col[at + lane * L] = PAD;  // lanes without a row
+            for (size_t q = 0; q < ns; ++q) {
+                for (int64_t r = steps[s0 + q].first; r < steps[s0 + q].second; ++r) {
+                    const int64_t rr = r - steps[s0 + q].first;
+                    const int64_t i = order[r];
                     const int64_t src = upper ? dg[i] + 1 : rp[i], len = rlen(i);
                     for (int sub = 0; sub < l; ++sub) {
                         const int64_t mine = len > sub ? (len - sub + l - 1) / l : 0;
-                        const int64_t e = at + 4 + (rr * l + sub) * L;
+                        const int64_t e = at + (16 * (int64_t)q + rr * l + sub) * L;
                         col[e] = (int32_t)(i - b0) | (int32_t)(mine << 18);
                         val[e] = upper ? dinv[i] : 0.0;
                         for (int64_t k = 1; k <= mine; ++k) {
@@ -1151,14 +1161,9 @@ static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, co
                 }
             }
         }
-        if (dry) continue;
         nsl[b] = (int64_t)sizes.size();
-        int64_t at = base[b];
-        for (size_t k = 0; k < sizes.size(); ++k) {  // slice k's descriptor: the size of slice k + ND
-            col[at] = k + ND < sizes.size() ? sizes[k + ND] : 0;
-            at += sizes[k] & ~3;
-        }
-        for (int k = 0; k < ND && k < (int)sizes.size(); ++k) first[(size_t)b * ND + k] = sizes[k];
+        soff[b] = (int64_t)szs.size();
+        szs.insert(szs.end(), sizes.begin(), sizes.end());
     }
     if (dry) return total;
     auto up = [&](auto &d, const auto &v) {
@@ -1167,7 +1172,8 @@ static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, co
     };
     up(D->base, base);
     up(D->nsl, nsl);
-    up(D->first, first);
+    up(D->soff, soff);
+    up(D->sz, szs);
     up(D->lpr, lpr);
     up(D->col, col);
     up(D->val, val);
@@ -1274,10 +1280,11 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             ring = wmax <= ilu_ring_chunk();
         }
         if (use_lds && !gmem && c.sweep_chain != 0 && force_lpr == 0) {
-            // the chain sweep (one wave per block, slices in order, 8 in flight) for
-            // deep, narrow level DAGs: measured ~0.77 us per level for the workgroup
-            // sweep on the footing smoother chunks; a chain slice costs a fraction of
-            // that, so chain when slices <= 3.5 x levels (both triangles)
+            // the chain sweep (one wave per block, 16-lane steps in order, up to 32
+            // steps of factor data in flight) for deep, narrow level DAGs: measured
+            // ~0.77 us per level for the workgroup sweep on the footing smoother
+            // chunks; a chain step costs a fraction of that, so chain when steps <=
+            // 3.5 x levels (both triangles)
             const std::vector<int64_t> bst = block_starts(n, nblocks, bnd);
             const std::vector<double> none;
             const int64_t sL = build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oL, gL, fL, false, nullptr, c);
@@ -1385,9 +1392,9 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
         return;
     }
     if (use_lds && chain) {
-        launch_ilu_blocks_chain(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, Lc.base.p, Lc.first.p, Lc.nsl.p,
-                                Lc.lpr.p, Lc.col.p, Lc.val.p, Uc.base.p, Uc.first.p, Uc.nsl.p, Uc.lpr.p, Uc.col.p,
-                                Uc.val.p, x, y, max_len, c.st);
+        launch_ilu_blocks_chain(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, Lc.base.p, Lc.soff.p, Lc.sz.p,
+                                Lc.nsl.p, Lc.lpr.p, Lc.col.p, Lc.val.p, Uc.base.p, Uc.soff.p, Uc.sz.p, Uc.nsl.p,
+                                Uc.lpr.p, Uc.col.p, Uc.val.p, x, y, max_len, c.st);
         return;
     }
     if (use_lds) {

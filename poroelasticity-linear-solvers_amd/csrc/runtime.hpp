@@ -284,8 +284,8 @@ struct RingTri {
 };
 // Chain-sweep stream of one triangle (kernels.hip, k_ilu_blocks_chain)
 struct ChainTri {
-    DBuf<int64_t> base, nsl;      // per block: first entry, slice count
-    DBuf<int32_t> first, lpr;     // per block: sizes of the first ilu_chain_depth() slices, lanes per row
+    DBuf<int64_t> base, soff, nsl;  // per block: first entry, first slice, slice count
+    DBuf<int32_t> sz, lpr;          // per slice: size | (8 entries per lane); per block: lanes per row
     DBuf<int32_t> col;
     DBuf<double> val;
 };

@@ -10,6 +10,7 @@
 #   bench                       the headline bench line (default flags)
 #   prof                        rocprofv3 --kernel-trace --stats of the headline
 #   prof_fe                     same for the assembled 3-D N=12 whole-block ILU solve
+#   prof_fe24                   same at 3-D N=24 (721,519 DoF; the FE SpMV layout), 10 its
 #   prof_footing                same for configs[2] (footing-inexact-ilu, band-LU Schur block)
 #   footing                     configs[2] bench on the assembled footing system (N=128)
 #   prof_footing_fe             rocprofv3 of that solve
@@ -59,6 +60,7 @@ for s in "$@"; do
       prof_amg) prof prof_amg --N 27 --inner hypre --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
       prof_amg59) prof prof_amg59 --inner hypre --steps 1 --warmup 1 --no-cpu --no-copy-probe ;;
       prof_fe) prof prof_fe --system fe --N 12 --inner ilu --steps 2 --warmup 1 --no-cpu --no-copy-probe ;;
+      prof_fe24) prof prof_fe24 --system fe --N 24 --inner ilu --steps 1 --warmup 1 --maxit 10 --no-cpu --no-copy-probe ;;
       configs)
         run configs/swelling2d-exact 400 python -u bench.py --config swelling2d-exact --steps 3 --no-copy-probe
         run configs/footing-inexact-ilu 400 python -u bench.py --config footing-inexact-ilu --steps 2 --no-copy-probe
