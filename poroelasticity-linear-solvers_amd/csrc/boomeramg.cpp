@@ -29,6 +29,7 @@
 #include <limits>
 #include <map>
 #include <queue>
+#include <thread>
 
 #include "amg_host.hpp"
 #include "kernels.hpp"
@@ -100,16 +101,62 @@ Pattern strength(const HostCSR &A, double theta, double mu) {
     return concat_pattern(n, part);
 }
 
+// S^T with every column's rows ascending (the sequential fill's order): per
+// thread column counts over its row range, offsets thread-major inside each
+// column, then every thread fills its rows -- memory-bound, on host threads
+// (the sequential transpose was ~1.6 s of the N=40 s block's RS pass)
 Pattern transpose(const Pattern &S) {
+    const int64_t n = S.n, nnz = (int64_t)S.ci.size();
     Pattern T;
-    T.n = S.n;
-    T.rp.assign(S.n + 1, 0);
-    for (int32_t j : S.ci) ++T.rp[j + 1];
-    for (int64_t j = 0; j < S.n; ++j) T.rp[j + 1] += T.rp[j];
-    T.ci.resize(S.ci.size());
-    std::vector<int64_t> pos(T.rp.begin(), T.rp.end() - 1);
-    for (int64_t i = 0; i < S.n; ++i)
-        for (int64_t k = S.rp[i]; k < S.rp[i + 1]; ++k) T.ci[pos[S.ci[k]]++] = (int32_t)i;
+    T.n = n;
+    T.rp.assign(n + 1, 0);
+    T.ci.resize(nnz);
+    int Tn = setup_threads();
+    if (nnz < (int64_t)1 << 20 || n < 1024) Tn = 1;
+    if (Tn == 1) {
+        for (int32_t j : S.ci) ++T.rp[j + 1];
+        for (int64_t j = 0; j < n; ++j) T.rp[j + 1] += T.rp[j];
+        std::vector<int64_t> pos(T.rp.begin(), T.rp.end() - 1);
+        for (int64_t i = 0; i < n; ++i)
+            for (int64_t k = S.rp[i]; k < S.rp[i + 1]; ++k) T.ci[pos[S.ci[k]]++] = (int32_t)i;
+        return T;
+    }
+    std::vector<int64_t> r0(Tn + 1);
+    for (int t = 0; t <= Tn; ++t) r0[t] = n * t / Tn;
+    std::vector<std::vector<int64_t>> cnt(Tn);
+    auto run = [&](auto fn) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < Tn; ++t) th.emplace_back(fn, t);
+        for (auto &x : th) x.join();
+    };
+    run([&](int t) {
+        cnt[t].assign(n, 0);
+        for (int64_t k = S.rp[r0[t]]; k < S.rp[r0[t + 1]]; ++k) ++cnt[t][S.ci[k]];
+    });
+    // column lengths, then per-thread starts inside each column (column ranges in parallel)
+    run([&](int t) {
+        for (int64_t j = r0[t]; j < r0[t + 1]; ++j) {
+            int64_t c = 0;
+            for (int q = 0; q < Tn; ++q) c += cnt[q][j];
+            T.rp[j + 1] = c;
+        }
+    });
+    for (int64_t j = 0; j < n; ++j) T.rp[j + 1] += T.rp[j];
+    run([&](int t) {
+        for (int64_t j = r0[t]; j < r0[t + 1]; ++j) {
+            int64_t o = T.rp[j];
+            for (int q = 0; q < Tn; ++q) {
+                const int64_t c = cnt[q][j];
+                cnt[q][j] = o;
+                o += c;
+            }
+        }
+    });
+    run([&](int t) {
+        std::vector<int64_t> &pos = cnt[t];
+        for (int64_t i = r0[t]; i < r0[t + 1]; ++i)
+            for (int64_t k = S.rp[i]; k < S.rp[i + 1]; ++k) T.ci[pos[S.ci[k]]++] = (int32_t)i;
+    });
     return T;
 }
 

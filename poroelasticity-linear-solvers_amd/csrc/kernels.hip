@@ -2512,10 +2512,10 @@ struct NwSlot {
 };
 
 __device__ __forceinline__ void nw_issue(const int32_t *col, const double *val, int64_t base, int32_t szf, int lane,
-                                         NwSlot &s) {
-    const int sz = szf & ~3;
+                                         NwSlot &s, int probe) {
     const int L = (szf & 1) ? 8 : 4;
-    s.nl = sz / L;
+    s.nl = (szf & ~3) / L;
+    const int sz = (probe & 16) ? 0 : (szf & ~3);  // (diagnostics: no factor traffic)
     // range-checked to the slice: lanes past nl and slices past the block's
     // end (size 0) read zeros without traffic; every path issues the same
     // 6 loads, so the compiler's vmcnt bookkeeping stays exact
@@ -2567,9 +2567,10 @@ __device__ __forceinline__ void nw_compute(const NwSlot &s, double *ys, int lane
     }
 }
 
+// probe (pls.ring_probe bits 3 / 4; diagnostics, results wrong): no compute / no factor traffic
 template <int LPR>
 __device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *sz, int64_t nsl, const int32_t *col,
-                                         const double *val, double *ys, int lane, bool upper) {
+                                         const double *val, double *ys, int lane, bool upper, int probe) {
     if (nsl <= 0) return;
     // slice sizes: lane l of `win` holds slice w0 + l, of `nxt` slice w0 + 64 + l
     // (loaded a window ahead, so picking from it never waits on a fresh load)
@@ -2586,7 +2587,7 @@ __device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *sz, int64_
 #pragma unroll
     for (int k = 0; k < NW_D; ++k) {
         const int32_t f = size_of(k);
-        nw_issue(col, val, ib, f, lane, s[k]);
+        nw_issue(col, val, ib, f, lane, s[k], probe);
         ib += f & ~3;
     }
     // whole rounds of NW_D slices without an exit inside (a loop exit between the
@@ -2602,26 +2603,27 @@ __device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *sz, int64_
         }
 #pragma unroll
         for (int k = 0; k < NW_D; ++k) {
-            nw_compute<LPR>(s[k], ys, lane, upper);
+            if (!(probe & 8)) nw_compute<LPR>(s[k], ys, lane, upper);
             const int32_t f = size_of(t0 + k);
-            nw_issue(col, val, ib, f, lane, s[k]);
+            nw_issue(col, val, ib, f, lane, s[k], probe);
             ib += f & ~3;
         }
     }
     const int rem = (int)(nsl - rounds * NW_D);
 #pragma unroll
     for (int k = 0; k < NW_D; ++k)
-        if (k < rem) nw_compute<LPR>(s[k], ys, lane, upper);
+        if (k < rem && !(probe & 8)) nw_compute<LPR>(s[k], ys, lane, upper);
 }
 
 __device__ __forceinline__ void nw_dispatch(int lpr, int64_t base, const int32_t *sz, int64_t nsl,
-                                            const int32_t *col, const double *val, double *ys, int lane, bool upper) {
+                                            const int32_t *col, const double *val, double *ys, int lane, bool upper,
+                                            int probe) {
     switch (lpr) {
-        case 16: nw_sweep<16>(base, sz, nsl, col, val, ys, lane, upper); break;
-        case 8: nw_sweep<8>(base, sz, nsl, col, val, ys, lane, upper); break;
-        case 4: nw_sweep<4>(base, sz, nsl, col, val, ys, lane, upper); break;
-        case 2: nw_sweep<2>(base, sz, nsl, col, val, ys, lane, upper); break;
-        default: nw_sweep<1>(base, sz, nsl, col, val, ys, lane, upper); break;
+        case 16: nw_sweep<16>(base, sz, nsl, col, val, ys, lane, upper, probe); break;
+        case 8: nw_sweep<8>(base, sz, nsl, col, val, ys, lane, upper, probe); break;
+        case 4: nw_sweep<4>(base, sz, nsl, col, val, ys, lane, upper, probe); break;
+        case 2: nw_sweep<2>(base, sz, nsl, col, val, ys, lane, upper, probe); break;
+        default: nw_sweep<1>(base, sz, nsl, col, val, ys, lane, upper, probe); break;
     }
 }
 
@@ -2640,8 +2642,9 @@ __global__ __launch_bounds__(64) void k_ilu_blocks_chain(
     const int lane = threadIdx.x;
     for (int64_t t = lane; t < len; t += 64) ys[t] = x[b0 + t];
     __syncthreads();
-    nw_dispatch(Llpr[blk], Lbase[blk], Lsz + Lsoff[blk], Lnsl[blk], Lcol, Lval, ys, lane, false);
-    nw_dispatch(Ulpr[blk], Ubase[blk], Usz + Usoff[blk], Unsl[blk], Ucol, Uval, ys, lane, true);
+    const int probe = __builtin_amdgcn_readfirstlane(ring_probe);
+    nw_dispatch(Llpr[blk], Lbase[blk], Lsz + Lsoff[blk], Lnsl[blk], Lcol, Lval, ys, lane, false, probe);
+    nw_dispatch(Ulpr[blk], Ubase[blk], Usz + Usoff[blk], Unsl[blk], Ucol, Uval, ys, lane, true, probe);
     __syncthreads();
     for (int64_t t = lane; t < len; t += 64) y[b0 + t] = ys[t];
 }
