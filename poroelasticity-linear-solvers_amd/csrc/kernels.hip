@@ -2539,7 +2539,7 @@ __device__ __forceinline__ void nw_issue(const int32_t *col, const double *val, 
 }
 
 template <int LPR>
-__device__ __forceinline__ void nw_compute(const NwSlot &s, double *ys, int lane, bool upper) {
+__device__ __forceinline__ void nw_compute(const NwSlot &s, double *ys, int lane, bool upper, int probe) {
     const int nsteps = s.nl >> 4;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // the slice's steps in order: step q is lanes 16q .. 16q + 15
@@ -2562,12 +2562,14 @@ __device__ __forceinline__ void nw_compute(const NwSlot &s, double *ys, int lane
             if (lg >= 2) acc += dpp_d<0x4E>(acc);
             if (lg >= 3) acc += dpp_d<0x141>(acc);
             if (lg >= 4) acc += dpp_d<0x140>(acc);
-            if ((lane & (LPR - 1)) == 0 && li != SW_ROW_PAD) ys[li] = upper ? (yi - acc) * s.v[0] : yi - acc;
+            if (!(probe & 32) && (lane & (LPR - 1)) == 0 && li != SW_ROW_PAD)
+                ys[li] = upper ? (yi - acc) * s.v[0] : yi - acc;
         }
     }
 }
 
-// probe (pls.ring_probe bits 3 / 4; diagnostics, results wrong): no compute / no factor traffic
+// probe (pls.ring_probe bits 3 / 4 / 5; diagnostics, results wrong): no compute / no factor
+// traffic / no LDS update of the row (no step waits on the previous one)
 template <int LPR>
 __device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *sz, int64_t nsl, const int32_t *col,
                                          const double *val, double *ys, int lane, bool upper, int probe) {
@@ -2603,7 +2605,7 @@ __device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *sz, int64_
         }
 #pragma unroll
         for (int k = 0; k < NW_D; ++k) {
-            if (!(probe & 8)) nw_compute<LPR>(s[k], ys, lane, upper);
+            if (!(probe & 8)) nw_compute<LPR>(s[k], ys, lane, upper, probe);
             const int32_t f = size_of(t0 + k);
             nw_issue(col, val, ib, f, lane, s[k], probe);
             ib += f & ~3;
@@ -2612,7 +2614,7 @@ __device__ __forceinline__ void nw_sweep(int64_t base, const int32_t *sz, int64_
     const int rem = (int)(nsl - rounds * NW_D);
 #pragma unroll
     for (int k = 0; k < NW_D; ++k)
-        if (k < rem && !(probe & 8)) nw_compute<LPR>(s[k], ys, lane, upper);
+        if (k < rem && !(probe & 8)) nw_compute<LPR>(s[k], ys, lane, upper, probe);
 }
 
 __device__ __forceinline__ void nw_dispatch(int lpr, int64_t base, const int32_t *sz, int64_t nsl,
