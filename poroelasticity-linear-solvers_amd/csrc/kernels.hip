@@ -2495,10 +2495,10 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
 // vmcnt covers <= 63 outstanding), i.e. up to 32 steps of look-ahead.
 //
 // Stream layout (per triangle, runtime.cpp build_chain_tri): a slice is nl *
-// L entries (nl = 16 x its steps, L = 4 or 8 entries per lane, lane-major),
-// lane l's header (col = local row | count << SW_ROW_BITS, SW_ROW_PAD: no
-// row; val = 1 / U_ii for the upper triangle) then its factor entries at l *
-// L; slices follow one another, and a separate array holds every slice's size
+// L entries (nl = 16 x its steps, L = 8 entries per lane, lane-major), lane
+// l's header (col = local row | count << SW_ROW_BITS, SW_ROW_PAD: no row; val
+// = 1 / U_ii for the upper triangle) then its factor entries at l * L, unused
+// ones (column 0, value 0: summed unmasked); slices follow one another, and a separate array holds every slice's size
 // | (L == 8), read 64 slices at a time into a vector register (lane l: slice
 // w0 + l) and picked with v_readlane.  A row's entries are dealt round robin
 // over its LPR lanes and the partial sums combined by the DPP tree of
@@ -2545,18 +2545,16 @@ __device__ __forceinline__ void nw_compute(const NwSlot &s, double *ys, int lane
     for (int q = 0; q < 4; ++q) {  // the slice's steps in order: step q is lanes 16q .. 16q + 15
         if (q < nsteps && (lane >> 4) == q) {
             const int32_t h = s.c[0];
-            const int32_t len = (int32_t)((uint32_t)h >> SW_ROW_BITS);
             const int32_t li = h & SW_ROW_PAD;
             // the row's own input first, then every dependency read before the first is consumed
             const double yi = ys[li != SW_ROW_PAD ? li : 0];
             double acc = 0.0, d[8];
+            // entries past a lane's count are stored as (column 0, value 0): no
+            // per-entry masking, and 0 * y adds nothing (the LDS sweep's sums bitwise)
 #pragma unroll
-            for (int u = 1; u < 8; ++u) d[u] = ys[u <= len ? s.c[u] : 0];
+            for (int u = 1; u < 8; ++u) d[u] = ys[s.c[u]];
 #pragma unroll
-            for (int u = 1; u < 8; ++u) {
-                const double t = __dmul_rn(s.v[u], d[u]);  // the LDS sweep's rounding (no contraction)
-                acc += (u <= len) ? t : 0.0;
-            }
+            for (int u = 1; u < 8; ++u) acc += __dmul_rn(s.v[u], d[u]);  // no contraction: the LDS sweep's rounding
             constexpr int lg = LPR >= 16 ? 4 : LPR >= 8 ? 3 : LPR >= 4 ? 2 : LPR >= 2 ? 1 : 0;
             if (lg >= 1) acc += dpp_d<0xB1>(acc);
             if (lg >= 2) acc += dpp_d<0x4E>(acc);

@@ -1131,11 +1131,9 @@ static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, co
         base[b] = (int64_t)col.size();
         for (size_t s0 = 0; s0 < steps.size(); s0 += 4) {
             const size_t ns = std::min<size_t>(4, steps.size() - s0);
-            int64_t mm = 0;
-            for (size_t q = 0; q < ns; ++q)
-                for (int64_t r = steps[s0 + q].first; r < steps[s0 + q].second; ++r)
-                    mm = std::max(mm, (rlen(order[r]) + l - 1) / l);
-            const int L = mm + 1 <= 4 ? 4 : 8;
+            // 8 entries per lane (header + 7; the lanes per row keep every share <= 7),
+            // unused ones (column 0, value 0): the kernel sums all 7 without masking
+            const int L = 8;
             const int64_t nl = 16 * (int64_t)ns, sz = nl * L;
             sizes.push_back((int32_t)(sz | (L == 8 ? 1 : 0)));
             const int64_t at = (int64_t)col.size();
