@@ -29,8 +29,24 @@ Ctx::Ctx() {
     comm = &g_self_comm;
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     partial.alloc(1024 * 136);
+    partial_n = 1024 * 136;
     dscal.alloc(4096);
     HIPCHK(hipHostMalloc((void **)&hscal, sizeof(double) * 4096, hipHostMallocDefault));
+    hscal_n = 4096;
+}
+void Ctx::ensure_partial(int64_t n, int64_t cols) {
+    const int64_t need = (int64_t)reduce_blocks(n) * std::max<int64_t>(cols, 1);
+    if (need > partial_n) {
+        HIPCHK(hipStreamSynchronize(st));
+        partial.alloc(need);
+        partial_n = need;
+    }
+    if (cols + 2 > hscal_n) {
+        HIPCHK(hipStreamSynchronize(st));
+        if (hscal) (void)hipHostFree(hscal);
+        HIPCHK(hipHostMalloc((void **)&hscal, sizeof(double) * (cols + 2), hipHostMallocDefault));
+        hscal_n = cols + 2;
+    }
 }
 Ctx::~Ctx() {
     if (hscal) (void)hipHostFree(hscal);
@@ -1926,8 +1942,12 @@ void KSP::resolve_side_norm(const std::string &side, const std::string &nt) {
     throw Error("KSP type '" + type + "' (prefix " + prefix + ") is not available (supported: gmres, cg, preonly)");
 }
 
-void KSP::ensure_work(Ctx &) {
+void KSP::ensure_work(Ctx &c) {
     if (type == "gmres") {
+        // CGS dots of up to restart + 1 columns: one partial per (column, block)
+        // (the context's default room, 136 columns at the largest grid, overflowed
+        // past ~450 iterations of a 1.3M-row solve)
+        c.ensure_partial(n, restart + 2);
         if (allocated_k != restart) {
             ldv = (n + 63) & ~(int64_t)63;  // 512-B aligned columns (16-B loads)
             V.alloc((size_t)(restart + 1) * ldv);

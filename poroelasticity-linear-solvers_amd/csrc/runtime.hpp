@@ -64,7 +64,9 @@ struct DBuf {
 struct Ctx {
     hipStream_t st = nullptr;
     Comm *comm = nullptr;   // global reductions (CommSelf unless distributed)
-    DBuf<double> partial;   // reduction partials (NB_MAX * 136)
+    DBuf<double> partial;   // reduction partials (>= NB_MAX * 136; ensure_partial grows it)
+    int64_t partial_n = 0;
+    int64_t hscal_n = 0;    // doubles in the pinned host mirror
     DBuf<double> dscal;     // device scalars
     double *hscal = nullptr;  // pinned host mirror
     bool sell_d16 = true;     // build SpMV layouts as SELL-64/D16 where every row fits
@@ -90,6 +92,9 @@ struct Ctx {
     ~Ctx();
     void sync() { HIPCHK(hipStreamSynchronize(st)); }
     void ensure_scan(int64_t n);
+    // room for `cols` reductions of n entries (CGS: one partial per column and block) and
+    // for `cols` + 2 doubles in the host mirror; setup only (frees the old buffers)
+    void ensure_partial(int64_t n, int64_t cols);
     // deterministic reductions returning host values (synchronising)
     double dot(int64_t n, const double *x, const double *y);
     double norm2(int64_t n, const double *x);

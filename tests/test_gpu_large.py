@@ -117,3 +117,30 @@ def test_full_size_three_way():
     for a in (b, x, r, x2):
         a.free()
     h.destroy()
+
+
+def test_gmres_longer_than_the_default_reduction_room():
+    """A GMRES cycle longer than the context's default CGS reduction room
+    (one partial per column and reduction block: 1024 x 136 doubles, i.e.
+    ~560 columns at the 247 blocks of this 1.0M-row system): restart =
+    maxit = 600 (footing.py's maxiter is 500, on 1.3M rows) runs to its last
+    iteration with finite, non-increasing residual estimates (round 3: the
+    buffer now grows with the restart length; before, the CGS partials of
+    columns past ~450 of footing N=128 overran it and faulted the GPU)."""
+    import lib._native as Nt
+    from lib.handle import Handle
+    opts = _opts(1, 1, {"s_pc_type": "jacobi", "fp_pc_type": "jacobi", "pls.inner_pc_type": "jacobi",
+                        "pls.solver_rtol": "1e-300", "pls.solver_atol": "0", "pls.solver_maxiter": "600"})
+    h = Handle.synthetic(3, 27, 20261015, 0.05, opts)
+    n = h.n
+    assert n >= 1_000_000
+    b, x = Nt.DeviceArray(n), Nt.DeviceArray(n)
+    h.rhs_device(7, b.p)
+    res = h.solve_device(b.p, x.p)
+    hist = h.history()
+    assert res.its == 600 and res.reason < 0
+    assert len(hist) == 601 and np.all(np.isfinite(hist)) and np.all(np.diff(hist) <= 0)
+    assert np.all(np.isfinite(x.download()))
+    b.free()
+    x.free()
+    h.destroy()
