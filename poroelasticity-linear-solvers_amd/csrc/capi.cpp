@@ -523,6 +523,9 @@ struct Handle {
         ctx.spmv_b3 = opt.flag("pls.spmv_b3", false);
         ctx.spmv_rcm = (int)opt.integer("pls.spmv_rcm", -1);
         ctx.sweep_chain = (int)opt.integer("pls.sweep_chain", -1);
+        if (opt.flag("pls.debug_bounds", false) || opt.integer("pls.debug_partial_cap", 0) > 0)
+            ctx.set_debug(opt.flag("pls.debug_bounds", false), opt.integer("pls.debug_partial_cap", 0),
+                          opt.flag("pls.debug_no_grow", false), opt.flag("pls.debug_unguarded", false));
         if (ctx.d16_sorted_lpr != 1 && ctx.d16_sorted_lpr != 2 && ctx.d16_sorted_lpr != 4 && ctx.d16_sorted_lpr != 8 &&
             ctx.d16_sorted_lpr != 16)
             throw Error("pls.d16_sorted_lpr must be 1, 2, 4, 8 or 16");

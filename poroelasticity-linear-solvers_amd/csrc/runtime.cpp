@@ -34,12 +34,50 @@ Ctx::Ctx() {
     HIPCHK(hipHostMalloc((void **)&hscal, sizeof(double) * 4096, hipHostMallocDefault));
     hscal_n = 4096;
 }
+static constexpr double CANARY_VALUE = -1.2345678901234567e300;
+
+static void alloc_partial(Ctx &c, int64_t count) {
+    c.partial.alloc(count + (c.debug_bounds ? Ctx::CANARY : 0));
+    c.partial_n = count;
+    if (c.debug_bounds) launch_set(Ctx::CANARY, CANARY_VALUE, c.partial.p + count, c.st);
+}
+void Ctx::set_debug(bool bounds, int64_t cap, bool no_grow, bool unguarded) {
+    HIPCHK(hipStreamSynchronize(st));
+    debug_bounds = bounds;
+    debug_no_grow = no_grow;
+    debug_unguarded = unguarded;
+    alloc_partial(*this, cap > 0 ? cap : partial_n);
+    HIPCHK(hipStreamSynchronize(st));
+}
+void Ctx::check_bounds() {
+    if (!debug_bounds) return;
+    std::vector<double> h(CANARY);
+    HIPCHK(hipMemcpyAsync(h.data(), partial.p + partial_n, sizeof(double) * CANARY, hipMemcpyDeviceToHost, st));
+    sync();
+    for (int64_t i = 0; i < CANARY; ++i)
+        if (h[i] != CANARY_VALUE)
+            throw Error("pls.debug_bounds: the canary behind the reduction partials was overwritten at +" +
+                        std::to_string(i) + " (room " + std::to_string(partial_n) + " doubles)");
+}
+double *Ctx::partials(int64_t n, int64_t cols) {
+    const int64_t need = (int64_t)reduce_blocks(n) * std::max<int64_t>(cols, 1);
+    if (need > partial_n && !debug_unguarded)
+        throw Error("reduction partials: " + std::to_string(cols) + " reductions of " + std::to_string(n) +
+                    " entries need " + std::to_string(need) + " doubles, the context holds " +
+                    std::to_string(partial_n) + " (missing ensure_partial)");
+    return partial.p;
+}
+double *Ctx::host_scalars(int64_t count) {
+    if (count > hscal_n)
+        throw Error("host scalar mirror: " + std::to_string(count) + " doubles requested, " + std::to_string(hscal_n) +
+                    " held (missing ensure_partial)");
+    return hscal;
+}
 void Ctx::ensure_partial(int64_t n, int64_t cols) {
     const int64_t need = (int64_t)reduce_blocks(n) * std::max<int64_t>(cols, 1);
-    if (need > partial_n) {
+    if (need > partial_n && !debug_no_grow) {
         HIPCHK(hipStreamSynchronize(st));
-        partial.alloc(need);
-        partial_n = need;
+        alloc_partial(*this, need);
     }
     if (cols + 2 > hscal_n) {
         HIPCHK(hipStreamSynchronize(st));
@@ -63,18 +101,20 @@ void Ctx::ensure_scan(int64_t n) {
     }
 }
 double Ctx::dot(int64_t n, const double *x, const double *y) {
-    launch_dot(n, x, y, partial.p, dscal.p, st);
+    launch_dot(n, x, y, partials(n, 1), dscal.p, st);
     comm->global_sum_dev(dscal.p, 1, st);
-    HIPCHK(hipMemcpyAsync(hscal, dscal.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    double *h = host_scalars(1);
+    HIPCHK(hipMemcpyAsync(h, dscal.p, sizeof(double), hipMemcpyDeviceToHost, st));
     sync();
-    return hscal[0];
+    return h[0];
 }
 double Ctx::norm2(int64_t n, const double *x) {
-    launch_dot(n, x, x, partial.p, dscal.p, st);
+    launch_dot(n, x, x, partials(n, 1), dscal.p, st);
     comm->global_sum_dev(dscal.p, 1, st);
-    HIPCHK(hipMemcpyAsync(hscal, dscal.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    double *h = host_scalars(1);
+    HIPCHK(hipMemcpyAsync(h, dscal.p, sizeof(double), hipMemcpyDeviceToHost, st));
     sync();
-    return std::sqrt(hscal[0]);
+    return std::sqrt(h[0]);
 }
 
 // ================================================================== CSR ===
@@ -1993,6 +2033,7 @@ void KSP::solve(const double *b, double *x, Ctx &c) {
     stat_its += its;
     stat_max = std::max<int64_t>(stat_max, its);
     ++stat_solves;
+    c.check_bounds();
 }
 
 KSP::~KSP() {
@@ -2047,14 +2088,15 @@ void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
                 pc->apply(t1p, vn, c);
             }
             const int k = (int)(loc_it + 1);
-            launch_mdot(n, k, nullptr, V.p, ldv, vn, c.partial.p, dh.p, c.st);
+            launch_mdot(n, k, nullptr, V.p, ldv, vn, c.partials(n, k), dh.p, c.st);
             c.comm->global_sum_dev(dh.p, k, c.st);
-            launch_maxpy_norm(n, k, V.p, ldv, dh.p, -1.0, vn, c.partial.p, dh.p + k, c.st);
+            launch_maxpy_norm(n, k, V.p, ldv, dh.p, -1.0, vn, c.partials(n, 1), dh.p + k, c.st);
             c.comm->global_sum_dev(dh.p + k, 1, c.st);
-            HIPCHK(hipMemcpyAsync(c.hscal, dh.p, sizeof(double) * (k + 1), hipMemcpyDeviceToHost, c.st));
+            double *hs = c.host_scalars(k + 1);
+            HIPCHK(hipMemcpyAsync(hs, dh.p, sizeof(double) * (k + 1), hipMemcpyDeviceToHost, c.st));
             c.sync();
-            for (int j = 0; j < k; ++j) H(j, loc_it) = c.hscal[j];
-            const double tt = std::sqrt(c.hscal[k]);
+            for (int j = 0; j < k; ++j) H(j, loc_it) = hs[j];
+            const double tt = std::sqrt(hs[k]);
             H(loc_it + 1, loc_it) = tt;
             double hapbnd = std::fabs(tt / grs[loc_it]);
             if (hapbnd > haptol) hapbnd = haptol;

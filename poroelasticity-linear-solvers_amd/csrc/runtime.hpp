@@ -95,6 +95,18 @@ struct Ctx {
     // room for `cols` reductions of n entries (CGS: one partial per column and block) and
     // for `cols` + 2 doubles in the host mirror; setup only (frees the old buffers)
     void ensure_partial(int64_t n, int64_t cols);
+    // every launch that writes `partial` / `hscal` takes its pointer from these:
+    // they throw Error when the request exceeds the room (the round-3 fault was a
+    // silent overrun of `partial` by a 453-column CGS block)
+    double *partials(int64_t n, int64_t cols);
+    double *host_scalars(int64_t count);
+    // pls.debug_bounds: a canary region behind `partial` (checked by check_bounds,
+    // which throws Error when it was written); pls.debug_partial_cap /
+    // pls.debug_no_grow / pls.debug_unguarded reproduce the round-3 overrun in tests
+    bool debug_bounds = false, debug_no_grow = false, debug_unguarded = false;
+    static constexpr int64_t CANARY = 1 << 16;
+    void set_debug(bool bounds, int64_t cap, bool no_grow, bool unguarded);
+    void check_bounds();
     // deterministic reductions returning host values (synchronising)
     double dot(int64_t n, const double *x, const double *y);
     double norm2(int64_t n, const double *x);

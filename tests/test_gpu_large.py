@@ -131,6 +131,8 @@ def test_gmres_longer_than_the_default_reduction_room():
     from lib.handle import Handle
     opts = _opts(1, 1, {"s_pc_type": "jacobi", "fp_pc_type": "jacobi", "pls.inner_pc_type": "jacobi",
                         "pls.solver_rtol": "1e-300", "pls.solver_atol": "0", "pls.solver_maxiter": "600"})
+    # pls.debug_bounds: a canary region behind the partials, checked after every KSP solve
+    opts["pls.debug_bounds"] = "1"
     h = Handle.synthetic(3, 27, 20261015, 0.05, opts)
     n = h.n
     assert n >= 1_000_000
@@ -144,3 +146,37 @@ def test_gmres_longer_than_the_default_reduction_room():
     b.free()
     x.free()
     h.destroy()
+
+
+def _long_cycle(extra):
+    import lib._native as Nt
+    from lib.handle import Handle
+    opts = _opts(1, 1, {"s_pc_type": "jacobi", "fp_pc_type": "jacobi", "pls.inner_pc_type": "jacobi",
+                        "pls.solver_rtol": "1e-300", "pls.solver_atol": "0", "pls.solver_maxiter": "600"})
+    opts.update(extra)
+    h = Handle.synthetic(3, 8, 20261015, 0.05, opts)  # 30,207 rows: 8 reduction blocks
+    b, x = Nt.DeviceArray(h.n), Nt.DeviceArray(h.n)
+    try:
+        h.rhs_device(7, b.p)
+        return h.solve_device(b.p, x.p)
+    finally:
+        b.free()
+        x.free()
+        h.destroy()
+
+
+def test_partials_overrun_is_caught():
+    """The round-3 failure mode, reproduced inside the canary: the context's
+    partials are capped at 100 doubles and not grown (the old fixed buffer,
+    scaled down) so a 600-column CGS cycle needs 8 x 600.  Unguarded, the
+    CGS partials of columns past 12 land in the canary region behind the
+    buffer and check_bounds reports it; with the launch-site guard (the
+    default) the first oversized launch throws before writing anything; with
+    growth (the default) the same cycle runs to its end, canary intact."""
+    base = {"pls.debug_bounds": "1", "pls.debug_partial_cap": "100", "pls.debug_no_grow": "1"}
+    with pytest.raises(RuntimeError, match="canary"):
+        _long_cycle(dict(base, **{"pls.debug_unguarded": "1"}))
+    with pytest.raises(RuntimeError, match="reduction partials"):
+        _long_cycle(base)
+    res = _long_cycle({"pls.debug_bounds": "1", "pls.debug_partial_cap": "100"})
+    assert res.its == 600
