@@ -390,6 +390,13 @@ def main():
     if mode == "error":
         print(f"[bench] error: {val}", file=sys.stderr, flush=True)
         raise SystemExit(2)
+    if (val > 1 and args.inner == "ilu" and not (args.replicas or args.scaling == "replicas")
+            and "pls.redundant_ilu=1" not in args.opt):
+        # PETSc's ILU refuses an MPIAIJ block (the library throws at setup): say so before launching
+        print("[bench] error: --inner ilu on a block sharded over several ranks is what PETSc refuses "
+              "(use --inner bjacobi, or --opt pls.redundant_ilu=1 for the one-rank ILU applied redundantly)",
+              file=sys.stderr, flush=True)
+        raise SystemExit(2)
     if mode == "spawn":
         raise SystemExit(spawn_ranks(val, sys.argv[1:]))
     footing_fe = args.system == "fe" and args.config.startswith("footing")

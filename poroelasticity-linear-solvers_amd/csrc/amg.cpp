@@ -346,6 +346,7 @@ HostCSR dense_inverse(const HostCSR &A) {
 // long rows (R = P^T, Galerkin coarse operators, the dense coarsest inverse)
 // stay CSR and take the workgroup-per-row kernel.
 void amg_layout(DevCSR &M, Ctx &c) {
+    M.rcm_auto = false;  // Galerkin operators: the RCM relabelling is for caller (FE) blocks
     if (M.nrows > 0 && M.nnz < 128 * M.nrows) build_sell(M, c);
 }
 

@@ -105,13 +105,16 @@ Pattern strength(const HostCSR &A, double theta, double mu) {
 // thread column counts over its row range, offsets thread-major inside each
 // column, then every thread fills its rows -- memory-bound, on host threads
 // (the sequential transpose was ~1.6 s of the N=40 s block's RS pass)
-Pattern transpose(const Pattern &S) {
+// (threads capped so the per-thread column counts, Tn x n, stay within nnz / 2
+// entries; `max_threads` 1 inside an already parallel caller)
+Pattern transpose(const Pattern &S, int max_threads = 0) {
     const int64_t n = S.n, nnz = (int64_t)S.ci.size();
     Pattern T;
     T.n = n;
     T.rp.assign(n + 1, 0);
     T.ci.resize(nnz);
-    int Tn = setup_threads();
+    int Tn = max_threads > 0 ? std::min(max_threads, setup_threads()) : setup_threads();
+    if (n > 0) Tn = (int)std::max<int64_t>(1, std::min<int64_t>(Tn, nnz / (2 * n)));
     if (nnz < (int64_t)1 << 20 || n < 1024) Tn = 1;
     if (Tn == 1) {
         for (int32_t j : S.ci) ++T.rp[j + 1];
@@ -251,11 +254,11 @@ struct LamBuckets {
     }
 };
 
-std::vector<int8_t> rs_first_pass(const Pattern &S) {
+std::vector<int8_t> rs_first_pass(const Pattern &S, int max_threads = 0) {
     const int64_t n = S.n;
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t0 = now();
-    const Pattern ST = transpose(S);
+    const Pattern ST = transpose(S, max_threads);
     const double t1 = now();
     std::vector<int64_t> lam(n);
     int64_t maxst = 0;
@@ -398,7 +401,7 @@ std::vector<int8_t> rs_partitioned(const Pattern &S, int64_t K, const std::vecto
                     if (S.ci[q] >= a && S.ci[q] < b) L.ci.push_back((int32_t)(S.ci[q] - a));
                 L.rp.push_back((int64_t)L.ci.size());
             }
-            const std::vector<int8_t> lc = rs_first_pass(L);
+            const std::vector<int8_t> lc = rs_first_pass(L, 1);  // inside parallel_rows: no nested pool
             std::copy(lc.begin(), lc.end(), cf.begin() + a);
         }
     });

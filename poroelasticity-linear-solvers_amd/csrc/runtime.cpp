@@ -460,6 +460,7 @@ static bool build_sell_rcm(DevCSR &M, Ctx &c) {
     S.xperm.alloc(n);
     HIPCHK(hipMemcpyAsync(S.xperm.p, ord.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
     S.nperm = n;
+    if (c.rcm_x.n < (size_t)n) c.rcm_x.alloc(n);
     c.sync();
     M.sell = std::move(Mp.sell);
     return true;
@@ -469,7 +470,7 @@ void build_sell(DevCSR &M, Ctx &c) {
     if (M.sell || M.nrows == 0) return;
     if (c.spmv_rcm != 0 && c.sell_d16 && !c.spmv_b3 && !M.halo && M.nrows == M.ncols && M.nrows >= 16384) {
         bool pads = c.spmv_rcm == 1;
-        if (!pads) {  // only where the plain plan pads (FE): the synthetic blocks keep their layout
+        if (!pads && M.rcm_auto) {  // only where the plain plan pads (FE): the synthetic blocks keep their layout
             std::vector<int64_t> sf;
             std::vector<int32_t> lp, rm;
             d16_plan(M, sf, lp, rm, c);
@@ -621,11 +622,13 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
     }
     if (M.sell && M.sell->d16) {
         DevSELL &S = *M.sell;
-        if (S.nperm) {  // RCM-relabelled columns: x in that order first
-            auto &xb = S.xbuf[c.st];
-            if (xb.n < (size_t)S.nperm) xb.alloc(S.nperm);
-            launch_gather_i32(S.nperm, S.xperm.p, x, xb.p, c.st);
-            x = xb.p;
+        if (S.nperm) {  // RCM-relabelled columns: x in that order first (the context's scratch)
+            if (c.rcm_x.n < (size_t)S.nperm) {  // a context other than the one the layout was built on
+                HIPCHK(hipStreamSynchronize(c.st));
+                c.rcm_x.alloc(S.nperm);
+            }
+            launch_gather_i32(S.nperm, S.xperm.p, x, c.rcm_x.p, c.st);
+            x = c.rcm_x.p;
         }
         if (S.b3_nslices)
             launch_b3_spmv(S.b3_nslices, S.b3_ntrip, S.b3ptr.p, S.b3map.p, S.b3col.p, S.b3val.p, x, y, alpha, beta, z,
@@ -1823,13 +1826,20 @@ struct PCRedundant : PC {
     hipEvent_t ev_a = nullptr, ev_b = nullptr;
 
     PCRedundant(const std::string &t, const DevCSR &M, Ctx &c,
-                const std::function<std::unique_ptr<PC>(const DevCSR &, Ctx &)> &factory, const std::string &prefix) {
+                const std::function<std::unique_ptr<PC>(const DevCSR &, Ctx &)> &factory, const std::string &prefix,
+                GatheredBlock *pre) {
         type = t;
         n = nloc = M.nrows;
         const Halo &H = *M.halo;
         const int G = c.comm->size;
-        std::vector<int64_t> srcslot, rank_rows;
-        const HostCSR Gh = gather_block(M, c, prefix, srcslot, maxloc, rank_rows);
+        GatheredBlock own;
+        if (!pre) {
+            own.G = gather_block(M, c, prefix, own.srcslot, own.maxloc, own.rank_rows);
+            pre = &own;
+        }
+        const HostCSR &Gh = pre->G;
+        const std::vector<int64_t> &srcslot = pre->srcslot, &rank_rows = pre->rank_rows;
+        maxloc = pre->maxloc;
         N = Gh.nrows;
         self = layout_ctx(c);
         // the ranks' rows: contiguous ranges in rank order -> the inner PC may restate
@@ -1872,8 +1882,8 @@ struct PCRedundant : PC {
 
 std::unique_ptr<PC> make_redundant(const std::string &type, const DevCSR &M, Ctx &c,
                                    const std::function<std::unique_ptr<PC>(const DevCSR &, Ctx &)> &factory,
-                                   const std::string &prefix) {
-    return std::make_unique<PCRedundant>(type, M, c, factory, prefix);
+                                   const std::string &prefix, GatheredBlock *pre) {
+    return std::make_unique<PCRedundant>(type, M, c, factory, prefix, pre);
 }
 
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
@@ -1890,18 +1900,19 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
                         std::to_string(c.comm ? c.comm->size : 1) +
                         " ranks: PETSc's ILU does not run on MPIAIJ matrices (use bjacobi, or pls.redundant_ilu 1 "
                         "for the one-rank ILU applied redundantly)");
+        GatheredBlock pre;
+        bool gathered = false;
         if (type == "hypre" && o.str("pls.hypre", "boomeramg") == "boomeramg" && o.flag("pls.hypre_dist", true)) {
             // BoomerAMG as under mpirun -np G: the np = G hierarchy, each rank smoothing its
             // own rows (Jacobi across ranks); needs ranks owning contiguous rows in rank order
-            std::vector<int64_t> srcslot, rank_rows;
-            int64_t maxloc = 0;
-            const HostCSR Gh = gather_block(M, c, prefix, srcslot, maxloc, rank_rows);
-            if (!rank_rows.empty()) return make_boomeramg_dist(M, Gh, rank_rows, o, prefix, c);
+            pre.G = gather_block(M, c, prefix, pre.srcslot, pre.maxloc, pre.rank_rows);
+            gathered = true;
+            if (!pre.rank_rows.empty()) return make_boomeramg_dist(M, pre.G, pre.rank_rows, o, prefix, c);
         }
         if (o.flag("pls.redundant_error", false))
             throw Error("PC type '" + type + "' (prefix " + prefix + ") acts on the whole parallel matrix (pls.redundant_error)");
         return make_redundant(type, M, c, [&](const DevCSR &Gm, Ctx &sc) { return make_pc(type, Gm, o, prefix, sc); },
-                              prefix);
+                              prefix, gathered ? &pre : nullptr);
     }
     if (type == "ilu") {
         if (o.integer(prefix + "pc_factor_levels", 0) != 0)
@@ -1909,7 +1920,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         auto pc = std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true), 0,
                                           (int)o.integer("pls.ilu_gmem", 0), (int)o.integer("pls.ilu_ring", 1));
         if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
-            if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
+        if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
         return pc;
     }
     if (type == "lu" || type == "cholesky") return make_lu(M, o, c);

@@ -85,6 +85,7 @@ struct Ctx {
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
     DBuf<char> scan_tmp;
     size_t scan_tmp_bytes = 0;
+    DBuf<double> rcm_x;  // x in RCM order for RCM-relabelled SpMV layouts (grown at layout build)
     // a redundant PC's gathered block: the rows each rank owns (contiguous, rank
     // order; empty when not) -- the classical AMG builds hypre's np = G hierarchy
     std::vector<int64_t> rank_rows;
@@ -139,10 +140,9 @@ struct DevSELL {
     DBuf<int32_t> s_in, s_halo;
     int64_t n_in = 0, n_halo = 0;
     // RCM-relabelled columns (FE matrices, pls.spmv_rcm): the product reads
-    // xp = x[xperm] (per-stream scratch) so a slice's gathers stay local
+    // xp = x[xperm] (Ctx::rcm_x) so a slice's gathers stay local
     int64_t nperm = 0;
     DBuf<int32_t> xperm;
-    std::map<hipStream_t, DBuf<double>> xbuf;
     int64_t bytes() const {  // bytes one product streams from the matrix
         return (d16 ? stored * 10 + nslices * (64 * 4 * nsegs + 20) + 8 + nrows_mapped * 4
                     : stored * 12 + (nslices + 1) * 8) +
@@ -172,6 +172,7 @@ struct DevCSR {
     int64_t max_row = 0;
     std::unique_ptr<DevSELL> sell;  // SpMV layout (built on demand)
     int tag = 0;                    // 1: outer operator A
+    bool rcm_auto = true;           // pls.spmv_rcm -1 may relabel this matrix (not AMG level operators)
 };
 // Build the SELL-64 copy used by every SpMV with this matrix.
 void build_sell(DevCSR &M, Ctx &c);
@@ -472,9 +473,15 @@ HostCSR gather_block(const DevCSR &M, Ctx &c, const std::string &prefix, std::ve
 std::unique_ptr<Ctx> layout_ctx(const Ctx &c);
 // local rows with global columns owned in contiguous rank ranges cst -> distributed DevCSR with halo
 void upload_dist(const HostCSR &L, const std::vector<int64_t> &cst, DevCSR &M, Ctx &c);
+// (a block gather_block already produced, consumed by make_redundant instead of gathering again)
+struct GatheredBlock {
+    HostCSR G;
+    std::vector<int64_t> srcslot, rank_rows;
+    int64_t maxloc = 0;
+};
 std::unique_ptr<PC> make_redundant(const std::string &type, const DevCSR &M, Ctx &c,
                                    const std::function<std::unique_ptr<PC>(const DevCSR &, Ctx &)> &factory,
-                                   const std::string &prefix);
+                                   const std::string &prefix, GatheredBlock *pre = nullptr);
 // Configure a KSP from programmatic defaults + options (setFromOptions order).
 std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const DevCSR *Amat, const DevCSR *Pmat,
                               const std::string &default_ksp, const std::string &default_pc, Ctx &c,

@@ -157,3 +157,13 @@ def test_bench_exits_nonzero_on_rank_count_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_refuses_sharded_ilu():
+    """--inner ilu with G > 1 ranks: the library refuses ILU on a sharded block
+    as PETSc does (MPIAIJ), so bench exits 2 before launching any rank."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--inner", "ilu"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "redundant_ilu" in r.stderr

@@ -443,7 +443,7 @@ def test_fieldsplit_fp(gpu, variant):
     db = dict(FS_INEXACT)
     if variant == "inexact_band_lu":  # the Schur block's LU on the band path
         db["pls.lu_path"] = "band"
-    if variant == "inexact_sparse_lu":  # ... on the sparse path (the footing configuration's)
+    elif variant == "inexact_sparse_lu":  # ... on the sparse path (the footing configuration's)
         db["pls.lu_path"] = "sparse"
     elif variant == "lower_ilu":
         db.update({"fp_fieldsplit_0_ksp_type": "preonly", "fp_fieldsplit_0_pc_type": "ilu",
