@@ -208,6 +208,19 @@ int pls_boomeramg_host_level(const pls_csr *A, const char *options, const char *
                              int64_t *nlevels, int64_t *n, int64_t *nc, int64_t *p_nnz, int8_t *cf, int64_t *p_rp,
                              int32_t *p_ci, double *p_v);
 
+/* Host-only analysis of the sparse LU (the MUMPS stand-in behind -pc_type lu
+ * past pls.lu_dense_max rows; petsc-options-exact:11-35,
+ * petsc-options-inexact:105-106) that `options` would build on A: ordering
+ * (pls.lu_nd*) and symbolic factorization only, no device needed.
+ * stats[0..9]: n, fronts, tree levels, largest front (p + q), factor doubles
+ * one solve reads (sum p (p + 2 q)), doubles stored, factorization flops,
+ * ordering s, symbolic s, largest separator.  When non-NULL: perm[n] (ND
+ * position -> row), front_of[n] (position -> front, fronts numbered in
+ * postorder so every front's pivots are contiguous) and parent[fronts]
+ * (-1 at the root); call with them NULL first to learn the front count.    */
+int pls_sparse_lu_analyze(const pls_csr *A, const char *options, double *stats, int64_t nstats, int32_t *perm,
+                          int32_t *front_of, int32_t *parent);
+
 /* Standalone inner Anderson mixing (lib/AndersonAcceleration.py:8-78): the
  * object a caller's own fixed-point loop holds, as the reference's
  * PreconditionerCC holds one per inner block (lib/Preconditioner.py:248-249).

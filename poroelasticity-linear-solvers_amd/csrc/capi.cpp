@@ -1525,6 +1525,20 @@ int pls_boomeramg_host_level(const pls_csr *A, const char *options, const char *
     })
 }
 
+int pls_sparse_lu_analyze(const pls_csr *A, const char *options, double *stats, int64_t nstats, int32_t *perm,
+                          int32_t *front_of, int32_t *parent) {
+    PLS_TRY({
+        if (!A || A->nrows != A->ncols) throw Error("pls_sparse_lu_analyze: square A required");
+        Options o;
+        o.parse(options);
+        HostCSR H;
+        H.nrows = H.ncols = A->nrows;
+        H.rp.assign(A->row_ptr, A->row_ptr + A->nrows + 1);
+        H.ci.assign(A->col, A->col + H.rp.back());
+        sparse_lu_analyze(H, o, stats, nstats, perm, front_of, parent);
+    })
+}
+
 // Standalone AndersonAcceleration (lib/AndersonAcceleration.py:8-78) on its
 // own stream and a single-rank communicator; the same mixer the block PC runs
 // for "inner accel order" > 0.

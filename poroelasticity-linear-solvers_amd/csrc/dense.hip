@@ -342,7 +342,9 @@ void launch_mf_extend(int nc, const MChild *C, int max_q, const int32_t *maps, c
 // blocks (the 2-way fp block: zero pressure diagonal) have zero scalar pivots
 // whose tile is still regular.
 #pragma clang fp contract(off)
-__global__ __launch_bounds__(DTPB) void k_mf_gj_diag(const MFront *F, int k, double *W, double *D, int32_t *fail) {
+// fail[0]: a zero pivot with static pivoting off (tau = 0); fail[1]: pivots replaced by +-tau
+__global__ __launch_bounds__(DTPB) void k_mf_gj_diag(const MFront *F, int k, double *W, double *D, int32_t *fail,
+                                                     double tau) {
     __shared__ double a[DB][DB + 1];
     __shared__ double v[DB][DB + 1];
     __shared__ int prow;
@@ -382,10 +384,19 @@ __global__ __launch_bounds__(DTPB) void k_mf_gj_diag(const MFront *F, int k, dou
             m[r][j] = t;
         }
         __syncthreads();
-        const double piv = a[p][p];
-        if (piv == 0.0) {
-            if (threadIdx.x == 0) atomicOr(fail, 1);
-            return;  // uniform across the workgroup
+        double piv = a[p][p];
+        if (fabs(piv) <= tau && k * DB + p < f.p) {  // static pivot (not on the identity padding) (MUMPS CNTL(4) semantics): perturb, count, refine later
+            if (tau <= 0.0) {
+                if (threadIdx.x == 0) atomicOr(fail, 1);
+                return;  // uniform across the workgroup
+            }
+            piv = piv < 0.0 ? -tau : tau;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                a[p][p] = piv;
+                atomicAdd(fail + 1, 1);
+            }
+            __syncthreads();
         }
         if (threadIdx.x < 2 * DB) {
             const int j = threadIdx.x & (DB - 1);
@@ -494,9 +505,9 @@ __global__ __launch_bounds__(DTPB) void k_mf_gj_colpanel(const MFront *F, int k,
 }
 
 void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, double *D, int32_t *fail,
-                       hipStream_t st) {
+                       double tau, hipStream_t st) {
     if (nf <= 0 || max_ldt <= 0) return;
-    k_mf_gj_diag<<<dim3(1, 1, (unsigned)nf), DTPB, 0, st>>>(F, k, W, D, fail);
+    k_mf_gj_diag<<<dim3(1, 1, (unsigned)nf), DTPB, 0, st>>>(F, k, W, D, fail, tau);
     k_mf_gj_rowpanel<<<dim3((unsigned)max_ldt, 1, (unsigned)nf), DTPB, 0, st>>>(F, k, W, D);
     if (max_ldt > 1) {
         k_mf_gj_update<<<dim3((unsigned)(max_ldt - 1), (unsigned)(max_ldt - 1), (unsigned)nf), DTPB, 0, st>>>(F, k, W);
@@ -504,17 +515,20 @@ void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, d
     }
 }
 
-// blockIdx.x: front row (U part rows [0, pp), then X part rows), blockIdx.y: front
+// blockIdx.x: front row (U part rows [0, p), then X part rows from pp), blockIdx.y: front.
+// Compact layout (no tile padding): U row r = [F11^-1 | F11^-1 F12] (p + q), X row = p.
 __global__ __launch_bounds__(256) void k_mf_store(const MFront *F, const MStore *S, const double *W, double *U,
                                                   double *X) {
     const MFront f = F[blockIdx.y];
     const MStore s = S[blockIdx.y];
-    const int64_t r = blockIdx.x, ld = (int64_t)f.ldt * DB, pp = (int64_t)f.pt * DB;
+    const int64_t r = blockIdx.x, ld = (int64_t)f.ldt * DB, pp = (int64_t)f.pt * DB, p = f.p, q = f.q;
     const double *src = W + f.ws + r * ld;
-    if (r < pp) {
-        for (int64_t c = threadIdx.x; c < ld; c += 256) U[s.uoff + r * ld + c] = src[c];
-    } else if (r < pp + f.q) {
-        for (int64_t c = threadIdx.x; c < pp; c += 256) X[s.xoff + (r - pp) * pp + c] = src[c];
+    if (r < p) {
+        double *dst = U + s.uoff + r * (p + q);
+        for (int64_t c = threadIdx.x; c < p + q; c += 256) dst[c] = src[c < p ? c : pp + (c - p)];
+    } else if (r >= pp && r < pp + q) {
+        double *dst = X + s.xoff + (r - pp) * p;
+        for (int64_t c = threadIdx.x; c < p; c += 256) dst[c] = src[c];
     }
 }
 void launch_mf_store(int nf, const MFront *F, const MStore *S, int max_rows, const double *W, double *U, double *X,

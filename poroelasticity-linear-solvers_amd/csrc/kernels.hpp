@@ -281,9 +281,11 @@ void launch_mf_extend(int nc, const MChild *C, int max_q, const int32_t *maps, c
                       hipStream_t st);
 // Step k of the partial Gauss-Jordan elimination of every front's pivot tiles
 // (front := [F11^-1, F11^-1 F12; -F21 F11^-1, F22 - F21 F11^-1 F12]); D: nf
-// 64 x 64 scratch tiles; fail |= 1 on a zero pivot.
+// 64 x 64 scratch tiles.  A pivot of magnitude <= tau (after partial pivoting
+// inside the tile) is replaced by +-tau and counted in fail[1] (static
+// pivoting); with tau = 0 an exact zero pivot sets fail[0] instead.
 void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, double *D, int32_t *fail,
-                       hipStream_t st);
+                       double tau, hipStream_t st);
 // Persistent factors: rows [0, 64 pt) of the front (U part, ld wide) to U + uoff
 // and rows [64 pt, 64 pt + q) x columns [0, 64 pt) (X part) to X + xoff.
 struct MStore {

@@ -387,6 +387,8 @@ void csr_bandwidths(const DevCSR &M, int64_t &kl, int64_t &ku, Ctx &c);
 std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c);
 // Sparse LU by nested dissection + multifrontal factorization (sparse_lu.cpp)
 std::unique_ptr<PC> make_sparse_lu(const DevCSR &M, const Options &o, Ctx &c);
+void sparse_lu_analyze(const HostCSR &A, const Options &o, double *stats, int64_t nstats, int32_t *perm = nullptr,
+                       int32_t *front_of = nullptr, int32_t *parent = nullptr);
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c);
 // Smoothed-aggregation AMG (amg.cpp; -pc_type gamg, and hypre with pls.hypre sa).

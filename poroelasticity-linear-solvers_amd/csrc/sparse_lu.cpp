@@ -34,162 +34,145 @@
 // order (children in tree order): the result does not depend on timing.
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <numeric>
 
+#include "nd_order.hpp"
 #include "runtime.hpp"
 
 namespace pls {
-namespace {
 
-struct NDTree {
-    std::vector<std::vector<int32_t>> piv;  // per node: its vertices
-    std::vector<std::vector<int32_t>> ch;   // children (tree order)
-    std::vector<int32_t> parent, depth;
-    int add(int par, int d) {
-        piv.emplace_back();
-        ch.emplace_back();
-        parent.push_back(par);
-        depth.push_back(d);
-        if (par >= 0) ch[par].push_back((int)piv.size() - 1);
-        return (int)piv.size() - 1;
-    }
+// Ordering + symbolic analysis (host): the dissection tree, pivots numbered in
+// postorder, every front's update rows (ND positions, ascending).
+struct LUSymbolic {
+    NDTree T;
+    std::vector<int32_t> post, pos, permh, front_of;
+    std::vector<int64_t> pstart;
+    std::vector<std::vector<int32_t>> st;
+    std::vector<int64_t> gp;
+    std::vector<int32_t> gi;
+    int64_t nfront = 0, nlevels = 0;
+    double t_order = 0, t_symbolic = 0;
 };
 
-// symmetrized adjacency of M's pattern without the diagonal
-void sym_graph(const HostCSR &A, std::vector<int64_t> &gp, std::vector<int32_t> &gi) {
-    const int64_t n = A.nrows;
-    std::vector<int64_t> deg(n + 1, 0);
-    for (int64_t i = 0; i < n; ++i)
-        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
-            if (A.ci[k] != i) {
-                ++deg[i + 1];
-                ++deg[A.ci[k] + 1];
-            }
-    for (int64_t i = 0; i < n; ++i) deg[i + 1] += deg[i];
-    std::vector<int32_t> tmp(deg[n]);
-    std::vector<int64_t> pos(deg.begin(), deg.end() - 1);
-    for (int64_t i = 0; i < n; ++i)
-        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
-            if (A.ci[k] != i) {
-                tmp[pos[i]++] = A.ci[k];
-                tmp[pos[A.ci[k]]++] = (int32_t)i;
-            }
-    gp.assign(n + 1, 0);
-    gi.clear();
-    gi.reserve(tmp.size());
-    for (int64_t i = 0; i < n; ++i) {
-        std::sort(tmp.begin() + deg[i], tmp.begin() + deg[i + 1]);
-        int32_t last = -1;
-        for (int64_t k = deg[i]; k < deg[i + 1]; ++k)
-            if (tmp[k] != last) gi.push_back(last = tmp[k]);
-        gp[i + 1] = (int64_t)gi.size();
-    }
+NDOptions lu_nd_options(const Options &o) {
+    NDOptions nd;
+    nd.leaf = std::max<int64_t>(1, o.integer("pls.lu_nd_leaf", 64));
+    nd.method = (int)o.integer("pls.lu_nd", 1);
+    nd.imbalance = o.num("pls.lu_nd_imbalance", 1.10);
+    nd.seeds = (int)o.integer("pls.lu_nd_seeds", 6);
+    nd.compress = o.flag("pls.lu_nd_compress", true);
+    nd.node_passes = (int)o.integer("pls.lu_nd_node_passes", 4);
+    nd.threads = (int)o.integer("pls.lu_nd_threads", 0);
+    return nd;
 }
 
-struct Dissector {
-    const std::vector<int64_t> &gp;
-    const std::vector<int32_t> &gi;
-    int64_t leaf;
-    std::vector<int32_t> stamp, lev;
-    int32_t cur = 0;
-    std::vector<int32_t> order;
-    Dissector(const std::vector<int64_t> &p, const std::vector<int32_t> &i, int64_t n, int64_t lf)
-        : gp(p), gi(i), leaf(lf), stamp(n, 0), lev(n, -1) {}
-
-    // BFS inside the stamped set from s: order (visit order), lev; returns the depth
-    int32_t bfs(int32_t s) {
-        order.clear();
-        order.push_back(s);
-        lev[s] = 0;
-        int32_t depth = 0;
-        for (size_t h = 0; h < order.size(); ++h) {
-            const int32_t u = order[h];
-            for (int64_t k = gp[u]; k < gp[u + 1]; ++k) {
-                const int32_t v = gi[k];
-                if (stamp[v] == cur && lev[v] < 0) {
-                    lev[v] = lev[u] + 1;
-                    depth = std::max(depth, lev[v]);
-                    order.push_back(v);
-                }
-            }
-        }
-        return depth;
-    }
-    void clear_lev(const std::vector<int32_t> &set) {
-        for (int32_t v : set) lev[v] = -1;
-    }
-
-    void run(NDTree &T, std::vector<int32_t> all) {
-        struct Work {
-            std::vector<int32_t> set;
-            int parent, depth;
-        };
-        std::vector<Work> stack;
-        stack.push_back({std::move(all), -1, 0});
-        while (!stack.empty()) {
-            Work w = std::move(stack.back());
-            stack.pop_back();
-            const int node = T.add(w.parent, w.depth);
-            if ((int64_t)w.set.size() <= leaf) {
-                T.piv[node] = std::move(w.set);
-                continue;
-            }
-            ++cur;
-            for (int32_t v : w.set) stamp[v] = cur;
-            // pseudo-peripheral start: two sweeps from the set's first vertex
-            int32_t s = w.set[0];
-            for (int sweep = 0; sweep < 2; ++sweep) {
-                bfs(s);
-                s = order.back();
-                clear_lev(order);
-            }
-            const int32_t depth = bfs(s);
-            if (order.size() < w.set.size()) {  // not connected: the component vs the rest
-                std::vector<int32_t> comp(order), rest;
-                for (int32_t v : w.set)
-                    if (lev[v] < 0) rest.push_back(v);
-                clear_lev(comp);
-                stack.push_back({std::move(rest), node, w.depth + 1});
-                stack.push_back({std::move(comp), node, w.depth + 1});
-                continue;
-            }
-            if (depth < 2) {  // no interior level to cut: a (dense) leaf
-                clear_lev(order);
-                T.piv[node] = std::move(w.set);
-                continue;
-            }
-            std::vector<int64_t> cnt(depth + 1, 0);
-            for (int32_t v : order) ++cnt[lev[v]];
-            const int64_t m = (int64_t)order.size();
-            int64_t below = 0, best = -1, best_sz = INT64_MAX, median = -1;
-            for (int32_t l = 0; l <= depth; ++l) {
-                const int64_t above = m - below - cnt[l];
-                if (l >= 1 && l < depth) {
-                    if (median < 0 && below + cnt[l] >= m / 2) median = l;
-                    if (below >= 3 * m / 10 && above >= 3 * m / 10 && cnt[l] < best_sz) {
-                        best = l;
-                        best_sz = cnt[l];
-                    }
-                }
-                below += cnt[l];
-            }
-            const int32_t L = (int32_t)(best >= 0 ? best : (median >= 0 ? median : 1));
-            std::vector<int32_t> a, b, sep;
-            for (int32_t v : order) (lev[v] < L ? a : lev[v] > L ? b : sep).push_back(v);
-            clear_lev(order);
-            T.piv[node] = std::move(sep);
-            if (!b.empty()) stack.push_back({std::move(b), node, w.depth + 1});
-            if (!a.empty()) stack.push_back({std::move(a), node, w.depth + 1});
-        }
-    }
-};
+namespace {
 
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 }  // namespace
+
+LUSymbolic lu_symbolic(const HostCSR &A, const Options &o) {
+    LUSymbolic Y;
+    const int64_t n = A.nrows;
+    const double t0 = now_s();
+    sym_graph(A, Y.gp, Y.gi);
+    Y.T = nested_dissection(Y.gp, Y.gi, n, lu_nd_options(o));
+    const NDTree &T = Y.T;
+    Y.nfront = (int64_t)T.piv.size();
+    // postorder: children before parents, subtrees contiguous
+    Y.post.reserve(Y.nfront);
+    {
+        std::vector<std::pair<int32_t, int32_t>> stk{{0, 0}};
+        while (!stk.empty()) {
+            auto &[v, k] = stk.back();
+            if (k < (int32_t)T.ch[v].size()) {
+                const int32_t cch = T.ch[v][k++];
+                stk.push_back({cch, 0});
+            } else {
+                Y.post.push_back(v);
+                stk.pop_back();
+            }
+        }
+    }
+    Y.pos.assign(n, 0);
+    Y.permh.assign(n, 0);
+    Y.front_of.assign(n, 0);
+    Y.pstart.assign(Y.nfront, 0);
+    {
+        int64_t k = 0;
+        for (int32_t f : Y.post) {
+            Y.pstart[f] = k;
+            for (int32_t v : T.piv[f]) {
+                Y.pos[v] = (int32_t)k;
+                Y.permh[k] = v;
+                Y.front_of[k] = f;
+                ++k;
+            }
+        }
+        if (k != n) throw Error("lu: the dissection does not cover every row");
+    }
+    const double t1 = now_s();
+    // update rows (ND positions, ascending) of every front
+    Y.st.assign(Y.nfront, {});
+    {
+        std::vector<int32_t> mark(n, -1);
+        for (int32_t f : Y.post) {
+            const int64_t pend = Y.pstart[f] + (int64_t)T.piv[f].size();
+            std::vector<int32_t> &s = Y.st[f];
+            auto add = [&](int32_t p) {
+                if (p >= pend && mark[p] != f) {
+                    mark[p] = f;
+                    s.push_back(p);
+                }
+            };
+            for (int32_t cch : T.ch[f])
+                for (int32_t p : Y.st[cch]) add(p);
+            for (int32_t v : T.piv[f])
+                for (int64_t k = Y.gp[v]; k < Y.gp[v + 1]; ++k) add(Y.pos[Y.gi[k]]);
+            std::sort(s.begin(), s.end());
+        }
+    }
+    int32_t maxd = 0;
+    for (int32_t d : T.depth) maxd = std::max(maxd, d);
+    Y.nlevels = maxd + 1;
+    Y.t_order = t1 - t0;
+    Y.t_symbolic = now_s() - t1;
+    return Y;
+}
+
+// Host-only analysis (pls_sparse_lu_analyze): sizes of the factorization the
+// options would build.  stats: n, fronts, levels, largest front (p + q),
+// factor doubles read per solve sum p (p + 2 q), doubles stored (padded layout),
+// factorization flops, ordering s, symbolic s, largest separator p
+void sparse_lu_analyze(const HostCSR &A, const Options &o, double *stats, int64_t nstats, int32_t *perm,
+                       int32_t *front_of, int32_t *parent) {
+    const LUSymbolic Y = lu_symbolic(A, o);
+    std::vector<int32_t> pnum(Y.nfront);  // postorder number of every front
+    for (size_t k = 0; k < Y.post.size(); ++k) pnum[Y.post[k]] = (int32_t)k;
+    for (int64_t k = 0; k < A.nrows; ++k) {
+        if (perm) perm[k] = Y.permh[k];
+        if (front_of) front_of[k] = pnum[Y.front_of[k]];
+    }
+    if (parent)
+        for (int32_t f = 0; f < (int32_t)Y.nfront; ++f)
+            parent[pnum[f]] = Y.T.parent[f] < 0 ? -1 : pnum[Y.T.parent[f]];
+    double v[10] = {(double)A.nrows, (double)Y.nfront, (double)Y.nlevels, 0, 0, 0, 0, Y.t_order, Y.t_symbolic, 0};
+    for (int32_t f = 0; f < (int32_t)Y.nfront; ++f) {
+        const double p = (double)Y.T.piv[f].size(), q = (double)Y.st[f].size();
+        const double pp = std::ceil(p / 64) * 64, ld = pp + std::ceil(q / 64) * 64;
+        v[3] = std::max(v[3], p + q);
+        v[4] += p * (p + 2 * q);
+        v[5] += pp * ld + q * pp;
+        v[6] += 2.0 / 3.0 * p * p * p + 2.0 * p * p * q + 2.0 * p * q * q;
+        v[9] = std::max(v[9], p);
+    }
+    for (int64_t k = 0; k < std::min<int64_t>(nstats, 10); ++k) stats[k] = v[k];
+}
 
 struct PCSparseLU : PC {
     int64_t nfront = 0, nlevels = 0;
@@ -205,6 +188,7 @@ struct PCSparseLU : PC {
     int64_t nq = 0;
     double setup_s[4] = {0, 0, 0, 0};  // ordering, symbolic, factorization, total
     double factor_gb = 0;
+    int static_pivots = 0;
 
     PCSparseLU(const DevCSR &M, const Options &o, Ctx &c) {
         type = "lu";
@@ -212,69 +196,13 @@ struct PCSparseLU : PC {
         if (M.ncols != n) throw Error("lu: block is not square");
         const double t0 = now_s();
         const HostCSR A = download(M, c);
-        // ---- ordering
-        std::vector<int64_t> gp;
-        std::vector<int32_t> gi;
-        sym_graph(A, gp, gi);
-        NDTree T;
-        {
-            Dissector D(gp, gi, n, std::max<int64_t>(1, o.integer("pls.lu_nd_leaf", 64)));
-            std::vector<int32_t> all(n);
-            std::iota(all.begin(), all.end(), 0);
-            D.run(T, std::move(all));
-        }
-        nfront = (int64_t)T.piv.size();
-        // postorder: children before parents, subtrees contiguous
-        std::vector<int32_t> post;
-        post.reserve(nfront);
-        {
-            std::vector<std::pair<int32_t, int32_t>> st{{0, 0}};
-            while (!st.empty()) {
-                auto &[v, k] = st.back();
-                if (k < (int32_t)T.ch[v].size()) {
-                    const int32_t cch = T.ch[v][k++];
-                    st.push_back({cch, 0});
-                } else {
-                    post.push_back(v);
-                    st.pop_back();
-                }
-            }
-        }
-        std::vector<int32_t> pos(n), permh(n), front_of(n);
-        std::vector<int64_t> pstart(nfront);
-        {
-            int64_t k = 0;
-            for (int32_t f : post) {
-                pstart[f] = k;
-                for (int32_t v : T.piv[f]) {
-                    pos[v] = (int32_t)k;
-                    permh[k] = v;
-                    front_of[k] = f;
-                    ++k;
-                }
-            }
-        }
-        const double t1 = now_s();
-        // ---- symbolic: update rows (ND positions, ascending) of every front
-        std::vector<std::vector<int32_t>> st(nfront);
-        {
-            std::vector<int32_t> mark(n, -1);
-            for (int32_t f : post) {
-                const int64_t pend = pstart[f] + (int64_t)T.piv[f].size();
-                std::vector<int32_t> &s = st[f];
-                auto add = [&](int32_t p) {
-                    if (p >= pend && mark[p] != f) {
-                        mark[p] = f;
-                        s.push_back(p);
-                    }
-                };
-                for (int32_t cch : T.ch[f])
-                    for (int32_t p : st[cch]) add(p);
-                for (int32_t v : T.piv[f])
-                    for (int64_t k = gp[v]; k < gp[v + 1]; ++k) add(pos[gi[k]]);
-                std::sort(s.begin(), s.end());
-            }
-        }
+        LUSymbolic Y = lu_symbolic(A, o);
+        const NDTree &T = Y.T;
+        nfront = Y.nfront;
+        const std::vector<int32_t> &post = Y.post, &pos = Y.pos, &permh = Y.permh, &front_of = Y.front_of;
+        const std::vector<int64_t> &pstart = Y.pstart;
+        const std::vector<std::vector<int32_t>> &st = Y.st;
+        const double t1 = t0 + Y.t_order;
         // ---- sizes, levels
         int32_t maxd = 0;
         for (int32_t d : T.depth) maxd = std::max(maxd, d);
@@ -289,10 +217,10 @@ struct PCSparseLU : PC {
             q[f] = (int64_t)st[f].size();
             pp[f] = (p[f] + 63) / 64 * 64;
             ld[f] = pp[f] + (q[f] + 63) / 64 * 64;
-            uoff[f] = usz;
-            usz += pp[f] * ld[f];
+            uoff[f] = usz;  // compact: U part p x (p + q), X part q x p (no tile padding)
+            usz += p[f] * (p[f] + q[f]);
             xoff[f] = xsz;
-            xsz += q[f] * pp[f];
+            xsz += q[f] * p[f];
             soff[f] = qoff[f] = ssz;
             ssz += q[f];
         }
@@ -339,9 +267,13 @@ struct PCSparseLU : PC {
         for (int64_t d = 0; d < nlevels; ++d) wsmax = std::max(wsmax, lev_ws[d]);
         DBuf<double> Wa(wsmax), Wb(wsmax), val(std::max<int64_t>(M.nnz, 1));
         HIPCHK(hipMemcpyAsync(val.p, A.v.data(), sizeof(double) * A.v.size(), hipMemcpyHostToDevice, c.st));
-        DBuf<int32_t> dmaps(maps.size()), fail(1);
+        DBuf<int32_t> dmaps(maps.size()), fail(2);
         HIPCHK(hipMemcpyAsync(dmaps.p, maps.data(), sizeof(int32_t) * maps.size(), hipMemcpyHostToDevice, c.st));
-        HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
+        HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t) * 2, c.st));
+        // static pivoting threshold: pls.lu_static_pivot x max |a_ij| (0: a zero pivot is an error)
+        double amax = 0.0;
+        for (double v : A.v) amax = std::max(amax, std::fabs(v));
+        const double tau = o.num("pls.lu_static_pivot", 64 * 2.220446049250313e-16) * amax;
         double *Wcur = Wa.p, *Wprev = Wb.p;
         std::vector<int64_t> prev_ws;  // workspace offsets of the previous (deeper) level's fronts
         constexpr int CH = 32768;      // fronts per batched launch (grid z / y limit)
@@ -400,7 +332,7 @@ struct PCSparseLU : PC {
                         }
                     }
                 }
-                for (int k = 0; k < max_pt; ++k) launch_mf_gj_step((int)hf.size(), dF.p, max_ldt, k, Wcur, Dt.p, fail.p, c.st);
+                for (int k = 0; k < max_pt; ++k) launch_mf_gj_step((int)hf.size(), dF.p, max_ldt, k, Wcur, Dt.p, fail.p, tau, c.st);
                 launch_mf_store((int)hf.size(), dF.p, dS.p, max_rows, Wcur, U.p, X.p, c.st);
                 HIPCHK(hipGetLastError());
                 c.sync();
@@ -409,17 +341,19 @@ struct PCSparseLU : PC {
             for (int32_t f : fl) prev_ws[f] = wsoff[f];
             std::swap(Wcur, Wprev);
         }
-        int32_t hfail = 0;
-        HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+        int32_t hfail[2] = {0, 0};
+        HIPCHK(hipMemcpyAsync(hfail, fail.p, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, c.st));
         c.sync();
-        if (hfail) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+        if (hfail[0]) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+        static_pivots = hfail[1];
         const double t3 = now_s();
         // ---- solve tables
         std::vector<MSolve> hS(nfront);
         std::vector<int32_t> hsl(std::max<int64_t>(ssz, 1));
         for (int32_t f : post) {
-            hS[f] = {pstart[f], qoff[f], uoff[f], xoff[f], soff[f], (int32_t)p[f], (int32_t)q[f], (int32_t)pp[f],
-                     (int32_t)ld[f]};
+            // compact factors: X rows are p long, U rows p + q (the kernels' "pp" / "ld")
+            hS[f] = {pstart[f], qoff[f], uoff[f], xoff[f], soff[f], (int32_t)p[f], (int32_t)q[f], (int32_t)p[f],
+                     (int32_t)(p[f] + q[f])};
             std::copy(st[f].begin(), st[f].end(), hsl.begin() + soff[f]);
         }
         std::vector<int32_t> hrf, hrl, hqf, hql, hpf, hpl;
@@ -474,6 +408,8 @@ struct PCSparseLU : PC {
         c.sync();
         Mref = &M;
         refine = (int)o.integer("pls.lu_refine", 1);
+        // perturbed pivots: the factorization is of a nearby matrix; refinement recovers the solve
+        if (static_pivots > 0) refine = std::max(refine, (int)o.integer("pls.lu_static_refine", 2));
         if (refine > 0 && !M.sell) build_sell(const_cast<DevCSR &>(M), c);
         setup_s[0] = t1 - t0;
         setup_s[1] = t2 - t1;
@@ -483,10 +419,11 @@ struct PCSparseLU : PC {
             int64_t maxf = 0;
             for (int32_t f : post) maxf = std::max(maxf, p[f] + q[f]);
             fprintf(stderr,
-                    "[sparse lu] n %lld: %lld fronts, %lld levels, largest front %lld, factors %.2f GB; setup: "
-                    "ordering %.2f s, symbolic %.2f s, factorization %.2f s, total %.2f s\n",
-                    (long long)n, (long long)nfront, (long long)nlevels, (long long)maxf, factor_gb, setup_s[0],
-                    setup_s[1], setup_s[2], setup_s[3]);
+                    "[sparse lu] n %lld: %lld fronts, %lld levels, largest front %lld, factors %.2f GB, %d static "
+                    "pivots, refinement steps %d; setup: ordering %.2f s, symbolic %.2f s, factorization %.2f s, "
+                    "total %.2f s\n",
+                    (long long)n, (long long)nfront, (long long)nlevels, (long long)maxf, factor_gb, static_pivots,
+                    refine, setup_s[0], setup_s[1], setup_s[2], setup_s[3]);
         }
     }
 

@@ -46,7 +46,7 @@ EXPORTS = [
     "pls_bench_spmv", "pls_rccl_unique_id", "pls_comm_create_rccl", "pls_comm_create_callback",
     "pls_comm_destroy", "pls_create_synthetic_dist", "pls_spmv_layout", "pls_update_matrices",
     "pls_bench_copy", "pls_create_dist", "pls_bench_global_sum", "pls_anderson_create",
-    "pls_anderson_next", "pls_anderson_destroy", "pls_boomeramg_host_level",
+    "pls_anderson_next", "pls_anderson_destroy", "pls_boomeramg_host_level", "pls_sparse_lu_analyze",
 ]
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
@@ -103,6 +103,7 @@ def lib():
     L.pls_anderson_destroy.argtypes = [vp]
     L.pls_boomeramg_host_level.argtypes = [C.POINTER(pls_csr), C.c_char_p, C.c_char_p, i64, C.POINTER(i64),
                                            C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), vp, vp, vp, vp]
+    L.pls_sparse_lu_analyze.argtypes = [C.POINTER(pls_csr), C.c_char_p, vp, i64, vp, vp, vp]
     L.pls_create_dist.argtypes = [C.POINTER(pls_csr), C.POINTER(pls_csr), C.POINTER(pls_csr), i64,
                                   vp, i64, vp, i64, vp, i64, vp, i64, C.c_char_p, vp, C.POINTER(vp)]
     _lib = L

@@ -259,3 +259,30 @@ def boomeramg_host_level(A, options: dict, prefix: str, level: int):
     ncols = nc.value if level < nl.value - 1 else n.value
     P = sp.csr_matrix((v[:nnz.value], ci[:nnz.value], rp), shape=(n.value, ncols))
     return nl.value, n.value, nc.value, cf, P
+
+
+LU_STATS = ("n", "fronts", "levels", "max_front", "solve_doubles", "stored_doubles", "flops", "order_s",
+            "symbolic_s", "max_separator")
+
+
+def sparse_lu_analyze(A, options: dict | None = None, tree: bool = False):
+    """Ordering + symbolic analysis of the sparse LU libpls would build on the
+    square matrix ``A`` (``pls_sparse_lu_analyze``; host only, no device):
+    fronts, tree levels, largest front, doubles one solve reads, doubles
+    stored, factorization flops, timings (keys: ``LU_STATS``).  With
+    ``tree``: (stats, perm, front_of, parent) -- ND position -> row, position ->
+    front (postorder numbers), the fronts' parents."""
+    ai, aj, av, nr, nc_ = N.csr_of(A)
+    m = N.pls_csr(nr, nc_, ai.ctypes.data_as(C.c_void_p), aj.ctypes.data_as(C.c_void_p), av.ctypes.data_as(C.c_void_p))
+    out = (C.c_double * len(LU_STATS))()
+    N.check(N.lib().pls_sparse_lu_analyze(C.byref(m), options_text(options or {}), out, len(LU_STATS), None, None,
+                                          None))
+    stats = dict(zip(LU_STATS, list(out)))
+    if not tree:
+        return stats
+    perm, front_of = np.zeros(nr, dtype=np.int32), np.zeros(nr, dtype=np.int32)
+    parent = np.zeros(int(stats["fronts"]), dtype=np.int32)
+    N.check(N.lib().pls_sparse_lu_analyze(C.byref(m), options_text(options or {}), out, len(LU_STATS),
+                                          perm.ctypes.data_as(C.c_void_p), front_of.ctypes.data_as(C.c_void_p),
+                                          parent.ctypes.data_as(C.c_void_p)))
+    return stats, perm, front_of, parent
