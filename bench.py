@@ -311,6 +311,31 @@ def launch_plan(gpus, env):
     return "run", W
 
 
+def hypre_semantics(opts, ranks):
+    """Which BoomerAMG run the classical AMG behind -pc_type hypre restates
+    (oracle/boomeramg.py; csrc/boomeramg.cpp) under these options."""
+    chunks = int(opts.get("pls.hypre_relax_chunks", 256))
+    cch = int(opts.get("pls.hypre_coarsen_chunks", 0))
+    crows = int(opts.get("pls.hypre_coarsen_min_rows", 65536))
+    if opts.get("pls.hypre_ranks"):
+        np_ = f"np = {opts['pls.hypre_ranks']} (pls.hypre_ranks)"
+    elif ranks > 1 and opts.get("pls.hypre_dist", "1") not in ("0", "false"):
+        np_ = f"np = {ranks} (the sharded block's ranks)"
+    elif cch == 1:
+        np_ = "np = 1"
+    elif cch > 1:
+        np_ = f"np = {cch} equal row partitions per level"
+    else:
+        np_ = (f"np = the most partitions <= min({chunks}, rows / {crows}) per level, halving until the "
+               "partition boundaries cut <= 2 % of the strong connections (1 if none)")
+    return {"coarsening": "HMIS = Ruge-Stueben first pass per process + PMIS stage (hypre_Rand measures, "
+                          "seeds 2747 + process)", "processes": np_,
+            "relax": (f"hybrid symmetric Gauss-Seidel (relax type 6) in K = {chunks} chunks per level "
+                      f"(hypre's OpenMP threads), at least {int(opts.get('pls.hypre_relax_min_rows', 1024))} "
+                      "rows per chunk"),
+            "hypre_K": chunks, "relax_min_rows": int(opts.get("pls.hypre_relax_min_rows", 1024))}
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -597,6 +622,8 @@ def main():
                          "layout_gbs": fmt_bytes / spmv_avg / 1e9 if spmv_avg > 0 else 0.0},
             "timings_s": {k: v for k, v in tm.items()},
         }
+        if any(v == "hypre" for k, v in opts.items() if k.endswith("pc_type")):
+            out["hypre_semantics"] = hypre_semantics(opts, world if sharded else 1)
         if not args.no_cpu and world == 1:
             _progress(rank, f"cpu baseline on the N={args.cpu_N} sample ...")
             out["cpu_baseline"] = cpu_baseline(args, params, db)

@@ -235,16 +235,97 @@ def coarsen_partition(S, n, K, max_cut=0.02):
     return None
 
 
+def hypre_rand(seed, count):
+    """``count`` values of hypre_Rand() after hypre_SeedRand(seed) (hypre's
+    utilities/random.c: the Park-Miller minimal standard generator, a = 16807,
+    m = 2^31 - 1 by Schrage's method, q = 127773, r = 2836; value = seed / m)."""
+    out = np.empty(count, dtype=np.float64)
+    s = int(seed)
+    for k in range(count):
+        hi, lo = divmod(s, 127773)
+        t = 16807 * lo - 2836 * hi
+        s = t if t > 0 else t + 2147483647
+        out[k] = s / 2147483647.0
+    return out
+
+
+def _pattern(S, n):
+    lens = np.asarray([len(r) for r in S], dtype=np.int64)
+    rows = np.repeat(np.arange(n, dtype=np.int64), lens)
+    cols = np.concatenate(S).astype(np.int64) if len(S) and lens.sum() else np.zeros(0, dtype=np.int64)
+    return rows, cols
+
+
+def pmis_stage(S, n, cf, part=None):
+    """HMIS's second stage (De Sterck, Yang & Heys 2006; hypre's CoarsenHMIS =
+    the Ruge-Stueben first pass inside every process, then CoarsenPMIS with
+    the first pass as the initial splitting, CF_init = 1):
+    * measure_i = |S^T_i| + a random number in [0, 1): process (partition) k
+      draws hypre_Rand() for its rows in order after hypre_SeedRand(2747 + k)
+      (hypre_BoomerAMGIndepSetInit);
+    * the first pass's C points without a strong dependency on another
+      partition's point stay C; every other point is undecided, or F when
+      |S^T_i| = 0 (measure < 1: no point depends on it);
+    * an undecided point with a strong dependency on a C point becomes F; then,
+      while points are undecided: every undecided point whose measure exceeds
+      the measures of all its undecided strong neighbours (S_i and S^T_i) is C
+      (the independent set), and the F marking repeats.  (Measures are
+      distinct with probability one; a round that selects nothing takes the
+      undecided point of largest (measure, -i) -- a guard hypre does not need.)"""
+    if n == 0:
+        return cf.copy()
+    rows, cols = _pattern(S, n)
+    lam = np.bincount(cols, minlength=n).astype(np.float64)
+    part = np.zeros(n, dtype=np.int64) if part is None else np.asarray(part, dtype=np.int64)
+    starts = np.flatnonzero(np.r_[True, part[1:] != part[:-1]])
+    ends = np.r_[starts[1:], n]
+    rnd = np.empty(n, dtype=np.float64)
+    for a, b in zip(starts.tolist(), ends.tolist()):
+        rnd[a:b] = hypre_rand(2747 + int(part[a]), b - a)
+    measure = lam + rnd
+    boundary = np.zeros(n, dtype=bool)
+    boundary[rows[part[rows] != part[cols]]] = True
+    state = np.where((np.asarray(cf) == C) & ~boundary, C, U).astype(np.int64)
+    state[(state == U) & (lam == 0)] = F
+    Sm = sp.csr_matrix((np.ones(rows.size), (rows, cols)), shape=(n, n))
+    sym = (Sm + Sm.T).tocsr()
+    sym.sort_indices()
+    nonempty = np.diff(sym.indptr) > 0
+    starts_nb = sym.indptr[:-1][nonempty]
+
+    def mark_f():
+        hasc = (Sm @ (state == C).astype(np.float64)) > 0
+        state[(state == U) & hasc] = F
+
+    mark_f()
+    while np.any(state == U):
+        und = state == U
+        m = np.where(und[sym.indices], measure[sym.indices], -1.0)
+        nbmax = np.full(n, -1.0)
+        if m.size:
+            nbmax[nonempty] = np.maximum.reduceat(m, starts_nb)
+        sel = und & (measure > nbmax)
+        if not sel.any():
+            cand = np.flatnonzero(und)
+            sel[cand[np.argmax(measure[cand])]] = True
+        state[sel] = C
+        mark_f()
+    return np.where(state == C, C, F).astype(np.int64)
+
+
 def coarsen(S, n, aggressive, num_paths, part=None):
-    """C/F splitting (HMIS).  part: the level's partition (hypre's HMIS runs the
-    first pass inside each process; libpls cuts levels of >= 2 x 65,536 rows
-    into partitions of at least that size whose boundaries cut <= 2 % of the
-    strong connections, pls.hypre_coarsen_*, so the pass runs on host
-    threads) -- None: one partition."""
-    cf = rs_partitioned(S, n, part)
+    """C/F splitting (HMIS = the Ruge-Stueben first pass inside every
+    partition, then the PMIS stage, ``pmis_stage``).  part: the level's
+    partition, hypre's processes (pls.hypre_ranks) or libpls's automatic
+    partitions (levels of >= 2 x 65,536 rows cut into partitions of at least
+    that size whose boundaries cut <= 2 % of the strong connections,
+    pls.hypre_coarsen_*, so the first pass runs on host threads; the result
+    is then BoomerAMG's HMIS with that many processes) -- None: one process."""
+    cf = pmis_stage(S, n, rs_partitioned(S, n, part), part)
     if aggressive:
         S2, cpts = second_strength(S, cf, num_paths)
-        cf2 = rs_partitioned(S2, len(cpts), None if part is None else part[cpts])
+        p2 = None if part is None else part[cpts]
+        cf2 = pmis_stage(S2, len(cpts), rs_partitioned(S2, len(cpts), p2), p2)
         cf = np.full(n, F, dtype=np.int64)
         cf[cpts[cf2 == C]] = C
     return cf

@@ -441,11 +441,106 @@ std::vector<int64_t> chunk_starts(int64_t n, int64_t K) {
     return st;
 }
 
+// oracle hypre_rand(): hypre_Rand() after hypre_SeedRand(seed), Park-Miller by Schrage
+struct HypreRand {
+    int64_t s;
+    explicit HypreRand(int64_t seed) : s(seed) {}
+    double next() {
+        const int64_t hi = s / 127773, lo = s % 127773;
+        const int64_t t = 16807 * lo - 2836 * hi;
+        s = t > 0 ? t : t + 2147483647;
+        return (double)s / 2147483647.0;
+    }
+};
+
+// oracle pmis_stage(): HMIS's PMIS stage over the first pass's splitting
+// (partition k = process k: seeds 2747 + k; boundary = a strong dependency on
+// another partition's point)
+std::vector<int8_t> pmis_stage(const Pattern &S, const std::vector<int8_t> &cf1, const std::vector<int64_t> &pst) {
+    const int64_t n = S.n;
+    if (n == 0) return cf1;
+    const int64_t K = (int64_t)pst.size() - 1;
+    const Pattern ST = transpose(S);
+    std::vector<int32_t> part(n, 0);
+    std::vector<double> measure(n);
+    for (int64_t k = 0; k < K; ++k) {
+        HypreRand r(2747 + k);
+        for (int64_t i = pst[k]; i < pst[k + 1]; ++i) {
+            part[i] = (int32_t)k;
+            measure[i] = (double)ST.len(i) + r.next();
+        }
+    }
+    const int T = setup_threads();
+    std::vector<int8_t> st(n);
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            bool boundary = false;
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1] && !boundary; ++q) boundary = part[S.ci[q]] != part[i];
+            st[i] = (cf1[i] == CPT && !boundary) ? CPT : (ST.len(i) == 0 ? FPT : UND);
+        }
+    });
+    std::vector<int8_t> nxt(n);
+    auto mark_f = [&]() {  // undecided points with a strong dependency on a C point -> F (reads st, writes nxt)
+        std::vector<int64_t> und(T, 0);
+        parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
+            for (int64_t i = i0; i < i1; ++i) {
+                int8_t s = st[i];
+                if (s == UND) {
+                    for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q)
+                        if (st[S.ci[q]] == CPT) {
+                            s = FPT;
+                            break;
+                        }
+                    und[t] += s == UND;
+                }
+                nxt[i] = s;
+            }
+        });
+        st.swap(nxt);
+        int64_t u = 0;
+        for (int64_t x : und) u += x;
+        return u;
+    };
+    for (int64_t left = mark_f(); left > 0; left = mark_f()) {
+        std::vector<int64_t> sel(T, 0);
+        parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
+            for (int64_t i = i0; i < i1; ++i) {
+                int8_t s = st[i];
+                if (s == UND) {
+                    bool best = true;
+                    const double mi = measure[i];
+                    for (int64_t q = S.rp[i]; q < S.rp[i + 1] && best; ++q)
+                        best = st[S.ci[q]] != UND || mi > measure[S.ci[q]];
+                    for (int64_t q = ST.rp[i]; q < ST.rp[i + 1] && best; ++q)
+                        best = st[ST.ci[q]] != UND || mi > measure[ST.ci[q]];
+                    if (best) {
+                        s = CPT;
+                        ++sel[t];
+                    }
+                }
+                nxt[i] = s;
+            }
+        });
+        st.swap(nxt);
+        int64_t ns = 0;
+        for (int64_t x : sel) ns += x;
+        if (ns == 0) {  // (the oracle's guard: ties of measures)
+            int64_t b = -1;
+            for (int64_t i = 0; i < n; ++i)
+                if (st[i] == UND && (b < 0 || measure[i] > measure[b])) b = i;
+            st[b] = CPT;
+        }
+    }
+    for (auto &s : st)
+        if (s != CPT) s = FPT;
+    return st;
+}
+
 std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths, const std::vector<int64_t> &pst) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double t0 = now();
     const int64_t K = (int64_t)pst.size() - 1;
-    std::vector<int8_t> cf = rs_partitioned(S, K, pst);
+    std::vector<int8_t> cf = pmis_stage(S, rs_partitioned(S, K, pst), pst);
     if (!aggressive) return cf;
     double t1 = now();
     std::vector<int32_t> cpts;
@@ -461,7 +556,8 @@ std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths, const 
         }
         pst2[K] = (int64_t)cpts.size();
     }
-    const std::vector<int8_t> cf2 = rs_partitioned(S2, K, pst2);  // (K: partitions, some possibly empty)
+    // (K: partitions, some possibly empty)
+    const std::vector<int8_t> cf2 = pmis_stage(S2, rs_partitioned(S2, K, pst2), pst2);
     if (std::getenv("PLS_AMG_TRACE"))
         fprintf(stderr, "[boomeramg coarsen] n %lld S nnz %lld: RS %.2f s; S2 (%zu C1 points, nnz %lld) %.2f s; RS2 %.2f s\n",
                 (long long)S.n, (long long)S.ci.size(), t1 - t0, cpts.size(), (long long)S2.ci.size(), t2 - t1, now() - t2);

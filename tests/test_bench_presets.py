@@ -167,3 +167,12 @@ def test_bench_refuses_sharded_ilu():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--inner", "ilu"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "redundant_ilu" in r.stderr
+
+
+def test_bench_records_hypre_semantics():
+    import bench
+    s = bench.hypre_semantics({"s_pc_type": "hypre"}, 1)
+    assert "PMIS" in s["coarsening"] and s["hypre_K"] == 256 and s["relax_min_rows"] == 1024
+    assert "np = 3" in bench.hypre_semantics({"pls.hypre_ranks": "3"}, 1)["processes"]
+    assert "np = 8 (the sharded" in bench.hypre_semantics({}, 8)["processes"]
+    assert bench.hypre_semantics({"pls.hypre_coarsen_chunks": "1"}, 1)["processes"] == "np = 1"

@@ -262,6 +262,42 @@ def test_partitioned_first_pass_is_per_partition():
     assert not np.array_equal(cf, rs_first_pass(S, n))  # the partition boundary changes the splitting
 
 
+def test_hypre_rand_is_the_minimal_standard_generator():
+    """hypre_Rand (Park-Miller, a = 16807, m = 2^31 - 1): the generator's
+    published check values from seed 1 (16807, 282475249, 1622650073; the
+    10,000th value 1043618065)."""
+    from oracle.boomeramg import hypre_rand
+    m = 2147483647
+    v = hypre_rand(1, 10000) * m
+    assert np.round(v[:3]).astype(np.int64).tolist() == [16807, 282475249, 1622650073]
+    assert int(round(v[-1])) == 1043618065
+
+
+@pytest.mark.parametrize("K", [1, 3, 8])
+def test_pmis_stage_properties(K):
+    """HMIS's PMIS stage over the per-partition first pass (lap2 and an
+    anisotropic operator, K partitions): interior first-pass C points stay C;
+    the points PMIS makes C form an independent set of S (no strong
+    connection between two of them); every F point strongly depends on a C
+    point or has no point depending on it."""
+    from oracle.boomeramg import chunk_ids, pmis_stage, rs_partitioned, transpose_lists
+    for A in (lap2(24), lap2(20, eps=0.05)):
+        n = A.shape[0]
+        S = strength(A)
+        part = chunk_ids(n, K)
+        cf1 = rs_partitioned(S, n, part)
+        cf = pmis_stage(S, n, cf1, part)
+        ST = transpose_lists(S, n)
+        boundary = np.array([bool(np.any(part[S[i]] != part[i])) for i in range(n)])
+        keep = (cf1 == C) & ~boundary
+        assert np.all(cf[keep] == C)
+        new = (cf == C) & ~keep
+        for i in np.flatnonzero(new):
+            assert not np.any(new[S[i]]), i
+        for i in np.flatnonzero(cf == F):
+            assert np.any(cf[S[i]] == C) or len(ST[i]) == 0, i
+
+
 @pytest.mark.parametrize("ranks", ["3", "2"])
 def test_libpls_host_setup_bitwise_ranks(ranks):
     """hypre under mpirun -np G (pls.hypre_ranks): libpls's host setup equals
