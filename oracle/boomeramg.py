@@ -263,17 +263,19 @@ def pmis_stage(S, n, cf, part=None):
     * measure_i = |S^T_i| + a random number in [0, 1): process (partition) k
       draws hypre_Rand() for its rows in order after hypre_SeedRand(2747 + k)
       (hypre_BoomerAMGIndepSetInit);
-    * the first pass's C points without a strong dependency on another
-      partition's point stay C; every other point is undecided, or F when
-      |S^T_i| = 0 (measure < 1: no point depends on it);
+    * points without a strong dependency on another partition's point keep
+      their first-pass decision; the boundary points (a strong dependency on
+      another partition's point: hypre's S_offd) are undecided, or F when
+      |S^T_i| = 0 (measure < 1: no point depends on it) -- one partition
+      (np = 1) is therefore the first pass itself;
     * an undecided point with a strong dependency on a C point becomes F; then,
       while points are undecided: every undecided point whose measure exceeds
       the measures of all its undecided strong neighbours (S_i and S^T_i) is C
       (the independent set), and the F marking repeats.  (Measures are
       distinct with probability one; a round that selects nothing takes the
       undecided point of largest (measure, -i) -- a guard hypre does not need.)"""
-    if n == 0:
-        return cf.copy()
+    if n == 0 or part is None or np.all(np.asarray(part) == np.asarray(part)[0]):
+        return np.asarray(cf).copy()  # one partition: no boundary points
     rows, cols = _pattern(S, n)
     lam = np.bincount(cols, minlength=n).astype(np.float64)
     part = np.zeros(n, dtype=np.int64) if part is None else np.asarray(part, dtype=np.int64)
@@ -285,7 +287,7 @@ def pmis_stage(S, n, cf, part=None):
     measure = lam + rnd
     boundary = np.zeros(n, dtype=bool)
     boundary[rows[part[rows] != part[cols]]] = True
-    state = np.where((np.asarray(cf) == C) & ~boundary, C, U).astype(np.int64)
+    state = np.where(boundary, U, np.asarray(cf)).astype(np.int64)
     state[(state == U) & (lam == 0)] = F
     Sm = sp.csr_matrix((np.ones(rows.size), (rows, cols)), shape=(n, n))
     sym = (Sm + Sm.T).tocsr()

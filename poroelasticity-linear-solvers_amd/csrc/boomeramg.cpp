@@ -458,7 +458,7 @@ struct HypreRand {
 // another partition's point)
 std::vector<int8_t> pmis_stage(const Pattern &S, const std::vector<int8_t> &cf1, const std::vector<int64_t> &pst) {
     const int64_t n = S.n;
-    if (n == 0) return cf1;
+    if (n == 0 || pst.size() <= 2) return cf1;  // one partition: no boundary points
     const int64_t K = (int64_t)pst.size() - 1;
     const Pattern ST = transpose(S);
     std::vector<int32_t> part(n, 0);
@@ -476,7 +476,7 @@ std::vector<int8_t> pmis_stage(const Pattern &S, const std::vector<int8_t> &cf1,
         for (int64_t i = i0; i < i1; ++i) {
             bool boundary = false;
             for (int64_t q = S.rp[i]; q < S.rp[i + 1] && !boundary; ++q) boundary = part[S.ci[q]] != part[i];
-            st[i] = (cf1[i] == CPT && !boundary) ? CPT : (ST.len(i) == 0 ? FPT : UND);
+            st[i] = !boundary ? cf1[i] : (ST.len(i) == 0 ? FPT : UND);
         }
     });
     std::vector<int8_t> nxt(n);

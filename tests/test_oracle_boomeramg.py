@@ -276,10 +276,11 @@ def test_hypre_rand_is_the_minimal_standard_generator():
 @pytest.mark.parametrize("K", [1, 3, 8])
 def test_pmis_stage_properties(K):
     """HMIS's PMIS stage over the per-partition first pass (lap2 and an
-    anisotropic operator, K partitions): interior first-pass C points stay C;
-    the points PMIS makes C form an independent set of S (no strong
-    connection between two of them); every F point strongly depends on a C
-    point or has no point depending on it."""
+    anisotropic operator, K partitions): points without a strong dependency
+    on another partition keep their first-pass decision (K = 1: the first
+    pass itself); the boundary points PMIS makes C form an independent set of
+    S; every boundary F point strongly depends on a C point or has no point
+    depending on it."""
     from oracle.boomeramg import chunk_ids, pmis_stage, rs_partitioned, transpose_lists
     for A in (lap2(24), lap2(20, eps=0.05)):
         n = A.shape[0]
@@ -289,12 +290,12 @@ def test_pmis_stage_properties(K):
         cf = pmis_stage(S, n, cf1, part)
         ST = transpose_lists(S, n)
         boundary = np.array([bool(np.any(part[S[i]] != part[i])) for i in range(n)])
-        keep = (cf1 == C) & ~boundary
-        assert np.all(cf[keep] == C)
-        new = (cf == C) & ~keep
-        for i in np.flatnonzero(new):
-            assert not np.any(new[S[i]]), i
-        for i in np.flatnonzero(cf == F):
+        assert np.array_equal(cf[~boundary], cf1[~boundary])
+        assert K > 1 or np.array_equal(cf, cf1)
+        newc = (cf == C) & boundary
+        for i in np.flatnonzero(newc):
+            assert not np.any(newc[S[i]]), i
+        for i in np.flatnonzero((cf == F) & boundary):
             assert np.any(cf[S[i]] == C) or len(ST[i]) == 0, i
 
 
