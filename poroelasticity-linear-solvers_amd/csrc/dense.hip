@@ -385,23 +385,19 @@ __global__ __launch_bounds__(DTPB) void k_mf_gj_diag(const MFront *F, int k, dou
         }
         __syncthreads();
         double piv = a[p][p];
-        if (fabs(piv) <= tau && k * DB + p < f.p) {  // static pivot (not on the identity padding) (MUMPS CNTL(4) semantics): perturb, count, refine later
+        __syncthreads();  // every wave holds the pivot before row p is normalized (a[p][p] := 1 below)
+        if (fabs(piv) <= tau && k * DB + p < f.p) {  // static pivot (MUMPS CNTL(4) semantics), not on the padding
             if (tau <= 0.0) {
                 if (threadIdx.x == 0) atomicOr(fail, 1);
-                return;  // uniform across the workgroup
+                return;  // uniform across the workgroup: every thread read the same pivot
             }
             piv = piv < 0.0 ? -tau : tau;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                a[p][p] = piv;
-                atomicAdd(fail + 1, 1);
-            }
-            __syncthreads();
+            if (threadIdx.x == 0) atomicAdd(fail + 1, 1);
         }
         if (threadIdx.x < 2 * DB) {
             const int j = threadIdx.x & (DB - 1);
-            double (*m)[DB + 1] = threadIdx.x < DB ? a : v;
-            m[p][j] = m[p][j] / piv;
+            if (threadIdx.x < DB) a[p][j] = j == p ? 1.0 : a[p][j] / piv;
+            else v[p][j] = v[p][j] / piv;
         }
         __syncthreads();
         double fv[DB * DB / DTPB];
