@@ -336,11 +336,16 @@ void launch_mf_extend(int nc, const MChild *C, int max_q, const int32_t *maps, c
 }
 
 // Gauss-Jordan step k, as launch_dense_invert but over the front's pivot tiles
-// only and batched over fronts (blockIdx.z).  The diagonal tile's inverse is
-// formed with partial pivoting inside the tile (row swaps on [T | I]): the block
-// elimination only needs D = T_kk^-1, however it is computed, and saddle-point
-// blocks (the 2-way fp block: zero pressure diagonal) have zero scalar pivots
-// whose tile is still regular.
+// only and batched over fronts (blockIdx.z).  The block elimination only needs
+// D = T_kk^-1, however it is computed; saddle-point blocks (the 2-way fp block:
+// zero pressure diagonal) have zero scalar pivots whose tile is still regular.
+// D is formed as LAPACK's getrf + getrs on the identity: LU with partial
+// pivoting in LDS, then L^-1 and U^-1 applied to P I.  (Round 3 formed it by
+// scalar Gauss-Jordan with partial pivoting: on footing's undrained solid
+// block -- Dirichlet rows of unit diagonal next to entries of 1e6 -- that left
+// ||K y - x|| / ||x|| at 2.4e-6 .. 7.9e-6 with 64-row leaves, where the LU
+// inverse gives 7.9e-11, LAPACK's own level; CPU restatement in
+// tools/mf_emulate.py.)
 #pragma clang fp contract(off)
 // fail[0]: a zero pivot with static pivoting off (tau = 0); fail[1]: pivots replaced by +-tau
 __global__ __launch_bounds__(DTPB) void k_mf_gj_diag(const MFront *F, int k, double *W, double *D, int32_t *fail,
@@ -358,6 +363,7 @@ __global__ __launch_bounds__(DTPB) void k_mf_gj_diag(const MFront *F, int k, dou
         v[i][j] = i == j ? 1.0 : 0.0;
     }
     __syncthreads();
+    // LU with partial pivoting: a := L \ U (unit L below the diagonal), rows of v = P I swapped alike
     for (int p = 0; p < DB; ++p) {
         if (threadIdx.x < DB) {  // wave 0: argmax |a[i][p]|, i >= p (ties: the smaller row)
             const int i = threadIdx.x;
@@ -385,29 +391,41 @@ __global__ __launch_bounds__(DTPB) void k_mf_gj_diag(const MFront *F, int k, dou
         }
         __syncthreads();
         double piv = a[p][p];
-        __syncthreads();  // every wave holds the pivot before row p is normalized (a[p][p] := 1 below)
+        __syncthreads();  // every wave holds the pivot before a[p][p] may change
         if (fabs(piv) <= tau && k * DB + p < f.p) {  // static pivot (MUMPS CNTL(4) semantics), not on the padding
             if (tau <= 0.0) {
                 if (threadIdx.x == 0) atomicOr(fail, 1);
                 return;  // uniform across the workgroup: every thread read the same pivot
             }
             piv = piv < 0.0 ? -tau : tau;
-            if (threadIdx.x == 0) atomicAdd(fail + 1, 1);
+            if (threadIdx.x == 0) {
+                a[p][p] = piv;
+                atomicAdd(fail + 1, 1);
+            }
         }
-        if (threadIdx.x < 2 * DB) {
-            const int j = threadIdx.x & (DB - 1);
-            if (threadIdx.x < DB) a[p][j] = j == p ? 1.0 : a[p][j] / piv;
-            else v[p][j] = v[p][j] / piv;
+        if (threadIdx.x > p && threadIdx.x < DB) a[threadIdx.x][p] = a[threadIdx.x][p] / piv;  // l_ip
+        __syncthreads();
+        for (int t = threadIdx.x; t < DB * DB; t += DTPB) {  // trailing update
+            const int i = t / DB, j = t % DB;
+            if (i > p && j > p) a[i][j] = a[i][j] - a[i][p] * a[p][j];
         }
         __syncthreads();
-        double fv[DB * DB / DTPB];
-        for (int u = 0; u < DB * DB / DTPB; ++u) fv[u] = a[(threadIdx.x + u * DTPB) / DB][p];
+    }
+    // v := L^-1 v
+    for (int p = 0; p < DB - 1; ++p) {
+        for (int t = threadIdx.x; t < DB * DB; t += DTPB) {
+            const int i = t / DB, j = t % DB;
+            if (i > p) v[i][j] = v[i][j] - a[i][p] * v[p][j];
+        }
         __syncthreads();
-        for (int u = 0; u < DB * DB / DTPB; ++u) {
-            const int t = threadIdx.x + u * DTPB, i = t / DB, j = t % DB;
-            if (i == p) continue;
-            a[i][j] = a[i][j] - fv[u] * a[p][j];
-            v[i][j] = v[i][j] - fv[u] * v[p][j];
+    }
+    // v := U^-1 v
+    for (int p = DB - 1; p >= 0; --p) {
+        if (threadIdx.x < DB) v[p][threadIdx.x] = v[p][threadIdx.x] / a[p][p];
+        __syncthreads();
+        for (int t = threadIdx.x; t < p * DB; t += DTPB) {
+            const int i = t / DB, j = t % DB;
+            v[i][j] = v[i][j] - a[i][p] * v[p][j];
         }
         __syncthreads();
     }

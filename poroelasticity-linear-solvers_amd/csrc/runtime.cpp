@@ -2075,7 +2075,7 @@ void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
         if (!right) pc->apply(t1p, v0, c);
         double res = c.norm2(n, v0);
         history.push_back(res);
-        if (monitor) printf("  %3d KSP Residual norm %.12e\n", its, res);
+        if (monitor) { printf("  %3d KSP Residual norm %.12e\n", its, res); fflush(stdout); }
         if (res == 0.0) {
             reason = CONVERGED_ATOL;
             rnorm = 0.0;
@@ -2139,7 +2139,7 @@ void KSP::solve_gmres(const double *b, double *x, Ctx &c) {
             its++;
             rnorm = res;
             history.push_back(res);
-            if (monitor) printf("  %3d KSP Residual norm %.12e\n", its, res);
+            if (monitor) { printf("  %3d KSP Residual norm %.12e\n", its, res); fflush(stdout); }
             reason = converged(its, res);
             if (hapend && !reason) {
                 reason = DIVERGED_BREAKDOWN;
