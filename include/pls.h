@@ -213,7 +213,8 @@ int pls_boomeramg_host_level(const pls_csr *A, const char *options, const char *
  * petsc-options-inexact:105-106) that `options` would build on A: ordering
  * (pls.lu_nd*) and symbolic factorization only, no device needed.
  * stats[0..9]: n, fronts, tree levels, largest front (p + q), factor doubles
- * one solve reads (sum p (p + 2 q)), doubles stored, factorization flops,
+ * stored and read once per solve (sum p (p + 2 q)), the fronts' dense
+ * workspace doubles (64-row tiles, summed over fronts), factorization flops,
  * ordering s, symbolic s, largest separator.  When non-NULL: perm[n] (ND
  * position -> row), front_of[n] (position -> front, fronts numbered in
  * postorder so every front's pivots are contiguous) and parent[fronts]

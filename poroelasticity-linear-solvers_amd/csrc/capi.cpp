@@ -1535,6 +1535,7 @@ int pls_sparse_lu_analyze(const pls_csr *A, const char *options, double *stats, 
         H.nrows = H.ncols = A->nrows;
         H.rp.assign(A->row_ptr, A->row_ptr + A->nrows + 1);
         H.ci.assign(A->col, A->col + H.rp.back());
+        if (A->val) H.v.assign(A->val, A->val + H.rp.back());
         sparse_lu_analyze(H, o, stats, nstats, perm, front_of, parent);
     })
 }

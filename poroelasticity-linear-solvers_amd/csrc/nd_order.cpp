@@ -40,12 +40,14 @@
 
 namespace pls {
 
-void sym_graph(const HostCSR &A, std::vector<int64_t> &gp, std::vector<int32_t> &gi) {
+void sym_graph(const HostCSR &A, std::vector<int64_t> &gp, std::vector<int32_t> &gi, bool skip_zeros) {
     const int64_t n = A.nrows;
+    skip_zeros = skip_zeros && A.v.size() == A.ci.size();
+    auto edge = [&](int64_t i, int64_t k) { return A.ci[k] != i && !(skip_zeros && A.v[k] == 0.0); };
     std::vector<int64_t> deg(n + 1, 0);
     for (int64_t i = 0; i < n; ++i)
         for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
-            if (A.ci[k] != i) {
+            if (edge(i, k)) {
                 ++deg[i + 1];
                 ++deg[A.ci[k] + 1];
             }
@@ -54,7 +56,7 @@ void sym_graph(const HostCSR &A, std::vector<int64_t> &gp, std::vector<int32_t> 
     std::vector<int64_t> pos(deg.begin(), deg.end() - 1);
     for (int64_t i = 0; i < n; ++i)
         for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k)
-            if (A.ci[k] != i) {
+            if (edge(i, k)) {
                 tmp[pos[i]++] = A.ci[k];
                 tmp[pos[A.ci[k]]++] = (int32_t)i;
             }

@@ -34,8 +34,11 @@ struct NDOptions {
     int threads = 0;           // host threads for independent subgraphs (0: setup_threads())
 };
 
-// symmetrized adjacency of M's pattern without the diagonal (sorted rows)
-void sym_graph(const HostCSR &A, std::vector<int64_t> &gp, std::vector<int32_t> &gi);
+// symmetrized adjacency of M's pattern without the diagonal (sorted rows);
+// skip_zeros: entries stored with value 0 are not edges (PETSc's MatMatMult
+// keeps structural zeros, e.g. in the Schur block selfp -- they add fill
+// without adding anything to the factors)
+void sym_graph(const HostCSR &A, std::vector<int64_t> &gp, std::vector<int32_t> &gi, bool skip_zeros = false);
 
 // nested dissection of the graph (gp, gi) on n vertices
 NDTree nested_dissection(const std::vector<int64_t> &gp, const std::vector<int32_t> &gi, int64_t n,

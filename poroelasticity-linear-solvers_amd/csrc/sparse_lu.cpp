@@ -80,7 +80,7 @@ LUSymbolic lu_symbolic(const HostCSR &A, const Options &o) {
     LUSymbolic Y;
     const int64_t n = A.nrows;
     const double t0 = now_s();
-    sym_graph(A, Y.gp, Y.gi);
+    sym_graph(A, Y.gp, Y.gi, true);  // stored zeros are not structure: they add no fill
     Y.T = nested_dissection(Y.gp, Y.gi, n, lu_nd_options(o));
     const NDTree &T = Y.T;
     Y.nfront = (int64_t)T.piv.size();
@@ -166,8 +166,9 @@ void sparse_lu_analyze(const HostCSR &A, const Options &o, double *stats, int64_
         const double p = (double)Y.T.piv[f].size(), q = (double)Y.st[f].size();
         const double pp = std::ceil(p / 64) * 64, ld = pp + std::ceil(q / 64) * 64;
         v[3] = std::max(v[3], p + q);
-        v[4] += p * (p + 2 * q);
-        v[5] += pp * ld + q * pp;
+        v[4] += p * (p + 2 * q);  // compact U (p x (p + q)) and X (q x p) parts: stored and read once per solve
+        v[5] += ld * ld;          // the front's dense workspace during the factorization (tiles padded)
+        (void)pp;
         v[6] += 2.0 / 3.0 * p * p * p + 2.0 * p * p * q + 2.0 * p * q * q;
         v[9] = std::max(v[9], p);
     }
@@ -255,6 +256,7 @@ struct PCSparseLU : PC {
             }
         for (int64_t i = 0; i < n; ++i)
             for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                if (A.v[k] == 0.0 && A.ci[k] != i) continue;  // stored zero: outside the (value) structure
                 const int32_t pi = pos[i], pj = pos[A.ci[k]];
                 const int32_t f = front_of[std::min(pi, pj)];
                 const int64_t r = local(f, pi), cc = local(f, pj);
@@ -407,7 +409,9 @@ struct PCSparseLU : PC {
         up(cidx, hci);
         c.sync();
         Mref = &M;
-        refine = (int)o.integer("pls.lu_refine", 1);
+        // iterative refinement steps (MUMPS's ICNTL(10), default 0): the front
+        // inverses (LU-based tile inverses) leave LAPACK-level residuals
+        refine = (int)o.integer("pls.lu_refine", 0);
         // perturbed pivots: the factorization is of a nearby matrix; refinement recovers the solve
         if (static_pivots > 0) refine = std::max(refine, (int)o.integer("pls.lu_static_refine", 2));
         if (refine > 0 && !M.sell) build_sell(const_cast<DevCSR &>(M), c);

@@ -261,7 +261,7 @@ def boomeramg_host_level(A, options: dict, prefix: str, level: int):
     return nl.value, n.value, nc.value, cf, P
 
 
-LU_STATS = ("n", "fronts", "levels", "max_front", "solve_doubles", "stored_doubles", "flops", "order_s",
+LU_STATS = ("n", "fronts", "levels", "max_front", "solve_doubles", "workspace_doubles", "flops", "order_s",
             "symbolic_s", "max_separator")
 
 

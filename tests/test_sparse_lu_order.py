@@ -56,11 +56,12 @@ def test_dissection_is_an_assembly_tree(blocks16, name, method):
     nf = int(st["fronts"])
     assert front_of[-1] == nf - 1 and parent[nf - 1] == -1
     assert np.all(parent[:-1] > np.arange(nf - 1))  # children before parents
-    # the assembly tree property: every off-diagonal entry couples a front with an ancestor (or itself)
+    # the assembly tree property: every nonzero couples a front with an ancestor (or itself)
     pos = np.empty(n, dtype=np.int64)
     pos[perm] = np.arange(n)
     C = M.tocoo()
-    fa, fb = front_of[pos[C.row]], front_of[pos[C.col]]
+    nz = C.data != 0.0  # stored zeros are not structure (they add no fill)
+    fa, fb = front_of[pos[C.row[nz]]], front_of[pos[C.col[nz]]]
     lo, hi = np.minimum(fa, fb), np.maximum(fa, fb)
     anc = lo.copy()
     for _ in range(int(st["levels"]) + 1):
