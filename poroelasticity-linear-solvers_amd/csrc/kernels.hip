@@ -2668,6 +2668,81 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
                                                              Lval, Ubase, Usoff, Usz, Unsl, Ulpr, Ucol, Uval, x, y);
 }
 
+// ============================================================ window sweep ====
+// Triangular sweeps of LDS-resident blocks in windows of 64 consecutive rows
+// (lane = row): y_w = T_w^-1 (b_w - A_{w,off} y_off) with T_w the window's
+// diagonal block of the triangle (unit lower for L, with the diagonal for U)
+// inverted once at setup and stored column-major ([k][lane]), and A_{w,off}
+// the rows' entries outside the window on the solved side (SELL: [k][lane],
+// block-local columns, padding = column 0 with value 0).  The dependent chain
+// of a block is its windows (len / 64 steps of a 64 x 64 GEMV) instead of its
+// levels: FE rows in natural order have ~1 row per level (the AMG smoother's
+// chunks: ~970 levels per 2,405-row chunk, 38 windows).  One wave per block;
+// LDS accesses of a wave complete in order, so no barrier.  Sums: the
+// off-window entries in stream order, then T^-1's row in k order.
+template <bool UP>
+__device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t *__restrict__ woff,
+                                          const int32_t *__restrict__ col, const double *__restrict__ val,
+                                          const double *__restrict__ tinv, double *ys, int lane) {
+    const int64_t nw = (len + 63) >> 6;
+    for (int64_t ww = 0; ww < nw; ++ww) {
+        const int64_t w = UP ? nw - 1 - ww : ww;
+        const int64_t r = w * 64 + lane;
+        const bool act = r < len;
+        const int64_t s0 = woff[w0 + w], s1 = woff[w0 + w + 1];
+        double acc = 0.0;
+#pragma unroll 4
+        for (int64_t e = s0 + lane; e < s1; e += 64) acc += __dmul_rn(val[e], ys[col[e]]);
+        const double t = act ? ys[r] - acc : 0.0;
+        const double *T = tinv + (w0 + w) * 4096 + lane;
+        double tv[64];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) tv[k] = __builtin_nontemporal_load(T + k * 64);
+        const int tlo = __double2loint(t), thi = __double2hiint(t);
+        double out = 0.0;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            const double tk = __hiloint2double(__builtin_amdgcn_readlane(thi, k), __builtin_amdgcn_readlane(tlo, k));
+            out += __dmul_rn(tv[k], tk);
+        }
+        if (act) ys[r] = out;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart,
+                                                          const int64_t *__restrict__ wstart,
+                                                          const int64_t *__restrict__ Lwoff, const int32_t *__restrict__ Lcol,
+                                                          const double *__restrict__ Lval, const double *__restrict__ Ltinv,
+                                                          const int64_t *__restrict__ Uwoff, const int32_t *__restrict__ Ucol,
+                                                          const double *__restrict__ Uval, const double *__restrict__ Utinv,
+                                                          const double *x, double *y) {
+    extern __shared__ __attribute__((aligned(16))) double ys[];
+    const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
+    int64_t b0, len;
+    block_range(blk, n, nblocks, bstart, b0, len);
+    const int lane = threadIdx.x;
+    for (int64_t t = lane; t < len; t += 64) ys[t] = x[b0 + t];
+    const int64_t w0 = wstart[blk];
+    win_sweep<false>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, lane);
+    win_sweep<true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, lane);
+    for (int64_t t = lane; t < len; t += 64) y[b0 + t] = ys[t];
+}
+
+void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
+                              const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
+                              const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,
+                              const double *x, double *y, int64_t max_len, hipStream_t st) {
+    static bool configured = false;
+    if (!configured) {
+        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_window, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)163840);
+        configured = true;
+    }
+    const size_t bytes = (size_t)std::max<int64_t>(max_len, 1) * 8;
+    k_ilu_blocks_window<<<(unsigned)nblocks, 64, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv,
+                                                              Uwoff, Ucol, Uval, Utinv, x, y);
+}
+
 // =========================================================== distribution ====
 // flag[c] = 1 for every column c (relative to the column space) of the matrix
 // that this rank does not own (own[c] < 0)

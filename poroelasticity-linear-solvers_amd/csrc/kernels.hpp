@@ -208,6 +208,14 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
                              const int32_t *Lcol, const double *Lval, const int64_t *Ubase, const int64_t *Usoff,
                              const int32_t *Usz, const int64_t *Unsl, const int32_t *Ulpr, const int32_t *Ucol,
                              const double *Uval, const double *x, double *y, int64_t max_len, hipStream_t st);
+// The window sweep (kernels.hip, k_ilu_blocks_window): LDS-resident blocks in
+// windows of 64 rows; per block its first window wstart[b] (nblocks + 1); per
+// triangle and window the off-window stream [woff[w], woff[w + 1]) ([k][lane]
+// SELL, block-local columns) and the window's inverse tinv[w * 4096 + k * 64 + lane].
+void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
+                              const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
+                              const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,
+                              const double *x, double *y, int64_t max_len, hipStream_t st);
 // The ring sweep (kernels.hip, k_ilu_blocks_ring): blocks of narrow levels whose
 // every level has <= ilu_ring_chunk() rows; per triangle chunk tables (coff per
 // block, cg first level, cp [start, end) positions), level orders ordL / ordU

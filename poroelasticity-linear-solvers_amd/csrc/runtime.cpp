@@ -10,6 +10,8 @@
 // as the CPU oracle evaluates them.
 #include "runtime.hpp"
 
+#include "amg_host.hpp"
+
 #include <climits>
 
 #include <algorithm>
@@ -1158,6 +1160,106 @@ static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order
 // slices of up to 4 consecutive steps (step q on lanes 16q .. 16q + 15).
 // Returns the step count, or -1 when a row does not fit (fv / dinv empty: a
 // dry run that only counts).
+// Window-sweep tables of one triangle of the (block-truncated) factors F (rp,
+// ci, fv, diagonal positions dg): per block, windows of 64 consecutive rows;
+// per window the rows' entries outside the window on the solved side (SELL,
+// [k][lane], block-local columns) and the inverse of the window's triangle --
+// unit lower (I + L_ww) or upper with the diagonal (U_ww) -- by row-wise
+// substitution in double precision without contraction, stored [k][lane].
+static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
+                             const std::vector<int32_t> &ci, const std::vector<int64_t> &dg,
+                             const std::vector<double> &fv, bool upper, WinTri &W, Ctx &c) {
+    std::vector<int64_t> wfirst(nblk + 1, 0);
+    for (int64_t b = 0; b < nblk; ++b) wfirst[b + 1] = wfirst[b] + (bst[b + 1] - bst[b] + 63) / 64;
+    const int64_t nw = wfirst[nblk];
+    std::vector<int64_t> wrow(nw), wend(nw);  // first row, end row of each window
+    for (int64_t b = 0; b < nblk; ++b)
+        for (int64_t w = wfirst[b]; w < wfirst[b + 1]; ++w) {
+            wrow[w] = bst[b] + (w - wfirst[b]) * 64;
+            wend[w] = std::min<int64_t>(wrow[w] + 64, bst[b + 1]);
+        }
+    auto off_range = [&](int64_t i, int64_t w, int64_t &k0, int64_t &k1) {  // entries of row i outside window w
+        if (!upper) {
+            k0 = rp[i];
+            k1 = k0;
+            while (k1 < dg[i] && ci[k1] < wrow[w]) ++k1;
+        } else {
+            k1 = rp[i + 1];
+            k0 = k1;
+            while (k0 > dg[i] + 1 && ci[k0 - 1] >= wend[w]) --k0;
+        }
+    };
+    std::vector<int64_t> woff(nw + 1, 0);
+    for (int64_t w = 0; w < nw; ++w) {
+        int64_t K = 0;
+        for (int64_t i = wrow[w]; i < wend[w]; ++i) {
+            int64_t k0, k1;
+            off_range(i, w, k0, k1);
+            K = std::max(K, k1 - k0);
+        }
+        woff[w + 1] = woff[w] + K * 64;
+    }
+    std::vector<int32_t> col(std::max<int64_t>(woff[nw], 1), 0);
+    std::vector<double> val(std::max<int64_t>(woff[nw], 1), 0.0), tinv((size_t)std::max<int64_t>(nw, 1) * 4096, 0.0);
+    amgh::parallel_rows(nw, amgh::setup_threads(), [&](int, int64_t w0, int64_t w1) {
+        std::vector<double> T(64 * 64), X(64 * 64);
+        for (int64_t w = w0; w < w1; ++w) {
+            int64_t b = std::upper_bound(wfirst.begin(), wfirst.end(), w) - wfirst.begin() - 1;
+            const int64_t r0 = wrow[w], m = wend[w] - r0, base = bst[b];
+            std::fill(T.begin(), T.end(), 0.0);
+            for (int64_t i = r0; i < wend[w]; ++i) {
+                const int lane = (int)(i - r0);
+                int64_t k0, k1;
+                off_range(i, w, k0, k1);
+                for (int64_t k = k0; k < k1; ++k) {
+                    col[woff[w] + (k - k0) * 64 + lane] = (int32_t)(ci[k] - base);
+                    val[woff[w] + (k - k0) * 64 + lane] = fv[k];
+                }
+                // the window's triangle, row-major T[i][j]
+                if (!upper) {
+                    T[lane * 64 + lane] = 1.0;
+                    for (int64_t k = k1; k < dg[i]; ++k) T[lane * 64 + (ci[k] - r0)] = fv[k];
+                } else {
+                    for (int64_t k = dg[i]; k < k0; ++k) T[lane * 64 + (ci[k] - r0)] = fv[k];
+                }
+            }
+            std::fill(X.begin(), X.end(), 0.0);
+            if (!upper) {  // X = T^-1, T unit lower: row i of X from rows j < i
+                for (int64_t i = 0; i < m; ++i) {
+                    X[i * 64 + i] = 1.0;
+                    for (int64_t j = 0; j < i; ++j) {
+                        double s = 0.0;
+                        for (int64_t k = j; k < i; ++k) s += T[i * 64 + k] * X[k * 64 + j];
+                        X[i * 64 + j] = -s;
+                    }
+                }
+            } else {  // T upper with its diagonal: rows from the last
+                for (int64_t i = m - 1; i >= 0; --i) {
+                    const double d = T[i * 64 + i];
+                    X[i * 64 + i] = 1.0 / d;
+                    for (int64_t j = i + 1; j < m; ++j) {
+                        double s = 0.0;
+                        for (int64_t k = i + 1; k <= j; ++k) s += T[i * 64 + k] * X[k * 64 + j];
+                        X[i * 64 + j] = -s / d;
+                    }
+                }
+            }
+            for (int64_t i = 0; i < 64; ++i)
+                for (int64_t k = 0; k < 64; ++k) tinv[(size_t)w * 4096 + k * 64 + i] = X[i * 64 + k];
+        }
+    });
+    W.nwin = nw;
+    W.woff.alloc(nw + 1);
+    W.col.alloc(col.size());
+    W.val.alloc(val.size());
+    W.tinv.alloc(tinv.size());
+    HIPCHK(hipMemcpyAsync(W.woff.p, woff.data(), sizeof(int64_t) * (nw + 1), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(W.col.p, col.data(), sizeof(int32_t) * col.size(), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(W.val.p, val.data(), sizeof(double) * val.size(), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(W.tinv.p, tinv.data(), sizeof(double) * tinv.size(), hipMemcpyHostToDevice, c.st));
+    c.sync();
+}
+
 static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
                                const std::vector<int32_t> &ci, const std::vector<int64_t> &dg,
                                const std::vector<double> &fv, const std::vector<double> &dinv,
@@ -1336,7 +1438,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                 for (size_t k = 0; k + 1 < g->size(); ++k) wmax = std::max<int64_t>(wmax, (*g)[k + 1] - (*g)[k]);
             ring = wmax <= ilu_ring_chunk();
         }
-        if (use_lds && !gmem && c.sweep_chain != 0 && force_lpr == 0) {
+        if (use_lds && !gmem && (c.sweep_chain != 0 || c.sweep_window == 1) && force_lpr == 0) {
             // the chain sweep (one wave per block, 16-lane steps in order, up to 32
             // steps of factor data in flight) for deep, narrow level DAGs: measured
             // ~0.77 us per level for the workgroup sweep on the footing smoother
@@ -1347,7 +1449,24 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             const int64_t sL = build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oL, gL, fL, false, nullptr, c);
             const int64_t sU = sL < 0 ? -1 : build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oU, gU, fU, true, nullptr, c);
             const int64_t lev = (int64_t)gL.size() - 1 + (int64_t)gU.size() - 1;
-            chain = sL >= 0 && sU >= 0 && (c.sweep_chain == 1 || 2 * (sL + sU) <= 7 * lev);
+            const bool deep = sL >= 0 && sU >= 0 && 2 * (sL + sU) <= 7 * lev;
+            chain = c.sweep_chain != 0 && sL >= 0 && sU >= 0 && (c.sweep_chain == 1 || deep);
+            // the window sweep where the chain would run (or forced): a block's
+            // dependent chain becomes its len / 64 windows
+            window = c.sweep_window == 1 || (c.sweep_window == -1 && c.sweep_chain != 1 && deep);
+            if (window) {
+                chain = false;
+                std::vector<double> fv(F.nnz);
+                if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
+                c.sync();
+                build_window_tri(nblocks, bst, rp, ci, dg, fv, false, Lw, c);
+                build_window_tri(nblocks, bst, rp, ci, dg, fv, true, Uw, c);
+                std::vector<int64_t> wf(nblocks + 1, 0);
+                for (int64_t b = 0; b < nblocks; ++b) wf[b + 1] = wf[b] + (bst[b + 1] - bst[b] + 63) / 64;
+                wstart.alloc(nblocks + 1);
+                HIPCHK(hipMemcpyAsync(wstart.p, wf.data(), sizeof(int64_t) * (nblocks + 1), hipMemcpyHostToDevice, c.st));
+                c.sync();
+            }
             if (chain) {
                 std::vector<double> fv(F.nnz), dv(n);
                 if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
@@ -1357,7 +1476,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                 build_chain_tri(nblocks, bst, rp, ci, dg, fv, dv, oU, gU, fU, true, &Uc, c);
             }
         }
-        if (use_lds && !chain) {
+        if (use_lds && !chain && !window) {
             const int max_lpr = gmem ? (ring ? 32 : 16) : 4;
             std::vector<int32_t> pL, pU, loL, loU, nlL, nlU;
             if (ring) {
@@ -1446,6 +1565,11 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
                                Ur.coff.p, Ur.cg.p, Ur.cp.p, Lr.ord.p, mapUL.p, Ur.ord.p, Lr.frp.p, Lr.fcol.p,
                                Lr.fval.p, Ur.frp.p, Ur.fcol.p, Ur.fval.p, x, y, sc.first.p, sc.second.p, c.st,
                                lds_tpb, bstart_h.empty() ? nullptr : bstart.p);
+        return;
+    }
+    if (use_lds && window) {
+        launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.col.p,
+                                 Lw.val.p, Lw.tinv.p, Uw.woff.p, Uw.col.p, Uw.val.p, Uw.tinv.p, x, y, max_len, c.st);
         return;
     }
     if (use_lds && chain) {
@@ -1806,6 +1930,7 @@ std::unique_ptr<Ctx> layout_ctx(const Ctx &c) {
     self->spmv_b3 = c.spmv_b3;
     self->spmv_rcm = c.spmv_rcm;
     self->sweep_chain = c.sweep_chain;
+    self->sweep_window = c.sweep_window;
     return self;
 }
 

@@ -80,6 +80,8 @@ struct Ctx {
     int spmv_rcm = -1;            // RCM-relabelled SpMV layout: -1 where the plain plan pads (FE), 0 never, 1 always
     int sweep_chain = -1;         // LDS-resident ILU / Gauss-Seidel blocks swept by one wave (k_ilu_blocks_chain):
                                   // -1 where the level DAG is deep and narrow, 0 never, 1 whenever rows fit
+    int sweep_window = -1;        // ... in 64-row windows with inverted window triangles (k_ilu_blocks_window):
+                                  // -1 where the chain sweep would be chosen, 0 never, 1 whenever rows fit
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
@@ -307,8 +309,20 @@ struct ChainTri {
     DBuf<int32_t> col;
     DBuf<double> val;
 };
+// Window-sweep tables of one triangle (kernels.hip, k_ilu_blocks_window)
+struct WinTri {
+    DBuf<int64_t> woff;  // per window: off-window stream offsets (nwin + 1)
+    DBuf<int32_t> col;
+    DBuf<double> val, tinv;  // tinv: per window the 64 x 64 inverse of its diagonal block, [k][lane]
+    int64_t nwin = 0;
+};
 struct PCILU : PC {
     int64_t nblocks = 1;
+    // window sweep (Ctx::sweep_window): LDS-resident blocks in 64-row windows with
+    // explicit inverses of the windows' triangles (one GEMV per window)
+    bool window = false;
+    WinTri Lw, Uw;
+    DBuf<int64_t> wstart;  // per block: its first window
     // chain sweep (Ctx::sweep_chain): LDS-resident blocks of deep, narrow level DAGs
     bool chain = false;
     ChainTri Lc, Uc;

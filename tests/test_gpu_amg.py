@@ -81,7 +81,7 @@ def _boomer_db(no_cf=True):
 @pytest.mark.parametrize("t", ["gamg", "hypre", "hypre-inexact", "hypre-inexact-cf", "hypre-inexact-dense", "hypre-sa",
                                "hypre-inexact-k1", "hypre-inexact-k256", "hypre-inexact-cf-k256",
                                "hypre-inexact-ranks3", "hypre-inexact-cf-ranks3", "hypre-inexact-k256-chain",
-                               "hypre-inexact-cf-chain"])
+                               "hypre-inexact-cf-chain", "hypre-inexact-k256-window", "hypre-inexact-cf-window"])
 def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
     """hypre: PETSc's defaults (HMIS / ext+i, no truncation, no aggressive
     level, C/F-ordered Gauss-Seidel); -inexact: petsc-options-inexact's
@@ -90,7 +90,9 @@ def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
     mostly sequential coarse levels); -sa: pls.hypre sa; -k1 / -k256:
     the hybrid Gauss-Seidel with one chunk (plain symmetric GS) / 256 chunks on
     every level (no row floor); -ranks3: hypre under mpirun -np 3; -chain:
-    every LDS-resident smoother chunk on the chain sweep (pls.sweep_chain 1)."""
+    every LDS-resident smoother chunk on the chain sweep (pls.sweep_chain 1);
+    -window: ... on the window sweep (pls.sweep_window 1: 64-row windows with
+    inverted window triangles)."""
     params = dict(BASE, **{"pc type": pc_type, "inner pc type": "lu"})
     extra = {"hypre-inexact": _boomer_db(), "hypre-inexact-cf": _boomer_db(False), "hypre-sa": {"pls.hypre": "sa"},
              "hypre-inexact-dense": dict(_boomer_db(), **{"pls.amg_gs_dense": "1"}),
@@ -99,7 +101,9 @@ def test_amg_pc_apply_matches_oracle(gpu, spec, pc_type, t):
              "hypre-inexact-ranks3": dict(_boomer_db(), **RANKS3),
              "hypre-inexact-cf-ranks3": dict(_boomer_db(False), **RANKS3),
              "hypre-inexact-k256-chain": dict(_boomer_db(), **K256, **{"pls.sweep_chain": "1"}),
-             "hypre-inexact-cf-chain": dict(_boomer_db(False), **{"pls.sweep_chain": "1"})}
+             "hypre-inexact-cf-chain": dict(_boomer_db(False), **{"pls.sweep_chain": "1"}),
+             "hypre-inexact-k256-window": dict(_boomer_db(), **K256, **{"pls.sweep_window": "1"}),
+             "hypre-inexact-cf-window": dict(_boomer_db(False), **{"pls.sweep_window": "1"})}
     db = _amg_db(t.split("-")[0], extra.get(t))
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)
@@ -279,11 +283,13 @@ def test_chain_sweep_matches_workgroup_sweep(gpu, N):
     db.update({"s_" + k: v for k, v in BOOMER.items()})
     v = np.random.default_rng(2).standard_normal(s.A.shape[0])
     out = []
-    for ch in ("0", "1"):
-        opts = dict(db, **{"pls.sweep_chain": ch})
+    for ch, win in (("0", "0"), ("1", "0"), ("0", "1")):
+        opts = dict(db, **{"pls.sweep_chain": ch, "pls.sweep_window": win})
         opts.update(params_to_options(params))
         h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
         out.append(h.pc_apply(v))
         assert np.array_equal(h.pc_apply(v), out[-1])
         h.destroy()
     assert np.max(np.abs(out[0] - out[1])) <= 1e-13 * np.max(np.abs(out[0]))
+    # the window sweep (64-row windows, inverted window triangles): the same operator to rounding
+    assert np.max(np.abs(out[0] - out[2])) <= 1e-12 * np.max(np.abs(out[0]))

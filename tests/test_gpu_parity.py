@@ -161,7 +161,8 @@ def test_spmv_matches_scipy(gpu, dim, N, segs):
 
 
 @pytest.mark.parametrize("pc_type", ["diagonal", "diagonal 3-way"])
-@pytest.mark.parametrize("inner", ["ilu", "jacobi", "bjacobi", "ilu-chain", "bjacobi-chain"])
+@pytest.mark.parametrize("inner", ["ilu", "jacobi", "bjacobi", "ilu-chain", "bjacobi-chain", "ilu-window",
+                                   "bjacobi-window"])
 def test_pc_apply_matches_oracle(gpu, pc_type, inner):
     """-chain: the LDS-resident ILU(0) sweeps forced onto the chain sweep (one
     wave per block walking its slices in order, pls.sweep_chain 1)."""
@@ -175,6 +176,8 @@ def test_pc_apply_matches_oracle(gpu, pc_type, inner):
             db[pre + "pc_bjacobi_blocks"] = "3"
     if inner.endswith("-chain"):
         db["pls.sweep_chain"] = "1"
+    if inner.endswith("-window"):  # 64-row windows with inverted window triangles (pls.sweep_window 1)
+        db["pls.sweep_window"] = "1"
     h = _handle(spec, params, db)
     o = _oracle(spec, params, db)
     rng = np.random.default_rng(2)
