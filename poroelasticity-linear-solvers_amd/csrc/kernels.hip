@@ -2677,35 +2677,81 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
 // block-local columns, padding = column 0 with value 0).  The dependent chain
 // of a block is its windows (len / 64 steps of a 64 x 64 GEMV) instead of its
 // levels: FE rows in natural order have ~1 row per level (the AMG smoother's
-// chunks: ~970 levels per 2,405-row chunk, 38 windows).  One wave per block;
-// LDS accesses of a wave complete in order, so no barrier.  Sums: the
+// chunks: ~970 levels per 2,405-row chunk, 38 windows).  One wave per block.
+// The next window's inverse and first WIN_KP stream entries per lane are
+// copied global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// instruction, WIN_NDMA per window) while the current window computes; a
+// counted s_waitcnt vmcnt(WIN_NDMA) retires the current window's copies only.
+// Entries past WIN_KP (rare) are read with ordinary loads.  Sums: the
 // off-window entries in stream order, then T^-1's row in k order.
+static constexpr int WIN_KP = 16;                                  // stream entries per lane staged per window
+static constexpr int WIN_NDMA = 32 + WIN_KP / 4 + WIN_KP / 2;      // 1-KiB copies per window (T^-1, col, val)
+static constexpr int WIN_BUF = 4096 * 8 + WIN_KP * 64 * 12;        // bytes of one staging buffer
+static_assert(WIN_NDMA == 44, "the counted waits below assume 44 copies per window");
+
+__device__ __forceinline__ void win_stage(int64_t wg, const int64_t *__restrict__ woff, const int32_t *__restrict__ col,
+                                          const double *__restrict__ val, const double *__restrict__ tinv,
+                                          char *buf, int lane) {
+    const char *t = (const char *)(tinv + wg * 4096) + lane * 16;
+#pragma unroll
+    for (int q = 0; q < 32; ++q)
+        __builtin_amdgcn_global_load_lds((const void *)(t + q * 1024), (__attribute__((address_space(3))) void *)(buf + q * 1024), 16, 0, 0);
+    const int64_t s0 = woff[wg];
+    const char *c = (const char *)(col + s0) + lane * 16;
+#pragma unroll
+    for (int q = 0; q < WIN_KP / 4; ++q)
+        __builtin_amdgcn_global_load_lds((const void *)(c + q * 1024),
+                                         (__attribute__((address_space(3))) void *)(buf + 32768 + q * 1024), 16, 0, 0);
+    const char *v = (const char *)(val + s0) + lane * 16;
+#pragma unroll
+    for (int q = 0; q < WIN_KP / 2; ++q)
+        __builtin_amdgcn_global_load_lds((const void *)(v + q * 1024),
+                                         (__attribute__((address_space(3))) void *)(buf + 32768 + WIN_KP * 256 + q * 1024), 16,
+                                         0, 0);
+}
+
+__device__ __forceinline__ void win_compute(int64_t w, int64_t len, int64_t wg, const int64_t *__restrict__ woff,
+                                            const int32_t *__restrict__ col, const double *__restrict__ val,
+                                            const char *buf, double *ys, int lane) {
+    const int64_t r = w * 64 + lane;
+    const bool act = r < len;
+    const int64_t s0 = woff[wg], s1 = woff[wg + 1];
+    const int K = (int)((s1 - s0) >> 6);
+    const int32_t *bc = (const int32_t *)(buf + 32768);
+    const double *bv = (const double *)(buf + 32768 + WIN_KP * 256);
+    double acc = 0.0;
+    const int kp = K < WIN_KP ? K : WIN_KP;
+    for (int k = 0; k < kp; ++k) acc += __dmul_rn(bv[k * 64 + lane], ys[bc[k * 64 + lane]]);
+    for (int64_t e = s0 + WIN_KP * 64 + lane; e < s1; e += 64) acc += __dmul_rn(val[e], ys[col[e]]);
+    const double t = act ? ys[r] - acc : 0.0;
+    const double *T = (const double *)buf + lane;
+    const int tlo = __double2loint(t), thi = __double2hiint(t);
+    double out = 0.0;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        const double tk = __hiloint2double(__builtin_amdgcn_readlane(thi, k), __builtin_amdgcn_readlane(tlo, k));
+        out += __dmul_rn(T[k * 64], tk);
+    }
+    if (act) ys[r] = out;
+}
+
 template <bool UP>
 __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t *__restrict__ woff,
                                           const int32_t *__restrict__ col, const double *__restrict__ val,
-                                          const double *__restrict__ tinv, double *ys, int lane) {
+                                          const double *__restrict__ tinv, double *ys, char *bufs, int lane) {
     const int64_t nw = (len + 63) >> 6;
+    if (nw == 0) return;
+    auto wi = [&](int64_t ww) { return UP ? nw - 1 - ww : ww; };
+    win_stage(w0 + wi(0), woff, col, val, tinv, bufs, lane);
     for (int64_t ww = 0; ww < nw; ++ww) {
-        const int64_t w = UP ? nw - 1 - ww : ww;
-        const int64_t r = w * 64 + lane;
-        const bool act = r < len;
-        const int64_t s0 = woff[w0 + w], s1 = woff[w0 + w + 1];
-        double acc = 0.0;
-#pragma unroll 4
-        for (int64_t e = s0 + lane; e < s1; e += 64) acc += __dmul_rn(val[e], ys[col[e]]);
-        const double t = act ? ys[r] - acc : 0.0;
-        const double *T = tinv + (w0 + w) * 4096 + lane;
-        double tv[64];
-#pragma unroll
-        for (int k = 0; k < 64; ++k) tv[k] = __builtin_nontemporal_load(T + k * 64);
-        const int tlo = __double2loint(t), thi = __double2hiint(t);
-        double out = 0.0;
-#pragma unroll
-        for (int k = 0; k < 64; ++k) {
-            const double tk = __hiloint2double(__builtin_amdgcn_readlane(thi, k), __builtin_amdgcn_readlane(tlo, k));
-            out += __dmul_rn(tv[k], tk);
+        char *cur = bufs + (ww & 1) * WIN_BUF;
+        if (ww + 1 < nw) {
+            win_stage(w0 + wi(ww + 1), woff, col, val, tinv, bufs + ((ww + 1) & 1) * WIN_BUF, lane);
+            asm volatile("s_waitcnt vmcnt(44)" ::: "memory");  // this window's copies (issued one window ago) landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (act) ys[r] = out;
+        win_compute(wi(ww), len, w0 + wi(ww), woff, col, val, cur, ys, lane);
     }
 }
 
@@ -2716,17 +2762,23 @@ __global__ __launch_bounds__(64) void k_ilu_blocks_window(int64_t n, int64_t nbl
                                                           const int64_t *__restrict__ Uwoff, const int32_t *__restrict__ Ucol,
                                                           const double *__restrict__ Uval, const double *__restrict__ Utinv,
                                                           const double *x, double *y) {
-    extern __shared__ __attribute__((aligned(16))) double ys[];
+    // one dynamic LDS array: two staging buffers, then the block solution
+    extern __shared__ __attribute__((aligned(16))) double lds_win[];
+    char *bufs = (char *)lds_win;
+    double *ys = (double *)(bufs + 2 * WIN_BUF);
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
     int64_t b0, len;
     block_range(blk, n, nblocks, bstart, b0, len);
     const int lane = threadIdx.x;
     for (int64_t t = lane; t < len; t += 64) ys[t] = x[b0 + t];
     const int64_t w0 = wstart[blk];
-    win_sweep<false>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, lane);
-    win_sweep<true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, lane);
+    win_sweep<false>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, bufs, lane);
+    win_sweep<true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, bufs, lane);
     for (int64_t t = lane; t < len; t += 64) y[b0 + t] = ys[t];
 }
+
+int ilu_window_max_rows() { return (163840 - 2 * WIN_BUF) / 8; }
+int ilu_window_stream_pad() { return WIN_KP * 64; }
 
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
@@ -2738,7 +2790,7 @@ void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart,
                                   (int)163840);
         configured = true;
     }
-    const size_t bytes = (size_t)std::max<int64_t>(max_len, 1) * 8;
+    const size_t bytes = 2 * (size_t)WIN_BUF + (size_t)std::max<int64_t>(max_len, 1) * 8;
     k_ilu_blocks_window<<<(unsigned)nblocks, 64, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv,
                                                               Uwoff, Ucol, Uval, Utinv, x, y);
 }

@@ -212,6 +212,11 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
 // windows of 64 rows; per block its first window wstart[b] (nblocks + 1); per
 // triangle and window the off-window stream [woff[w], woff[w + 1]) ([k][lane]
 // SELL, block-local columns) and the window's inverse tinv[w * 4096 + k * 64 + lane].
+// The col / val streams carry ilu_window_stream_pad() entries of padding at
+// their end (the staging copies read a fixed count); blocks of at most
+// ilu_window_max_rows() rows.
+int ilu_window_max_rows();
+int ilu_window_stream_pad();
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
                               const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,

@@ -1199,8 +1199,9 @@ static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, cons
         }
         woff[w + 1] = woff[w] + K * 64;
     }
-    std::vector<int32_t> col(std::max<int64_t>(woff[nw], 1), 0);
-    std::vector<double> val(std::max<int64_t>(woff[nw], 1), 0.0), tinv((size_t)std::max<int64_t>(nw, 1) * 4096, 0.0);
+    // (the staging copies read a fixed number of entries past a window's start: padding at the end)
+    std::vector<int32_t> col(woff[nw] + ilu_window_stream_pad(), 0);
+    std::vector<double> val(woff[nw] + ilu_window_stream_pad(), 0.0), tinv((size_t)std::max<int64_t>(nw, 1) * 4096, 0.0);
     amgh::parallel_rows(nw, amgh::setup_threads(), [&](int, int64_t w0, int64_t w1) {
         std::vector<double> T(64 * 64), X(64 * 64);
         for (int64_t w = w0; w < w1; ++w) {
@@ -1453,7 +1454,8 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             chain = c.sweep_chain != 0 && sL >= 0 && sU >= 0 && (c.sweep_chain == 1 || deep);
             // the window sweep where the chain would run (or forced): a block's
             // dependent chain becomes its len / 64 windows
-            window = c.sweep_window == 1 || (c.sweep_window == -1 && c.sweep_chain != 1 && deep);
+            window = (c.sweep_window == 1 || (c.sweep_window == -1 && c.sweep_chain != 1 && deep)) &&
+                     blen <= ilu_window_max_rows();
             if (window) {
                 chain = false;
                 std::vector<double> fv(F.nnz);
