@@ -2689,14 +2689,24 @@ static constexpr int WIN_NDMA = 32 + WIN_KP / 4 + WIN_KP / 2;      // 1-KiB copi
 static constexpr int WIN_BUF = 4096 * 8 + WIN_KP * 64 * 12;        // bytes of one staging buffer
 static_assert(WIN_NDMA == 44, "the counted waits below assume 44 copies per window");
 
-__device__ __forceinline__ void win_stage(int64_t wg, const int64_t *__restrict__ woff, const int32_t *__restrict__ col,
+// a block's window stream offsets, 64 per vector register (lane l: window j * 64 + l),
+// picked with v_readlane: no scalar load (and its latency) per window
+struct WinOff {
+    int64_t r[3];
+    __device__ __forceinline__ int64_t at(int64_t w) const {
+        const int j = (int)(w >> 6), l = (int)(w & 63);
+        const int64_t v = j == 0 ? r[0] : j == 1 ? r[1] : r[2];
+        return readlane64(v, l);
+    }
+};
+
+__device__ __forceinline__ void win_stage(int64_t wg, int64_t s0, const int32_t *__restrict__ col,
                                           const double *__restrict__ val, const double *__restrict__ tinv,
                                           char *buf, int lane) {
     const char *t = (const char *)(tinv + wg * 4096) + lane * 16;
 #pragma unroll
     for (int q = 0; q < 32; ++q)
         __builtin_amdgcn_global_load_lds((const void *)(t + q * 1024), (__attribute__((address_space(3))) void *)(buf + q * 1024), 16, 0, 0);
-    const int64_t s0 = woff[wg];
     const char *c = (const char *)(col + s0) + lane * 16;
 #pragma unroll
     for (int q = 0; q < WIN_KP / 4; ++q)
@@ -2710,12 +2720,11 @@ __device__ __forceinline__ void win_stage(int64_t wg, const int64_t *__restrict_
                                          0, 0);
 }
 
-__device__ __forceinline__ void win_compute(int64_t w, int64_t len, int64_t wg, const int64_t *__restrict__ woff,
+__device__ __forceinline__ void win_compute(int64_t w, int64_t len, int64_t s0, int64_t s1,
                                             const int32_t *__restrict__ col, const double *__restrict__ val,
                                             const char *buf, double *ys, int lane) {
     const int64_t r = w * 64 + lane;
     const bool act = r < len;
-    const int64_t s0 = woff[wg], s1 = woff[wg + 1];
     const int K = (int)((s1 - s0) >> 6);
     const int32_t *bc = (const int32_t *)(buf + 32768);
     const double *bv = (const double *)(buf + 32768 + WIN_KP * 256);
@@ -2741,17 +2750,22 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
                                           const double *__restrict__ tinv, double *ys, char *bufs, int lane) {
     const int64_t nw = (len + 63) >> 6;
     if (nw == 0) return;
+    WinOff wo;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (nothing else in flight yet)
     auto wi = [&](int64_t ww) { return UP ? nw - 1 - ww : ww; };
-    win_stage(w0 + wi(0), woff, col, val, tinv, bufs, lane);
+    win_stage(w0 + wi(0), wo.at(wi(0)), col, val, tinv, bufs, lane);
     for (int64_t ww = 0; ww < nw; ++ww) {
         char *cur = bufs + (ww & 1) * WIN_BUF;
         if (ww + 1 < nw) {
-            win_stage(w0 + wi(ww + 1), woff, col, val, tinv, bufs + ((ww + 1) & 1) * WIN_BUF, lane);
+            win_stage(w0 + wi(ww + 1), wo.at(wi(ww + 1)), col, val, tinv, bufs + ((ww + 1) & 1) * WIN_BUF, lane);
             asm volatile("s_waitcnt vmcnt(44)" ::: "memory");  // this window's copies (issued one window ago) landed
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        win_compute(wi(ww), len, w0 + wi(ww), woff, col, val, cur, ys, lane);
+        const int64_t w = wi(ww);
+        win_compute(w, len, wo.at(w), wo.at(w + 1), col, val, cur, ys, lane);
     }
 }
 
@@ -2777,7 +2791,7 @@ __global__ __launch_bounds__(64) void k_ilu_blocks_window(int64_t n, int64_t nbl
     for (int64_t t = lane; t < len; t += 64) y[b0 + t] = ys[t];
 }
 
-int ilu_window_max_rows() { return (163840 - 2 * WIN_BUF) / 8; }
+int ilu_window_max_rows() { return std::min((163840 - 2 * WIN_BUF) / 8, 3 * 64 * 64 - 64); }  // (WinOff: <= 191 windows)
 int ilu_window_stream_pad() { return WIN_KP * 64; }
 
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
