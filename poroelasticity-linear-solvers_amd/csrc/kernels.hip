@@ -2677,122 +2677,184 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
 // block-local columns, padding = column 0 with value 0).  The dependent chain
 // of a block is its windows (len / 64 steps of a 64 x 64 GEMV) instead of its
 // levels: FE rows in natural order have ~1 row per level (the AMG smoother's
-// chunks: ~970 levels per 2,405-row chunk, 38 windows).  One wave per block.
-// The next window's inverse and first WIN_KP stream entries per lane are
-// copied global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
-// instruction, WIN_NDMA per window) while the current window computes; a
-// counted s_waitcnt vmcnt(WIN_NDMA) retires the current window's copies only.
-// Entries past WIN_KP (rare) are read with ordinary loads.  Sums: the
-// off-window entries in stream order, then T^-1's row in k order.
-static constexpr int WIN_KP = 16;                                  // stream entries per lane staged per window
-static constexpr int WIN_NDMA = 32 + WIN_KP / 4 + WIN_KP / 2;      // 1-KiB copies per window (T^-1, col, val)
-static constexpr int WIN_BUF = 4096 * 8 + WIN_KP * 64 * 12;        // bytes of one staging buffer
-static_assert(WIN_NDMA == 44, "the counted waits below assume 44 copies per window");
+// chunks: ~970 levels per 2,405-row chunk, 38 windows).
+// Four waves per block: wave q takes the stream entries k = q, q + 4, ... and
+// the inverse's columns [16 q, 16 q + 16); the partial sums meet in LDS in a
+// fixed order (two barriers per window).  Each wave prefetches its share of
+// the next window (16 columns of T^-1, WIN_KPW stream entries per lane) into
+// registers, reloading each right after its use with range-checked buffer
+// loads (the zero triangle of T^-1 and entries past the window's stream read
+// 0 without traffic), so a window's data was requested a window earlier and
+// the register set stays small enough for the compiler to count the loads in
+// flight.  (One wave with all 64 columns spilled to AGPRs and drained vmcnt at
+// every window; staging through LDS by LDS-DMA cost ~4.4 us per window in
+// 1-KiB copies.)  Rows have at most WIN_KP off-window entries (the setup
+// keeps other blocks on the other sweeps), so every load is of fixed count.
+static constexpr int WIN_NW = 4, WIN_KPW = 8;
+static constexpr int WIN_KP = WIN_NW * WIN_KPW;  // stream entries per row (every one prefetched); blocks with more use other sweeps
 
 // a block's window stream offsets, 64 per vector register (lane l: window j * 64 + l),
 // picked with v_readlane: no scalar load (and its latency) per window
 struct WinOff {
     int64_t r[3];
-    __device__ __forceinline__ int64_t at(int64_t w) const {
+    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: three readlanes, a scalar select
         const int j = (int)(w >> 6), l = (int)(w & 63);
-        const int64_t v = j == 0 ? r[0] : j == 1 ? r[1] : r[2];
-        return readlane64(v, l);
+        const int64_t a = readlane64(r[0], l), b = readlane64(r[1], l), c = readlane64(r[2], l);
+        return j == 0 ? a : (j == 1 ? b : c);
     }
 };
 
-__device__ __forceinline__ void win_stage(int64_t wg, int64_t s0, const int32_t *__restrict__ col,
-                                          const double *__restrict__ val, const double *__restrict__ tinv,
-                                          char *buf, int lane) {
-    const char *t = (const char *)(tinv + wg * 4096) + lane * 16;
-#pragma unroll
-    for (int q = 0; q < 32; ++q)
-        __builtin_amdgcn_global_load_lds((const void *)(t + q * 1024), (__attribute__((address_space(3))) void *)(buf + q * 1024), 16, 0, 0);
-    const char *c = (const char *)(col + s0) + lane * 16;
-#pragma unroll
-    for (int q = 0; q < WIN_KP / 4; ++q)
-        __builtin_amdgcn_global_load_lds((const void *)(c + q * 1024),
-                                         (__attribute__((address_space(3))) void *)(buf + 32768 + q * 1024), 16, 0, 0);
-    const char *v = (const char *)(val + s0) + lane * 16;
-#pragma unroll
-    for (int q = 0; q < WIN_KP / 2; ++q)
-        __builtin_amdgcn_global_load_lds((const void *)(v + q * 1024),
-                                         (__attribute__((address_space(3))) void *)(buf + 32768 + WIN_KP * 256 + q * 1024), 16,
-                                         0, 0);
+// a wave-uniform value forced into scalar registers (buffer resources must be SGPRs;
+// without this the compiler may build them in VGPRs and waterfall every load)
+__device__ __forceinline__ int64_t sgpr64(int64_t v) {
+    const int32_t lo = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(uint64_t)v);
+    const int32_t hi = __builtin_amdgcn_readfirstlane((int32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t win_rsrc(const void *base, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)sgpr64((int64_t)(uintptr_t)base), (short)0,
+                                             __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
 
-__device__ __forceinline__ void win_compute(int64_t w, int64_t len, int64_t s0, int64_t s1,
-                                            const int32_t *__restrict__ col, const double *__restrict__ val,
-                                            const char *buf, double *ys, int lane) {
-    const int64_t r = w * 64 + lane;
-    const bool act = r < len;
-    const int K = (int)((s1 - s0) >> 6);
-    const int32_t *bc = (const int32_t *)(buf + 32768);
-    const double *bv = (const double *)(buf + 32768 + WIN_KP * 256);
-    double acc = 0.0;
-    const int kp = K < WIN_KP ? K : WIN_KP;
-    for (int k = 0; k < kp; ++k) acc += __dmul_rn(bv[k * 64 + lane], ys[bc[k * 64 + lane]]);
-    for (int64_t e = s0 + WIN_KP * 64 + lane; e < s1; e += 64) acc += __dmul_rn(val[e], ys[col[e]]);
-    const double t = act ? ys[r] - acc : 0.0;
-    const double *T = (const double *)buf + lane;
-    const int tlo = __double2loint(t), thi = __double2hiint(t);
-    double out = 0.0;
+struct WinBuf {  // one wave's share of a window's data in registers
+    double tv[16], sv[WIN_KPW];
+    int32_t sc[WIN_KPW];
+};
+
+// Range-checked buffer loads issued through inline asm: the compiler does not
+// track them, so it cannot drain them at the loop header (its waits for
+// loop-carried loads were vmcnt(0)); the sweep counts them itself -- every
+// window issues WIN_LOADS of them -- and win_wait ties the registers to the
+// wait (no use or copy can move above it).
+static constexpr int WIN_LOADS = 16 + 2 * WIN_KPW;
+__device__ __forceinline__ double win_ld64(__amdgpu_buffer_rsrc_t r, int off) {
+    double v;
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+    return v;
+}
+__device__ __forceinline__ int32_t win_ld32(__amdgpu_buffer_rsrc_t r, int off) {
+    int32_t v;
+    asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+    return v;
+}
+template <int N>
+__device__ __forceinline__ void win_wait(WinBuf &B) {  // vmcnt(N), B's registers pinned to it
+    asm volatile("s_waitcnt vmcnt(%c0)" ::"n"(N) : "memory");
 #pragma unroll
-    for (int k = 0; k < 64; ++k) {
-        const double tk = __hiloint2double(__builtin_amdgcn_readlane(thi, k), __builtin_amdgcn_readlane(tlo, k));
-        out += __dmul_rn(T[k * 64], tk);
-    }
-    if (act) ys[r] = out;
+    for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(B.tv[k]));
+#pragma unroll
+    for (int u = 0; u < WIN_KPW; ++u) asm volatile("" : "+v"(B.sv[u]), "+v"(B.sc[u]));
 }
 
 template <bool UP>
 __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t *__restrict__ woff,
                                           const int32_t *__restrict__ col, const double *__restrict__ val,
-                                          const double *__restrict__ tinv, double *ys, char *bufs, int lane) {
+                                          const double *__restrict__ tinv, double *ys, double *part, int lane,
+                                          int q) {
     const int64_t nw = (len + 63) >> 6;
     if (nw == 0) return;
     WinOff wo;
 #pragma unroll
     for (int j = 0; j < 3; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (nothing else in flight yet)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the offsets (ordinary loads) before the counted ones
     auto wi = [&](int64_t ww) { return UP ? nw - 1 - ww : ww; };
-    win_stage(w0 + wi(0), wo.at(wi(0)), col, val, tinv, bufs, lane);
-    for (int64_t ww = 0; ww < nw; ++ww) {
-        char *cur = bufs + (ww & 1) * WIN_BUF;
-        if (ww + 1 < nw) {
-            win_stage(w0 + wi(ww + 1), wo.at(wi(ww + 1)), col, val, tinv, bufs + ((ww + 1) & 1) * WIN_BUF, lane);
-            asm volatile("s_waitcnt vmcnt(44)" ::: "memory");  // this window's copies (issued one window ago) landed
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // T^-1[k][lane] is zero above (L) / below (U) the diagonal: those lanes read out of range
+    auto toff = [&](int k) { return (UP ? k >= lane : k <= lane) ? (k * 64 + lane) * 8 : 0x40000000; };
+    auto sk = [&](int u) { return (u * WIN_NW + q) * 64 + lane; };  // this wave's u-th stream slot
+    // every window's loads, WIN_LOADS in one fixed order (past the block: 0 bytes in range, no traffic)
+    auto issue = [&](int64_t ww, WinBuf &B) {
+        const int64_t ok = ww < nw ? 1 : 0;
+        const int64_t w = wi(ww < nw ? ww : 0);
+        const int64_t s0 = wo.at(w), s1 = wo.at(w + 1);
+        const auto rt = win_rsrc(tinv + (w0 + w) * 4096, ok * 32768);
+        const auto rc = win_rsrc(col + s0, ok * (s1 - s0) * 4);
+        const auto rv = win_rsrc(val + s0, ok * (s1 - s0) * 8);
+#pragma unroll
+        for (int u = 0; u < WIN_KPW; ++u) {
+            B.sc[u] = win_ld32(rc, sk(u) * 4);
+            B.sv[u] = win_ld64(rv, sk(u) * 8);
         }
-        const int64_t w = wi(ww);
-        win_compute(w, len, wo.at(w), wo.at(w + 1), col, val, cur, ys, lane);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) B.tv[k] = win_ld64(rt, toff(16 * q + k));
+    };
+    // one window, branch-free (a window past the block computes zeros into a dummy slot)
+    auto compute = [&](int64_t ww, const WinBuf &B) {
+        const int64_t w = wi(ww < nw ? ww : 0);
+        const int64_t r = w * 64 + lane;
+        const bool act = ww < nw && r < len;
+        double d[WIN_KPW];
+#pragma unroll
+        for (int u = 0; u < WIN_KPW; ++u) d[u] = ys[B.sc[u]];
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < WIN_KPW; ++u) acc += __dmul_rn(B.sv[u], d[u]);
+        part[q * 64 + lane] = acc;
+        __syncthreads();
+        const double rhs = ys[act ? r : 0];
+        const double t = act ? rhs - (((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane]) : 0.0;
+        const int tlo = __double2loint(t), thi = __double2hiint(t);
+        double out = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int kk = 16 * q + k;
+            const double tk = __hiloint2double(__builtin_amdgcn_readlane(thi, kk), __builtin_amdgcn_readlane(tlo, kk));
+            out += __dmul_rn(B.tv[k], tk);
+        }
+        __syncthreads();  // every wave has read part[] (t) before it is overwritten
+        part[q * 64 + lane] = out;
+        __syncthreads();
+        const double yr = ((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane];
+        ys[act ? r : len + lane] = yr;  // every wave writes the same value (its own later reads see it)
+        __syncthreads();                // part[] free for the next window
+    };
+    WinBuf A, B;
+    issue(0, A);
+    issue(1, B);
+    for (int64_t ww = 0; ww < nw; ww += 2) {  // two windows per trip: loads of window ww + 2 fly during ww + 1
+        win_wait<WIN_LOADS>(A);               // A's loads are older than B's WIN_LOADS
+        compute(ww, A);
+        issue(ww + 2, A);
+        win_wait<WIN_LOADS>(B);
+        compute(ww + 1, B);
+        issue(ww + 3, B);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the prefetches past the block: nothing in range)
 }
 
-__global__ __launch_bounds__(64) void k_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart,
-                                                          const int64_t *__restrict__ wstart,
-                                                          const int64_t *__restrict__ Lwoff, const int32_t *__restrict__ Lcol,
-                                                          const double *__restrict__ Lval, const double *__restrict__ Ltinv,
-                                                          const int64_t *__restrict__ Uwoff, const int32_t *__restrict__ Ucol,
-                                                          const double *__restrict__ Uval, const double *__restrict__ Utinv,
-                                                          const double *x, double *y) {
-    // one dynamic LDS array: two staging buffers, then the block solution
+__global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart,
+                                                           const int64_t *__restrict__ wstart,
+                                                           const int64_t *__restrict__ Lwoff, const int32_t *__restrict__ Lcol,
+                                                           const double *__restrict__ Lval, const double *__restrict__ Ltinv,
+                                                           const int64_t *__restrict__ Uwoff, const int32_t *__restrict__ Ucol,
+                                                           const double *__restrict__ Uval, const double *__restrict__ Utinv,
+                                                           const double *x, double *y) {
+    // one dynamic LDS array: the partial sums (4 x 64), then the block solution
     extern __shared__ __attribute__((aligned(16))) double lds_win[];
-    char *bufs = (char *)lds_win;
-    double *ys = (double *)(bufs + 2 * WIN_BUF);
+    double *part = lds_win, *ys = lds_win + 256;
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
     int64_t b0, len;
     block_range(blk, n, nblocks, bstart, b0, len);
-    const int lane = threadIdx.x;
-    for (int64_t t = lane; t < len; t += 64) ys[t] = x[b0 + t];
-    const int64_t w0 = wstart[blk];
-    win_sweep<false>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, bufs, lane);
-    win_sweep<true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, bufs, lane);
-    for (int64_t t = lane; t < len; t += 64) y[b0 + t] = ys[t];
+    const int lane = threadIdx.x & 63;
+    const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (v_readlane's lane is a scalar)
+    for (int64_t t = threadIdx.x; t < len; t += 256) ys[t] = x[b0 + t];
+    __syncthreads();
+    // block bounds as scalars (buffer resources built from them must live in SGPRs)
+    auto uni = [](int64_t v) {
+        const int32_t lo = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(uint64_t)v);
+        const int32_t hi = __builtin_amdgcn_readfirstlane((int32_t)((uint64_t)v >> 32));
+        return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+    };
+    len = uni(len);
+    const int64_t w0 = uni(wstart[blk]);
+    win_sweep<false>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q);
+    win_sweep<true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q);
+    __syncthreads();
+    for (int64_t t = threadIdx.x; t < len; t += 256) y[b0 + t] = ys[t];
 }
 
-int ilu_window_max_rows() { return std::min((163840 - 2 * WIN_BUF) / 8, 3 * 64 * 64 - 64); }  // (WinOff: <= 191 windows)
-int ilu_window_stream_pad() { return WIN_KP * 64; }
+int ilu_window_max_rows() { return 163840 / 8 - 256 - 64; }  // LDS: partial sums, the block, a dummy slot per lane
+int ilu_window_stream_pad() { return 0; }
+int ilu_window_max_entries() { return WIN_KP; }
 
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
@@ -2804,8 +2866,8 @@ void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart,
                                   (int)163840);
         configured = true;
     }
-    const size_t bytes = 2 * (size_t)WIN_BUF + (size_t)std::max<int64_t>(max_len, 1) * 8;
-    k_ilu_blocks_window<<<(unsigned)nblocks, 64, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv,
+    const size_t bytes = (size_t)(256 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
+    k_ilu_blocks_window<<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv,
                                                               Uwoff, Ucol, Uval, Utinv, x, y);
 }
 

@@ -217,6 +217,7 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
 // ilu_window_max_rows() rows.
 int ilu_window_max_rows();
 int ilu_window_stream_pad();
+int ilu_window_max_entries();  // off-window entries per row the kernel handles
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
                               const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,

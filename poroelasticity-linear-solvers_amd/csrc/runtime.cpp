@@ -1166,6 +1166,23 @@ static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order
 // [k][lane], block-local columns) and the inverse of the window's triangle --
 // unit lower (I + L_ww) or upper with the diagonal (U_ww) -- by row-wise
 // substitution in double precision without contraction, stored [k][lane].
+// Largest number of off-window entries of a row (the kernel's limit: ilu_window_max_entries())
+static int64_t window_max_entries(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
+                                  const std::vector<int32_t> &ci, const std::vector<int64_t> &dg) {
+    int64_t kmax = 0;
+    for (int64_t b = 0; b < nblk; ++b)
+        for (int64_t i = bst[b]; i < bst[b + 1]; ++i) {
+            const int64_t w0 = bst[b] + (i - bst[b]) / 64 * 64, w1 = std::min<int64_t>(w0 + 64, bst[b + 1]);
+            int64_t kl = 0, ku = 0;
+            for (int64_t k = rp[i]; k < rp[i + 1]; ++k) {
+                kl += ci[k] < w0;
+                ku += ci[k] >= w1;
+            }
+            kmax = std::max(kmax, std::max(kl, ku));
+        }
+    return kmax;
+}
+
 static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
                              const std::vector<int32_t> &ci, const std::vector<int64_t> &dg,
                              const std::vector<double> &fv, bool upper, WinTri &W, Ctx &c) {
@@ -1455,7 +1472,8 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             // the window sweep where the chain would run (or forced): a block's
             // dependent chain becomes its len / 64 windows
             window = (c.sweep_window == 1 || (c.sweep_window == -1 && c.sweep_chain != 1 && deep)) &&
-                     blen <= ilu_window_max_rows();
+                     blen <= ilu_window_max_rows() &&
+                     window_max_entries(nblocks, bst, rp, ci, dg) <= ilu_window_max_entries();
             if (window) {
                 chain = false;
                 std::vector<double> fv(F.nnz);
