@@ -3,6 +3,7 @@ solves, so the PC is linear and its cost fixed) on the assembled footing
 system -- isolates the smoother / LU kernels from the outer iteration count.
 
 usage: python tools/pc_bench.py N inner [key=value ...]   (inner: hypre | ilu | lu)
+       N = s<M> for the 3-D swelling system at N=M (whole-block PCs on s and fp, "diagonal")
 """
 import os
 import sys
@@ -18,15 +19,34 @@ from lib.handle import Handle, params_to_options  # noqa: E402
 
 
 def main():
-    N, inner = int(sys.argv[1]), sys.argv[2]
-    extra = dict(kv.split("=", 1) for kv in sys.argv[3:])
+    inner = sys.argv[2]
+    swelling = sys.argv[1].startswith("s")
+    N = int(sys.argv[1][1:] if swelling else sys.argv[1])
+    # variants: key=value arguments, several variants separated by "--" (one assembly for all)
+    variants, cur = [], []
+    for arg in sys.argv[3:]:
+        if arg == "--":
+            variants.append(cur)
+            cur = []
+        else:
+            cur.append(arg)
+    variants.append(cur)
     Nat.check(Nat.lib().pls_set_device(0))
-    s = assemble_footing(N, "undrained")
+    if swelling:
+        from lib.fe_swelling import assemble_swelling
+        s = assemble_swelling(3, N, "diagonal")
+    else:
+        s = assemble_footing(N, "undrained")
+    for v in variants:
+        run(s, N, inner, swelling, dict(kv.split("=", 1) for kv in v))
+
+
+def run(s, N, inner, swelling, extra):
     params = {"solver type": "gmres", "solver atol": 1e-4, "solver rtol": 1e-6, "solver maxiter": 10,
-              "pc type": "undrained", "inner ksp type": "preonly", "inner pc type": inner, "inner accel order": 0,
-              "AAR order": 5, "AAR p": 5, "AAR omega": 1, "AAR beta": 1}
+              "pc type": "diagonal" if swelling else "undrained", "inner ksp type": "preonly", "inner pc type": inner,
+              "inner accel order": 0, "AAR order": 5, "AAR p": 5, "AAR omega": 1, "AAR beta": 1}
     db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "s_ksp_type": "preonly", "s_pc_type": inner,
-          "fp_ksp_type": "preonly", "fp_pc_type": "lu"}
+          "fp_ksp_type": "preonly", "fp_pc_type": inner if swelling else "lu"}
     if inner == "hypre":
         for k, v in {"P_max": "4", "agg_nl": "1", "agg_num_paths": "2", "coarsen_type": "HMIS",
                      "interp_type": "ext+i", "no_CF": "true"}.items():
@@ -49,8 +69,10 @@ def main():
         h.pc_apply_device(dx.p, dy.p)
     dy.download()
     dt = (time.perf_counter() - t1) / reps
-    print(f"footing N={N} n={n} inner={inner} {extra}: setup {t_setup:.2f} s; PC apply {1e3 * dt:.3f} ms (wall, device-resident)",
-          flush=True)
+    print(f"{'swelling 3-D' if swelling else 'footing'} N={N} n={n} inner={inner} {extra}: setup {t_setup:.2f} s; "
+          f"PC apply {1e3 * dt:.3f} ms (wall, device-resident)", flush=True)
+    dx.free()
+    dy.free()
     h.destroy()
 
 
