@@ -51,7 +51,8 @@ Setup, level l (A_l square CSR, sorted columns), single rank:
   plus every other weak a_in; each strong F neighbour k (ascending) spreads
   a_ik over bar(a_kl) = a_kl if a_kl a_kk < 0 else 0: D = sum over k's row
   (storage order) of bar(a_kl) for l in C^_i or l = i; D = 0 adds a_ik to
-  d~, else w_l += a_ik bar(a_kl) / D for l in C^_i and d~ += a_ik bar(a_ki) / D;
+  d~, else with hypre's distribute = a_ik / D: w_l += distribute bar(a_kl) for
+  l in C^_i and d~ += distribute bar(a_ki);
   P_ij = -w_j / d~.  Then P_max truncation: rows with more than P_max entries
   keep the P_max largest |P_ij| (ties: smaller j), rescaled by (row sum) /
   (kept sum) (both in column order) when the kept sum is nonzero.  Exact
@@ -448,13 +449,14 @@ def ext_i_interp(A, S, cf):
             if D == 0.0:
                 dt += a_ik
                 continue
+            distribute = a_ik / D  # hypre's ext+i: distribute = a_ik / sum, then distribute * a_kl
             for l, a in zip(kc, kv):
                 if a * dk >= 0.0:
                     continue
                 if l in chat:
-                    w[l] = w.get(l, 0.0) + a_ik * a / D
+                    w[l] = w.get(l, 0.0) + distribute * a
                 elif l == i:
-                    dt += a_ik * a / D
+                    dt += distribute * a
         rows.append({int(cidx[j]): -wv / dt for j, wv in w.items()} if dt != 0.0 else {})
     return _csr_from_rows(rows, int((cf == C).sum()))
 

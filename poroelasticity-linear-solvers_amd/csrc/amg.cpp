@@ -58,24 +58,30 @@ int setup_threads() {
     return std::max(1, std::min(t, 64));
 }
 
-// Concatenate per-thread row ranges (ci/v/row lengths) into one CSR.
+// Concatenate per-thread row ranges (ci/v/row lengths) into one CSR (each
+// part copied into place by a thread of its own).
 void concat_rows(HostCSR &C, std::vector<HostCSR> &part) {
-    int64_t nnz = 0;
-    for (auto &p : part) nnz += (int64_t)p.ci.size();
-    C.rp.assign(1, 0);
-    C.rp.reserve(C.nrows + 1);
-    C.ci.resize(nnz);
-    C.v.resize(nnz);
-    int64_t off = 0;
-    for (auto &p : part) {
-        for (size_t k = 1; k < p.rp.size(); ++k) C.rp.push_back(off + p.rp[k]);
-        std::copy(p.ci.begin(), p.ci.end(), C.ci.begin() + off);
-        std::copy(p.v.begin(), p.v.end(), C.v.begin() + off);
-        off += (int64_t)p.ci.size();
-        HostCSR().rp.swap(p.rp);
-        std::vector<int32_t>().swap(p.ci);
-        std::vector<double>().swap(p.v);
+    const size_t T = part.size();
+    std::vector<int64_t> row0(T + 1, 0), nz0(T + 1, 0);
+    for (size_t t = 0; t < T; ++t) {
+        row0[t + 1] = row0[t] + (part[t].rp.empty() ? 0 : (int64_t)part[t].rp.size() - 1);
+        nz0[t + 1] = nz0[t] + (int64_t)part[t].ci.size();
     }
+    C.rp.assign(row0[T] + 1, 0);
+    C.ci.resize(nz0[T]);
+    C.v.resize(nz0[T]);
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            HostCSR &p = part[t];
+            for (size_t k = 1; k < p.rp.size(); ++k) C.rp[row0[t] + k] = nz0[t] + p.rp[k];
+            std::copy(p.ci.begin(), p.ci.end(), C.ci.begin() + nz0[t]);
+            std::copy(p.v.begin(), p.v.end(), C.v.begin() + nz0[t]);
+            HostCSR().rp.swap(p.rp);
+            std::vector<int32_t>().swap(p.ci);
+            std::vector<double>().swap(p.v);
+        });
+    for (auto &x : th) x.join();
 }
 
 // C = A B, row i accumulating over A's row in storage order (csr_matmat);
@@ -145,23 +151,23 @@ bool galerkin_fused(const HostCSR &A, const HostCSR &P, int64_t nc, double max_b
         th.emplace_back([&, t] {
             const int64_t a0 = nc * t / T, a1 = nc * (t + 1) / T;
             std::vector<double> acc((size_t)((a1 - a0) * nc), 0.0), ap(nc, 0.0);
-            std::vector<char> mark(nc, 0);
-            std::vector<int32_t> cols;
+            std::vector<uint8_t> mark(nc, 0);
+            std::vector<int32_t> cols(nc + 1);
             for (int64_t k = 0; k < P.nrows; ++k) {
                 bool touch = false;
                 for (int64_t q = P.rp[k]; q < P.rp[k + 1] && !touch; ++q) touch = P.ci[q] >= a0 && P.ci[q] < a1;
                 if (!touch) continue;
-                cols.clear();  // (AP)_k, as spgemm_rows sums it
+                // (AP)_k, as spgemm_rows sums it (ap is all zero between rows;
+                // the touched list grows branch-free)
+                int64_t ncol = 0;
                 for (int64_t kk = A.rp[k]; kk < A.rp[k + 1]; ++kk) {
                     const int32_t kp = A.ci[kk];
                     const double av = A.v[kk];
                     for (int64_t jj = P.rp[kp]; jj < P.rp[kp + 1]; ++jj) {
                         const int32_t b = P.ci[jj];
-                        if (!mark[b]) {
-                            mark[b] = 1;
-                            ap[b] = 0.0;
-                            cols.push_back(b);
-                        }
+                        cols[ncol] = b;
+                        ncol += mark[b] ^ 1;
+                        mark[b] = 1;
                         ap[b] += av * P.v[jj];
                     }
                 }
@@ -170,10 +176,15 @@ bool galerkin_fused(const HostCSR &A, const HostCSR &P, int64_t nc, double max_b
                     if (a < a0 || a >= a1) continue;
                     const double p = P.v[q];
                     double *row = acc.data() + (a - a0) * nc;
-                    for (int32_t b : cols)
+                    for (int64_t u = 0; u < ncol; ++u) {
+                        const int32_t b = cols[u];
                         if (ap[b] != 0.0) row[b] += p * ap[b];
+                    }
                 }
-                for (int32_t b : cols) mark[b] = 0;
+                for (int64_t u = 0; u < ncol; ++u) {
+                    mark[cols[u]] = 0;
+                    ap[cols[u]] = 0.0;
+                }
             }
             HostCSR &out = part[t];
             out.rp.assign(1, 0);

@@ -47,19 +47,29 @@ struct Pattern {  // CSR sparsity (strong dependencies)
     int64_t len(int64_t i) const { return rp[i + 1] - rp[i]; }
 };
 
-// concatenate per-thread pattern parts (rows in order)
+// concatenate per-thread pattern parts (rows in order); the parts are copied
+// into place by their own threads (one serial copy of S was ~0.4 s at N=59)
 Pattern concat_pattern(int64_t n, std::vector<Pattern> &part) {
     Pattern S;
     S.n = n;
-    S.rp.reserve(n + 1);
-    int64_t off = 0;
-    for (auto &p : part) {
-        for (size_t k = 1; k < p.rp.size(); ++k) S.rp.push_back(off + p.rp[k]);
-        S.ci.insert(S.ci.end(), p.ci.begin(), p.ci.end());
-        off += (int64_t)p.ci.size();
-        Pattern().rp.swap(p.rp);
-        std::vector<int32_t>().swap(p.ci);
+    const size_t T = part.size();
+    std::vector<int64_t> row0(T + 1, 0), nz0(T + 1, 0);
+    for (size_t t = 0; t < T; ++t) {
+        row0[t + 1] = row0[t] + (part[t].rp.empty() ? 0 : (int64_t)part[t].rp.size() - 1);
+        nz0[t + 1] = nz0[t] + (int64_t)part[t].ci.size();
     }
+    S.rp.assign(n + 1, 0);
+    S.ci.resize(nz0[T]);
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            Pattern &p = part[t];
+            for (size_t k = 1; k < p.rp.size(); ++k) S.rp[row0[t] + k] = nz0[t] + p.rp[k];
+            std::copy(p.ci.begin(), p.ci.end(), S.ci.begin() + nz0[t]);
+            Pattern().rp.swap(p.rp);
+            std::vector<int32_t>().swap(p.ci);
+        });
+    for (auto &x : th) x.join();
     return S;
 }
 
@@ -202,30 +212,29 @@ struct Tournament {
 // a lambda change is O(1) word updates and a selection a few word scans,
 // where the tournament compares O(log n) siblings (random reads of lambda).
 // lambda <= 2 max |S^T_i| (it starts at |S^T_i| and grows once per point of
-// S^T_i that becomes F).
+// S^T_i that becomes F).  The buckets' words are interleaved (word w of
+// bucket b at w * NB + b), so a point's lambda moving by one touches one cache
+// line, and the points a C point updates (its neighbours, close in index) a
+// few more.
 struct LamBuckets {
-    int64_t w0 = 0, w1 = 0, w2 = 0, top = -1;
-    std::vector<std::vector<uint64_t>> b0, b1, b2;
+    int64_t NB = 0, w0 = 0, w1 = 0, w2 = 0, top = -1;
+    std::vector<uint64_t> b0, b1, b2;
     std::vector<int64_t> cnt;
     LamBuckets(int64_t n, int64_t maxlam) {
+        NB = maxlam + 1;
         w0 = (n + 63) / 64;
         w1 = (w0 + 63) / 64;
         w2 = (w1 + 63) / 64;
-        b0.resize(maxlam + 1);
-        b1.resize(maxlam + 1);
-        b2.resize(maxlam + 1);
-        cnt.assign(maxlam + 1, 0);
+        b0.assign((size_t)(w0 * NB), 0);
+        b1.assign((size_t)(w1 * NB), 0);
+        b2.assign((size_t)(w2 * NB), 0);
+        cnt.assign(NB, 0);
     }
     void insert(int64_t b, int64_t i) {
-        if (b0[b].empty()) {
-            b0[b].assign(w0, 0);
-            b1[b].assign(w1, 0);
-            b2[b].assign(w2, 0);
-        }
-        uint64_t &x0 = b0[b][i >> 6];
+        uint64_t &x0 = b0[(i >> 6) * NB + b];
         if (!x0) {
-            uint64_t &x1 = b1[b][i >> 12];
-            if (!x1) b2[b][i >> 18] |= 1ull << ((i >> 12) & 63);
+            uint64_t &x1 = b1[(i >> 12) * NB + b];
+            if (!x1) b2[(i >> 18) * NB + b] |= 1ull << ((i >> 12) & 63);
             x1 |= 1ull << ((i >> 6) & 63);
         }
         x0 |= 1ull << (i & 63);
@@ -233,24 +242,23 @@ struct LamBuckets {
         if (b > top) top = b;
     }
     void erase(int64_t b, int64_t i) {
-        uint64_t &x0 = b0[b][i >> 6];
+        uint64_t &x0 = b0[(i >> 6) * NB + b];
         x0 &= ~(1ull << (i & 63));
         if (!x0) {
-            uint64_t &x1 = b1[b][i >> 12];
+            uint64_t &x1 = b1[(i >> 12) * NB + b];
             x1 &= ~(1ull << ((i >> 6) & 63));
-            if (!x1) b2[b][i >> 18] &= ~(1ull << ((i >> 12) & 63));
+            if (!x1) b2[(i >> 18) * NB + b] &= ~(1ull << ((i >> 12) & 63));
         }
         --cnt[b];
     }
     int64_t best() {  // the largest lambda's smallest point, -1: none left
         while (top >= 0 && cnt[top] == 0) --top;
         if (top < 0) return -1;
-        const std::vector<uint64_t> &B2 = b2[top];
         int64_t k2 = 0;
-        while (!B2[k2]) ++k2;
-        const int64_t k1 = (k2 << 6) | __builtin_ctzll(B2[k2]);
-        const int64_t k0 = (k1 << 6) | __builtin_ctzll(b1[top][k1]);
-        return (k0 << 6) | __builtin_ctzll(b0[top][k0]);
+        while (!b2[k2 * NB + top]) ++k2;
+        const int64_t k1 = (k2 << 6) | __builtin_ctzll(b2[k2 * NB + top]);
+        const int64_t k0 = (k1 << 6) | __builtin_ctzll(b1[k1 * NB + top]);
+        return (k0 << 6) | __builtin_ctzll(b0[k0 * NB + top]);
     }
 };
 
@@ -355,13 +363,15 @@ Pattern second_strength(const Pattern &S, const std::vector<int8_t> &cf, int pat
     parallel_rows(m, T, [&](int t, int64_t c0, int64_t c1) {
         Pattern &P = part[t];
         P.rp.assign(1, 0);
-        std::vector<int32_t> cnt(n, 0), touched;
+        std::vector<int32_t> cnt(n, 0), tbuf(n + 1);
         for (int64_t c = c0; c < c1; ++c) {
             const int64_t i = cpts[c];
-            touched.clear();
+            int64_t nt = 0;
             auto bump = [&](int32_t j) {
                 if (loc[j] < 0 || j == i) return;
-                if (cnt[j]++ == 0) touched.push_back(j);
+                tbuf[nt] = j;
+                nt += cnt[j] == 0;
+                ++cnt[j];
             };
             for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) bump(S.ci[q]);
             for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
@@ -369,7 +379,8 @@ Pattern second_strength(const Pattern &S, const std::vector<int8_t> &cf, int pat
                 for (int64_t r = S.rp[k]; r < S.rp[k + 1]; ++r) bump(S.ci[r]);
             }
             std::vector<int32_t> row;
-            for (int32_t j : touched) {
+            for (int64_t u = 0; u < nt; ++u) {
+                const int32_t j = tbuf[u];
                 if (cnt[j] >= paths) row.push_back(loc[j]);
                 cnt[j] = 0;
             }
@@ -389,22 +400,47 @@ std::vector<int8_t> rs_partitioned(const Pattern &S, int64_t K, const std::vecto
     const int64_t n = S.n;
     if (K <= 1 || n == 0) return rs_first_pass(S);
     std::vector<int8_t> cf(n, FPT);
-    parallel_rows(K, setup_threads(), [&](int, int64_t k0, int64_t k1) {
-        for (int64_t k = k0; k < k1; ++k) {
+    // partitions on host threads; with fewer partitions than threads each
+    // partition's extraction and transpose get the spare threads
+    const int T = setup_threads();
+    const int Tk = (int)std::max<int64_t>(1, T / K);
+    auto nowp = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double ts = nowp();
+    // (threads over partitions directly: parallel_rows keeps >= 8 items per thread)
+    const int Tp = (int)std::min<int64_t>(K, T);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < Tp; ++t) pool.emplace_back([&, t] {
+        for (int64_t k = K * t / Tp; k < K * (t + 1) / Tp; ++k) {
             const int64_t a = part_start[k], b = part_start[k + 1];
             if (b <= a) continue;
             Pattern L;
             L.n = b - a;
-            L.rp.assign(1, 0);
-            for (int64_t i = a; i < b; ++i) {
-                for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q)
-                    if (S.ci[q] >= a && S.ci[q] < b) L.ci.push_back((int32_t)(S.ci[q] - a));
-                L.rp.push_back((int64_t)L.ci.size());
-            }
-            const std::vector<int8_t> lc = rs_first_pass(L, 1);  // inside parallel_rows: no nested pool
+            L.rp.assign(L.n + 1, 0);
+            auto inside = [&](int32_t j) { return j >= a && j < b; };
+            parallel_rows(L.n, Tk, [&](int, int64_t i0, int64_t i1) {
+                for (int64_t i = i0; i < i1; ++i) {
+                    int64_t c = 0;
+                    for (int64_t q = S.rp[a + i]; q < S.rp[a + i + 1]; ++q) c += inside(S.ci[q]);
+                    L.rp[i + 1] = c;
+                }
+            });
+            for (int64_t i = 0; i < L.n; ++i) L.rp[i + 1] += L.rp[i];
+            L.ci.resize(L.rp[L.n]);
+            parallel_rows(L.n, Tk, [&](int, int64_t i0, int64_t i1) {
+                for (int64_t i = i0; i < i1; ++i) {
+                    int64_t o = L.rp[i];
+                    for (int64_t q = S.rp[a + i]; q < S.rp[a + i + 1]; ++q)
+                        if (inside(S.ci[q])) L.ci[o++] = (int32_t)(S.ci[q] - a);
+                }
+            });
+            const double tx = nowp();
+            const std::vector<int8_t> lc = rs_first_pass(L, Tk);
+            if (std::getenv("PLS_AMG_TRACE"))
+                fprintf(stderr, "[rs_partitioned] part %lld: extracted %.3f, passed %.3f s\n", (long long)k, tx - ts, nowp() - ts);
             std::copy(lc.begin(), lc.end(), cf.begin() + a);
         }
     });
+    for (auto &x : pool) x.join();
     return cf;
 }
 
@@ -540,7 +576,12 @@ std::vector<int8_t> coarsen(const Pattern &S, bool aggressive, int paths, const 
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     double t0 = now();
     const int64_t K = (int64_t)pst.size() - 1;
-    std::vector<int8_t> cf = pmis_stage(S, rs_partitioned(S, K, pst), pst);
+    std::vector<int8_t> cf = rs_partitioned(S, K, pst);
+    const double tr = now();
+    cf = pmis_stage(S, cf, pst);
+    if (std::getenv("PLS_AMG_TRACE"))
+        fprintf(stderr, "[boomeramg coarsen] n %lld K %lld: first pass %.2f s, PMIS stage %.2f s\n", (long long)S.n,
+                (long long)K, tr - t0, now() - tr);
     if (!aggressive) return cf;
     double t1 = now();
     std::vector<int32_t> cpts;
@@ -572,39 +613,60 @@ struct RowSet {
     std::vector<std::vector<int32_t>> col;
     std::vector<std::vector<double>> val;
 };
-HostCSR to_csr(const RowSet &R, int64_t ncols) {
+HostCSR to_csr(RowSet &R, int64_t ncols) {  // (R's rows are released)
     HostCSR P;
-    P.nrows = (int64_t)R.col.size();
+    const int64_t n = (int64_t)R.col.size();
+    P.nrows = n;
     P.ncols = ncols;
-    P.rp.assign(1, 0);
-    for (size_t i = 0; i < R.col.size(); ++i) {
-        for (size_t k = 0; k < R.col[i].size(); ++k)
-            if (R.val[i][k] != 0.0) {
-                P.ci.push_back(R.col[i][k]);
-                P.v.push_back(R.val[i][k]);
-            }
-        P.rp.push_back((int64_t)P.ci.size());
-    }
+    P.rp.assign(n + 1, 0);
+    const int T = setup_threads();
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            int64_t c = 0;
+            for (double x : R.val[i]) c += x != 0.0;
+            P.rp[i + 1] = c;
+        }
+    });
+    for (int64_t i = 0; i < n; ++i) P.rp[i + 1] += P.rp[i];
+    P.ci.resize(P.rp[n]);
+    P.v.resize(P.rp[n]);
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            int64_t o = P.rp[i];
+            for (size_t k = 0; k < R.col[i].size(); ++k)
+                if (R.val[i][k] != 0.0) {
+                    P.ci[o] = R.col[i][k];
+                    P.v[o++] = R.val[i][k];
+                }
+            std::vector<int32_t>().swap(R.col[i]);
+            std::vector<double>().swap(R.val[i]);
+        }
+    });
     return P;
 }
 
 // dense accumulator of one thread: first-touch order kept, sorted on output
-struct Acc {
+struct Acc {  // sparse accumulator: v is all zero between rows, the touched list grows branch-free
     std::vector<double> v;
-    std::vector<char> on;
-    std::vector<int32_t> touched;
-    explicit Acc(int64_t n) : v(n, 0.0), on(n, 0) {}
+    std::vector<uint8_t> on;
+    std::vector<int32_t> buf;
+    int64_t cnt = 0;
+    explicit Acc(int64_t n) : v(n, 0.0), on(n, 0), buf(n + 1) {}
     void add(int32_t j, double x) {
-        if (!on[j]) {
-            on[j] = 1;
-            v[j] = 0.0;
-            touched.push_back(j);
-        }
+        buf[cnt] = j;
+        cnt += on[j] ^ 1;
+        on[j] = 1;
         v[j] += x;
     }
+    int32_t *begin() { return buf.data(); }
+    int32_t *end() { return buf.data() + cnt; }
+    void sort() { std::sort(begin(), end()); }
     void clear() {
-        for (int32_t j : touched) on[j] = 0;
-        touched.clear();
+        for (int64_t u = 0; u < cnt; ++u) {
+            on[buf[u]] = 0;
+            v[buf[u]] = 0.0;
+        }
+        cnt = 0;
     }
 };
 
@@ -696,10 +758,10 @@ HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> 
                     const auto &pv = R.val[Q[u]];
                     for (size_t e = 0; e < pc.size(); ++e) acc.add(pc[e], w * pv[e]);
                 }
-                std::sort(acc.touched.begin(), acc.touched.end());
+                acc.sort();
                 std::vector<int32_t> cc;
                 std::vector<double> vv;
-                for (int32_t j : acc.touched) {
+                for (int32_t j : acc) {
                     cc.push_back(j);
                     vv.push_back(acc.v[j]);
                 }
@@ -778,17 +840,18 @@ HostCSR ext_i(const HostCSR &A, const Pattern &S, const std::vector<int8_t> &cf)
                     dt += a_ik;
                     continue;
                 }
+                const double distribute = a_ik / D;  // (hypre's ext+i: one division per strong F neighbour)
                 for (int64_t r = A.rp[k]; r < A.rp[k + 1]; ++r) {
                     const int32_t l = A.ci[r];
                     const double a = A.v[r];
                     if (a * dk >= 0.0) continue;
-                    if (chat[l]) w.add(l, a_ik * a / D);
-                    else if (l == i) dt += a_ik * a / D;
+                    if (chat[l]) w.add(l, distribute * a);
+                    else if (l == i) dt += distribute * a;
                 }
             }
-            std::sort(w.touched.begin(), w.touched.end());
+            w.sort();
             if (dt != 0.0)
-                for (int32_t j : w.touched) {
+                for (int32_t j : w) {
                     R.col[i].push_back(cidx[j]);
                     R.val[i].push_back(-w.v[j] / dt);
                 }
@@ -859,7 +922,6 @@ HostCSR chunk_part(const HostCSR &A, const std::vector<int32_t> &idx, const std:
     std::vector<int32_t> cid(n);
     for (size_t k = 0; k + 1 < cst.size(); ++k)
         for (int64_t i = cst[k]; i < cst[k + 1]; ++i) cid[i] = (int32_t)k;
-    auto chunk = [&](int64_t i) { return cid[i]; };
     std::vector<int32_t> loc;
     const bool all = idx.empty();
     if (!all) {
@@ -869,24 +931,45 @@ HostCSR chunk_part(const HostCSR &A, const std::vector<int32_t> &idx, const std:
     const int64_t m = all ? n : (int64_t)idx.size();
     HostCSR T;
     T.nrows = T.ncols = m;
-    T.rp.assign(1, 0);
-    for (int64_t r = 0; r < m; ++r) {
+    T.rp.assign(m + 1, 0);
+    // rows in parallel: count, then fill (the same entries in the same order)
+    std::vector<int64_t> bad(setup_threads(), -1);
+    auto scan = [&](int64_t r, auto emit) {
         const int64_t i = all ? r : idx[r];
-        const int64_t ch = chunk(i);
+        const int32_t ch = cid[i];
         bool has_diag = false;
         for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
             const int32_t j = all ? A.ci[k] : loc[A.ci[k]];
-            if (j < 0 || (part == 1 && j > r) || (part == 2 && j < r) || chunk(A.ci[k]) != ch) continue;
+            if (j < 0 || (part == 1 && j > r) || (part == 2 && j < r) || cid[A.ci[k]] != ch) continue;
             if (j == r) {
                 if (A.v[k] == 0.0) break;
                 has_diag = true;
             }
-            T.ci.push_back(j);
-            T.v.push_back(A.v[k]);
+            emit(j, A.v[k]);
         }
-        if (!has_diag) throw Error("boomeramg: zero diagonal entry on a Gauss-Seidel level (row " + std::to_string(i) + ")");
-        T.rp.push_back((int64_t)T.ci.size());
-    }
+        return has_diag;
+    };
+    parallel_rows(m, setup_threads(), [&](int t, int64_t r0, int64_t r1) {
+        for (int64_t r = r0; r < r1; ++r) {
+            int64_t c = 0;
+            if (!scan(r, [&](int32_t, double) { ++c; }) && bad[t] < 0) bad[t] = all ? r : idx[r];
+            T.rp[r + 1] = c;
+        }
+    });
+    for (int64_t b : bad)
+        if (b >= 0) throw Error("boomeramg: zero diagonal entry on a Gauss-Seidel level (row " + std::to_string(b) + ")");
+    for (int64_t r = 0; r < m; ++r) T.rp[r + 1] += T.rp[r];
+    T.ci.resize(T.rp[m]);
+    T.v.resize(T.rp[m]);
+    parallel_rows(m, setup_threads(), [&](int, int64_t r0, int64_t r1) {
+        for (int64_t r = r0; r < r1; ++r) {
+            int64_t o = T.rp[r];
+            scan(r, [&](int32_t j, double v) {
+                T.ci[o] = j;
+                T.v[o++] = v;
+            });
+        }
+    });
     return T;
 }
 
@@ -991,12 +1074,19 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
         if (nc == 0 || nc == A.nrows) break;
         t0 = now();
         const HostCSR P = aggressive ? multipass(A, S, cf) : truncate(ext_i(A, S, cf), p.pmax);
+        const double tp = now();
         const HostCSR R = amgh::transpose(P);
         tm[3] += now() - t0;
+        if (std::getenv("PLS_AMG_TRACE"))
+            fprintf(stderr, "[boomeramg level %lld] interp %.2f s, transpose %.2f s\n", (long long)nlev, tp - t0, now() - tp);
         t0 = now();
         HostCSR Ac;
         if (!galerkin_fused(A, P, nc, p.rap_bytes, Ac)) Ac = spgemm(R, spgemm(A, P));
         tm[4] += now() - t0;
+        if (std::getenv("PLS_AMG_TRACE"))
+            fprintf(stderr, "[boomeramg level %lld] n %lld nnz %lld -> nc %lld (P nnz %lld, Ac nnz %lld): RAP %.2f s\n",
+                    (long long)nlev, (long long)A.nrows, (long long)A.ci.size(), (long long)nc, (long long)P.ci.size(),
+                    (long long)Ac.ci.size(), now() - t0);
         on_level(A, cf, P, R, nc, parts);
         if (!parts.empty()) {  // the coarse level's rank sizes: C points per rank
             std::vector<int64_t> np(parts.size(), 0);
@@ -1010,20 +1100,26 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
     return A;
 }
 
-// level count of a triangular solve with T (lower: forward, else backward)
-int64_t tri_levels(const HostCSR &T, bool upper) {
-    const int64_t n = T.nrows;
-    std::vector<int64_t> lev(n, 0);
-    int64_t top = 0;
-    for (int64_t t = 0; t < n; ++t) {
-        const int64_t i = upper ? n - 1 - t : t;
-        int64_t l = 0;
-        for (int64_t k = T.rp[i]; k < T.rp[i + 1]; ++k)
-            if (T.ci[k] != i) l = std::max(l, lev[T.ci[k]] + 1);
-        lev[i] = l;
-        top = std::max(top, l + 1);
-    }
-    return top;
+// level count of a triangular solve with T (lower: forward, else backward);
+// T couples rows only inside the chunks [cp[q], cp[q + 1]), swept in parallel
+int64_t tri_levels(const HostCSR &T, bool upper, const std::vector<int64_t> &cp) {
+    std::vector<int64_t> lev(T.nrows, 0);
+    const int64_t nch = (int64_t)cp.size() - 1;
+    std::vector<int64_t> top(setup_threads(), 0);
+    parallel_rows(nch, setup_threads(), [&](int th, int64_t q0, int64_t q1) {
+        for (int64_t q = q0; q < q1; ++q) {
+            const int64_t a = cp[q], b = cp[q + 1];
+            for (int64_t t = a; t < b; ++t) {
+                const int64_t i = upper ? b - 1 - (t - a) : t;
+                int64_t l = 0;
+                for (int64_t k = T.rp[i]; k < T.rp[i + 1]; ++k)
+                    if (T.ci[k] != i) l = std::max(l, lev[T.ci[k]] + 1);
+                lev[i] = l;
+                top[th] = std::max(top[th], l + 1);
+            }
+        }
+    });
+    return *std::max_element(top.begin(), top.end());
 }
 
 // Hybrid symmetric Gauss-Seidel through dense per-chunk inverses (mostly
@@ -1224,7 +1320,7 @@ struct PCBoomer : PC {
                 // a sweep's critical path (levels of both triangles, one chunk per
                 // workgroup) against the bytes of the dense chunk inverses: mostly
                 // sequential chunks (every row a level of its own) go dense
-                const int64_t nlev = tri_levels(lo, false), nlev_u = tri_levels(up, true);
+                const int64_t nlev = tri_levels(lo, false, cp), nlev_u = tri_levels(up, true, cp);
                 const int64_t ldc = PCSGSDense::ld_for(cp);
                 const double dense_bytes = (double)((int64_t)cp.size() - 1) * ldc * ldc * 8.0;
                 const double t_dense = (double)rs->m * ldc * 8.0 / 5e12 + 5e-6;
@@ -1316,6 +1412,11 @@ struct PCBoomer : PC {
         std::unique_ptr<DevCSR> cur;
         const int me = dist ? c.comm->rank : 0;
         std::vector<int64_t> cps_last;  // dist: the coarsest level's rank starts
+        if (std::getenv("PLS_AMG_TRACE") && !dist) {
+            const double td = now();
+            HostCSR Hd = download(M, c);
+            fprintf(stderr, "[boomeramg %s] download %.2f s (nnz %lld)\n", prefix.c_str(), now() - td, (long long)Hd.ci.size());
+        }
         HostCSR A = host_setup(dist ? *global : download(M, c), prm,
                                [&](const HostCSR &Al, const std::vector<int8_t> &cf, const HostCSR &P, const HostCSR &R,
                                    int64_t nc, const std::vector<int64_t> &parts) {
