@@ -359,29 +359,49 @@ Pattern second_strength(const Pattern &S, const std::vector<int8_t> &cf, int pat
         }
     const int64_t m = (int64_t)cpts.size();
     const int T = setup_threads();
+    // SC: every row of S restricted to the C1 points, in C1 numbering -- the
+    // path counts then run over ~1/10 of S's entries with an m-sized counter
+    Pattern SC;
+    SC.n = n;
+    SC.rp.assign(n + 1, 0);
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            int64_t c = 0;
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) c += loc[S.ci[q]] >= 0;
+            SC.rp[i + 1] = c;
+        }
+    });
+    for (int64_t i = 0; i < n; ++i) SC.rp[i + 1] += SC.rp[i];
+    SC.ci.resize(SC.rp[n]);
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            int64_t o = SC.rp[i];
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q)
+                if (loc[S.ci[q]] >= 0) SC.ci[o++] = loc[S.ci[q]];
+        }
+    });
     std::vector<Pattern> part(T);
     parallel_rows(m, T, [&](int t, int64_t c0, int64_t c1) {
         Pattern &P = part[t];
         P.rp.assign(1, 0);
-        std::vector<int32_t> cnt(n, 0), tbuf(n + 1);
+        std::vector<int32_t> cnt(m, 0), tbuf(m + 1), row;
         for (int64_t c = c0; c < c1; ++c) {
             const int64_t i = cpts[c];
             int64_t nt = 0;
-            auto bump = [&](int32_t j) {
-                if (loc[j] < 0 || j == i) return;
-                tbuf[nt] = j;
-                nt += cnt[j] == 0;
-                ++cnt[j];
+            auto bump_row = [&](int64_t k) {
+                for (int64_t r = SC.rp[k]; r < SC.rp[k + 1]; ++r) {
+                    const int32_t j = SC.ci[r];
+                    tbuf[nt] = j;
+                    nt += (cnt[j] == 0) & (j != c);
+                    cnt[j] += j != c;
+                }
             };
-            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) bump(S.ci[q]);
-            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
-                const int32_t k = S.ci[q];
-                for (int64_t r = S.rp[k]; r < S.rp[k + 1]; ++r) bump(S.ci[r]);
-            }
-            std::vector<int32_t> row;
+            bump_row(i);
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) bump_row(S.ci[q]);
+            row.clear();
             for (int64_t u = 0; u < nt; ++u) {
                 const int32_t j = tbuf[u];
-                if (cnt[j] >= paths) row.push_back(loc[j]);
+                if (cnt[j] >= paths) row.push_back(j);
                 cnt[j] = 0;
             }
             std::sort(row.begin(), row.end());
@@ -496,30 +516,60 @@ std::vector<int8_t> pmis_stage(const Pattern &S, const std::vector<int8_t> &cf1,
     const int64_t n = S.n;
     if (n == 0 || pst.size() <= 2) return cf1;  // one partition: no boundary points
     const int64_t K = (int64_t)pst.size() - 1;
-    const Pattern ST = transpose(S);
+    const int T = setup_threads();
     std::vector<int32_t> part(n, 0);
+    for (int64_t k = 0; k < K; ++k) std::fill(part.begin() + pst[k], part.begin() + pst[k + 1], (int32_t)k);
+    // boundary points (the only ones PMIS decides; the rest keep the first pass's marker)
+    std::vector<int32_t> bidx(n, -1);
+    std::vector<std::vector<int32_t>> bl(T);
+    parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            bool boundary = false;
+            for (int64_t q = S.rp[i]; q < S.rp[i + 1] && !boundary; ++q) boundary = part[S.ci[q]] != part[i];
+            if (boundary) bl[t].push_back((int32_t)i);
+        }
+    });
+    std::vector<int32_t> B;
+    for (auto &v : bl) B.insert(B.end(), v.begin(), v.end());
+    const int64_t nb = (int64_t)B.size();
+    for (int64_t b = 0; b < nb; ++b) bidx[B[b]] = (int32_t)b;
+    // S^T restricted to the boundary points' rows: per thread, the entries j -> i
+    // (i a boundary point) of its row range, then merged in row order
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> te(T);
+    parallel_rows(n, T, [&](int t, int64_t j0, int64_t j1) {
+        for (int64_t j = j0; j < j1; ++j)
+            for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q)
+                if (bidx[S.ci[q]] >= 0) te[t].emplace_back(bidx[S.ci[q]], (int32_t)j);
+    });
+    std::vector<int64_t> trp(nb + 1, 0);
+    for (auto &v : te)
+        for (auto &e : v) ++trp[e.first + 1];
+    for (int64_t b = 0; b < nb; ++b) trp[b + 1] += trp[b];
+    std::vector<int32_t> tci(trp[nb]);
+    {
+        std::vector<int64_t> pos(trp.begin(), trp.end() - 1);
+        for (auto &v : te)  // threads in row order: every S^T row ascending
+            for (auto &e : v) tci[pos[e.first]++] = e.second;
+    }
     std::vector<double> measure(n);
     for (int64_t k = 0; k < K; ++k) {
         HypreRand r(2747 + k);
         for (int64_t i = pst[k]; i < pst[k + 1]; ++i) {
-            part[i] = (int32_t)k;
-            measure[i] = (double)ST.len(i) + r.next();
+            const double u = r.next();
+            measure[i] = bidx[i] >= 0 ? (double)(trp[bidx[i] + 1] - trp[bidx[i]]) + u : 0.0;
         }
     }
-    const int T = setup_threads();
-    std::vector<int8_t> st(n);
-    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
-        for (int64_t i = i0; i < i1; ++i) {
-            bool boundary = false;
-            for (int64_t q = S.rp[i]; q < S.rp[i + 1] && !boundary; ++q) boundary = part[S.ci[q]] != part[i];
-            st[i] = !boundary ? cf1[i] : (ST.len(i) == 0 ? FPT : UND);
-        }
-    });
-    std::vector<int8_t> nxt(n);
-    auto mark_f = [&]() {  // undecided points with a strong dependency on a C point -> F (reads st, writes nxt)
+    std::vector<int8_t> st(cf1);
+    for (int64_t b = 0; b < nb; ++b) st[B[b]] = trp[b + 1] == trp[b] ? FPT : UND;
+    std::vector<int8_t> nxt(nb);
+    auto apply = [&]() {
+        for (int64_t b = 0; b < nb; ++b) st[B[b]] = nxt[b];
+    };
+    auto mark_f = [&]() {  // undecided points with a strong dependency on a C point -> F
         std::vector<int64_t> und(T, 0);
-        parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
-            for (int64_t i = i0; i < i1; ++i) {
+        parallel_rows(nb, T, [&](int t, int64_t b0, int64_t b1) {
+            for (int64_t b = b0; b < b1; ++b) {
+                const int64_t i = B[b];
                 int8_t s = st[i];
                 if (s == UND) {
                     for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q)
@@ -529,46 +579,46 @@ std::vector<int8_t> pmis_stage(const Pattern &S, const std::vector<int8_t> &cf1,
                         }
                     und[t] += s == UND;
                 }
-                nxt[i] = s;
+                nxt[b] = s;
             }
         });
-        st.swap(nxt);
+        apply();
         int64_t u = 0;
         for (int64_t x : und) u += x;
         return u;
     };
     for (int64_t left = mark_f(); left > 0; left = mark_f()) {
         std::vector<int64_t> sel(T, 0);
-        parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
-            for (int64_t i = i0; i < i1; ++i) {
+        parallel_rows(nb, T, [&](int t, int64_t b0, int64_t b1) {
+            for (int64_t b = b0; b < b1; ++b) {
+                const int64_t i = B[b];
                 int8_t s = st[i];
                 if (s == UND) {
                     bool best = true;
                     const double mi = measure[i];
                     for (int64_t q = S.rp[i]; q < S.rp[i + 1] && best; ++q)
                         best = st[S.ci[q]] != UND || mi > measure[S.ci[q]];
-                    for (int64_t q = ST.rp[i]; q < ST.rp[i + 1] && best; ++q)
-                        best = st[ST.ci[q]] != UND || mi > measure[ST.ci[q]];
+                    for (int64_t q = trp[b]; q < trp[b + 1] && best; ++q) best = st[tci[q]] != UND || mi > measure[tci[q]];
                     if (best) {
                         s = CPT;
                         ++sel[t];
                     }
                 }
-                nxt[i] = s;
+                nxt[b] = s;
             }
         });
-        st.swap(nxt);
+        apply();
         int64_t ns = 0;
         for (int64_t x : sel) ns += x;
         if (ns == 0) {  // (the oracle's guard: ties of measures)
-            int64_t b = -1;
-            for (int64_t i = 0; i < n; ++i)
-                if (st[i] == UND && (b < 0 || measure[i] > measure[b])) b = i;
-            st[b] = CPT;
+            int64_t bb = -1;
+            for (int64_t b = 0; b < nb; ++b)
+                if (st[B[b]] == UND && (bb < 0 || measure[B[b]] > measure[B[bb]])) bb = b;
+            st[B[bb]] = CPT;
         }
     }
-    for (auto &s : st)
-        if (s != CPT) s = FPT;
+    for (auto &x : st)
+        if (x != CPT) x = FPT;
     return st;
 }
 
