@@ -143,13 +143,50 @@ HostCSR spgemm(const HostCSR &A, const HostCSR &B) {
 // used while nc^2 doubles stay small (max_bytes).
 bool galerkin_fused(const HostCSR &A, const HostCSR &P, int64_t nc, double max_bytes, HostCSR &C) {
     if ((double)nc * (double)nc * 8.0 > max_bytes) return false;
+    // the dense slabs (nc^2 doubles, zeroed and scanned) only pay when A P
+    // would be big: a mildly coarsened level (nc ~ n / 3) goes row-wise
+    if ((double)nc * (double)nc > 4.0 * (double)A.ci.size()) return false;
     C.nrows = C.ncols = nc;
     const int T = (int)std::max<int64_t>(1, std::min<int64_t>(setup_threads(), nc));
     std::vector<HostCSR> part(T);
+    // coarse-row ranges: equal shares of the (AP)_k work (a fine row's |A_k|
+    // spread over its P row's coarse points), each boundary then moved within
+    // +-1/4 share to where the fewest fine rows straddle it (a straddling row's
+    // (AP)_k is computed by both threads)
+    std::vector<int64_t> bound(T + 1, 0);
+    bound[T] = nc;
+    if (T > 1) {
+        std::vector<double> w(nc + 1, 0.0);
+        std::vector<int64_t> cross(nc + 1, 0);
+        for (int64_t k = 0; k < P.nrows; ++k) {
+            const int64_t b = P.rp[k], e = P.rp[k + 1];
+            if (e == b) continue;
+            const double c = (double)(A.rp[k + 1] - A.rp[k]) / (double)(e - b);
+            for (int64_t q = b; q < e; ++q) w[P.ci[q] + 1] += c;
+            ++cross[P.ci[b] + 1];  // straddles boundaries a with P.ci[b] < a <= P.ci[e - 1]
+            --cross[P.ci[e - 1] + 1];
+        }
+        for (int64_t a = 0; a < nc; ++a) {
+            w[a + 1] += w[a];
+            cross[a + 1] += cross[a];
+        }
+        int64_t a = 0;
+        for (int t = 1; t < T; ++t) {
+            const double target = w[nc] * t / T;
+            while (a < nc && w[a] < target) ++a;
+            const int64_t lo = std::max<int64_t>(bound[t - 1] + 1, a - nc / (4 * T)), hi = std::min<int64_t>(nc - 1, a + nc / (4 * T));
+            int64_t best = std::max<int64_t>(bound[t - 1] + 1, std::min<int64_t>(a, nc - 1));
+            for (int64_t x = lo; x <= hi; ++x)
+                if (cross[x] < cross[best]) best = x;
+            bound[t] = std::min<int64_t>(best, nc);
+        }
+        for (int t = 1; t <= T; ++t) bound[t] = std::max(bound[t], bound[t - 1]);
+    }
+    std::vector<int64_t> ncomp(T, 0);
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t) {
         th.emplace_back([&, t] {
-            const int64_t a0 = nc * t / T, a1 = nc * (t + 1) / T;
+            const int64_t a0 = bound[t], a1 = bound[t + 1];
             std::vector<double> acc((size_t)((a1 - a0) * nc), 0.0), ap(nc, 0.0);
             std::vector<uint8_t> mark(nc, 0);
             std::vector<int32_t> cols(nc + 1);
@@ -157,6 +194,7 @@ bool galerkin_fused(const HostCSR &A, const HostCSR &P, int64_t nc, double max_b
                 bool touch = false;
                 for (int64_t q = P.rp[k]; q < P.rp[k + 1] && !touch; ++q) touch = P.ci[q] >= a0 && P.ci[q] < a1;
                 if (!touch) continue;
+                ++ncomp[t];
                 // (AP)_k, as spgemm_rows sums it (ap is all zero between rows;
                 // the touched list grows branch-free)
                 int64_t ncol = 0;
@@ -200,6 +238,12 @@ bool galerkin_fused(const HostCSR &A, const HostCSR &P, int64_t nc, double max_b
         });
     }
     for (auto &x : th) x.join();
+    if (std::getenv("PLS_AMG_TRACE")) {
+        int64_t tot = 0;
+        for (int64_t x : ncomp) tot += x;
+        fprintf(stderr, "[galerkin_fused] %d threads: (AP)_k rows formed %lld for %lld fine rows\n", T, (long long)tot,
+                (long long)P.nrows);
+    }
     concat_rows(C, part);
     return true;
 }

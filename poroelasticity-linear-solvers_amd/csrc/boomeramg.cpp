@@ -762,6 +762,7 @@ HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> 
         });
         std::vector<int32_t> pts;
         for (auto &f : found) pts.insert(pts.end(), f.begin(), f.end());
+        if (std::getenv("PLS_AMG_TRACE") && n > 100000) fprintf(stderr, "[multipass] pass %d: %zu points\n", p, pts.size());
         if (pts.empty()) break;
         for (int32_t i : pts) pass[i] = p;
         parallel_rows((int64_t)pts.size(), T, [&](int, int64_t t0, int64_t t1) {
