@@ -738,9 +738,23 @@ static void do_setup(Handle &H) {
         build_sell(H.Ms_fp, c);
         build_sell(H.Mf_p, c);
     }
+    // (PLS_SETUP_TRACE: wall time of the setup stages on stderr)
+    const bool trace = std::getenv("PLS_SETUP_TRACE") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    c.sync();
+    double t0 = now();
+    auto stage = [&](const char *what) {
+        if (!trace) return;
+        c.sync();
+        const double t1 = now();
+        fprintf(stderr, "[setup] %s %.2f s\n", what, t1 - t0);
+        t0 = t1;
+    };
+    stage("blocks extracted");
     // inner solvers (setup_elliptic_solver / setup_fieldsplit; options win)
     const Options &o = H.opt;
     H.ksp_s = make_ksp("s_", o, &H.Ks, &H.Ks, H.inner_ksp, H.inner_pc, c);
+    stage("s block solver");
     if (H.three_way) {
         H.ksp_f = make_ksp("f_", o, &H.Kf, &H.Kf, H.inner_ksp, H.inner_pc, c);
         H.ksp_p = make_ksp("p_", o, &H.Kp, &H.Kp, H.inner_ksp, H.inner_pc, c);
@@ -805,6 +819,7 @@ static void do_setup(Handle &H) {
         }
     }
 fp_done:
+    stage(H.three_way ? "f / p / diff block solvers" : "fp block solver");
     // the inner Anderson history lives as long as the preconditioner object
     // (lib/Preconditioner.py: created in __init__, not in setUp)
     if (!H.mixer_ready) {
