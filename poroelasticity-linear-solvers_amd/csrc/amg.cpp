@@ -35,18 +35,45 @@ HostCSR transpose(const HostCSR &A) {
     HostCSR T;
     T.nrows = A.ncols;
     T.ncols = A.nrows;
-    T.rp.assign(A.ncols + 1, 0);
-    for (int32_t j : A.ci) ++T.rp[j + 1];
-    for (int64_t j = 0; j < A.ncols; ++j) T.rp[j + 1] += T.rp[j];
-    T.ci.resize(A.ci.size());
-    T.v.resize(A.v.size());
-    std::vector<int64_t> pos(T.rp.begin(), T.rp.end() - 1);
-    for (int64_t i = 0; i < A.nrows; ++i)
-        for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
-            const int64_t p = pos[A.ci[k]]++;
-            T.ci[p] = (int32_t)i;
-            T.v[p] = A.v[k];
+    const int64_t n = A.nrows, m = A.ncols, nnz = (int64_t)A.ci.size();
+    T.rp.assign(m + 1, 0);
+    T.ci.resize(nnz);
+    T.v.resize(nnz);
+    // per thread column counts over its row range, thread-major offsets inside every
+    // column, then every thread fills its rows: each column's rows stay ascending
+    int Tn = setup_threads();
+    if (m > 0) Tn = (int)std::max<int64_t>(1, std::min<int64_t>(Tn, nnz / (2 * m)));
+    if (nnz < (int64_t)1 << 20 || n < 1024) Tn = 1;
+    std::vector<int64_t> r0(Tn + 1);
+    for (int t = 0; t <= Tn; ++t) r0[t] = n * t / Tn;
+    std::vector<std::vector<int64_t>> cnt(Tn);
+    auto run = [&](auto fn) {
+        std::vector<std::thread> th;
+        for (int t = 0; t < Tn; ++t) th.emplace_back(fn, t);
+        for (auto &x : th) x.join();
+    };
+    run([&](int t) {
+        cnt[t].assign(m, 0);
+        for (int64_t k = A.rp[r0[t]]; k < A.rp[r0[t + 1]]; ++k) ++cnt[t][A.ci[k]];
+    });
+    for (int64_t j = 0; j < m; ++j) {
+        int64_t o = T.rp[j];
+        for (int t = 0; t < Tn; ++t) {
+            const int64_t c = cnt[t][j];
+            cnt[t][j] = o;
+            o += c;
         }
+        T.rp[j + 1] = o;
+    }
+    run([&](int t) {
+        std::vector<int64_t> &pos = cnt[t];
+        for (int64_t i = r0[t]; i < r0[t + 1]; ++i)
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                const int64_t q = pos[A.ci[k]]++;
+                T.ci[q] = (int32_t)i;
+                T.v[q] = A.v[k];
+            }
+    });
     return T;  // rows ascending (i visited in order)
 }
 

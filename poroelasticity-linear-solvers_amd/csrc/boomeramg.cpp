@@ -251,6 +251,26 @@ struct LamBuckets {
         }
         --cnt[b];
     }
+    // i from bucket b to b + d (d = +-1): the two words are neighbours in memory
+    void move(int64_t b, int64_t d, int64_t i) {
+        uint64_t *w = &b0[(i >> 6) * NB + b];
+        const uint64_t bit = 1ull << (i & 63);
+        w[0] &= ~bit;
+        if (!w[0]) {
+            uint64_t &x1 = b1[(i >> 12) * NB + b];
+            x1 &= ~(1ull << ((i >> 6) & 63));
+            if (!x1) b2[(i >> 18) * NB + b] &= ~(1ull << ((i >> 12) & 63));
+        }
+        if (!w[d]) {
+            uint64_t &x1 = b1[(i >> 12) * NB + b + d];
+            if (!x1) b2[(i >> 18) * NB + b + d] |= 1ull << ((i >> 12) & 63);
+            x1 |= 1ull << ((i >> 6) & 63);
+        }
+        w[d] |= bit;
+        --cnt[b];
+        ++cnt[b + d];
+        if (b + d > top) top = b + d;
+    }
     int64_t best() {  // the largest lambda's smallest point, -1: none left
         while (top >= 0 && cnt[top] == 0) --top;
         if (top < 0) return -1;
@@ -312,31 +332,34 @@ std::vector<int8_t> rs_first_pass(const Pattern &S, int max_threads = 0) {
             }
         }
     } else {
+        // lk: lambda of an undecided point, -1 once decided (one int32 array:
+        // one random access per neighbour instead of state + lambda)
+        std::vector<int32_t> lk(n);
         LamBuckets B(n, 2 * maxst + 1);
-        for (int64_t i = 0; i < n; ++i)
+        for (int64_t i = 0; i < n; ++i) {
+            lk[i] = st[i] == UND ? (int32_t)lam[i] : -1;
             if (st[i] == UND) B.insert(lam[i], i);
-        auto make_f = [&](int64_t j) {  // j undecided, in bucket lam[j]
+        }
+        auto make_f = [&](int64_t j) {  // j undecided, in bucket lk[j]
             st[j] = FPT;
-            B.erase(lam[j], j);
+            B.erase(lk[j], j);
+            lk[j] = -1;
             for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q) {
                 const int32_t k = S.ci[q];
-                if (st[k] == UND) {
-                    B.erase(lam[k], k);
-                    B.insert(++lam[k], k);
-                }
+                if (lk[k] >= 0) B.move(lk[k]++, 1, k);
             }
         };
         for (int64_t i; (i = B.best()) >= 0;) {
             st[i] = CPT;
-            B.erase(lam[i], i);
+            B.erase(lk[i], i);
+            lk[i] = -1;
             for (int64_t q = ST.rp[i]; q < ST.rp[i + 1]; ++q)
-                if (st[ST.ci[q]] == UND) make_f(ST.ci[q]);
+                if (lk[ST.ci[q]] >= 0) make_f(ST.ci[q]);
             for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
                 const int32_t k = S.ci[q];
-                if (st[k] != UND) continue;
-                B.erase(lam[k], k);
-                B.insert(--lam[k], k);
-                if (lam[k] == 0) make_f(k);
+                if (lk[k] < 0) continue;
+                B.move(lk[k]--, -1, k);
+                if (lk[k] == 0) make_f(k);
             }
         }
     }
@@ -840,7 +863,8 @@ HostCSR ext_i(const HostCSR &A, const Pattern &S, const std::vector<int8_t> &cf)
     const int T = setup_threads();
     parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
         std::vector<char> chat(n, 0), strong(n, 0);
-        std::vector<int32_t> chat_list;
+        std::vector<int32_t> chat_list, fk;
+        std::vector<double> fa, fD;
         Acc w(n);
         for (int64_t i = i0; i < i1; ++i) {
             if (cf[i] == CPT) {
@@ -865,39 +889,84 @@ HostCSR ext_i(const HostCSR &A, const Pattern &S, const std::vector<int8_t> &cf)
                     }
                 }
             }
+            // every l in C^_i is entered in w up front (adding +0.0 to its +0.0), so
+            // the loops below add to w.v directly
+            for (int32_t l : chat_list) w.add(l, 0.0);
             double dt = 0.0;
             for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
                 const int32_t j = A.ci[k];
                 const double a = A.v[k];
                 if (j == i) dt += a;
-                else if (chat[j]) w.add(j, a);
+                else if (chat[j]) w.v[j] += a;
                 else if (strong[j]) continue;
                 else dt += a;
             }
-            int64_t ak = A.rp[i];  // A's row i is sorted and S_i ascending: merge for a_ik
+            // the strong F neighbours k (S_i order) with a_ik (A's row i is sorted, S_i ascending: merge)
+            fk.clear();
+            fa.clear();
+            int64_t ak = A.rp[i];
             for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
                 const int32_t k = S.ci[q];
                 if (cf[k] != FPT) continue;
                 while (A.ci[ak] < k) ++ak;
-                const double a_ik = A.v[ak];
-                const double dk = diag[k];
-                double D = 0.0;
-                for (int64_t r = A.rp[k]; r < A.rp[k + 1]; ++r) {
-                    const int32_t l = A.ci[r];
-                    const double a = A.v[r];
-                    if ((chat[l] || l == i) && a * dk < 0.0) D += a;
+                fk.push_back(k);
+                fa.push_back(A.v[ak]);
+            }
+            // D_k = sum over k's row (storage order) of a_kl with a_kl a_kk < 0 and l in C^_i or
+            // l = i -- four neighbours' sums interleaved (four independent add chains; a
+            // skipped entry adds +0.0, which leaves D unchanged since D is never -0.0)
+            const size_t nfk = fk.size();
+            fD.resize(nfk);
+            chat[i] = 1;  // (the l = i case; chat holds C points only, i is F)
+            for (size_t g = 0; g < nfk; g += 4) {
+                int64_t b[4], len[4];
+                double dk[4], D[4] = {0.0, 0.0, 0.0, 0.0};
+                int64_t L = 0;
+                for (int u = 0; u < 4; ++u) {
+                    if (g + u < nfk) {
+                        b[u] = A.rp[fk[g + u]];
+                        len[u] = A.rp[fk[g + u] + 1] - b[u];
+                        dk[u] = diag[fk[g + u]];
+                    } else {
+                        b[u] = 0;
+                        len[u] = 0;
+                        dk[u] = 0.0;
+                    }
+                    L = std::max(L, len[u]);
                 }
+                for (int64_t r = 0; r < L; ++r)
+                    for (int u = 0; u < 4; ++u)
+                        if (r < len[u]) {
+                            const int64_t x = b[u] + r;
+                            const double a = A.v[x];
+                            D[u] += (chat[A.ci[x]] && a * dk[u] < 0.0) ? a : 0.0;
+                        }
+                for (int u = 0; u < 4 && g + u < nfk; ++u) fD[g + u] = D[u];
+            }
+            chat[i] = 0;
+            for (size_t f = 0; f < nfk; ++f) {
+                const int32_t k = fk[f];
+                const double a_ik = fa[f];
+                const double dk = diag[k];
+                const double D = fD[f];
                 if (D == 0.0) {
                     dt += a_ik;
                     continue;
                 }
                 const double distribute = a_ik / D;  // (hypre's ext+i: one division per strong F neighbour)
-                for (int64_t r = A.rp[k]; r < A.rp[k + 1]; ++r) {
+                // branch-free: entries outside C^_i or of the wrong sign add +0.0 to a +0.0
+                // (l not in C^_i) or to a nonzero / +0.0 sum (w.v is never -0.0), i.e. nothing
+                const int64_t rb = A.rp[k], re = A.rp[k + 1];
+                double *wv = w.v.data();
+                for (int64_t r = rb; r < re; ++r) {
                     const int32_t l = A.ci[r];
                     const double a = A.v[r];
-                    if (a * dk >= 0.0) continue;
-                    if (chat[l]) w.add(l, distribute * a);
-                    else if (l == i) dt += distribute * a;
+                    wv[l] += (chat[l] && a * dk < 0.0) ? distribute * a : 0.0;
+                }
+                const int32_t *pi = std::lower_bound(A.ci.data() + rb, A.ci.data() + re, (int32_t)i);
+                if (pi != A.ci.data() + re && *pi == i) {
+                    const double a = A.v[pi - A.ci.data()];
+                    if (a * dk < 0.0) dt += distribute * a;
                 }
             }
             w.sort();
@@ -1095,6 +1164,13 @@ BParams parse_params(const Options &o, const std::string &prefix) {
 
 // The host setup (oracle PCBoomerAMG.__init__): on_level(A, cf, P, R, nc) for
 // every level, then the coarsest operator is returned.  tm: stage seconds.
+// a level's big host arrays are released on a detached thread (unmapping a
+// few GB costs ~0.1 s per GB on the setup's critical path)
+template <class T>
+void free_later(T &&x) {
+    std::thread([y = std::move(x)] {}).detach();
+}
+
 template <class F>
 HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -1104,7 +1180,7 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
     std::vector<int64_t> parts = rank_sizes(p.ranks, A.nrows);
     while (A.nrows > 9 && nlev < p.max_levels - 1) {
         double t0 = now();
-        const Pattern S = strength(A, p.theta, p.mu);
+        Pattern S = strength(A, p.theta, p.mu);
         tm[1] += now() - t0;
         t0 = now();
         const bool aggressive = nlev < p.agg_nl;
@@ -1124,9 +1200,9 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
         for (int8_t v : cf) nc += v == CPT;
         if (nc == 0 || nc == A.nrows) break;
         t0 = now();
-        const HostCSR P = aggressive ? multipass(A, S, cf) : truncate(ext_i(A, S, cf), p.pmax);
+        HostCSR P = aggressive ? multipass(A, S, cf) : truncate(ext_i(A, S, cf), p.pmax);
         const double tp = now();
-        const HostCSR R = amgh::transpose(P);
+        HostCSR R = amgh::transpose(P);
         tm[3] += now() - t0;
         if (std::getenv("PLS_AMG_TRACE"))
             fprintf(stderr, "[boomeramg level %lld] interp %.2f s, transpose %.2f s\n", (long long)nlev, tp - t0, now() - tp);
@@ -1145,6 +1221,10 @@ HostCSR host_setup(HostCSR A, const BParams &p, F on_level, double *tm) {
                 for (int64_t i = pst[q]; i < pst[q + 1]; ++i) np[q] += cf[i] == CPT;
             parts.swap(np);
         }
+        free_later(std::move(S));
+        free_later(std::move(P));
+        free_later(std::move(R));
+        free_later(std::move(A));
         A = std::move(Ac);
         ++nlev;
     }
