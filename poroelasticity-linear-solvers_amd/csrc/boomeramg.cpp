@@ -73,14 +73,19 @@ Pattern concat_pattern(int64_t n, std::vector<Pattern> &part) {
     return S;
 }
 
-// oracle strength(): hypre CreateS with strong_threshold theta, max_row_sum mu
+// oracle strength(): hypre CreateS with strong_threshold theta, max_row_sum mu.
+// Two passes over the rows (threshold and count, then fill) into arrays sized
+// once: per-thread push_back growth on GBs of output serialised the threads
+// on page faults
 Pattern strength(const HostCSR &A, double theta, double mu) {
     const int64_t n = A.nrows;
     const int T = setup_threads();
-    std::vector<Pattern> part(T);
-    parallel_rows(n, T, [&](int t, int64_t i0, int64_t i1) {
-        Pattern &P = part[t];
-        P.rp.assign(1, 0);
+    Pattern S;
+    S.n = n;
+    S.rp.assign(n + 1, 0);
+    std::vector<double> thr(n);
+    std::vector<int8_t> mode(n);  // 0: no strong dependencies, 1: d >= 0 (a < thr), 2: d < 0 (a > thr)
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
         for (int64_t i = i0; i < i1; ++i) {
             double d = 0.0, rs = 0.0;
             double smin = std::numeric_limits<double>::infinity(), smax = -smin;
@@ -96,19 +101,38 @@ Pattern strength(const HostCSR &A, double theta, double mu) {
                     smax = std::max(smax, a);
                 }
             }
+            int64_t c = 0;
+            mode[i] = 0;
             if (noff > 0 && !(mu < 1.0 && std::fabs(rs) > mu * std::fabs(d))) {
                 const bool pos = d >= 0.0;
-                const double thr = theta * (pos ? smin : smax);
+                const double t = theta * (pos ? smin : smax);
+                thr[i] = t;
+                mode[i] = pos ? 1 : 2;
                 for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
                     if (A.ci[k] == i) continue;
                     const double a = A.v[k];
-                    if (pos ? a < thr : a > thr) P.ci.push_back(A.ci[k]);
+                    c += pos ? a < t : a > t;
                 }
             }
-            P.rp.push_back((int64_t)P.ci.size());
+            S.rp[i + 1] = c;
         }
     });
-    return concat_pattern(n, part);
+    for (int64_t i = 0; i < n; ++i) S.rp[i + 1] += S.rp[i];
+    S.ci.resize(S.rp[n]);
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            if (!mode[i]) continue;
+            const bool pos = mode[i] == 1;
+            const double t = thr[i];
+            int64_t o = S.rp[i];
+            for (int64_t k = A.rp[i]; k < A.rp[i + 1]; ++k) {
+                if (A.ci[k] == i) continue;
+                const double a = A.v[k];
+                if (pos ? a < t : a > t) S.ci[o++] = A.ci[k];
+            }
+        }
+    });
+    return S;
 }
 
 // S^T with every column's rows ascending (the sequential fill's order): per
