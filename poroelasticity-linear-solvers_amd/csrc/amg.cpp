@@ -105,8 +105,8 @@ void concat_rows(HostCSR &C, std::vector<HostCSR> &part) {
             std::copy(p.ci.begin(), p.ci.end(), C.ci.begin() + nz0[t]);
             std::copy(p.v.begin(), p.v.end(), C.v.begin() + nz0[t]);
             HostCSR().rp.swap(p.rp);
-            std::vector<int32_t>().swap(p.ci);
-            std::vector<double>().swap(p.v);
+            hvec<int32_t>().swap(p.ci);
+            hvec<double>().swap(p.v);
         });
     for (auto &x : th) x.join();
 }
@@ -417,7 +417,7 @@ HostCSR dense_inverse(const HostCSR &A) {
     D.nrows = D.ncols = n;
     D.rp.resize(n + 1);
     D.ci.resize(n * n);
-    D.v = X;
+    D.v.assign(X.begin(), X.end());
     for (int64_t i = 0; i <= n; ++i) D.rp[i] = i * n;
     for (int64_t i = 0; i < n; ++i)
         for (int64_t j = 0; j < n; ++j) D.ci[i * n + j] = (int32_t)j;

@@ -3,6 +3,7 @@
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -25,6 +26,25 @@ void parallel_rows(int64_t n, int T, F fn) {
     }
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t) th.emplace_back(fn, t, n * t / T, n * (t + 1) / T);
+    for (auto &x : th) x.join();
+}
+
+// fn(t, i0, i1) over blocks of `block` rows handed out to T threads on demand
+// (rows of very different cost, results written per row); init(t) once per thread
+template <class I, class F>
+void parallel_dynamic(int64_t n, int T, int64_t block, I init, F fn) {
+    T = (int)std::max<int64_t>(1, std::min<int64_t>(T, (n + block - 1) / block));
+    std::atomic<int64_t> next{0};
+    auto run = [&](int t) {
+        init(t);
+        for (int64_t i0; (i0 = next.fetch_add(block)) < n;) fn(t, i0, std::min(n, i0 + block));
+    };
+    if (T == 1) {
+        run(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(run, t);
     for (auto &x : th) x.join();
 }
 

@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <limits>
 #include <map>
+#include <memory>
 #include <queue>
 #include <thread>
 
@@ -40,10 +41,10 @@ namespace pls {
 namespace {
 using namespace amgh;
 
-struct Pattern {  // CSR sparsity (strong dependencies)
+struct Pattern {  // CSR sparsity (strong dependencies); arrays sized by their writers (hvec)
     int64_t n = 0;
-    std::vector<int64_t> rp{0};
-    std::vector<int32_t> ci;
+    hvec<int64_t> rp{0};
+    hvec<int32_t> ci;
     int64_t len(int64_t i) const { return rp[i + 1] - rp[i]; }
 };
 
@@ -67,7 +68,7 @@ Pattern concat_pattern(int64_t n, std::vector<Pattern> &part) {
             for (size_t k = 1; k < p.rp.size(); ++k) S.rp[row0[t] + k] = nz0[t] + p.rp[k];
             std::copy(p.ci.begin(), p.ci.end(), S.ci.begin() + nz0[t]);
             Pattern().rp.swap(p.rp);
-            std::vector<int32_t>().swap(p.ci);
+            hvec<int32_t>().swap(p.ci);
         });
     for (auto &x : th) x.join();
     return S;
@@ -812,10 +813,18 @@ HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> 
         if (std::getenv("PLS_AMG_TRACE") && n > 100000) fprintf(stderr, "[multipass] pass %d: %zu points\n", p, pts.size());
         if (pts.empty()) break;
         for (int32_t i : pts) pass[i] = p;
-        parallel_rows((int64_t)pts.size(), T, [&](int, int64_t t0, int64_t t1) {
-            Acc acc(nc);
+        struct State {
+            Acc acc;
             std::vector<int32_t> Q;
             std::vector<double> aq;
+            explicit State(int64_t nc) : acc(nc) {}
+        };
+        std::vector<std::unique_ptr<State>> state(T);
+        parallel_dynamic((int64_t)pts.size(), T, 256, [&](int th) { state[th] = std::make_unique<State>(nc); },
+                         [&](int th, int64_t t0, int64_t t1) {
+            Acc &acc = state[th]->acc;
+            std::vector<int32_t> &Q = state[th]->Q;
+            std::vector<double> &aq = state[th]->aq;
             for (int64_t t = t0; t < t1; ++t) {
                 const int64_t i = pts[t];
                 Q.clear();
@@ -885,11 +894,22 @@ HostCSR ext_i(const HostCSR &A, const Pattern &S, const std::vector<int8_t> &cf)
     R.col.resize(n);
     R.val.resize(n);
     const int T = setup_threads();
-    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
-        std::vector<char> chat(n, 0), strong(n, 0);
+    // rows of very different cost (C rows are free, F rows on a dense Galerkin
+    // level ~|S_i| x |A_k|): blocks of rows on demand
+    struct State {
+        std::vector<char> chat, strong;
         std::vector<int32_t> chat_list, fk;
         std::vector<double> fa, fD;
-        Acc w(n);
+        Acc w;
+        explicit State(int64_t n) : chat(n, 0), strong(n, 0), w(n) {}
+    };
+    std::vector<std::unique_ptr<State>> state(T);
+    parallel_dynamic(n, T, 16, [&](int t) { state[t] = std::make_unique<State>(n); }, [&](int t, int64_t i0, int64_t i1) {
+        State &X = *state[t];
+        std::vector<char> &chat = X.chat, &strong = X.strong;
+        std::vector<int32_t> &chat_list = X.chat_list, &fk = X.fk;
+        std::vector<double> &fa = X.fa, &fD = X.fD;
+        Acc &w = X.w;
         for (int64_t i = i0; i < i1; ++i) {
             if (cf[i] == CPT) {
                 R.col[i] = {cidx[i]};

@@ -373,7 +373,7 @@ static bool build_b3(const DevCSR &M, DevSELL &S, std::vector<int32_t> &singles,
 // Reverse Cuthill-McKee order of a square pattern (host): per component, BFS
 // from a pseudo-peripheral vertex visiting neighbours by increasing degree,
 // then reversed.  order[new] = old.
-static std::vector<int32_t> rcm_order(const std::vector<int64_t> &rp, const std::vector<int32_t> &ci, int64_t n) {
+static std::vector<int32_t> rcm_order(const hvec<int64_t> &rp, const hvec<int32_t> &ci, int64_t n) {
     std::vector<int32_t> order, lev(n, -1);
     order.reserve(n);
     std::vector<char> done(n, 0);

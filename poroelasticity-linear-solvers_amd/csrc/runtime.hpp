@@ -192,11 +192,35 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha = 1.
           const double *z = nullptr);
 
 // Host copy of a CSR matrix (setup-time algebra: fieldsplit blocks, AMG hierarchy).
+// std::allocator whose value-initialisation is default-initialisation: a
+// resize(n) of a host matrix array leaves it unwritten (its writer fills it,
+// on as many threads as it likes) instead of zeroing GBs on one thread
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new ((void *)p) U;
+    }
+    template <class U, class... Args>
+    void construct(U *p, Args &&...args) {
+        ::new ((void *)p) U(std::forward<Args>(args)...);
+    }
+};
+template <class T>
+using hvec = std::vector<T, NoInitAlloc<T>>;
+
 struct HostCSR {
     int64_t nrows = 0, ncols = 0;
-    std::vector<int64_t> rp{0};
-    std::vector<int32_t> ci;
-    std::vector<double> v;
+    hvec<int64_t> rp{0};
+    hvec<int32_t> ci;
+    hvec<double> v;
 };
 HostCSR download(const DevCSR &M, Ctx &c);
 void upload(const HostCSR &H, DevCSR &M, Ctx &c);
