@@ -232,78 +232,80 @@ struct Tournament {
     }
 };
 
-// The same argmax (lambda, -i) by lambda buckets (round 3): per bucket a
-// three-level bitmap over the points, the smallest index its first set bit --
-// a lambda change is O(1) word updates and a selection a few word scans,
-// where the tournament compares O(log n) siblings (random reads of lambda).
-// lambda <= 2 max |S^T_i| (it starts at |S^T_i| and grows once per point of
-// S^T_i that becomes F).  The buckets' words are interleaved (word w of
-// bucket b at w * NB + b), so a point's lambda moving by one touches one cache
-// line, and the points a C point updates (its neighbours, close in index) a
-// few more.
-struct LamBuckets {
-    int64_t NB = 0, w0 = 0, w1 = 0, w2 = 0, top = -1;
-    std::vector<uint64_t> b0, b1, b2;
+// The same argmax by groups (round 4; round 3 kept a per-point bitmap per
+// lambda bucket): the points in groups of 64, each
+// group's largest lambda over its undecided points kept in gmax, and the
+// groups in lambda buckets (a two-level bitmap per bucket over the groups:
+// ~1 MB at 2.5M points, where a per-point bitmap per bucket was ~50 MB and
+// every lambda change a DRAM access).  A lambda change rescans its group's 64
+// lambdas only when it lowers the group's maximum; a selection takes the top
+// bucket's first group and that group's first point at the top lambda --
+// the largest lambda, ties to the smallest index, as before.
+struct GroupMax {
+    const std::vector<int32_t> &lk;
+    int64_t n, ng, w1, w2, NB, top = -1;
+    std::vector<int32_t> gmax;
+    std::vector<uint64_t> b0, b1;
     std::vector<int64_t> cnt;
-    LamBuckets(int64_t n, int64_t maxlam) {
-        NB = maxlam + 1;
-        w0 = (n + 63) / 64;
-        w1 = (w0 + 63) / 64;
+    GroupMax(const std::vector<int32_t> &l, int64_t n_, int64_t maxlam) : lk(l), n(n_) {
+        ng = (n + 63) / 64;
+        w1 = (ng + 63) / 64;
         w2 = (w1 + 63) / 64;
-        b0.assign((size_t)(w0 * NB), 0);
-        b1.assign((size_t)(w1 * NB), 0);
-        b2.assign((size_t)(w2 * NB), 0);
+        NB = maxlam + 1;
+        gmax.assign(ng, -1);
+        b0.assign((size_t)(NB * w1), 0);
+        b1.assign((size_t)(NB * w2), 0);
         cnt.assign(NB, 0);
-    }
-    void insert(int64_t b, int64_t i) {
-        uint64_t &x0 = b0[(i >> 6) * NB + b];
-        if (!x0) {
-            uint64_t &x1 = b1[(i >> 12) * NB + b];
-            if (!x1) b2[(i >> 18) * NB + b] |= 1ull << ((i >> 12) & 63);
-            x1 |= 1ull << ((i >> 6) & 63);
+        for (int64_t g = 0; g < ng; ++g) {
+            gmax[g] = scan(g);
+            if (gmax[g] >= 0) insert(gmax[g], g);
         }
-        x0 |= 1ull << (i & 63);
-        ++cnt[b];
-        if (b > top) top = b;
     }
-    void erase(int64_t b, int64_t i) {
-        uint64_t &x0 = b0[(i >> 6) * NB + b];
-        x0 &= ~(1ull << (i & 63));
-        if (!x0) {
-            uint64_t &x1 = b1[(i >> 12) * NB + b];
-            x1 &= ~(1ull << ((i >> 6) & 63));
-            if (!x1) b2[(i >> 18) * NB + b] &= ~(1ull << ((i >> 12) & 63));
-        }
-        --cnt[b];
+    int32_t scan(int64_t g) const {
+        int32_t m = -1;
+        const int64_t e = std::min(n, (g + 1) * 64);
+        for (int64_t i = g * 64; i < e; ++i) m = std::max(m, lk[i]);
+        return m;
     }
-    // i from bucket b to b + d (d = +-1): the two words are neighbours in memory
-    void move(int64_t b, int64_t d, int64_t i) {
-        uint64_t *w = &b0[(i >> 6) * NB + b];
-        const uint64_t bit = 1ull << (i & 63);
-        w[0] &= ~bit;
-        if (!w[0]) {
-            uint64_t &x1 = b1[(i >> 12) * NB + b];
-            x1 &= ~(1ull << ((i >> 6) & 63));
-            if (!x1) b2[(i >> 18) * NB + b] &= ~(1ull << ((i >> 12) & 63));
-        }
-        if (!w[d]) {
-            uint64_t &x1 = b1[(i >> 12) * NB + b + d];
-            if (!x1) b2[(i >> 18) * NB + b + d] |= 1ull << ((i >> 12) & 63);
-            x1 |= 1ull << ((i >> 6) & 63);
-        }
-        w[d] |= bit;
-        --cnt[b];
-        ++cnt[b + d];
-        if (b + d > top) top = b + d;
+    void insert(int64_t v, int64_t g) {
+        uint64_t &x = b0[v * w1 + (g >> 6)];
+        if (!x) b1[v * w2 + (g >> 12)] |= 1ull << ((g >> 6) & 63);
+        x |= 1ull << (g & 63);
+        ++cnt[v];
+        if (v > top) top = v;
     }
-    int64_t best() {  // the largest lambda's smallest point, -1: none left
+    void erase(int64_t v, int64_t g) {
+        uint64_t &x = b0[v * w1 + (g >> 6)];
+        x &= ~(1ull << (g & 63));
+        if (!x) b1[v * w2 + (g >> 12)] &= ~(1ull << ((g >> 6) & 63));
+        --cnt[v];
+    }
+    // lk[i] went from oldv to newv (-1: decided)
+    void changed(int64_t i, int32_t oldv, int32_t newv) {
+        const int64_t g = i >> 6;
+        const int32_t m = gmax[g];
+        if (newv > m) {
+            if (m >= 0) erase(m, g);
+            gmax[g] = newv;
+            insert(newv, g);
+        } else if (oldv == m && newv < oldv) {
+            const int32_t nm = scan(g);
+            if (nm != m) {
+                erase(m, g);
+                gmax[g] = nm;
+                if (nm >= 0) insert(nm, g);
+            }
+        }
+    }
+    int64_t best() {
         while (top >= 0 && cnt[top] == 0) --top;
         if (top < 0) return -1;
-        int64_t k2 = 0;
-        while (!b2[k2 * NB + top]) ++k2;
-        const int64_t k1 = (k2 << 6) | __builtin_ctzll(b2[k2 * NB + top]);
-        const int64_t k0 = (k1 << 6) | __builtin_ctzll(b1[k1 * NB + top]);
-        return (k0 << 6) | __builtin_ctzll(b0[k0 * NB + top]);
+        int64_t k1 = 0;
+        while (!b1[top * w2 + k1]) ++k1;
+        const int64_t k0 = (k1 << 6) | __builtin_ctzll(b1[top * w2 + k1]);
+        const int64_t g = (k0 << 6) | __builtin_ctzll(b0[top * w1 + k0]);
+        for (int64_t i = g * 64;; ++i)
+            if (lk[i] == top) return i;
     }
 };
 
@@ -360,30 +362,33 @@ std::vector<int8_t> rs_first_pass(const Pattern &S, int max_threads = 0) {
         // lk: lambda of an undecided point, -1 once decided (one int32 array:
         // one random access per neighbour instead of state + lambda)
         std::vector<int32_t> lk(n);
-        LamBuckets B(n, 2 * maxst + 1);
-        for (int64_t i = 0; i < n; ++i) {
-            lk[i] = st[i] == UND ? (int32_t)lam[i] : -1;
-            if (st[i] == UND) B.insert(lam[i], i);
-        }
-        auto make_f = [&](int64_t j) {  // j undecided, in bucket lk[j]
+        for (int64_t i = 0; i < n; ++i) lk[i] = st[i] == UND ? (int32_t)lam[i] : -1;
+        GroupMax B(lk, n, 2 * maxst + 1);
+        auto make_f = [&](int64_t j) {  // j undecided
             st[j] = FPT;
-            B.erase(lk[j], j);
+            const int32_t o = lk[j];
             lk[j] = -1;
+            B.changed(j, o, -1);
             for (int64_t q = S.rp[j]; q < S.rp[j + 1]; ++q) {
                 const int32_t k = S.ci[q];
-                if (lk[k] >= 0) B.move(lk[k]++, 1, k);
+                if (lk[k] >= 0) {
+                    ++lk[k];
+                    B.changed(k, lk[k] - 1, lk[k]);
+                }
             }
         };
         for (int64_t i; (i = B.best()) >= 0;) {
             st[i] = CPT;
-            B.erase(lk[i], i);
+            const int32_t o = lk[i];
             lk[i] = -1;
+            B.changed(i, o, -1);
             for (int64_t q = ST.rp[i]; q < ST.rp[i + 1]; ++q)
                 if (lk[ST.ci[q]] >= 0) make_f(ST.ci[q]);
             for (int64_t q = S.rp[i]; q < S.rp[i + 1]; ++q) {
                 const int32_t k = S.ci[q];
                 if (lk[k] < 0) continue;
-                B.move(lk[k]--, -1, k);
+                --lk[k];
+                B.changed(k, lk[k] + 1, lk[k]);
                 if (lk[k] == 0) make_f(k);
             }
         }
