@@ -575,7 +575,10 @@ void launch_scatter(int64_t n, const int64_t *idx, const double *x, double *y, h
 }
 
 // ---------------------------------------------- deterministic reductions --
-static constexpr int NB_MAX = 1024;
+// up to 4096 blocks (16 waves per CU): with 1024 the multi-vector CGS
+// kernels (k_mdot / k_maxpy_norm) held 4 waves per CU and read the Krylov
+// basis at ~2.8 TB/s (profiles/r04_hyp59)
+static constexpr int NB_MAX = 4096;
 int reduce_blocks(int64_t n) {
     int64_t nb = (n + 4095) / 4096;
     if (nb < 1) nb = 1;

@@ -31,8 +31,8 @@ static CommSelf g_self_comm;
 Ctx::Ctx() {
     comm = &g_self_comm;
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    partial.alloc(1024 * 136);
-    partial_n = 1024 * 136;
+    partial.alloc(4096 * 136);
+    partial_n = 4096 * 136;
     dscal.alloc(4096);
     HIPCHK(hipHostMalloc((void **)&hscal, sizeof(double) * 4096, hipHostMallocDefault));
     hscal_n = 4096;

@@ -64,7 +64,7 @@ struct DBuf {
 struct Ctx {
     hipStream_t st = nullptr;
     Comm *comm = nullptr;   // global reductions (CommSelf unless distributed)
-    DBuf<double> partial;   // reduction partials (>= NB_MAX * 136; ensure_partial grows it)
+    DBuf<double> partial;   // reduction partials (NB_MAX (4096) x 136 at first; ensure_partial grows it)
     int64_t partial_n = 0;
     int64_t hscal_n = 0;    // doubles in the pinned host mirror
     DBuf<double> dscal;     // device scalars
