@@ -650,7 +650,31 @@ __global__ __launch_bounds__(TPB) void k_mdot(int64_t n, int k, const double *__
 #pragma unroll
     for (int u = 0; u < MDOT_NJ; ++u) a[u] = 0.0;
     const double *v0 = V + (int64_t)j0 * ldv;
-    for (int64_t i = s + 2 * threadIdx.x; i + 1 < e; i += 2 * TPB) {
+    int64_t i = s + 2 * threadIdx.x;
+    // two row pairs per trip, all their loads issued before the FMAs (twice the
+    // bytes in flight; the same per-thread summation order as one pair a trip)
+    for (; i + 2 * TPB + 1 < e; i += 4 * TPB) {
+        const cgs_d2 wa = *reinterpret_cast<const cgs_d2 *>(w + i);
+        const cgs_d2 wb = *reinterpret_cast<const cgs_d2 *>(w + i + 2 * TPB);
+        cgs_d2 va[MDOT_NJ], vb[MDOT_NJ];
+#pragma unroll
+        for (int u = 0; u < MDOT_NJ; ++u) {
+            if (u < nj) {
+                va[u] = *reinterpret_cast<const cgs_d2 *>(v0 + (int64_t)u * ldv + i);
+                vb[u] = *reinterpret_cast<const cgs_d2 *>(v0 + (int64_t)u * ldv + i + 2 * TPB);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < MDOT_NJ; ++u) {
+            if (u < nj) {
+                a[u] += va[u].x * wa.x;
+                a[u] += va[u].y * wa.y;
+                a[u] += vb[u].x * wb.x;
+                a[u] += vb[u].y * wb.y;
+            }
+        }
+    }
+    for (; i + 1 < e; i += 2 * TPB) {
         const cgs_d2 wi = *reinterpret_cast<const cgs_d2 *>(w + i);
 #pragma unroll
         for (int u = 0; u < MDOT_NJ; ++u) {
@@ -720,7 +744,46 @@ __global__ __launch_bounds__(TPB) void k_maxpy_norm(int64_t n, int k, const doub
     int64_t s, e;
     chunk_even(n, gridDim.x, blockIdx.x, s, e);
     double a = 0.0;
-    for (int64_t i = s + 2 * threadIdx.x; i + 1 < e; i += 2 * TPB) {
+    int64_t i = s + 2 * threadIdx.x;
+    // two row pairs per trip (loads of both ahead of their FMAs; the norm sums
+    // the pairs in the same order as one pair a trip)
+    for (; i + 2 * TPB + 1 < e; i += 4 * TPB) {
+        cgs_d2 ta = *reinterpret_cast<const cgs_d2 *>(w + i);
+        cgs_d2 tb = *reinterpret_cast<const cgs_d2 *>(w + i + 2 * TPB);
+        int j = 0;
+        for (; j + 8 <= k; j += 8) {
+            cgs_d2 va[8], vb[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                va[u] = *reinterpret_cast<const cgs_d2 *>(V + (int64_t)(j + u) * ldv + i);
+                vb[u] = *reinterpret_cast<const cgs_d2 *>(V + (int64_t)(j + u) * ldv + i + 2 * TPB);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const double hj = (j + u) < 512 ? hs[j + u] : h[j + u];
+                ta.x -= hj * va[u].x;
+                ta.y -= hj * va[u].y;
+                tb.x -= hj * vb[u].x;
+                tb.y -= hj * vb[u].y;
+            }
+        }
+        for (; j < k; ++j) {
+            const cgs_d2 va = *reinterpret_cast<const cgs_d2 *>(V + (int64_t)j * ldv + i);
+            const cgs_d2 vb = *reinterpret_cast<const cgs_d2 *>(V + (int64_t)j * ldv + i + 2 * TPB);
+            const double hj = j < 512 ? hs[j] : h[j];
+            ta.x -= hj * va.x;
+            ta.y -= hj * va.y;
+            tb.x -= hj * vb.x;
+            tb.y -= hj * vb.y;
+        }
+        *reinterpret_cast<cgs_d2 *>(w + i) = ta;
+        *reinterpret_cast<cgs_d2 *>(w + i + 2 * TPB) = tb;
+        a += ta.x * ta.x;
+        a += ta.y * ta.y;
+        a += tb.x * tb.x;
+        a += tb.y * tb.y;
+    }
+    for (; i + 1 < e; i += 2 * TPB) {
         cgs_d2 t = *reinterpret_cast<const cgs_d2 *>(w + i);
         int j = 0;
         for (; j + 8 <= k; j += 8) {
