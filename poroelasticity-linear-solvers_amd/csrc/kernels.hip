@@ -17,7 +17,6 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdio>
-#include <cstdlib>
 
 namespace pls {
 
@@ -701,62 +700,12 @@ __global__ __launch_bounds__(TPB) void k_mdot(int64_t n, int k, const double *__
     }
 }
 
-// The same dots column by column: a block's w rows stay in registers (up to
-// CMP_MAX row pairs per thread) and each basis column's chunk is streamed on
-// its own -- one long contiguous run per column instead of k interleaved
-// streams 82 MB apart (k_mdot fell from 6.3 TB/s at k = 1 to 2.2 TB/s at
-// k = 30).  Per (column, thread) the pairs are summed in the same order as
-// k_mdot, so the partials are bitwise the same.
-static constexpr int CMP_MAX = 16;
-__global__ __launch_bounds__(TPB) void k_mdot_cols(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
-                                                   const double *__restrict__ w, double *partial) {
-    __shared__ double lds[TPB / 64];
-    const int nb = gridDim.x;
-    int64_t s, e;
-    chunk_even(n, nb, blockIdx.x, s, e);
-    cgs_d2 wr[CMP_MAX];
-    int np = 0;
-#pragma unroll
-    for (int m = 0; m < CMP_MAX; ++m) {
-        const int64_t i = s + 2 * threadIdx.x + (int64_t)m * 2 * TPB;
-        if (i + 1 < e) {
-            wr[m] = *reinterpret_cast<const cgs_d2 *>(w + i);
-            np = m + 1;
-        }
-    }
-    const bool odd = ((e - s) & 1) && threadIdx.x == 0;
-    const double wl = odd ? w[e - 1] : 0.0;
-    for (int u = 0; u < k; ++u) {
-        const double *vu = V + (int64_t)u * ldv;
-        cgs_d2 v[CMP_MAX];
-#pragma unroll
-        for (int m = 0; m < CMP_MAX; ++m)
-            if (m < np) v[m] = *reinterpret_cast<const cgs_d2 *>(vu + s + 2 * threadIdx.x + (int64_t)m * 2 * TPB);
-        double a = 0.0;
-#pragma unroll
-        for (int m = 0; m < CMP_MAX; ++m)
-            if (m < np) {
-                a += v[m].x * wr[m].x;
-                a += v[m].y * wr[m].y;
-            }
-        if (odd) a += vu[e - 1] * wl;
-        const double r = block_sum(a, lds);
-        if (threadIdx.x == 0) partial[(int64_t)u * nb + blockIdx.x] = r;
-    }
-}
-
 void launch_mdot(int64_t n, int k, const double *const *, const double *V, int64_t ldv, const double *w,
                  double *partial, double *out, hipStream_t st) {
     if (k <= 0) return;
     const int nb = reduce_blocks(n);
-    int64_t c = (n + nb - 1) / nb;
-    c = (c + 1) & ~(int64_t)1;
-    if (c <= (int64_t)CMP_MAX * 2 * TPB && !std::getenv("PLS_MDOT_ROWS")) {
-        k_mdot_cols<<<nb, TPB, 0, st>>>(n, k, V, ldv, w, partial);
-    } else {
-        dim3 grid(nb, (k + MDOT_NJ - 1) / MDOT_NJ);
-        k_mdot<<<grid, TPB, 0, st>>>(n, k, V, ldv, w, partial);
-    }
+    dim3 grid(nb, (k + MDOT_NJ - 1) / MDOT_NJ);
+    k_mdot<<<grid, TPB, 0, st>>>(n, k, V, ldv, w, partial);
     k_final<<<k, TPB, 0, st>>>(nb, partial, out, 0);
 }
 
@@ -871,69 +820,10 @@ __global__ __launch_bounds__(TPB) void k_maxpy_norm(int64_t n, int k, const doub
     }
 }
 
-// The same update column by column (w's rows in registers, each column's
-// chunk streamed on its own, as k_mdot_cols): per row the columns are
-// subtracted j ascending and the norm sums the pairs in k_maxpy_norm's order
-__global__ __launch_bounds__(TPB) void k_maxpy_norm_cols(int64_t n, int k, const double *__restrict__ V, int64_t ldv,
-                                                         const double *__restrict__ h, double *__restrict__ w,
-                                                         double *partial) {
-    __shared__ double lds[TPB / 64];
-    int64_t s, e;
-    chunk_even(n, gridDim.x, blockIdx.x, s, e);
-    cgs_d2 t[CMP_MAX];
-    int np = 0;
-#pragma unroll
-    for (int m = 0; m < CMP_MAX; ++m) {
-        const int64_t i = s + 2 * threadIdx.x + (int64_t)m * 2 * TPB;
-        if (i + 1 < e) {
-            t[m] = *reinterpret_cast<const cgs_d2 *>(w + i);
-            np = m + 1;
-        }
-    }
-    const bool odd = ((e - s) & 1) && threadIdx.x == 0;
-    double tl = odd ? w[e - 1] : 0.0;
-    for (int j = 0; j < k; ++j) {
-        const double *vj = V + (int64_t)j * ldv;
-        const double hj = h[j];
-        cgs_d2 v[CMP_MAX];
-#pragma unroll
-        for (int m = 0; m < CMP_MAX; ++m)
-            if (m < np) v[m] = *reinterpret_cast<const cgs_d2 *>(vj + s + 2 * threadIdx.x + (int64_t)m * 2 * TPB);
-#pragma unroll
-        for (int m = 0; m < CMP_MAX; ++m)
-            if (m < np) {
-                t[m].x -= hj * v[m].x;
-                t[m].y -= hj * v[m].y;
-            }
-        if (odd) tl -= hj * vj[e - 1];
-    }
-    double a = 0.0;
-#pragma unroll
-    for (int m = 0; m < CMP_MAX; ++m)
-        if (m < np) {
-            *reinterpret_cast<cgs_d2 *>(w + s + 2 * threadIdx.x + (int64_t)m * 2 * TPB) = t[m];
-            a += t[m].x * t[m].x;
-            a += t[m].y * t[m].y;
-        }
-    if (odd) {
-        w[e - 1] = tl;
-        a += tl * tl;
-    }
-    if (partial) {
-        a = block_sum(a, lds);
-        if (threadIdx.x == 0) partial[blockIdx.x] = a;
-    }
-}
-
 void launch_maxpy_norm(int64_t n, int k, const double *V, int64_t ldv, const double *h_dev, double,
                        double *w, double *partial, double *out, hipStream_t st) {
     const int nb = reduce_blocks(n);
-    int64_t c = (n + nb - 1) / nb;
-    c = (c + 1) & ~(int64_t)1;
-    if (c <= (int64_t)CMP_MAX * 2 * TPB && !std::getenv("PLS_MDOT_ROWS"))
-        k_maxpy_norm_cols<<<nb, TPB, 0, st>>>(n, k, V, ldv, h_dev, w, out ? partial : nullptr);
-    else
-        k_maxpy_norm<<<nb, TPB, 0, st>>>(n, k, V, ldv, h_dev, w, out ? partial : nullptr);
+    k_maxpy_norm<<<nb, TPB, 0, st>>>(n, k, V, ldv, h_dev, w, out ? partial : nullptr);
     if (out) k_final<<<1, TPB, 0, st>>>(nb, partial, out, 0);  // ||w||^2 (rank-local)
 }
 
