@@ -1963,58 +1963,13 @@ void launch_lds_fill(int64_t nslices, const int32_t *s_start, const int32_t *s_n
 // levels come from vector registers (lane l: level gbase + l) filled by one
 // gather per 62 levels and read with v_readlane -- no scalar loads in the
 // loop, whose lgkmcnt waits would be paid at every LDS access.
-typedef int ring_i4 __attribute__((ext_vector_type(4)));
 template <int P>
 struct Sw2Slot {
     int32_t c[P + 1];
     double v[P + 1];
     int64_t base, L;  // L: entries incl. header; base < 0: this wave has no slice
     int l2;           // ring sweep: log2 of the slice's lanes per row (slice starts carry it in bits 0-2)
-    // ring sweep: the slot's raw 16-byte loads (inline asm, counted by the sweep)
-    // and how many were issued (0: the wave is idle at the slot's level)
-    ring_i4 rc[(P + 1) / 4], rv[(P + 1) / 2];
-    int nl;
 };
-
-// The ring sweep's slot loads: range-checked buffer loads through inline asm
-// that only waves with a slice at the level issue.  The compiler does not see
-// them, so it neither drains them nor counts them; the sweep waits for a slot
-// with vmcnt(loads issued after it) -- 0, 6 or 12, the two younger slots'
-// counts -- and pins the slot's registers to that wait.  (Issued on every
-// path, as in round 2, the 16 waves' 6 loads per level were the sweep's cost:
-// ~16 x 6 load issues per level through one CU, most of them idle waves'.)
-__device__ __forceinline__ ring_i4 ring_ld128(__amdgpu_buffer_rsrc_t r, int off) {
-    ring_i4 v;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
-    return v;
-}
-__device__ __forceinline__ int64_t ring_sgpr64(int64_t v) {
-    const int32_t lo = __builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(uint64_t)v);
-    const int32_t hi = __builtin_amdgcn_readfirstlane((int32_t)((uint64_t)v >> 32));
-    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-template <int P>
-__device__ __forceinline__ void ring_wait(Sw2Slot<P> &s, int younger) {
-    if (younger >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else if (younger >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int q = 0; q < (P + 1) / 4; ++q) asm volatile("" : "+v"(s.rc[q]));
-#pragma unroll
-    for (int q = 0; q < (P + 1) / 2; ++q) asm volatile("" : "+v"(s.rv[q]));
-#pragma unroll
-    for (int q = 0; q < (P + 1) / 4; ++q) {
-        s.c[4 * q + 0] = s.rc[q][0];
-        s.c[4 * q + 1] = s.rc[q][1];
-        s.c[4 * q + 2] = s.rc[q][2];
-        s.c[4 * q + 3] = s.rc[q][3];
-    }
-#pragma unroll
-    for (int q = 0; q < (P + 1) / 2; ++q) {
-        s.v[2 * q + 0] = __builtin_bit_cast(double, ((uint64_t)(uint32_t)s.rv[q][1] << 32) | (uint32_t)s.rv[q][0]);
-        s.v[2 * q + 1] = __builtin_bit_cast(double, ((uint64_t)(uint32_t)s.rv[q][3] << 32) | (uint32_t)s.rv[q][2]);
-    }
-}
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
     const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)(uint64_t)v, l);
@@ -2086,32 +2041,39 @@ __device__ __forceinline__ void sw2_issue(Sw2Ctx &x, int64_t g, Sw2Slot<P> &s) {
     const int64_t L = base >= 0 ? (next - base) >> 6 : 0;
     s.base = base;
     s.L = L;
+    if (R && (ring_probe & 4)) {  // diagnostics: no prefetch at all
+        s.base = base;
+#pragma unroll
+        for (int u = 0; u <= P; ++u) { s.c[u] = 0; s.v[u] = 0.0; }
+        return;
+    }
     if (R) {
         // ring sweep: buffer loads through per-slot descriptors bounded to the
-        // slice (entries past it are range-checked away: no traffic, reads
-        // return 0); a wave without a slice at the level issues none (nl = 0,
-        // ring_wait counts it)
+        // slice (0 bytes for an idle wave): entries past the slice and idle
+        // waves' loads are range-checked away (no traffic, reads return 0),
+        // and every path issues the same loads, which keeps the compiler's
+        // vmcnt bookkeeping exact -- using this slot two levels later waits for
+        // its own loads only (a branch around them made it wait for everything
+        // in flight, the prefetch issued this level included)
         static_assert((P + 1) % 8 == 0, "the ring sweep's slot is one lane's first P + 1 entries (a multiple of 8)");
-        const bool act = base >= 0 && !(ring_probe & 4);  // (probe bit 2: no prefetch at all, diagnostics)
-        s.nl = act ? (P + 1) / 4 + (P + 1) / 2 : 0;
-        if (act) {
-            const int nc = !(ring_probe & 1) ? (int)(L * 64 * 4) : 0;
-            const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(uintptr_t)ring_sgpr64((int64_t)(uintptr_t)(x.col + base)), (short)0,
-                __builtin_amdgcn_readfirstlane(nc), 0x00020000);
-            const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(uintptr_t)ring_sgpr64((int64_t)(uintptr_t)(x.val + base)), (short)0,
-                __builtin_amdgcn_readfirstlane(2 * nc), 0x00020000);
-            const int off = x.lane * (int)L;  // lane-major, L a multiple of P + 1
+        const int64_t b = base >= 0 ? base : 0;
+        const int nc = (base >= 0 && !(ring_probe & 1)) ? (int)(L * 64 * 4) : 0;
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void *)(x.col + b), (short)0, nc, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void *)(x.val + b), (short)0, 2 * nc, 0x00020000);
+        const int off = x.lane * (int)L;  // lane-major, L a multiple of P + 1
 #pragma unroll
-            for (int q = 0; q < (P + 1) / 4; ++q) s.rc[q] = ring_ld128(rc, (off + 4 * q) * 4);
+        for (int q = 0; q < (P + 1) / 4; ++q) {
+            const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(rc, (off + 4 * q) * 4, 0, 0);
+            s.c[4 * q + 0] = (int32_t)c4[0];
+            s.c[4 * q + 1] = (int32_t)c4[1];
+            s.c[4 * q + 2] = (int32_t)c4[2];
+            s.c[4 * q + 3] = (int32_t)c4[3];
+        }
 #pragma unroll
-            for (int q = 0; q < (P + 1) / 2; ++q) s.rv[q] = ring_ld128(rv, (off + 2 * q) * 8);
-        } else {
-#pragma unroll
-            for (int q = 0; q < (P + 1) / 4; ++q) s.rc[q] = ring_i4{0, 0, 0, 0};
-#pragma unroll
-            for (int q = 0; q < (P + 1) / 2; ++q) s.rv[q] = ring_i4{0, 0, 0, 0};
+        for (int q = 0; q < (P + 1) / 2; ++q) {
+            const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rv, (off + 2 * q) * 8, 0, 0);
+            s.v[2 * q + 0] = __builtin_bit_cast(double, ((uint64_t)v4[1] << 32) | v4[0]);
+            s.v[2 * q + 1] = __builtin_bit_cast(double, ((uint64_t)v4[3] << 32) | v4[2]);
         }
         return;
     }
@@ -2226,12 +2188,10 @@ __device__ __forceinline__ void ring_chunk(Sw2Ctx &x, int64_t g) {
 }
 
 template <int P, int LPR, bool W, bool R>
-__device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, Sw2Slot<P> &cur, const Sw2Slot<P> &mid,
-                                          Sw2Slot<P> &ahead) {
+__device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P> &cur, Sw2Slot<P> &ahead) {
     if (R) ring_chunk(x, g);
     if (g + 2 >= x.gbase + 64) x.refill(g);
     sw2_issue<P, R>(x, g + 2, ahead);
-    if (R) ring_wait<P>(cur, mid.nl + ahead.nl);  // cur's loads: older than the g + 1 and g + 2 slots
     if (cur.base >= 0 && !(R && (ring_probe & 2))) {  // (probe bit 1: no compute, diagnostics)
         const int32_t h = cur.c[0];
         const int32_t len = W ? (int32_t)cur.L - 1 : (int32_t)((uint32_t)h >> SW_ROW_BITS);
@@ -2286,14 +2246,13 @@ __device__ __forceinline__ void sweep2(Sw2Ctx &x, int64_t g0) {
     sw2_issue<P, R>(x, g0, s0);
     sw2_issue<P, R>(x, g0 + 1, s1);
     for (int64_t g = g0;;) {
-        sw2_level<P, LPR, W, R>(x, g, s0, s1, s2);
+        sw2_level<P, LPR, W, R>(x, g, s0, s2);
         if (++g >= x.g1) break;
-        sw2_level<P, LPR, W, R>(x, g, s1, s2, s0);
+        sw2_level<P, LPR, W, R>(x, g, s1, s0);
         if (++g >= x.g1) break;
-        sw2_level<P, LPR, W, R>(x, g, s2, s0, s1);
+        sw2_level<P, LPR, W, R>(x, g, s2, s1);
         if (++g >= x.g1) break;
     }
-    if (R) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the last levels' prefetches, past g1)
 }
 
 // Round-robin sweep for deep, narrow level DAGs (about one slice per level:
