@@ -1597,7 +1597,9 @@ struct PCBoomer : PC {
             HostCSR Hd = download(M, c);
             fprintf(stderr, "[boomeramg %s] download %.2f s (nnz %lld)\n", prefix.c_str(), now() - td, (long long)Hd.ci.size());
         }
-        HostCSR A = host_setup(dist ? *global : download(M, c), prm,
+        HostCSR Ahost = dist ? *global : download(M, c);
+        const double t_dl = now() - t0;
+        HostCSR A = host_setup(std::move(Ahost), prm,
                                [&](const HostCSR &Al, const std::vector<int8_t> &cf, const HostCSR &P, const HostCSR &R,
                                    int64_t nc, const std::vector<int64_t> &parts) {
             const double t1 = now();
@@ -1674,6 +1676,9 @@ struct PCBoomer : PC {
             tm[5] += now() - t1;
         }, tm);
         tm[0] = now() - t0 - (tm[1] + tm[2] + tm[3] + tm[4] + tm[5]);
+        if (std::getenv("PLS_AMG_TRACE"))
+            fprintf(stderr, "[boomeramg %s] download/copy %.2f s, untimed in the level loop %.2f s\n", prefix.c_str(), t_dl,
+                    tm[0] - t_dl);
         if (!lv.empty() || dist) {  // (sharded: the coarsest operator is the gathered global one)
             cur = std::make_unique<DevCSR>();
             upload(A, *cur, c);
