@@ -214,7 +214,8 @@ bool galerkin_fused(const HostCSR &A, const HostCSR &P, int64_t nc, double max_b
     for (int t = 0; t < T; ++t) {
         th.emplace_back([&, t] {
             const int64_t a0 = bound[t], a1 = bound[t + 1];
-            std::vector<double> acc((size_t)((a1 - a0) * nc), 0.0), ap(nc, 0.0);
+            hvec<double> acc((size_t)((a1 - a0) * nc), 0.0);  // (huge pages: the scatter's rows are 120 KB apart)
+            std::vector<double> ap(nc, 0.0);
             std::vector<uint8_t> mark(nc, 0);
             std::vector<int32_t> cols(nc + 1);
             for (int64_t k = 0; k < P.nrows; ++k) {

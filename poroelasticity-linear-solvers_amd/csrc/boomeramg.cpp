@@ -242,12 +242,12 @@ struct Tournament {
 // bucket's first group and that group's first point at the top lambda --
 // the largest lambda, ties to the smallest index, as before.
 struct GroupMax {
-    const std::vector<int32_t> &lk;
+    const hvec<int32_t> &lk;
     int64_t n, ng, w1, w2, NB, top = -1;
     std::vector<int32_t> gmax;
     std::vector<uint64_t> b0, b1;
     std::vector<int64_t> cnt;
-    GroupMax(const std::vector<int32_t> &l, int64_t n_, int64_t maxlam) : lk(l), n(n_) {
+    GroupMax(const hvec<int32_t> &l, int64_t n_, int64_t maxlam) : lk(l), n(n_) {
         ng = (n + 63) / 64;
         w1 = (ng + 63) / 64;
         w2 = (w1 + 63) / 64;
@@ -361,7 +361,7 @@ std::vector<int8_t> rs_first_pass(const Pattern &S, int max_threads = 0) {
     } else {
         // lk: lambda of an undecided point, -1 once decided (one int32 array:
         // one random access per neighbour instead of state + lambda)
-        std::vector<int32_t> lk(n);
+        hvec<int32_t> lk(n);
         for (int64_t i = 0; i < n; ++i) lk[i] = st[i] == UND ? (int32_t)lam[i] : -1;
         GroupMax B(lk, n, 2 * maxst + 1);
         auto make_f = [&](int64_t j) {  // j undecided

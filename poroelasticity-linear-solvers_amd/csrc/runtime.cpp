@@ -13,6 +13,7 @@
 #include "amg_host.hpp"
 
 #include <climits>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <thread>
@@ -24,6 +25,17 @@
 #include <sstream>
 
 namespace pls {
+
+void *huge_alloc(size_t bytes) {
+    const size_t len = (bytes + HUGE_ALLOC_MIN - 1) & ~(HUGE_ALLOC_MIN - 1);
+    void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) throw std::bad_alloc();
+    (void)madvise(p, len, MADV_HUGEPAGE);
+    return p;
+}
+void huge_free(void *p, size_t bytes) {
+    if (p) (void)munmap(p, (bytes + HUGE_ALLOC_MIN - 1) & ~(HUGE_ALLOC_MIN - 1));
+}
 
 // ============================================================== context ===
 static CommSelf g_self_comm;

@@ -195,6 +195,14 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha = 1.
 // std::allocator whose value-initialisation is default-initialisation: a
 // resize(n) of a host matrix array leaves it unwritten (its writer fills it,
 // on as many threads as it likes) instead of zeroing GBs on one thread
+// Arrays of 2 MB and more are mapped on their own with MADV_HUGEPAGE (the
+// boxes run transparent huge pages in madvise mode): the setup's random
+// accesses over GB-sized host matrices (the Galerkin product's P rows, the
+// first pass's lambda array) otherwise miss the TLB on 4 KB pages, and a
+// first touch costs one fault per 4 KB.
+void *huge_alloc(size_t bytes);
+void huge_free(void *p, size_t bytes);
+static constexpr size_t HUGE_ALLOC_MIN = (size_t)2 << 20;
 template <class T>
 struct NoInitAlloc : std::allocator<T> {
     template <class U>
@@ -204,6 +212,14 @@ struct NoInitAlloc : std::allocator<T> {
     NoInitAlloc() = default;
     template <class U>
     NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+    T *allocate(size_t n) {
+        if (n * sizeof(T) >= HUGE_ALLOC_MIN) return static_cast<T *>(huge_alloc(n * sizeof(T)));
+        return std::allocator<T>::allocate(n);
+    }
+    void deallocate(T *p, size_t n) noexcept {
+        if (n * sizeof(T) >= HUGE_ALLOC_MIN) huge_free(p, n * sizeof(T));
+        else std::allocator<T>::deallocate(p, n);
+    }
     template <class U>
     void construct(U *p) noexcept {
         ::new ((void *)p) U;
