@@ -781,7 +781,10 @@ std::vector<int32_t> coarse_index(const std::vector<int8_t> &cf, int64_t &nc) {
     return ci;
 }
 
-// oracle multipass_interp()
+// oracle multipass_interp().  Rows live in per-thread arenas of fixed-size
+// blocks (a row never straddles blocks, so its pointers stay valid while later
+// passes read it); C rows point at cidx and a 1.0 -- no per-row allocations
+// (5M std::vector rows were ~10M mallocs and a serial 240 MB init at N=59).
 HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> &cf) {
     const int64_t n = A.nrows;
     int64_t nc = 0;
@@ -789,15 +792,37 @@ HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> 
     std::vector<int32_t> pass(n, -1);
     for (int64_t i = 0; i < n; ++i)
         if (cf[i] == CPT) pass[i] = 0;
-    RowSet R;
-    R.col.resize(n);
-    R.val.resize(n);
-    for (int64_t i = 0; i < n; ++i)
-        if (cf[i] == CPT) {
-            R.col[i] = {cidx[i]};
-            R.val[i] = {1.0};
+    struct RowRef {
+        const int32_t *c;
+        const double *v;
+        int64_t len;
+    };
+    static const double one = 1.0;
+    hvec<RowRef> ref(n);
+    for (int64_t i = 0; i < n; ++i) ref[i] = cf[i] == CPT ? RowRef{&cidx[i], &one, 1} : RowRef{nullptr, nullptr, 0};
+    struct Arena {
+        const int64_t BLK = (int64_t)1 << 18;
+        std::vector<std::unique_ptr<int32_t[]>> cb;
+        std::vector<std::unique_ptr<double[]>> vb;
+        int64_t used = 0, cap = 0;
+        void room(int64_t m) {  // m entries contiguous
+            if (used + m <= cap) return;
+            cap = std::max(BLK, m);
+            cb.emplace_back(new int32_t[cap]);
+            vb.emplace_back(new double[cap]);
+            used = 0;
         }
+    };
     const int T = setup_threads();
+    struct State {
+        Acc acc;
+        std::vector<int32_t> Q;
+        std::vector<double> aq;
+        Arena ar;
+        explicit State(int64_t nc) : acc(nc) {}
+    };
+    std::vector<std::unique_ptr<State>> state(T);
+    for (int t = 0; t < T; ++t) state[t] = std::make_unique<State>(nc);
     for (int p = 1;; ++p) {
         // the points of pass p, decided from the passes before p (rows in parallel, kept in order)
         std::vector<std::vector<int32_t>> found(T);
@@ -818,18 +843,11 @@ HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> 
         if (std::getenv("PLS_AMG_TRACE") && n > 100000) fprintf(stderr, "[multipass] pass %d: %zu points\n", p, pts.size());
         if (pts.empty()) break;
         for (int32_t i : pts) pass[i] = p;
-        struct State {
-            Acc acc;
-            std::vector<int32_t> Q;
-            std::vector<double> aq;
-            explicit State(int64_t nc) : acc(nc) {}
-        };
-        std::vector<std::unique_ptr<State>> state(T);
-        parallel_dynamic((int64_t)pts.size(), T, 256, [&](int th) { state[th] = std::make_unique<State>(nc); },
-                         [&](int th, int64_t t0, int64_t t1) {
-            Acc &acc = state[th]->acc;
-            std::vector<int32_t> &Q = state[th]->Q;
-            std::vector<double> &aq = state[th]->aq;
+        parallel_dynamic((int64_t)pts.size(), T, 256, [](int) {}, [&](int th, int64_t t0, int64_t t1) {
+            State &X = *state[th];
+            Acc &acc = X.acc;
+            std::vector<int32_t> &Q = X.Q;
+            std::vector<double> &aq = X.aq;
             for (int64_t t = t0; t < t1; ++t) {
                 const int64_t i = pts[t];
                 Q.clear();
@@ -866,24 +884,51 @@ HostCSR multipass(const HostCSR &A, const Pattern &S, const std::vector<int8_t> 
                     const double a = aq[u];
                     if (a == 0.0) continue;
                     const double w = -(a < 0.0 ? alpha : beta) * a / d;
-                    const auto &pc = R.col[Q[u]];
-                    const auto &pv = R.val[Q[u]];
-                    for (size_t e = 0; e < pc.size(); ++e) acc.add(pc[e], w * pv[e]);
+                    const RowRef &r = ref[Q[u]];
+                    for (int64_t e = 0; e < r.len; ++e) acc.add(r.c[e], w * r.v[e]);
                 }
                 acc.sort();
-                std::vector<int32_t> cc;
-                std::vector<double> vv;
+                const int64_t m = acc.end() - acc.begin();
+                X.ar.room(m);
+                int32_t *cc = X.ar.cb.back().get() + X.ar.used;
+                double *vv = X.ar.vb.back().get() + X.ar.used;
+                int64_t e = 0;
                 for (int32_t j : acc) {
-                    cc.push_back(j);
-                    vv.push_back(acc.v[j]);
+                    cc[e] = j;
+                    vv[e++] = acc.v[j];
                 }
+                X.ar.used += m;
                 acc.clear();
-                R.col[i] = std::move(cc);
-                R.val[i] = std::move(vv);
+                ref[i] = RowRef{cc, vv, m};
             }
         });
     }
-    return to_csr(R, nc);
+    // the CSR (exact zeros dropped), rows in parallel
+    HostCSR P;
+    P.nrows = n;
+    P.ncols = nc;
+    P.rp.assign(n + 1, 0);
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            int64_t c = 0;
+            for (int64_t e = 0; e < ref[i].len; ++e) c += ref[i].v[e] != 0.0;
+            P.rp[i + 1] = c;
+        }
+    });
+    for (int64_t i = 0; i < n; ++i) P.rp[i + 1] += P.rp[i];
+    P.ci.resize(P.rp[n]);
+    P.v.resize(P.rp[n]);
+    parallel_rows(n, T, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            int64_t o = P.rp[i];
+            for (int64_t e = 0; e < ref[i].len; ++e)
+                if (ref[i].v[e] != 0.0) {
+                    P.ci[o] = ref[i].c[e];
+                    P.v[o++] = ref[i].v[e];
+                }
+        }
+    });
+    return P;
 }
 
 // oracle ext_i_interp()
