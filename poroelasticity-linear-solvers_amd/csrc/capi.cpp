@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -12,6 +13,7 @@
 
 #include "../../include/pls.h"
 #include "runtime.hpp"
+#include "amg_host.hpp"
 
 namespace pls {
 
@@ -611,35 +613,46 @@ void BlockPC::apply(const double *x, double *y, Ctx &c) {
 }
 
 // ------------------------------------------------------------ setup path ---
+// rows permuted and re-sorted into the internal field order; rows on host
+// threads (the footing N=128 system's three 68.8M-entry matrices took ~8 s of
+// pls_create on one thread)
 static void permute_host(const pls_csr *M, const std::vector<int64_t> &perm, const std::vector<int64_t> &inv,
-                         std::vector<int64_t> &rp, std::vector<int32_t> &ci, std::vector<double> &v) {
+                         hvec<int64_t> &rp, hvec<int32_t> &ci, hvec<double> &v) {
     const int64_t n = (int64_t)perm.size();
     rp.assign(n + 1, 0);
     for (int64_t i = 0; i < n; ++i) rp[i + 1] = rp[i] + (M->row_ptr[perm[i] + 1] - M->row_ptr[perm[i]]);
     ci.resize(rp[n]);
     v.resize(rp[n]);
-    std::vector<std::pair<int32_t, double>> row;
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t o = perm[i];
-        row.clear();
-        for (int64_t k = M->row_ptr[o]; k < M->row_ptr[o + 1]; ++k) {
-            const int32_t cc = M->col[k];
-            if (cc < 0 || cc >= n) throw Error("column index out of range");
-            row.emplace_back((int32_t)inv[cc], M->val[k]);
+    std::atomic<bool> bad{false};
+    amgh::parallel_rows(n, amgh::setup_threads(), [&](int, int64_t i0, int64_t i1) {
+        std::vector<std::pair<int32_t, double>> row;
+        for (int64_t i = i0; i < i1; ++i) {
+            const int64_t o = perm[i];
+            row.clear();
+            for (int64_t k = M->row_ptr[o]; k < M->row_ptr[o + 1]; ++k) {
+                const int32_t cc = M->col[k];
+                if (cc < 0 || cc >= n) {
+                    bad = true;
+                    row.emplace_back(0, 0.0);
+                    continue;
+                }
+                row.emplace_back((int32_t)inv[cc], M->val[k]);
+            }
+            std::sort(row.begin(), row.end(), [](auto &a, auto &b) { return a.first < b.first; });
+            for (size_t t = 0; t < row.size(); ++t) {
+                ci[rp[i] + t] = row[t].first;
+                v[rp[i] + t] = row[t].second;
+            }
         }
-        std::sort(row.begin(), row.end(), [](auto &a, auto &b) { return a.first < b.first; });
-        for (size_t t = 0; t < row.size(); ++t) {
-            ci[rp[i] + t] = row[t].first;
-            v[rp[i] + t] = row[t].second;
-        }
-    }
+    });
+    if (bad) throw Error("column index out of range");
 }
 
 static void upload_permuted(const pls_csr *M, Handle &H, const std::vector<int64_t> &inv, DevCSR &out) {
     if (M->nrows != H.n || M->ncols != H.n) throw Error("matrix must be n x n with n = ns + nf + np");
-    std::vector<int64_t> rp;
-    std::vector<int32_t> ci;
-    std::vector<double> v;
+    hvec<int64_t> rp;
+    hvec<int32_t> ci;
+    hvec<double> v;
     permute_host(M, H.perm, inv, rp, ci, v);
     upload_csr(out, H.n, H.n, rp.data(), ci.data(), v.data(), H.ctx);
 }
