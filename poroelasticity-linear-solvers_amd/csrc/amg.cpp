@@ -430,7 +430,10 @@ HostCSR dense_inverse(const HostCSR &A) {
 // stay CSR and take the workgroup-per-row kernel.
 void amg_layout(DevCSR &M, Ctx &c) {
     M.rcm_auto = false;  // Galerkin operators: the RCM relabelling is for caller (FE) blocks
-    if (M.nrows > 0 && M.nnz < 128 * M.nrows) build_sell(M, c);
+    // short rows (interpolation P: ~7 per row) stay CSR, 8 lanes per row: in
+    // SELL-64 a slice's few entries per lane leave each wave one dependent
+    // round trip per slice (P e at N=59: 0.34-0.44 ms for 37M entries)
+    if (M.nrows > 0 && M.nnz < 128 * M.nrows && (double)M.nnz >= c.amg_csr_below * (double)M.nrows) build_sell(M, c);
 }
 
 }  // namespace amgh

@@ -1964,6 +1964,7 @@ std::unique_ptr<Ctx> layout_ctx(const Ctx &c) {
     self->spmv_rcm = c.spmv_rcm;
     self->sweep_chain = c.sweep_chain;
     self->sweep_window = c.sweep_window;
+    self->amg_csr_below = c.amg_csr_below;
     return self;
 }
 

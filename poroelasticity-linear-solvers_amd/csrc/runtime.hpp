@@ -82,6 +82,7 @@ struct Ctx {
                                   // -1 where the level DAG is deep and narrow, 0 never, 1 whenever rows fit
     int sweep_window = -1;        // ... in 64-row windows with inverted window triangles (k_ilu_blocks_window):
                                   // -1 where the chain sweep would be chosen, 0 never, 1 whenever rows fit
+    double amg_csr_below = 16.0;  // AMG operators with fewer entries per row than this stay CSR (pls.amg_csr_below)
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
