@@ -2177,8 +2177,28 @@ __device__ __forceinline__ void ring_chunk(Sw2Ctx &x, int64_t g) {
     const int64_t c0 = x.rin.cp[2 * x.ck], c1 = x.rin.cp[2 * x.ck + 1];
     for (int64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
         double v = x.rin.src[x.rin.src_idx[x.b0 + t]];
-        // far dependencies (older than the ring keeps, final before this chunk)
-        for (int64_t e = x.rin.frp[x.b0 + t]; e < x.rin.frp[x.b0 + t + 1]; ++e) v -= x.rin.fval[e] * x.ypos[x.rin.fcol[e]];
+        // far dependencies (older than the ring keeps, final before this chunk),
+        // eight at a time: their column / value loads, then their eight ypos
+        // gathers, are all in flight before the subtractions, which run in the
+        // stream's order (one entry at a time, every load waited for in turn,
+        // was ~2 global latencies per far entry -- most of the N=24 sweep's
+        // skeleton time)
+        const int64_t e0 = x.rin.frp[x.b0 + t], e1 = x.rin.frp[x.b0 + t + 1];
+        for (int64_t e = e0; e < e1; e += 8) {
+            int32_t fc[8];
+            double fv[8], yv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t k = e + u < e1 ? e + u : e0;
+                fc[u] = x.rin.fcol[k];
+                fv[u] = x.rin.fval[k];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) yv[u] = x.ypos[fc[u]];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (e + u < e1) v -= fv[u] * yv[u];
+        }
         x.ring[t & (RING_SLOTS - 1)] = v;
     }
     __syncthreads();
