@@ -527,7 +527,6 @@ struct Handle {
         ctx.sweep_chain = (int)opt.integer("pls.sweep_chain", -1);
         ctx.sweep_window = (int)opt.integer("pls.sweep_window", -1);
         ctx.amg_csr_below = opt.num("pls.amg_csr_below", 16.0);
-        ctx.d16_heavy_first = opt.flag("pls.d16_heavy_first", true);
         if (opt.flag("pls.debug_bounds", false) || opt.integer("pls.debug_partial_cap", 0) > 0)
             ctx.set_debug(opt.flag("pls.debug_bounds", false), opt.integer("pls.debug_partial_cap", 0),
                           opt.flag("pls.debug_no_grow", false), opt.flag("pls.debug_unguarded", false));

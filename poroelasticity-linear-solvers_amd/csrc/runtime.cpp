@@ -542,7 +542,6 @@ void build_sell(DevCSR &M, Ctx &c) {
             c.sync();
             M.sell = std::move(S);
             if (M.halo) classify_halo_slices(M, c);
-            else if (c.d16_heavy_first) order_heavy_slices(*M.sell, c);
             return;
         }
         if (b3) {  // the other rows do not fit D16: plain layouts for the whole matrix
@@ -568,23 +567,6 @@ void build_sell(DevCSR &M, Ctx &c) {
     HIPCHK(hipGetLastError());
     c.sync();
     M.sell = std::move(S);
-}
-
-void order_heavy_slices(DevSELL &S, Ctx &c) {
-    const int64_t ns = S.nslices;
-    if (ns < 1024) return;
-    std::vector<int64_t> sp(ns + 1);
-    HIPCHK(hipMemcpyAsync(sp.data(), S.sptr.p, sizeof(int64_t) * (ns + 1), hipMemcpyDeviceToHost, c.st));
-    c.sync();
-    const double mean = (double)(sp[ns] - sp[0]) / (double)ns;
-    std::vector<int32_t> heavy, light;
-    for (int64_t s = 0; s < ns; ++s) ((double)(sp[s + 1] - sp[s]) > 1.5 * mean ? heavy : light).push_back((int32_t)s);
-    if (heavy.empty() || light.empty()) return;
-    heavy.insert(heavy.end(), light.begin(), light.end());
-    S.s_order.alloc(ns);
-    HIPCHK(hipMemcpyAsync(S.s_order.p, heavy.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, c.st));
-    c.sync();
-    S.n_order = ns;
 }
 
 void classify_halo_slices(DevCSR &M, Ctx &c) {
@@ -667,7 +649,7 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
             launch_b3_spmv(S.b3_nslices, S.b3_ntrip, S.b3ptr.p, S.b3map.p, S.b3col.p, S.b3val.p, x, y, alpha, beta, z,
                            M.tag, c.st);
         launch_d16_spmv(M.nrows, S.nslices, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y, alpha,
-                        beta, z, M.tag, ghost, nlocal, c.d16_unroll, c.st, S.n_order ? S.s_order.p : nullptr,
+                        beta, z, M.tag, ghost, nlocal, c.d16_unroll, c.st, nullptr,
                         S.nrows_mapped ? S.rowmap.p : nullptr);
         return;
     }
@@ -1983,7 +1965,6 @@ std::unique_ptr<Ctx> layout_ctx(const Ctx &c) {
     self->sweep_chain = c.sweep_chain;
     self->sweep_window = c.sweep_window;
     self->amg_csr_below = c.amg_csr_below;
-    self->d16_heavy_first = c.d16_heavy_first;
     return self;
 }
 

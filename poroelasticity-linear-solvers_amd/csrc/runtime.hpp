@@ -83,7 +83,6 @@ struct Ctx {
     int sweep_window = -1;        // ... in 64-row windows with inverted window triangles (k_ilu_blocks_window):
                                   // -1 where the chain sweep would be chosen, 0 never, 1 whenever rows fit
     double amg_csr_below = 16.0;  // AMG operators with fewer entries per row than this stay CSR (pls.amg_csr_below)
-    bool d16_heavy_first = true;  // D16 products launch their heavy slices first (pls.d16_heavy_first)
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
@@ -143,11 +142,6 @@ struct DevSELL {
     // run while the halo exchange is in flight)
     DBuf<int32_t> s_in, s_halo;
     int64_t n_in = 0, n_halo = 0;
-    // single-rank products: heavy slices (> 1.5x the mean entries) first, the
-    // rest after, each group in its own order (a block's heavy rows at its end
-    // -- the fp block's pressure rows -- otherwise run as the launch's tail)
-    DBuf<int32_t> s_order;
-    int64_t n_order = 0;
     // RCM-relabelled columns (FE matrices, pls.spmv_rcm): the product reads
     // xp = x[xperm] (Ctx::rcm_x) so a slice's gathers stay local
     int64_t nperm = 0;
@@ -195,7 +189,6 @@ void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_
 // product overlaps the halo exchange with the interior slices).  build_sell
 // calls it for matrices with a halo.
 void classify_halo_slices(DevCSR &M, Ctx &c);
-void order_heavy_slices(DevSELL &S, Ctx &c);
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha = 1.0, double beta = 0.0,
           const double *z = nullptr);
 
