@@ -2184,6 +2184,11 @@ __device__ __forceinline__ void ring_chunk(Sw2Ctx &x, int64_t g) {
         // was ~2 global latencies per far entry -- most of the N=24 sweep's
         // skeleton time)
         const int64_t e0 = x.rin.frp[x.b0 + t], e1 = x.rin.frp[x.b0 + t + 1];
+        if (ring_probe & 64) {  // (diagnostics: the one-at-a-time loop, for A/B timing)
+            for (int64_t e = e0; e < e1; ++e) v -= x.rin.fval[e] * x.ypos[x.rin.fcol[e]];
+            x.ring[t & (RING_SLOTS - 1)] = v;
+            continue;
+        }
         for (int64_t e = e0; e < e1; e += 8) {
             int32_t fc[8];
             double fv[8], yv[8];
