@@ -1373,6 +1373,15 @@ static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, co
 
 PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int force_lpr, int gmem_mode,
              int ring_mode, bool sgs_factors, const std::vector<int64_t> *bounds) {
+    const bool trace = std::getenv("PLS_ILU_TRACE") != nullptr && M.nrows > 100000;
+    auto tnow = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double tm0 = tnow();
+    auto mark = [&](const char *what) {
+        if (!trace) return;
+        const double t = tnow();
+        fprintf(stderr, "[pcilu n %lld] %s %.3f s\n", (long long)M.nrows, what, t - tm0);
+        tm0 = t;
+    };
     exact = exact_lu;
     sgs = sgs_factors && !exact_lu;
     allow_lds = lds;
@@ -1420,9 +1429,11 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
     HIPCHK(hipMemcpyAsync(dg.data(), diag.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c.st));
     c.sync();
     // numeric factorization, level by level (global levels of the forward sweep)
+    mark("extract + download");
     std::vector<int32_t> ordL;
     std::vector<int64_t> Lptr;
     nlev_L = level_order(n, rp, ci, false, ordL, Lptr);
+    mark("level order");
     if (sgs) {
         launch_sgs_factor(n, F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p, fail.p, c.st);
         HIPCHK(hipGetLastError());
@@ -1455,10 +1466,13 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
     if (nblocks >= 64 || (fits_lds && allow_lds) || gmem) {
         std::vector<int32_t> oL, oU;
         std::vector<int64_t> gL, gU, fL, fU;
+        mark("factor");
         block_level_groups(n, nblocks, rp, ci, false, oL, gL, fL, bnd);
         block_level_groups(n, nblocks, rp, ci, true, oU, gU, fU, bnd);
+        mark("block level groups");
         build_tri_sell(*this, rp, dg, oL, gL, &fL, false, Lf, c);
         build_tri_sell(*this, rp, dg, oU, gU, &fU, true, Uf, c);
+        mark("tri sell");
         nlev_U = (int64_t)gU.size() - 1;
         use_lds = (allow_lds && fits_lds) || gmem;
         lds_gmem = gmem;
@@ -1479,6 +1493,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             const std::vector<double> none;
             const int64_t sL = build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oL, gL, fL, false, nullptr, c);
             const int64_t sU = sL < 0 ? -1 : build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oU, gU, fU, true, nullptr, c);
+            mark("chain plan");
             const int64_t lev = (int64_t)gL.size() - 1 + (int64_t)gU.size() - 1;
             const bool deep = sL >= 0 && sU >= 0 && 2 * (sL + sU) <= 7 * lev;
             chain = c.sweep_chain != 0 && sL >= 0 && sU >= 0 && (c.sweep_chain == 1 || deep);
@@ -1494,6 +1509,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                 c.sync();
                 build_window_tri(nblocks, bst, rp, ci, dg, fv, false, Lw, c);
                 build_window_tri(nblocks, bst, rp, ci, dg, fv, true, Uw, c);
+                mark("window triangles");
                 std::vector<int64_t> wf(nblocks + 1, 0);
                 for (int64_t b = 0; b < nblocks; ++b) wf[b + 1] = wf[b] + (bst[b + 1] - bst[b] + 63) / 64;
                 wstart.alloc(nblocks + 1);
