@@ -315,7 +315,7 @@ def hypre_semantics(opts, ranks):
     """Which BoomerAMG run the classical AMG behind -pc_type hypre restates
     (oracle/boomeramg.py; csrc/boomeramg.cpp) under these options."""
     chunks = int(opts.get("pls.hypre_relax_chunks", 256))
-    cch = int(opts.get("pls.hypre_coarsen_chunks", 0))
+    cch = int(opts.get("pls.hypre_coarsen_chunks", 1))
     crows = int(opts.get("pls.hypre_coarsen_min_rows", 65536))
     if opts.get("pls.hypre_ranks"):
         np_ = f"np = {opts['pls.hypre_ranks']} (pls.hypre_ranks)"

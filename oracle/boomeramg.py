@@ -500,8 +500,8 @@ def chunk_ids(n, K):
 def rank_sizes(spec, n):
     """Level-0 rank sizes of ``pls.hypre_ranks`` ("G": PETSc's split of n rows over
     G ranks, or "n0,n1,..."): BoomerAMG as it runs under mpirun -np G -- the
-    HMIS first pass inside every rank (the cross-rank PMIS stage is not
-    restated: boundary decisions are the ranks' own), a coarse level's rank
+    HMIS first pass inside every rank, then the PMIS stage over the ranks'
+    boundary points (``pmis_stage``), a coarse level's rank
     owns the C points of its rows, and each rank's rows are cut into its
     threads' chunks (pls.hypre_relax_chunks / G threads per rank).  None: one rank."""
     if spec is None or str(spec) == "":
@@ -590,9 +590,10 @@ class PCBoomerAMG:
             raise ValueError("grid_sweeps_all must be >= 1")
         self.chunks = int(db.get("pls.hypre_relax_chunks", 256))
         self.chunk_rows = int(db.get("pls.hypre_relax_min_rows", 1024))
-        # coarsening partition: 0 = up to pls.hypre_relax_chunks partitions of at least
-        # pls.hypre_coarsen_min_rows (65536) rows, 1 = none, K > 1 = K partitions
-        self.coarsen_chunks = int(db.get("pls.hypre_coarsen_chunks", 0))
+        # coarsening partition: 1 = none (default: BoomerAMG on one process, np = 1),
+        # K > 1 = K equal partitions, 0 = up to pls.hypre_relax_chunks partitions of at
+        # least pls.hypre_coarsen_min_rows (65536) rows (an opt-in speed-up of the setup)
+        self.coarsen_chunks = int(db.get("pls.hypre_coarsen_chunks", 1))
         self.coarsen_rows = int(db.get("pls.hypre_coarsen_min_rows", 65536))
         if self.chunks < 1 or self.chunk_rows < 0:
             raise ValueError("pls.hypre_relax_chunks must be >= 1, pls.hypre_relax_min_rows >= 0")

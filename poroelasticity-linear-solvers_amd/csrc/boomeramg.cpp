@@ -1191,7 +1191,7 @@ struct BParams {
     double theta = 0.25, mu = 0.9, rap_bytes = 16e9;
     int64_t pmax = 0, agg_nl = 0, max_levels = 25;
     int64_t chunks = 256, chunk_rows = 1024;  // hybrid Gauss-Seidel partition (pls.hypre_relax_*)
-    int64_t coarsen_chunks = 0, coarsen_rows = 65536;  // HMIS partitions (pls.hypre_coarsen_*): 0 = auto, 1 = none
+    int64_t coarsen_chunks = 1, coarsen_rows = 65536;  // HMIS partitions (pls.hypre_coarsen_*): 1 = none (np = 1, default), 0 = auto
     int paths = 1, K = 1;
     bool no_cf = false;
     std::string ranks;  // pls.hypre_ranks: the level-0 rank partition ("G" or "n0,n1,..."), hypre under mpirun -np G
@@ -1241,7 +1241,7 @@ BParams parse_params(const Options &o, const std::string &prefix) {
     p.rap_bytes = o.num("pls.amg_rap_dense_gb", 16.0) * 1e9;
     p.chunks = o.integer("pls.hypre_relax_chunks", 256);
     p.chunk_rows = o.integer("pls.hypre_relax_min_rows", 1024);
-    p.coarsen_chunks = o.integer("pls.hypre_coarsen_chunks", 0);
+    p.coarsen_chunks = o.integer("pls.hypre_coarsen_chunks", 1);
     p.coarsen_rows = o.integer("pls.hypre_coarsen_min_rows", 65536);
     p.ranks = o.str("pls.hypre_ranks", "");
     if (p.chunks < 1 || p.chunk_rows < 0)

@@ -481,9 +481,22 @@ struct Handle {
     std::unique_ptr<Ctx> ctx2;            // second stream: the DIFF sweep runs beside the FS sweep
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
     bool concurrent_3way = false;
+    // 2-way pressure-first pipeline (pls.fp_pipeline): the fp block's heavy
+    // BJACOBI blocks (the pressure rows: ~5x the levels of the fluid blocks)
+    // get their t = x_fp - P_fp,s y_s rows first and sweep on the second
+    // stream while the fluid rows' product runs (same sums, same blocks)
+    struct {
+        bool on = false;
+        int64_t b_split = 0, nb = 0, r_split = 0, n_hi = 0, n_lo = 0;
+        int rr = 0;  // the heavy blocks' sweep: round robin over groups of rr waves (0: every wave per level)
+        DBuf<int32_t> sl_hi, sl_lo;  // Mfp_s slices holding rows >= r_split / the rest
+        hipEvent_t ev_t = nullptr, ev_p = nullptr;
+    } fpp;
     ~Handle() {
         if (ev_in) (void)hipEventDestroy(ev_in);
         if (ev_out) (void)hipEventDestroy(ev_out);
+        if (fpp.ev_t) (void)hipEventDestroy(fpp.ev_t);
+        if (fpp.ev_p) (void)hipEventDestroy(fpp.ev_p);
     }
     // result
     pls_result res{};
@@ -526,6 +539,7 @@ struct Handle {
         ctx.spmv_rcm = (int)opt.integer("pls.spmv_rcm", -1);
         ctx.sweep_chain = (int)opt.integer("pls.sweep_chain", -1);
         ctx.sweep_window = (int)opt.integer("pls.sweep_window", -1);
+        ctx.ilu_view = (int)opt.integer("pls.ilu_view", 0);
         ctx.amg_csr_below = opt.num("pls.amg_csr_below", 16.0);
         if (opt.flag("pls.debug_bounds", false) || opt.integer("pls.debug_partial_cap", 0) > 0)
             ctx.set_debug(opt.flag("pls.debug_bounds", false), opt.integer("pls.debug_partial_cap", 0),
@@ -546,9 +560,26 @@ void BlockPC::apply(const double *x, double *y, Ctx &c) {
         H.ksp_s->solve(x, y, c);
         T.end(T_PC_SOLID);
         T.begin(T_PC_FLUID);
-        // t = x_fp - P_fp,s y_s   (Preconditioner.py:232-233, fused)
-        spmv(H.Mfp_s, y, H.t_fp.p, c, -1.0, 1.0, x + ns);
-        H.ksp_fp->solve(H.t_fp.p, y + ns, c);
+        if (H.fpp.on) {
+            // the heavy blocks' rows of t first, their sweep on the second stream
+            // while the other rows' product and sweep run here (a PREONLY solve)
+            auto &F = H.fpp;
+            Ctx &c2 = *H.ctx2;
+            PCILU *pc = static_cast<PCILU *>(H.ksp_fp->pc);
+            spmv_slices(H.Mfp_s, y, H.t_fp.p, c, -1.0, 1.0, x + ns, F.sl_hi.p, F.n_hi);
+            HIPCHK(hipEventRecord(F.ev_t, c.st));
+            HIPCHK(hipStreamWaitEvent(c2.st, F.ev_t, 0));
+            pc->apply_blocks(H.t_fp.p, y + ns, c2, F.b_split, F.nb, F.rr);
+            HIPCHK(hipEventRecord(F.ev_p, c2.st));
+            spmv_slices(H.Mfp_s, y, H.t_fp.p, c, -1.0, 1.0, x + ns, F.sl_lo.p, F.n_lo);
+            pc->apply_blocks(H.t_fp.p, y + ns, c, 0, F.b_split);
+            HIPCHK(hipStreamWaitEvent(c.st, F.ev_p, 0));
+            H.ksp_fp->note_preonly();
+        } else {
+            // t = x_fp - P_fp,s y_s   (Preconditioner.py:232-233, fused)
+            spmv(H.Mfp_s, y, H.t_fp.p, c, -1.0, 1.0, x + ns);
+            H.ksp_fp->solve(H.t_fp.p, y + ns, c);
+        }
         T.end(T_PC_FLUID);
     } else {
         const double *xs = x, *xf = x + ns, *xp = x + ns + nf;
@@ -658,6 +689,75 @@ static void upload_permuted(const pls_csr *M, Handle &H, const std::vector<int64
     upload_csr(out, H.n, H.n, rp.data(), ci.data(), v.data(), H.ctx);
 }
 
+// The 2-way PC's fp solve with PREONLY + BJACOBI(ILU(0)) on the LDS sweep:
+// when the last blocks (the pressure rows of the field-major fp block) carry
+// well over the median block's levels, their rows of t = x_fp - P_fp,s y_s are
+// computed first and swept on a second stream beside the rest of the product
+// (the headline N=59: 11 pressure blocks of 263 levels per triangle, ~500 us,
+// against 56 for the fluid blocks).  Results are bitwise those of the plain
+// path: the same per-row sums and per-block sweeps.  pls.fp_pipeline 0 turns
+// it off.
+static void setup_fp_pipeline(Handle &H) {
+    auto &F = H.fpp;
+    F.on = false;
+    if (H.three_way || H.distributed || !H.opt.flag("pls.fp_pipeline", true)) return;
+    if (!H.ksp_fp || H.ksp_fp->type != "preonly" || H.mixer.order > 0) return;
+    PCILU *pc = dynamic_cast<PCILU *>(H.ksp_fp->pc);
+    if (!pc || !pc->can_apply_blocks() || pc->nblocks < 8 || pc->block_levels_h.size() != (size_t)pc->nblocks) return;
+    const DevCSR &M = H.Mfp_s;
+    if (!M.sell || !M.sell->d16 || M.halo || M.sell->nperm || M.sell->b3_nslices || M.sell->nrows_mapped) return;
+    const int64_t nb = pc->nblocks;
+    std::vector<int64_t> lev(pc->block_levels_h);
+    std::vector<int64_t> srt(lev);
+    std::nth_element(srt.begin(), srt.begin() + nb / 2, srt.end());
+    const int64_t med = srt[nb / 2];
+    int64_t b = nb;
+    while (b > 0 && lev[b - 1] >= 2 * med) --b;
+    if (b == nb || nb - b > nb / 8 || b == 0) return;  // no heavy tail, or too much of the block
+    const DevSELL &S = *M.sell;
+    std::vector<int64_t> sf(S.nslices + 1);
+    HIPCHK(hipMemcpyAsync(sf.data(), S.sfirst.p, sizeof(int64_t) * sf.size(), hipMemcpyDeviceToHost, H.ctx.st));
+    H.ctx.sync();
+    const int64_t r_split = pc->block_start_h[b];
+    std::vector<int32_t> hi, lo;
+    for (int64_t s = 0; s < S.nslices; ++s) (sf[s + 1] > r_split ? hi : lo).push_back((int32_t)s);
+    F.sl_hi.alloc(std::max<size_t>(hi.size(), 1));
+    F.sl_lo.alloc(std::max<size_t>(lo.size(), 1));
+    if (!hi.empty())
+        HIPCHK(hipMemcpyAsync(F.sl_hi.p, hi.data(), sizeof(int32_t) * hi.size(), hipMemcpyHostToDevice, H.ctx.st));
+    if (!lo.empty())
+        HIPCHK(hipMemcpyAsync(F.sl_lo.p, lo.data(), sizeof(int32_t) * lo.size(), hipMemcpyHostToDevice, H.ctx.st));
+    H.ctx.sync();
+    if (!H.ctx2) H.ctx2 = std::make_unique<Ctx>();
+    if (!F.ev_t) HIPCHK(hipEventCreateWithFlags(&F.ev_t, hipEventDisableTiming));
+    if (!F.ev_p) HIPCHK(hipEventCreateWithFlags(&F.ev_p, hipEventDisableTiming));
+    // the heavy blocks' levels hold a few slices each: waves in groups of the
+    // next power of two >= the most slices of any of their levels own the
+    // levels round robin, so factor data is requested (waves / group) levels
+    // ahead -- under the concurrent product's HBM traffic the two-level
+    // pipeline of the plain sweep exposed the load latency (measured: the 11
+    // pressure blocks took 1.24 ms beside the product, ~0.5 ms alone)
+    int64_t msl = 0;
+    for (int64_t k = b; k < nb; ++k) msl = std::max(msl, pc->block_maxsl_h.empty() ? 16 : pc->block_maxsl_h[k]);
+    int grp = 1;
+    while (grp < msl) grp *= 2;
+    const int64_t rr_opt = H.opt.integer("pls.fp_pipeline_rr", -1);  // -1 auto, 0 off, a group size forced
+    if (rr_opt > 16 || (rr_opt > 0 && (rr_opt & (rr_opt - 1))))
+        throw Error("pls.fp_pipeline_rr must be -1 (auto), 0 or a power of two <= 16");
+    F.rr = rr_opt >= 0 ? (int)rr_opt : (grp <= 4 && pc->lds_tpb == 1024 ? grp : 0);
+    F.b_split = b;
+    F.nb = nb;
+    F.r_split = r_split;
+    F.n_hi = (int64_t)hi.size();
+    F.n_lo = (int64_t)lo.size();
+    F.on = true;
+    if (H.ctx.ilu_view)
+        fprintf(stderr, "[pls fp pipeline] blocks [%lld, %lld) first (levels >= %lld, median %lld), rows from %lld, "
+                "slices %lld + %lld, round-robin groups %d (most slices per level %lld)\n", (long long)b, (long long)nb,
+                (long long)(2 * med), (long long)med, (long long)r_split, (long long)F.n_hi, (long long)F.n_lo, F.rr,
+                (long long)msl);
+}
+
 static void alloc_work(Handle &H) {
     H.t_fp.alloc(std::max<int64_t>(H.nf + H.np, 1));
     H.t_s.alloc(std::max<int64_t>(H.ns, 1));
@@ -689,6 +789,7 @@ static void alloc_work(Handle &H) {
             H.concurrent_3way = true;
         }
     }
+    setup_fp_pipeline(H);
 }
 
 static void do_setup(Handle &H) {

@@ -2290,10 +2290,14 @@ __device__ __forceinline__ void sweep2(Sw2Ctx &x, int64_t g0) {
 // computing the current one, so its data has nw levels' time to arrive.  A
 // level's extra slices (rare) run inline.  Per-row sums are sweep2's (same
 // entries, same order): results are bitwise those of sweep2.
+// S > 1 (levels of a few slices: the pressure blocks of the headline's fp
+// block, ~2 slices per level): groups of S waves own the levels round robin,
+// wave k of a group the level's slice k, so data has nw / S levels to arrive.
 template <int P, int LPR, bool W>
-__device__ __forceinline__ void sweep_rr(Sw2Ctx &x, int64_t g0) {
+__device__ __forceinline__ void sweep_rr(Sw2Ctx &x, int64_t g0, int S = 1) {
     const int64_t g1 = x.g1;
-    const int nw = x.nw, w = x.wave;
+    const int ng = x.nw / S, w = x.wave / S, ks = x.wave % S;  // level groups; this wave's group / slice
+    const int nw = ng;
     const int64_t nown = g1 - g0 > w ? (g1 - g0 - w + nw - 1) / nw : 0;  // own levels of this wave
     int64_t jb = 0, ms0 = 0, ms1 = 0, mb = -1, me = -1;  // lane l: own level jb + l (first slice, end, entry range)
     auto refill = [&](int64_t j0) {
@@ -2302,8 +2306,8 @@ __device__ __forceinline__ void sweep_rr(Sw2Ctx &x, int64_t g0) {
         if (j0 + x.lane < nown) {
             ms0 = x.gslice[g];
             ms1 = x.gslice[g + 1];
-            mb = ms1 > ms0 ? x.sptr[ms0] : -1;
-            me = ms1 > ms0 ? x.sptr[ms0 + 1] : -1;
+            mb = ms1 > ms0 + ks ? x.sptr[ms0 + ks] : -1;
+            me = ms1 > ms0 + ks ? x.sptr[ms0 + ks + 1] : -1;
         } else {
             ms0 = ms1 = 0;
             mb = me = -1;
@@ -2354,7 +2358,7 @@ __device__ __forceinline__ void sweep_rr(Sw2Ctx &x, int64_t g0) {
         sw2_finish<LPR, W, false>(x, h, cur.v[0], acc);
         const int l = (int)(j - jb);
         const int64_t s0 = readlane64(ms0, l), s1 = readlane64(ms1, l);
-        for (int64_t sl = s0 + 1; sl < s1; ++sl) sw2_slice_inline<LPR, W, false>(x, sl);
+        for (int64_t sl = s0 + ks + S; sl < s1; sl += S) sw2_slice_inline<LPR, W, false>(x, sl);
     };
     Sw2Slot<P> A, B;
     refill(0);
@@ -2386,21 +2390,22 @@ __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int
                                             const int32_t *__restrict__ col, const double *__restrict__ val,
                                             double *ys, double *ring = nullptr, double *ypos = nullptr,
                                             int64_t b0 = 0, int64_t ck0 = 0, int64_t ck1 = 0, RingIn rin = {},
-                                            bool rr = false) {
+                                            int rr = 0) {
     if (g0 >= g1) return;
     Sw2Ctx x{gslice, sptr, col, val, ys, g1, 0, 0, 0, 0, lane, wave, nw, upper,
              ring, ypos, 0, ck0, ck1, ck0 < ck1 ? rin.cg[ck0] : INT64_MAX, b0, ck0, rin};
-    if (!R && rr) {  // deep, narrow levels: round-robin over the waves
+    if (!R && rr) {  // deep, narrow levels: round-robin over groups of rr waves (a power of two <= nw)
+        const int S = rr <= nw ? rr : nw;
         if (W) {
-            if (lpr == 16) sweep_rr<P, 16, W>(x, g0);
-            else if (lpr == 8) sweep_rr<P, 8, W>(x, g0);
-            else if (lpr == 4) sweep_rr<P, 4, W>(x, g0);
-            else if (lpr == 2) sweep_rr<P, 2, W>(x, g0);
-            else sweep_rr<P, 1, W>(x, g0);
+            if (lpr == 16) sweep_rr<P, 16, W>(x, g0, S);
+            else if (lpr == 8) sweep_rr<P, 8, W>(x, g0, S);
+            else if (lpr == 4) sweep_rr<P, 4, W>(x, g0, S);
+            else if (lpr == 2) sweep_rr<P, 2, W>(x, g0, S);
+            else sweep_rr<P, 1, W>(x, g0, S);
         } else {
-            if (lpr == 4) sweep_rr<P, 4, W>(x, g0);
-            else if (lpr == 2) sweep_rr<P, 2, W>(x, g0);
-            else sweep_rr<P, 1, W>(x, g0);
+            if (lpr == 4) sweep_rr<P, 4, W>(x, g0, S);
+            else if (lpr == 2) sweep_rr<P, 2, W>(x, g0, S);
+            else sweep_rr<P, 1, W>(x, g0, S);
         }
         return;
     }
@@ -2446,9 +2451,10 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
                                                          const double *__restrict__ Uval,
                                                          const int32_t *__restrict__ Ulpr, const double *x,
                                                          double *y, int64_t *__restrict__ prof, int rr,
-                                                         const int64_t *__restrict__ bstart) {
+                                                         const int64_t *__restrict__ bstart, int64_t blk_hi) {
     extern __shared__ __attribute__((aligned(16))) double lds_y[];
-    const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
+    // blocks [blk_hi - gridDim.x, blk_hi), the last (heaviest) first
+    const int64_t blk = blk_hi - 1 - (int64_t)blockIdx.x;
     int64_t b0, len;
     block_range(blk, n, nblocks, bstart, b0, len);
     double *ys = GMEM ? y + b0 : lds_y;
@@ -2461,10 +2467,10 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
         for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
     __syncthreads();
     sweep_block<SW_P, GMEM>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol, Lval, ys,
-                            nullptr, nullptr, 0, 0, 0, {}, rr != 0);
+                            nullptr, nullptr, 0, 0, 0, {}, rr);
     if (prof) t1 = wall_clock64();
     sweep_block<SW_P, GMEM>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol, Uval, ys,
-                            nullptr, nullptr, 0, 0, 0, {}, rr != 0);
+                            nullptr, nullptr, 0, 0, 0, {}, rr);
     if (!GMEM)
         for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
     if (prof && threadIdx.x == 0) {  // diagnostics (option pls.sweep_profile): 100 MHz wall clock
@@ -2551,9 +2557,17 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const int64_t *Lsptr, const int32_t *Lcol, const double *Lval, const int32_t *Llpr,
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
-                           int64_t *prof, bool gmem, int tpb, int rr, const int64_t *bstart, int64_t max_len) {
+                           int64_t *prof, bool gmem, int tpb, int rr, const int64_t *bstart, int64_t max_len,
+                           int64_t blk_lo, int64_t blk_hi) {
     // tpb: threads per workgroup, 64 .. 1024 (narrow levels: fewer waves, cheaper barriers)
     if (tpb < 64 || tpb > 1024 || (tpb & 63)) tpb = 1024;
+    // block subset [blk_lo, blk_hi) (blk_hi < 0: every block)
+    if (blk_hi < 0) {
+        blk_lo = 0;
+        blk_hi = nblocks;
+    }
+    if (blk_lo < 0 || blk_hi > nblocks || blk_lo >= blk_hi) return;
+    const unsigned grid = (unsigned)(blk_hi - blk_lo);
     static bool configured = false;
     if (!configured) {
         (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2561,14 +2575,13 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
         configured = true;
     }
     if (gmem) {
-        k_ilu_blocks_lds<true><<<(unsigned)nblocks, tpb, 0, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
-                                                                  Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof, rr, bstart);
+        k_ilu_blocks_lds<true><<<grid, tpb, 0, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr, Ugoff, Ugslice,
+                                                     Usptr, Ucol, Uval, Ulpr, x, y, prof, rr, bstart, blk_hi);
         return;
     }
     const size_t bytes = (size_t)(max_len > 0 ? max_len : n / nblocks + 1) * 8;
-    k_ilu_blocks_lds<false><<<(unsigned)nblocks, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval,
-                                                                     Llpr, Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y,
-                                                                     prof, rr, bstart);
+    k_ilu_blocks_lds<false><<<grid, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr, Ugoff,
+                                                        Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof, rr, bstart, blk_hi);
 }
 
 // ======================================================= chain sweep ====
@@ -2786,12 +2799,20 @@ static constexpr int WIN_KP = WIN_NW * WIN_KPW;  // stream entries per row (ever
 
 // a block's window stream offsets, 64 per vector register (lane l: window j * 64 + l),
 // picked with v_readlane: no scalar load (and its latency) per window
+// (WIN_OFFR registers hold 64 * WIN_OFFR offsets: every window of a block up to
+// ilu_window_max_rows() rows plus the end offset -- 316 for 20,160 rows)
+static constexpr int WIN_OFFR = 5;
 struct WinOff {
-    int64_t r[3];
-    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: three readlanes, a scalar select
+    int64_t r[WIN_OFFR];
+    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: WIN_OFFR readlanes, scalar selects
         const int j = (int)(w >> 6), l = (int)(w & 63);
-        const int64_t a = readlane64(r[0], l), b = readlane64(r[1], l), c = readlane64(r[2], l);
-        return j == 0 ? a : (j == 1 ? b : c);
+        int64_t v = readlane64(r[0], l);
+#pragma unroll
+        for (int k = 1; k < WIN_OFFR; ++k) {
+            const int64_t t = readlane64(r[k], l);
+            v = j == k ? t : v;
+        }
+        return v;
     }
 };
 
@@ -2846,7 +2867,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     if (nw == 0) return;
     WinOff wo;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
+    for (int j = 0; j < WIN_OFFR; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the offsets (ordinary loads) before the counted ones
     auto wi = [&](int64_t ww) { return UP ? nw - 1 - ww : ww; };
     // T^-1[k][lane] is zero above (L) / below (U) the diagonal: those lanes read out of range
@@ -2944,6 +2965,7 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
 }
 
 int ilu_window_max_rows() { return 163840 / 8 - 256 - 64; }  // LDS: partial sums, the block, a dummy slot per lane
+static_assert((163840 / 8 - 256 - 64 + 63) / 64 + 1 <= 64 * WIN_OFFR, "window offsets exceed WinOff's registers");
 int ilu_window_stream_pad() { return 0; }
 int ilu_window_max_entries() { return WIN_KP; }
 

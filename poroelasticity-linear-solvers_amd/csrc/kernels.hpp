@@ -194,7 +194,8 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
                            int64_t *prof = nullptr, bool gmem = false, int tpb = 1024, int rr = 0,
-                           const int64_t *bstart = nullptr, int64_t max_len = 0);
+                           const int64_t *bstart = nullptr, int64_t max_len = 0, int64_t blk_lo = 0,
+                           int64_t blk_hi = -1);  // blocks [blk_lo, blk_hi) only (blk_hi < 0: all)
 int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in registers
 // The chain sweep (kernels.hip, k_ilu_blocks_chain): one wave per LDS-resident
 // block walks its slices in order with ilu_chain_depth() slices in flight

@@ -661,6 +661,17 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
     launch_spmv(M.nrows, M.nnz, M.rp.p, M.ci.p, M.val.p, x, y, alpha, beta, z, c.st);
 }
 
+// the slices slist[0 .. count) of a D16 layout (rows of those slices only; the
+// per-row sums are spmv()'s): the 2-way PC's pressure-first pipeline
+void spmv_slices(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z,
+                 const int32_t *slist, int64_t count) {
+    if (!M.sell || !M.sell->d16 || M.halo || M.sell->nperm || M.sell->b3_nslices || M.sell->nrows_mapped)
+        throw Error("spmv_slices: plain D16 layouts only");
+    const DevSELL &S = *M.sell;
+    launch_d16_spmv(M.nrows, count, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y, alpha, beta,
+                    z, M.tag, nullptr, M.ncols, c.d16_unroll, c.st, slist, nullptr);
+}
+
 // ============================================================== options ===
 void Options::parse(const char *text) {
     if (!text) return;
@@ -937,7 +948,8 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
                           const std::vector<int64_t> &dg, const std::vector<int32_t> &order,
                           const std::vector<int64_t> &grp, const std::vector<int64_t> &goff, bool upper, LdsTri &D,
                           Ctx &c, const std::vector<int32_t> *posof = nullptr,
-                          const std::vector<int32_t> *row_lo = nullptr, const std::vector<int32_t> *near_len = nullptr) {
+                          const std::vector<int32_t> *row_lo = nullptr, const std::vector<int32_t> *near_len = nullptr,
+                          std::vector<int64_t> *blk_maxsl = nullptr) {
     const int64_t ng = (int64_t)grp.size() - 1, nblk = (int64_t)goff.size() - 1;
     const int W = ilu_lds_lane_entries();
     auto rlen = [&](int64_t i) -> int64_t {
@@ -1014,6 +1026,32 @@ static void build_lds_tri(const PCILU &P, int64_t n, int64_t nb, int force_lpr, 
     }
     gsl[ng] = (int64_t)s_start.size();
     const int64_t ns = (int64_t)s_start.size();
+    if (blk_maxsl) {  // per block: the most slices any level has (max over both triangles)
+        blk_maxsl->resize(nblk, 0);
+        for (int64_t b = 0; b < nblk; ++b)
+            for (int64_t g = goff[b]; g < goff[b + 1]; ++g) (*blk_maxsl)[b] = std::max((*blk_maxsl)[b], gsl[g + 1] - gsl[g]);
+    }
+    if (c.ilu_view >= 2 && !posof) {
+        // per block: levels, slices beyond the 16 waves (run inline with dependent
+        // loads), slices whose lanes hold more than the W prefetched entries
+        int64_t worst_inline = 0, worst_lev = 0, worst_long = 0, wmax = 0, b_inl = 0;
+        for (int64_t b = 0; b < nblk; ++b) {
+            int64_t inl = 0, lng = 0;
+            for (int64_t g = goff[b]; g < goff[b + 1]; ++g) {
+                const int64_t s = gsl[g + 1] - gsl[g];
+                wmax = std::max(wmax, s);
+                inl += std::max<int64_t>(0, s - 16);
+                for (int64_t k = gsl[g]; k < gsl[g + 1]; ++k) lng += (sptr[k + 1] - sptr[k]) / 64 - 1 > W;
+            }
+            if (inl > worst_inline) { worst_inline = inl; b_inl = b; }
+            worst_lev = std::max(worst_lev, goff[b + 1] - goff[b]);
+            worst_long = std::max(worst_long, lng);
+        }
+        fprintf(stderr, "[pls ilu lds %s] blocks %lld: max levels %lld, max slices per level %lld, inline slices "
+                "(beyond 16 waves) max %lld (block %lld), slices with > %d entries per lane max %lld\n",
+                upper ? "U" : "L", (long long)nblk, (long long)worst_lev, (long long)wmax, (long long)worst_inline,
+                (long long)b_inl, W, (long long)worst_long);
+    }
     auto up = [&](auto &d, const auto &v) {
         d.alloc(std::max<size_t>(v.size(), 1));
         if (!v.empty())
@@ -1470,6 +1508,9 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         block_level_groups(n, nblocks, rp, ci, false, oL, gL, fL, bnd);
         block_level_groups(n, nblocks, rp, ci, true, oU, gU, fU, bnd);
         mark("block level groups");
+        block_levels_h.resize(nblocks);
+        for (int64_t b = 0; b < nblocks; ++b) block_levels_h[b] = (fL[b + 1] - fL[b]) + (fU[b + 1] - fU[b]);
+        block_start_h = block_starts(n, nblocks, bnd);
         build_tri_sell(*this, rp, dg, oL, gL, &fL, false, Lf, c);
         build_tri_sell(*this, rp, dg, oU, gU, &fU, true, Uf, c);
         mark("tri sell");
@@ -1558,9 +1599,9 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                 c.sync();
             }
             build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oL, gL, fL, false, Ls, c, ring ? &pL : nullptr,
-                          ring ? &loL : nullptr, ring ? &nlL : nullptr);
+                          ring ? &loL : nullptr, ring ? &nlL : nullptr, &block_maxsl_h);
             build_lds_tri(*this, n, nblocks, force_lpr, max_lpr, rp, dg, oU, gU, fU, true, Us, c, ring ? &pU : nullptr,
-                          ring ? &loU : nullptr, ring ? &nlU : nullptr);
+                          ring ? &loU : nullptr, ring ? &nlU : nullptr, &block_maxsl_h);
             // threads per workgroup: as few waves as the widest level's slices need
             // (narrow, deep levels -- FE rows in their natural order, nearly one
             // level per row -- pay a workgroup barrier per level: 16 waves cost
@@ -1600,6 +1641,26 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             build_tri_sell(*this, rp, dg, ordU, Uptr, nullptr, true, Uf, c);
         }
     }
+    if (c.ilu_view)
+        fprintf(stderr, "[pls ilu] type %s n %lld blocks %lld max_len %lld levels %lld/%lld sweep %s\n", type.c_str(),
+                (long long)n, (long long)nblocks, (long long)max_len, (long long)nlev_L, (long long)nlev_U,
+                sweep_kind());
+}
+
+void PCILU::apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64_t b_hi, int rr_group) {
+    if (!can_apply_blocks()) throw Error("PCILU: block subsets need the LDS sweep");
+    const int rr = rr_group > 0 ? rr_group : (lds_rr ? 1 : 0);
+    launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
+                          Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, nullptr, false, lds_tpb, rr,
+                          bstart_h.empty() ? nullptr : bstart.p, max_len, b_lo, b_hi);
+}
+
+const char *PCILU::sweep_kind() const {
+    if (!use_lds) return csr_levels ? "levels-csr" : "levels";
+    if (ring) return "ring";
+    if (window) return "window";
+    if (chain) return "chain";
+    return lds_gmem ? "gmem" : "lds";
 }
 
 void PCILU::apply(const double *x, double *y, Ctx &c) {

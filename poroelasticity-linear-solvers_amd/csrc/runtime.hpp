@@ -82,6 +82,7 @@ struct Ctx {
                                   // -1 where the level DAG is deep and narrow, 0 never, 1 whenever rows fit
     int sweep_window = -1;        // ... in 64-row windows with inverted window triangles (k_ilu_blocks_window):
                                   // -1 where the chain sweep would be chosen, 0 never, 1 whenever rows fit
+    int ilu_view = 0;             // print every ILU / Gauss-Seidel PC's sweep choice to stderr (pls.ilu_view)
     double amg_csr_below = 16.0;  // AMG operators with fewer entries per row than this stay CSR (pls.amg_csr_below)
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
@@ -191,6 +192,8 @@ void extract_csr(const DevCSR &src, int64_t r0, int64_t r1, WindowSpec w, int64_
 void classify_halo_slices(DevCSR &M, Ctx &c);
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha = 1.0, double beta = 0.0,
           const double *z = nullptr);
+void spmv_slices(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z,
+                 const int32_t *slist, int64_t count);
 
 // Host copy of a CSR matrix (setup-time algebra: fieldsplit blocks, AMG hierarchy).
 // std::allocator whose value-initialisation is default-initialisation: a
@@ -406,6 +409,16 @@ struct PCILU : PC {
           int gmem_mode = 0, int ring_mode = 1, bool sgs_factors = false, const std::vector<int64_t> *bounds = nullptr);
     bool reentrant() const override { return profile_tag.empty(); }
     void apply(const double *x, double *y, Ctx &c) override;
+    const char *sweep_kind() const;  // which apply kernel serves this PC (pls.ilu_view)
+    // the plain LDS sweep can run a subset of its blocks (the 2-way PC's
+    // pressure-first pipeline, capi.cpp BlockPC::apply): levels (L + U) and
+    // first row of every block, host copies made at setup
+    std::vector<int64_t> block_levels_h, block_start_h, block_maxsl_h;  // maxsl: most slices of any level
+    bool can_apply_blocks() const {
+        return use_lds && !ring && !window && !chain && !lds_gmem && profile_tag.empty() && !exact && !sgs;
+    }
+    // rr_group > 0: the round-robin sweep with groups of that many waves per level (a power of two)
+    void apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64_t b_hi, int rr_group = 0);
 };
 // Exact LU of a block small enough for a dense inverse (dense.hip): K^-1 is
 // formed once (blocked Gauss-Jordan, no pivoting, like the sparse path) and
@@ -494,6 +507,15 @@ struct KSP {
     void set_type_defaults();
     void resolve_side_norm(const std::string &side, const std::string &nt);
     void solve(const double *b, double *x, Ctx &c);
+    // a PREONLY solve whose PC was applied by the caller (BlockPC's fp pipeline): its bookkeeping
+    void note_preonly() {
+        history.clear();
+        its = 1;
+        reason = CONVERGED_ITS;
+        stat_its += 1;
+        stat_max = std::max<int64_t>(stat_max, 1);
+        ++stat_solves;
+    }
   private:
     void ensure_work(Ctx &c);
     void solve_gmres(const double *b, double *x, Ctx &c);

@@ -176,3 +176,6 @@ def test_bench_records_hypre_semantics():
     assert "np = 3" in bench.hypre_semantics({"pls.hypre_ranks": "3"}, 1)["processes"]
     assert "np = 8 (the sharded" in bench.hypre_semantics({}, 8)["processes"]
     assert bench.hypre_semantics({"pls.hypre_coarsen_chunks": "1"}, 1)["processes"] == "np = 1"
+    # default on one rank: BoomerAMG's np = 1 run (no automatic coarsening partitions)
+    assert bench.hypre_semantics({"s_pc_type": "hypre"}, 1)["processes"] == "np = 1"
+    assert "the most partitions" in bench.hypre_semantics({"pls.hypre_coarsen_chunks": "0"}, 1)["processes"]

@@ -177,7 +177,8 @@ def _blocks():
 
 
 @pytest.mark.parametrize("db", [{}, INEXACT, dict(INEXACT, **{"pls.hypre_coarsen_chunks": "7"}),
-                                dict(INEXACT, **{"pls.hypre_relax_min_rows": "64", "pls.hypre_coarsen_min_rows": "200"})],
+                                dict(INEXACT, **{"pls.hypre_relax_min_rows": "64", "pls.hypre_coarsen_min_rows": "200",
+                                                 "pls.hypre_coarsen_chunks": "0"})],
                          ids=["defaults", "inexact", "inexact-7-partitions", "inexact-chunked"])
 def test_libpls_host_setup_bitwise(db):
     from lib.handle import boomeramg_host_level
