@@ -189,6 +189,13 @@ int pls_get_result(pls_handle *h, pls_result *res);
 int pls_get_history(pls_handle *h, double *hist, int32_t cap);
 int pls_get_timings(pls_handle *h, pls_timings *t);
 int pls_reset_timings(pls_handle *h);
+/* Totals of one inner (or the outer) KSP since the handle's setup, by options
+ * prefix ("s_", "f_", "p_", "diff_", "fp_", "fp_fieldsplit_0_", ..., "global_"):
+ * stats[0] solves, [1] iterations, [2] most iterations of one solve, [3] solves
+ * that ended with a negative KSPConvergedReason (PETSc's -ksp_converged_reason
+ * per solve, summed; the reference's own output is the outer count only,
+ * lib/AbstractPhysics.py:77-78).                                              */
+int pls_get_ksp_stats(pls_handle *h, const char *prefix, int64_t stats[4]);
 
 /* Export a device matrix of the handle to host CSR (tests / parity):
  * which: 0 = A, 1 = P, 2 = P_diff (field-major order).  Call once with

@@ -489,6 +489,17 @@ struct Handle {
         bool on = false;
         int64_t b_split = 0, nb = 0, r_split = 0, n_hi = 0, n_lo = 0;
         int rr = 0;  // the heavy blocks' sweep: round robin over groups of rr waves (0: every wave per level)
+        size_t lds = 0;  // LDS the concurrent product's workgroups reserve (pls.fp_pipeline_lds)
+        int tpb = 0, depth = 2;  // the heavy blocks' sweep: threads per workgroup, levels in flight
+        bool profiled = false;
+        // CU-masked streams (pls.fp_pipeline_cus R > 0): the heavy sweep on R
+        // reserved CUs, the concurrent product on the others -- with every CU
+        // open to both, the product's workgroups (dispatched first) kept the
+        // sweep's from starting until the product drained (measured: the 11
+        // sweep workgroups all started ~0.75 ms late)
+        std::unique_ptr<Ctx> c_p, c_lo;
+        hipEvent_t ev_lo = nullptr;
+        int cus = 0;
         DBuf<int32_t> sl_hi, sl_lo;  // Mfp_s slices holding rows >= r_split / the rest
         hipEvent_t ev_t = nullptr, ev_p = nullptr;
     } fpp;
@@ -497,6 +508,7 @@ struct Handle {
         if (ev_out) (void)hipEventDestroy(ev_out);
         if (fpp.ev_t) (void)hipEventDestroy(fpp.ev_t);
         if (fpp.ev_p) (void)hipEventDestroy(fpp.ev_p);
+        if (fpp.ev_lo) (void)hipEventDestroy(fpp.ev_lo);
     }
     // result
     pls_result res{};
@@ -540,6 +552,7 @@ struct Handle {
         ctx.sweep_chain = (int)opt.integer("pls.sweep_chain", -1);
         ctx.sweep_window = (int)opt.integer("pls.sweep_window", -1);
         ctx.ilu_view = (int)opt.integer("pls.ilu_view", 0);
+        ctx.sweep_swin = (int)opt.integer("pls.sweep_swin", 0);
         ctx.amg_csr_below = opt.num("pls.amg_csr_below", 16.0);
         if (opt.flag("pls.debug_bounds", false) || opt.integer("pls.debug_partial_cap", 0) > 0)
             ctx.set_debug(opt.flag("pls.debug_bounds", false), opt.integer("pls.debug_partial_cap", 0),
@@ -564,16 +577,49 @@ void BlockPC::apply(const double *x, double *y, Ctx &c) {
             // the heavy blocks' rows of t first, their sweep on the second stream
             // while the other rows' product and sweep run here (a PREONLY solve)
             auto &F = H.fpp;
-            Ctx &c2 = *H.ctx2;
+            Ctx &c2 = F.c_p ? *F.c_p : *H.ctx2;
+            Ctx &clo = F.c_lo ? *F.c_lo : c;
             PCILU *pc = static_cast<PCILU *>(H.ksp_fp->pc);
+            // pls.ilu_view 3: per-block start / end of both launches, once (diagnostics)
+            DBuf<int64_t> prof;
+            if (H.ctx.ilu_view >= 3 && !F.profiled) prof.alloc(F.nb * 8);
             spmv_slices(H.Mfp_s, y, H.t_fp.p, c, -1.0, 1.0, x + ns, F.sl_hi.p, F.n_hi);
             HIPCHK(hipEventRecord(F.ev_t, c.st));
             HIPCHK(hipStreamWaitEvent(c2.st, F.ev_t, 0));
-            pc->apply_blocks(H.t_fp.p, y + ns, c2, F.b_split, F.nb, F.rr);
+            pc->apply_blocks(H.t_fp.p, y + ns, c2, F.b_split, F.nb, F.rr, F.tpb, F.depth, prof.p);
             HIPCHK(hipEventRecord(F.ev_p, c2.st));
-            spmv_slices(H.Mfp_s, y, H.t_fp.p, c, -1.0, 1.0, x + ns, F.sl_lo.p, F.n_lo);
-            pc->apply_blocks(H.t_fp.p, y + ns, c, 0, F.b_split);
+            if (F.c_lo) HIPCHK(hipStreamWaitEvent(clo.st, F.ev_t, 0));
+            // (pls.fp_pipeline_lds: its workgroups reserve LDS they do not use)
+            spmv_slices(H.Mfp_s, y, H.t_fp.p, clo, -1.0, 1.0, x + ns, F.sl_lo.p, F.n_lo, F.lds);
+            if (F.c_lo) {
+                HIPCHK(hipEventRecord(F.ev_lo, clo.st));
+                HIPCHK(hipStreamWaitEvent(c.st, F.ev_lo, 0));
+            }
+            pc->apply_blocks(H.t_fp.p, y + ns, c, 0, F.b_split, 0, 0, 2, prof.p);
             HIPCHK(hipStreamWaitEvent(c.st, F.ev_p, 0));
+            if (prof.p) {
+                F.profiled = true;
+                std::vector<int64_t> hp(F.nb * 8);
+                HIPCHK(hipMemcpyAsync(hp.data(), prof.p, sizeof(int64_t) * hp.size(), hipMemcpyDeviceToHost, c.st));
+                c.sync();
+                int64_t t0 = INT64_MAX;
+                for (int64_t b = 0; b < F.nb; ++b) t0 = std::min(t0, hp[b * 8]);
+                auto span = [&](int64_t b0, int64_t b1, const char *what) {
+                    int64_t s0 = INT64_MAX, s1 = 0, e1 = 0;
+                    double dsum = 0;
+                    for (int64_t b = b0; b < b1; ++b) {
+                        s0 = std::min(s0, hp[b * 8]);
+                        s1 = std::max(s1, hp[b * 8]);
+                        e1 = std::max(e1, hp[b * 8 + 2]);
+                        dsum += (hp[b * 8 + 2] - hp[b * 8]) * 0.01;
+                    }
+                    fprintf(stderr, "[pls fp pipeline] %s blocks [%lld, %lld): starts %+.1f .. %+.1f us, last end %+.1f us, "
+                            "mean duration %.1f us\n", what, (long long)b0, (long long)b1, (s0 - t0) * 0.01,
+                            (s1 - t0) * 0.01, (e1 - t0) * 0.01, dsum / std::max<int64_t>(1, b1 - b0));
+                };
+                span(F.b_split, F.nb, "heavy");
+                span(0, F.b_split, "light");
+            }
             H.ksp_fp->note_preonly();
         } else {
             // t = x_fp - P_fp,s y_s   (Preconditioner.py:232-233, fused)
@@ -744,7 +790,60 @@ static void setup_fp_pipeline(Handle &H) {
     const int64_t rr_opt = H.opt.integer("pls.fp_pipeline_rr", -1);  // -1 auto, 0 off, a group size forced
     if (rr_opt > 16 || (rr_opt > 0 && (rr_opt & (rr_opt - 1))))
         throw Error("pls.fp_pipeline_rr must be -1 (auto), 0 or a power of two <= 16");
-    F.rr = rr_opt >= 0 ? (int)rr_opt : (grp <= 4 && pc->lds_tpb == 1024 ? grp : 0);
+    // default: 8 waves (levels of <= 8 slices need no more) with 6 levels of
+    // factor data in flight -- the heavy blocks sweep beside the product, whose
+    // HBM traffic stretches a load's latency past the plain sweep's two levels
+    const bool deep = msl <= 8 && H.opt.integer("pls.fp_pipeline_depth", 2) == 6;
+    F.rr = rr_opt >= 0 ? (int)rr_opt : 0;
+    F.tpb = deep && F.rr == 0 ? 512 : 0;
+    F.depth = deep && F.rr == 0 ? 6 : 2;
+    // the sweep holds max_len * 8 bytes of the CU's 160 KiB: reserve more than what is left
+    const int64_t left = 163840 - pc->max_len * 8;
+    const int64_t lds_opt = H.opt.integer("pls.fp_pipeline_lds", 0);
+    F.lds = (size_t)(lds_opt >= 0 ? lds_opt : (left < 16384 ? ((left + 1024) & ~int64_t(1023)) : 0));
+    // reserved CUs: the heavy blocks' count rounded up to a multiple of 8 (one per XCD)
+    int ncu = 0, dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int64_t cus_opt = H.opt.integer("pls.fp_pipeline_cus", -1);
+    const int want = (int)(cus_opt >= 0 ? cus_opt : (nb - b + 7) / 8 * 8);
+    F.cus = (want >= nb - b && want <= ncu / 4) ? want : 0;
+    F.c_p.reset();
+    F.c_lo.reset();
+    if (F.cus > 0) {
+        const uint32_t words = (uint32_t)((ncu + 31) / 32);
+        std::vector<uint32_t> mp(words, 0), ml(words, 0);
+        // which mask bits: pls.fp_pipeline_cu_layout 0 -- bits [0, R) (one per XCD in turn
+        // if the driver deals bits round robin over the XCDs), 1 -- R / 8 consecutive
+        // bits at the start of every 1/8 of the mask (XCD-major bit order)
+        const int64_t layout = H.opt.integer("pls.fp_pipeline_cu_layout", 0);
+        for (int k = 0; k < ncu; ++k) {
+            const int per = ncu / 8;
+            const bool res = layout == 1 ? (k % per) < F.cus / 8 : k < F.cus;
+            (res ? mp : ml)[k / 32] |= 1u << (k % 32);
+        }
+        // (a driver without CU masking: plain streams, F.cus = 0)
+        auto masked = [&](const std::vector<uint32_t> &m) -> std::unique_ptr<Ctx> {
+            auto cx = std::make_unique<Ctx>();
+            hipStream_t s = nullptr;
+            if (hipExtStreamCreateWithCUMask(&s, words, m.data()) != hipSuccess) {
+                (void)hipGetLastError();
+                return nullptr;
+            }
+            HIPCHK(hipStreamDestroy(cx->st));
+            cx->st = s;
+            cx->d16_unroll = H.ctx.d16_unroll;
+            return cx;
+        };
+        F.c_p = masked(mp);
+        F.c_lo = F.c_p ? masked(ml) : nullptr;
+        if (!F.c_p || !F.c_lo) {
+            F.c_p.reset();
+            F.c_lo.reset();
+            F.cus = 0;
+        }
+        if (!F.ev_lo) HIPCHK(hipEventCreateWithFlags(&F.ev_lo, hipEventDisableTiming));
+    }
     F.b_split = b;
     F.nb = nb;
     F.r_split = r_split;
@@ -753,9 +852,10 @@ static void setup_fp_pipeline(Handle &H) {
     F.on = true;
     if (H.ctx.ilu_view)
         fprintf(stderr, "[pls fp pipeline] blocks [%lld, %lld) first (levels >= %lld, median %lld), rows from %lld, "
-                "slices %lld + %lld, round-robin groups %d (most slices per level %lld)\n", (long long)b, (long long)nb,
+                "slices %lld + %lld, round-robin groups %d (most slices per level %lld), product LDS reserve %zu, "
+                "sweep tpb %d depth %d, reserved CUs %d\n", (long long)b, (long long)nb,
                 (long long)(2 * med), (long long)med, (long long)r_split, (long long)F.n_hi, (long long)F.n_lo, F.rr,
-                (long long)msl);
+                (long long)msl, F.lds, F.tpb, F.depth, F.cus);
 }
 
 static void alloc_work(Handle &H) {
@@ -1584,6 +1684,32 @@ int pls_get_timings(pls_handle *hh, pls_timings *t) {
         t->spmv_calls = H.timers.spmv_calls;
     })
 }
+int pls_get_ksp_stats(pls_handle *hh, const char *prefix, int64_t *stats) {
+    PLS_TRY({
+        Handle &H = *reinterpret_cast<Handle *>(hh);
+        if (!prefix || !stats) throw Error("pls_get_ksp_stats: null argument");
+        const std::string want(prefix);
+        const KSP *found = nullptr;
+        std::vector<const KSP *> all = {H.ksp_s.get(), H.ksp_f.get(), H.ksp_p.get(), H.ksp_pd.get(), H.ksp_fp.get(),
+                                        H.outer.get()};
+        if (H.ksp_fp && H.ksp_fp->pc)
+            if (const PCFieldSplit *fs = dynamic_cast<const PCFieldSplit *>(H.ksp_fp->pc)) {
+                all.push_back(fs->k0.get());
+                all.push_back(fs->k1.get());
+            }
+        if (H.fs_fp) {
+            all.push_back(H.fs_fp->k0.get());
+            all.push_back(H.fs_fp->k1.get());
+        }
+        for (const KSP *k : all)
+            if (k && k->prefix == want) found = k;
+        if (!found) throw Error("pls_get_ksp_stats: no inner solver with prefix '" + want + "'");
+        stats[0] = found->stat_solves;
+        stats[1] = found->stat_its;
+        stats[2] = found->stat_max;
+        stats[3] = found->stat_div;
+    })
+}
 int pls_reset_timings(pls_handle *hh) { PLS_TRY(reinterpret_cast<Handle *>(hh)->timers.reset()) }
 
 int pls_export_matrix(pls_handle *hh, int which, int64_t *nrows, int64_t *nnz, int64_t *row_ptr, int32_t *col,
@@ -1660,6 +1786,14 @@ int pls_sparse_lu_analyze(const pls_csr *A, const char *options, double *stats, 
                           int32_t *front_of, int32_t *parent) {
     PLS_TRY({
         if (!A || A->nrows != A->ncols) throw Error("pls_sparse_lu_analyze: square A required");
+        if (A->nrows < 0 || !A->row_ptr || (A->nrows > 0 && !A->col))
+            throw Error("pls_sparse_lu_analyze: negative size or null arrays");
+        // the pattern is indexed directly by the symbolic analysis: validate it first
+        if (A->row_ptr[0] != 0) throw Error("pls_sparse_lu_analyze: row_ptr[0] must be 0");
+        for (int64_t i = 0; i < A->nrows; ++i)
+            if (A->row_ptr[i + 1] < A->row_ptr[i]) throw Error("pls_sparse_lu_analyze: row_ptr must be nondecreasing");
+        for (int64_t k = 0; k < A->row_ptr[A->nrows]; ++k)
+            if (A->col[k] < 0 || A->col[k] >= A->ncols) throw Error("pls_sparse_lu_analyze: column index out of range");
         Options o;
         o.parse(options);
         HostCSR H;

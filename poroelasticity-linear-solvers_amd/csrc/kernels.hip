@@ -1536,24 +1536,24 @@ template <int G2, int SEG>
 static void d16_dispatch(unsigned g, hipStream_t st, int64_t nrows, int64_t ns, const int64_t *sptr,
                          const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
                          const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
-                         int tag, const double *ghost, int32_t nl, const int32_t *slist, const int32_t *rm) {
+                         int tag, const double *ghost, int32_t nl, const int32_t *slist, const int32_t *rm, size_t shm) {
     if (ghost) {
-        if (tag) k_d16_spmv<G2, 1, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
-        else k_d16_spmv<G2, 0, true, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
+        if (tag) k_d16_spmv<G2, 1, true, SEG><<<g, TPB, shm, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
+        else k_d16_spmv<G2, 0, true, SEG><<<g, TPB, shm, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
     } else {
-        if (tag) k_d16_spmv<G2, 1, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
-        else k_d16_spmv<G2, 0, false, SEG><<<g, TPB, 0, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
+        if (tag) k_d16_spmv<G2, 1, false, SEG><<<g, TPB, shm, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
+        else k_d16_spmv<G2, 0, false, SEG><<<g, TPB, shm, st>>>(nrows, ns, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, ghost, nl, slist, rm);
     }
 }
 template <int SEG>
 static void d16_unrolled(int unroll, unsigned g, hipStream_t st, int64_t nrows, int64_t nslices, const int64_t *sptr,
                          const int64_t *sfirst, const int32_t *slpr, const uint16_t *dl, const double *dv,
                          const int32_t *seg, const double *x, double *y, double alpha, double beta, const double *z,
-                         int tag, const double *ghost, int32_t nl, const int32_t *slist, const int32_t *rm) {
+                         int tag, const double *ghost, int32_t nl, const int32_t *slist, const int32_t *rm, size_t shm) {
     switch (unroll) {
-        case 1: d16_dispatch<1, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm); break;
-        case 2: d16_dispatch<2, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm); break;
-        default: d16_dispatch<4, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm); break;
+        case 1: d16_dispatch<1, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm, shm); break;
+        case 2: d16_dispatch<2, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm, shm); break;
+        default: d16_dispatch<4, SEG>(g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rm, shm); break;
     }
 }
 static int d16_xcd_host = 0;
@@ -1565,13 +1565,13 @@ void set_d16_xcd(int on) {
 void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const int64_t *sfirst, const int32_t *slpr,
                      const uint16_t *dl, const double *dv, const int32_t *seg, int nsegs, const double *x, double *y,
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
-                     int unroll, hipStream_t st, const int32_t *slist, const int32_t *rowmap) {
+                     int unroll, hipStream_t st, const int32_t *slist, const int32_t *rowmap, size_t lds_reserve) {
     if (nslices <= 0) return;
     unsigned g = grid_for(nslices, TPB / 64);
     if (d16_xcd_host) g = (g + 7) / 8 * 8;  // every XCD range the same length (surplus blocks exit)
     const int32_t nl = (int32_t)nlocal;
-    if (nsegs == 8) d16_unrolled<8>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rowmap);
-    else d16_unrolled<4>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rowmap);
+    if (nsegs == 8) d16_unrolled<8>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rowmap, lds_reserve);
+    else d16_unrolled<4>(unroll, g, st, nrows, nslices, sptr, sfirst, slpr, dl, dv, seg, x, y, alpha, beta, z, tag, ghost, nl, slist, rowmap, lds_reserve);
 }
 
 // ============================================================ SELL/B3 ======
@@ -2212,11 +2212,11 @@ __device__ __forceinline__ void ring_chunk(Sw2Ctx &x, int64_t g) {
     x.cnext = x.ck < x.cend ? x.rin.cg[x.ck] : INT64_MAX;
 }
 
-template <int P, int LPR, bool W, bool R>
+template <int P, int LPR, bool W, bool R, int D = 2>
 __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P> &cur, Sw2Slot<P> &ahead) {
     if (R) ring_chunk(x, g);
-    if (g + 2 >= x.gbase + 64) x.refill(g);
-    sw2_issue<P, R>(x, g + 2, ahead);
+    if (g + D >= x.gbase + 64) x.refill(g);
+    sw2_issue<P, R>(x, g + D, ahead);
     if (cur.base >= 0 && !(R && (ring_probe & 2))) {  // (probe bit 1: no compute, diagnostics)
         const int32_t h = cur.c[0];
         const int32_t len = W ? (int32_t)cur.L - 1 : (int32_t)((uint32_t)h >> SW_ROW_BITS);
@@ -2264,8 +2264,30 @@ __device__ __forceinline__ void sw2_level(Sw2Ctx &x, int64_t g, const Sw2Slot<P>
     __syncthreads();
 }
 
-template <int P, int LPR, bool W, bool R>
+// D > 2: D levels of factor data in flight (D + 1 register slots, indexed by
+// compile-time constants in the unrolled loop) -- for narrow levels under
+// concurrent HBM traffic, where a load's latency exceeds two levels' time
+template <int P, int LPR, bool W, int D>
+__device__ __forceinline__ void sweep2_deep(Sw2Ctx &x, int64_t g0) {
+    x.refill(g0);
+    Sw2Slot<P> s[D + 1];
+#pragma unroll
+    for (int k = 0; k < D; ++k) sw2_issue<P, false>(x, g0 + k, s[k]);
+    for (int64_t g = g0;;) {
+#pragma unroll
+        for (int k = 0; k <= D; ++k) {
+            sw2_level<P, LPR, W, false, D>(x, g, s[k], s[(k + D) % (D + 1)]);
+            if (++g >= x.g1) return;
+        }
+    }
+}
+
+template <int P, int LPR, bool W, bool R, int D = 2>
 __device__ __forceinline__ void sweep2(Sw2Ctx &x, int64_t g0) {
+    if (D != 2 && !R) {
+        sweep2_deep<P, LPR, W, D>(x, g0);
+        return;
+    }
     x.refill(g0);
     Sw2Slot<P> s0, s1, s2;
     sw2_issue<P, R>(x, g0, s0);
@@ -2384,7 +2406,7 @@ __device__ __forceinline__ void sweep_rr(Sw2Ctx &x, int64_t g0, int S = 1) {
     }
 }
 
-template <int P, bool W, bool R = false>
+template <int P, bool W, bool R = false, int D = 2>
 __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int lane, int wave, int nw, bool upper,
                                             const int64_t *__restrict__ gslice, const int64_t *__restrict__ sptr,
                                             const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -2415,16 +2437,16 @@ __device__ __forceinline__ void sweep_block(int64_t g0, int64_t g1, int lpr, int
         return;
     }
     if (W) {  // the y-resident sweep: 8 / 16 lanes for long rows
-        if (lpr == 16) sweep2<P, 16, W, R>(x, g0);
-        else if (lpr == 8) sweep2<P, 8, W, R>(x, g0);
-        else if (lpr == 4) sweep2<P, 4, W, R>(x, g0);
-        else if (lpr == 2) sweep2<P, 2, W, R>(x, g0);
-        else sweep2<P, 1, W, R>(x, g0);
+        if (lpr == 16) sweep2<P, 16, W, R, D>(x, g0);
+        else if (lpr == 8) sweep2<P, 8, W, R, D>(x, g0);
+        else if (lpr == 4) sweep2<P, 4, W, R, D>(x, g0);
+        else if (lpr == 2) sweep2<P, 2, W, R, D>(x, g0);
+        else sweep2<P, 1, W, R, D>(x, g0);
         return;
     }
-    if (lpr == 4) sweep2<P, 4, W, R>(x, g0);
-    else if (lpr == 2) sweep2<P, 2, W, R>(x, g0);
-    else sweep2<P, 1, W, R>(x, g0);
+    if (lpr == 4) sweep2<P, 4, W, R, D>(x, g0);
+    else if (lpr == 2) sweep2<P, 2, W, R, D>(x, g0);
+    else sweep2<P, 1, W, R, D>(x, g0);
 }
 
 static constexpr int SW_P = 7;  // factor entries per lane kept in registers per pipeline slot
@@ -2437,8 +2459,9 @@ static constexpr int RING_P = 7, RING_TPB = 1024;
 // blocks longer than the LDS holds, with the wide slice headers (W).  All waves of the workgroup share the CU's
 // vector L1, so y written by one wave before __syncthreads() is seen by the
 // others after it (workgroup-scope coherence, no cache maintenance needed).
-template <bool GMEM>
-__global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *__restrict__ Lgoff,
+// D: levels of factor data in flight (2; deeper with fewer threads: TPBMAX)
+template <bool GMEM, int D = 2, int TPBMAX = 1024>
+__global__ __launch_bounds__(TPBMAX) void k_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *__restrict__ Lgoff,
                                                          const int64_t *__restrict__ Lgslice,
                                                          const int64_t *__restrict__ Lsptr,
                                                          const int32_t *__restrict__ Lcol,
@@ -2466,11 +2489,11 @@ __global__ __launch_bounds__(1024) void k_ilu_blocks_lds(int64_t n, int64_t nblo
     if (!GMEM || x != y)
         for (int64_t t = threadIdx.x; t < len; t += blockDim.x) ys[t] = x[b0 + t];
     __syncthreads();
-    sweep_block<SW_P, GMEM>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol, Lval, ys,
-                            nullptr, nullptr, 0, 0, 0, {}, rr);
+    sweep_block<SW_P, GMEM, false, D>(Lgoff[blk], Lgoff[blk + 1], Llpr[blk], lane, wave, nw, false, Lgslice, Lsptr, Lcol,
+                                      Lval, ys, nullptr, nullptr, 0, 0, 0, {}, rr);
     if (prof) t1 = wall_clock64();
-    sweep_block<SW_P, GMEM>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol, Uval, ys,
-                            nullptr, nullptr, 0, 0, 0, {}, rr);
+    sweep_block<SW_P, GMEM, false, D>(Ugoff[blk], Ugoff[blk + 1], Ulpr[blk], lane, wave, nw, true, Ugslice, Usptr, Ucol,
+                                      Uval, ys, nullptr, nullptr, 0, 0, 0, {}, rr);
     if (!GMEM)
         for (int64_t t = threadIdx.x; t < len; t += blockDim.x) y[b0 + t] = ys[t];
     if (prof && threadIdx.x == 0) {  // diagnostics (option pls.sweep_profile): 100 MHz wall clock
@@ -2558,7 +2581,7 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const int64_t *Ugoff, const int64_t *Ugslice, const int64_t *Usptr, const int32_t *Ucol,
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
                            int64_t *prof, bool gmem, int tpb, int rr, const int64_t *bstart, int64_t max_len,
-                           int64_t blk_lo, int64_t blk_hi) {
+                           int64_t blk_lo, int64_t blk_hi, int depth) {
     // tpb: threads per workgroup, 64 .. 1024 (narrow levels: fewer waves, cheaper barriers)
     if (tpb < 64 || tpb > 1024 || (tpb & 63)) tpb = 1024;
     // block subset [blk_lo, blk_hi) (blk_hi < 0: every block)
@@ -2580,6 +2603,18 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
         return;
     }
     const size_t bytes = (size_t)(max_len > 0 ? max_len : n / nblocks + 1) * 8;
+    if (depth == 6 && tpb <= 512 && rr == 0) {  // 6 levels in flight, at most 8 waves (register room)
+        static bool conf6 = false;
+        if (!conf6) {
+            (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds<false, 6, 512>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)163840);
+            conf6 = true;
+        }
+        k_ilu_blocks_lds<false, 6, 512><<<grid, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr,
+                                                                 Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof,
+                                                                 rr, bstart, blk_hi);
+        return;
+    }
     k_ilu_blocks_lds<false><<<grid, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval, Llpr, Ugoff,
                                                         Ugslice, Usptr, Ucol, Uval, Ulpr, x, y, prof, rr, bstart, blk_hi);
 }
@@ -2982,6 +3017,220 @@ void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart,
     const size_t bytes = (size_t)(256 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
     k_ilu_blocks_window<<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv,
                                                               Uwoff, Ucol, Uval, Utinv, x, y);
+}
+
+// ======================================================= super-window sweep ==
+// Triangular sweeps of blocks too long for LDS (whole FE blocks: ~47k rows at
+// 3-D N=12, 353k at N=24, whose level DAGs are ~1,440 / ~2,985 levels deep).
+// Rows are cut into windows of 64 (lane = row) and consecutive windows into
+// super-windows (build_swin_tri): per super-window, in processing order,
+//   1. all waves stage the super-window's packed window inverses and near
+//      streams into LDS, and every row's input minus its far terms (entries
+//      before the super-window, read from the block solution in global
+//      memory -- final since earlier super-windows) goes to LDS;
+//   2. one wave walks the windows: t = input - near terms (LDS gathers),
+//      y = T_w^-1 t (a 64 x 64 triangular GEMV from LDS, t broadcast with
+//      v_readlane), y to LDS -- no barrier between windows (a wave's LDS
+//      accesses complete in order);
+//   3. the super-window's y to global memory.
+// The dependent chain is the windows' GEMVs (len / 64 per triangle) instead of
+// the levels; no global load sits on it.  L: input x, output y; U: in place on
+// y.  Sums: far terms, near terms (stream order), then the window inverse --
+// the explicit inverses reassociate the substitution's sums (<= 1e-12 against
+// the level-order sweeps, tests/test_gpu_sweeps.py).
+static constexpr int SWIN_TPB = 256, SWIN_TRI = 2080;
+
+// global -> LDS copies of the staged streams: 8 x 16 bytes in flight per thread
+__device__ __forceinline__ void swin_copy(const double *__restrict__ src, double *dst, int64_t n, int tid) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const bool al = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+    if (!al) {
+        for (int64_t k = tid; k < n; k += SWIN_TPB) dst[k] = src[k];
+        return;
+    }
+    const int64_t n2 = n >> 1;
+    const d2 *s2 = reinterpret_cast<const d2 *>(src);
+    d2 *t2 = reinterpret_cast<d2 *>(dst);
+    for (int64_t k0 = 0; k0 < n2; k0 += 8 * SWIN_TPB) {
+        d2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = k0 + u * SWIN_TPB + tid;
+            v[u] = k < n2 ? s2[k] : d2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = k0 + u * SWIN_TPB + tid;
+            if (k < n2) t2[k] = v[u];
+        }
+    }
+    if ((n & 1) && tid == 0) dst[n - 1] = src[n - 1];
+}
+__device__ __forceinline__ void swin_copy32(const int32_t *__restrict__ src, int32_t *dst, int64_t n, int tid) {
+    for (int64_t k0 = 0; k0 < n; k0 += 8 * SWIN_TPB) {
+        int32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = k0 + u * SWIN_TPB + tid;
+            v[u] = k < n ? src[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = k0 + u * SWIN_TPB + tid;
+            if (k < n) dst[k] = v[u];
+        }
+    }
+}
+
+template <bool UP>
+__device__ __forceinline__ void swin_sweep(int64_t len, int64_t bs0, int64_t bs1, const int64_t *__restrict__ sw,
+                                           const int64_t *__restrict__ wnear, const int32_t *__restrict__ ncol,
+                                           const double *__restrict__ nval, const int64_t *__restrict__ wfar,
+                                           const int32_t *__restrict__ fcol, const double *__restrict__ fval,
+                                           const double *__restrict__ tinv, int64_t wfirst, const double *in,
+                                           double *out, double *lds) {
+    double *ys = lds;            // the super-window's rows (<= 512)
+    double *tb = lds + 512;      // the window's t, broadcast
+    double *ts = lds + 576;      // staged inverses, then near values
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int64_t s = bs0; s < bs1; ++s) {
+        const int64_t w0 = sw[4 * s], nwn = sw[4 * s + 1], r0 = sw[4 * s + 2], r1 = sw[4 * s + 3];
+        // 1. stage: inverses (nwn * 2080 doubles), near values and columns
+        const int64_t nt = nwn * SWIN_TRI, e0 = wnear[w0], ne = wnear[w0 + nwn] - e0;
+        double *nv = ts + nt;
+        int32_t *nc = reinterpret_cast<int32_t *>(nv + ne);
+        // (eight 16-byte loads in flight per thread, then their LDS stores: the copies
+        // are latency-bound, one round trip per round)
+        // (pls.ring_probe bits 256 / 512 / 1024: no staging / far terms / window chain --
+        // timing diagnostics, results wrong)
+        const int probe = ring_probe;
+        if (!(probe & 256)) {
+            swin_copy(reinterpret_cast<const double *>(tinv) + w0 * SWIN_TRI, ts, nt, tid);
+            swin_copy(nval + e0, nv, ne, tid);
+            swin_copy32(ncol + e0, nc, ne, tid);
+        }
+        // far terms: one row per thread (64-row slices: [k][lane] streams), eight gathers in flight
+        for (int64_t r = r0 + tid; r < r1; r += SWIN_TPB) {
+            const int64_t w = wfirst + (r >> 6), l = r & 63;
+            const int64_t f0 = wfar[w], K = (probe & 512) ? 0 : (wfar[w + 1] - f0) >> 6;
+            double acc = 0.0;
+            const double xin = in[r];
+            for (int64_t k = 0; k < K; k += 8) {
+                int32_t cc[8];
+                double vv[8], yy[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t kk = k + u < K ? k + u : K - 1;  // (clamped: the value is zeroed below)
+                    cc[u] = fcol[f0 + kk * 64 + l];
+                    vv[u] = fval[f0 + kk * 64 + l];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) yy[u] = out[cc[u]];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += __dmul_rn(k + u < K ? vv[u] : 0.0, yy[u]);
+            }
+            ys[r - r0] = xin - acc;
+        }
+        __syncthreads();
+        // 2. the windows, one wave
+        if (wave == 0 && !(probe & 1024)) {
+            for (int64_t j0 = 0; j0 < nwn; ++j0) {
+                const int64_t j = UP ? nwn - 1 - j0 : j0;
+                const int64_t w = w0 + j, wr = (w - wfirst) * 64;  // window's first row (block-local)
+                const bool act = wr + lane < len;
+                const int64_t q0 = wnear[w] - e0, K = (wnear[w + 1] - wnear[w]) >> 6;
+                // near terms, eight at a time: their column / value reads, then the
+                // eight y gathers, all issued before the first is used (branch-free:
+                // padding and the tail read entry 0 with value 0)
+                double acc = 0.0;
+                for (int64_t k0 = 0; k0 < K; k0 += 8) {
+                    int32_t cc[8];
+                    double vv[8], yy[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int64_t q = q0 + (k0 + u < K ? k0 + u : 0) * 64 + lane;
+                        cc[u] = nc[q];
+                        vv[u] = k0 + u < K ? nv[q] : 0.0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) yy[u] = ys[cc[u]];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc += __dmul_rn(vv[u], yy[u]);
+                }
+                const double t = act ? ys[wr - r0 + lane] - acc : 0.0;
+                tb[lane] = t;  // broadcast through LDS (one wave: in order, no barrier)
+                const double *T = ts + j * SWIN_TRI;
+                // y = T^-1 t: 16 columns per step, their LDS reads (T column entries and
+                // the broadcast t_k) issued together; four partial sums (k mod 4) added
+                // in a fixed order
+                double ya[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k0 = 0; k0 < 64; k0 += 16) {
+                    double a[16], tk[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        const int k = k0 + u;
+                        const bool nz = UP ? lane <= k : lane >= k;
+                        const int off = UP ? k * (k + 1) / 2 + lane : 64 * k - k * (k - 1) / 2 + (lane - k);
+                        a[u] = T[nz ? off : 0];
+                        tk[u] = tb[k];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        const int k = k0 + u;
+                        const bool nz = UP ? lane <= k : lane >= k;
+                        ya[u & 3] = __fma_rn(nz ? a[u] : 0.0, tk[u], ya[u & 3]);
+                    }
+                }
+                const double y = (ya[0] + ya[1]) + (ya[2] + ya[3]);
+                if (act) ys[wr - r0 + lane] = y;
+            }
+        }
+        __syncthreads();
+        // 3. the super-window's solution to global memory (far terms of later super-windows read it)
+        for (int64_t r = r0 + tid; r < r1; r += SWIN_TPB) out[r] = ys[r - r0];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(SWIN_TPB) void k_ilu_blocks_swin(
+    int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart, const int64_t *__restrict__ wstart,
+    const int64_t *__restrict__ Lbsw, const int64_t *__restrict__ Lsw, const int64_t *__restrict__ Lwnear,
+    const int32_t *__restrict__ Lncol, const double *__restrict__ Lnval, const int64_t *__restrict__ Lwfar,
+    const int32_t *__restrict__ Lfcol, const double *__restrict__ Lfval, const double *__restrict__ Ltinv,
+    const int64_t *__restrict__ Ubsw, const int64_t *__restrict__ Usw, const int64_t *__restrict__ Uwnear,
+    const int32_t *__restrict__ Uncol, const double *__restrict__ Unval, const int64_t *__restrict__ Uwfar,
+    const int32_t *__restrict__ Ufcol, const double *__restrict__ Ufval, const double *__restrict__ Utinv,
+    const double *x, double *y) {
+    extern __shared__ __attribute__((aligned(16))) double lds_sw[];
+    const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
+    int64_t b0, len;
+    block_range(blk, n, nblocks, bstart, b0, len);
+    const int64_t wf = wstart[blk];
+    swin_sweep<false>(len, Lbsw[blk], Lbsw[blk + 1], Lsw, Lwnear, Lncol, Lnval, Lwfar, Lfcol + 0, Lfval, Ltinv, wf,
+                      x + b0, y + b0, lds_sw);
+    swin_sweep<true>(len, Ubsw[blk], Ubsw[blk + 1], Usw, Uwnear, Uncol, Unval, Uwfar, Ufcol, Ufval, Utinv, wf, y + b0,
+                     y + b0, lds_sw);
+}
+
+int ilu_swin_lds_budget() { return 163840 - 576 * 8 - 1024; }
+
+void launch_ilu_blocks_swin(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
+                            const int64_t *Lbsw, const int64_t *Lsw, const int64_t *Lwnear, const int32_t *Lncol,
+                            const double *Lnval, const int64_t *Lwfar, const int32_t *Lfcol, const double *Lfval,
+                            const double *Ltinv, const int64_t *Ubsw, const int64_t *Usw, const int64_t *Uwnear,
+                            const int32_t *Uncol, const double *Unval, const int64_t *Uwfar, const int32_t *Ufcol,
+                            const double *Ufval, const double *Utinv, const double *x, double *y, int64_t lds_bytes,
+                            hipStream_t st) {
+    static bool configured = false;
+    if (!configured) {
+        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_swin, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)163840);
+        configured = true;
+    }
+    k_ilu_blocks_swin<<<(unsigned)nblocks, SWIN_TPB, (size_t)lds_bytes, st>>>(
+        n, nblocks, bstart, wstart, Lbsw, Lsw, Lwnear, Lncol, Lnval, Lwfar, Lfcol, Lfval, Ltinv, Ubsw, Usw, Uwnear,
+        Uncol, Unval, Uwfar, Ufcol, Ufval, Utinv, x, y);
 }
 
 // =========================================================== distribution ====

@@ -153,7 +153,9 @@ void launch_d16_spmv(int64_t nrows, int64_t nslices, const int64_t *sptr, const 
                      double alpha, double beta, const double *z, int tag, const double *ghost, int64_t nlocal,
                      int unroll /* 8-entry groups per lane in flight: 1, 2 or 4 */, hipStream_t st,
                      const int32_t *slist = nullptr /* nslices entries: the slices to process */,
-                     const int32_t *rowmap = nullptr /* slice position -> row (SELL-C-sigma) */);
+                     const int32_t *rowmap = nullptr /* slice position -> row (SELL-C-sigma) */,
+                     size_t lds_reserve = 0 /* dynamic LDS per workgroup, unused: keeps the product's
+                                               workgroups off CUs whose LDS a sweep holds */);
 // SELL/B3: row triples sharing one column list (FE vector fields), see kernels.hip
 void launch_triple_flags(int64_t n, const int64_t *rp, const int32_t *ci, uint8_t *flag, hipStream_t st);
 int b3_lanes_per_triple();
@@ -195,8 +197,19 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
                            const double *Uval, const int32_t *Ulpr, const double *x, double *y, hipStream_t st,
                            int64_t *prof = nullptr, bool gmem = false, int tpb = 1024, int rr = 0,
                            const int64_t *bstart = nullptr, int64_t max_len = 0, int64_t blk_lo = 0,
-                           int64_t blk_hi = -1);  // blocks [blk_lo, blk_hi) only (blk_hi < 0: all)
-int ilu_lds_lane_entries();  // factor entries per lane the LDS sweep keeps in registers
+                           int64_t blk_hi = -1,  // blocks [blk_lo, blk_hi) only (blk_hi < 0: all)
+                           int depth = 2);       // levels in flight: 2, or 6 with tpb <= 512
+
+int ilu_lds_lane_entries();
+// super-window sweep (blocks too long for LDS): see kernels.hip
+void launch_ilu_blocks_swin(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
+                            const int64_t *Lbsw, const int64_t *Lsw, const int64_t *Lwnear, const int32_t *Lncol,
+                            const double *Lnval, const int64_t *Lwfar, const int32_t *Lfcol, const double *Lfval,
+                            const double *Ltinv, const int64_t *Ubsw, const int64_t *Usw, const int64_t *Uwnear,
+                            const int32_t *Uncol, const double *Unval, const int64_t *Uwfar, const int32_t *Ufcol,
+                            const double *Ufval, const double *Utinv, const double *x, double *y, int64_t lds_bytes,
+                            hipStream_t st);
+int ilu_swin_lds_budget();  // bytes of LDS a super-window's staged inverses + near streams may take  // factor entries per lane the LDS sweep keeps in registers
 // The chain sweep (kernels.hip, k_ilu_blocks_chain): one wave per LDS-resident
 // block walks its slices in order with ilu_chain_depth() slices in flight
 // (deep, narrow level DAGs).  Per triangle and block: first slice's entry

@@ -664,12 +664,12 @@ void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, dou
 // the slices slist[0 .. count) of a D16 layout (rows of those slices only; the
 // per-row sums are spmv()'s): the 2-way PC's pressure-first pipeline
 void spmv_slices(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z,
-                 const int32_t *slist, int64_t count) {
+                 const int32_t *slist, int64_t count, size_t lds_reserve) {
     if (!M.sell || !M.sell->d16 || M.halo || M.sell->nperm || M.sell->b3_nslices || M.sell->nrows_mapped)
         throw Error("spmv_slices: plain D16 layouts only");
     const DevSELL &S = *M.sell;
     launch_d16_spmv(M.nrows, count, S.sptr.p, S.sfirst.p, S.slpr.p, S.dl.p, S.val.p, S.seg.p, S.nsegs, x, y, alpha, beta,
-                    z, M.tag, nullptr, M.ncols, c.d16_unroll, c.st, slist, nullptr);
+                    z, M.tag, nullptr, M.ncols, c.d16_unroll, c.st, slist, nullptr, lds_reserve);
 }
 
 // ============================================================== options ===
@@ -1329,6 +1329,201 @@ static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, cons
     c.sync();
 }
 
+// Super-window sweep tables of one triangle (kernels.hip, k_ilu_blocks_swin)
+// for blocks too long for LDS.  Rows are cut into windows of 64 (from the
+// block's first row, as build_window_tri), consecutive windows into
+// super-windows in processing order (ascending for L, descending for U) as
+// long as their staged data -- the packed window inverses (2,080 doubles) and
+// the near streams -- fit ilu_swin_lds_budget() (at most 8 windows).  A row's
+// entries on the solved side split three ways: in its own window (into the
+// window's triangle, inverted as build_window_tri does), near (in its super-
+// window, another window: SELL [k][lane], column = row - the super-window's
+// first row, read from LDS) and far (before the super-window: SELL, block-
+// local row, read from the block solution in global memory).  Padding entries
+// carry column 0 and value 0.
+static void build_swin_tri(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
+                           const std::vector<int32_t> &ci, const std::vector<int64_t> &dg,
+                           const std::vector<double> &fv, bool upper, SwinTri &W, Ctx &c) {
+    std::vector<int64_t> wfirst(nblk + 1, 0);
+    for (int64_t b = 0; b < nblk; ++b) wfirst[b + 1] = wfirst[b] + (bst[b + 1] - bst[b] + 63) / 64;
+    const int64_t nw = wfirst[nblk];
+    std::vector<int64_t> wrow(nw), wend(nw), wblk(nw);  // first / end row (global), block
+    for (int64_t b = 0; b < nblk; ++b)
+        for (int64_t w = wfirst[b]; w < wfirst[b + 1]; ++w) {
+            wrow[w] = bst[b] + (w - wfirst[b]) * 64;
+            wend[w] = std::min<int64_t>(wrow[w] + 64, bst[b + 1]);
+            wblk[w] = b;
+        }
+    // solved-side entries of row i: [s0, s1) in column order
+    auto side = [&](int64_t i, int64_t &s0, int64_t &s1) {
+        if (!upper) {
+            s0 = rp[i];
+            s1 = dg[i];
+        } else {
+            s0 = dg[i] + 1;
+            s1 = rp[i + 1];
+        }
+    };
+    // counts of row i's near / far entries for a super-window spanning rows [lo, hi) (global)
+    auto counts = [&](int64_t i, int64_t w, int64_t lo, int64_t hi, int64_t &nn, int64_t &nf) {
+        int64_t s0, s1;
+        side(i, s0, s1);
+        nn = nf = 0;
+        for (int64_t k = s0; k < s1; ++k) {
+            const int64_t cc = ci[k];
+            if (cc >= wrow[w] && cc < wend[w]) continue;  // own window: the triangle
+            if (cc >= lo && cc < hi) ++nn;
+            else ++nf;
+        }
+    };
+    auto win_near = [&](int64_t w, int64_t lo, int64_t hi) {  // the window's near entries per lane (max over rows)
+        int64_t K = 0;
+        for (int64_t i = wrow[w]; i < wend[w]; ++i) {
+            int64_t nn, nf;
+            counts(i, w, lo, hi, nn, nf);
+            K = std::max(K, nn);
+        }
+        return K;
+    };
+    const int64_t budget = ilu_swin_lds_budget(), TRI = 2080;
+    // super-windows, per block in processing order (greedy)
+    std::vector<int64_t> bsw(nblk + 1, 0), sw;  // sw: 4 per super-window
+    std::vector<int64_t> swof(nw, 0);           // window -> super-window
+    int64_t max_stage = 0;
+    for (int64_t b = 0; b < nblk; ++b) {
+        const int64_t W0 = wfirst[b], W1 = wfirst[b + 1];
+        int64_t k = 0;
+        const int64_t nwb = W1 - W0;
+        while (k < nwb) {
+            const int64_t first = upper ? W1 - 1 - k : W0 + k;
+            int64_t cnt = 0, bytes = 0;
+            for (;;) {
+                if (k + cnt >= nwb || cnt == 8) break;
+                const int64_t w = upper ? W1 - 1 - (k + cnt) : W0 + k + cnt;
+                // the super-window's rows if w joins: [lo, hi)
+                const int64_t lo = upper ? wrow[w] : wrow[first], hi = upper ? wend[first] : wend[w];
+                const int64_t add = TRI * 8 + win_near(w, lo, hi) * 64 * 12;
+                if (cnt > 0 && bytes + add > budget) break;
+                bytes += add;
+                ++cnt;
+            }
+            const int64_t last = upper ? W1 - 1 - (k + cnt - 1) : W0 + k + cnt - 1;
+            const int64_t wlo = std::min(first, last);
+            sw.push_back(wlo);  // first window (ascending storage)
+            sw.push_back(cnt);
+            sw.push_back(wrow[wlo] - bst[b]);
+            sw.push_back(wend[std::max(first, last)] - bst[b]);
+            for (int64_t w = wlo; w < wlo + cnt; ++w) swof[w] = (int64_t)sw.size() / 4 - 1;
+            max_stage = std::max(max_stage, bytes);
+            k += cnt;
+        }
+        bsw[b + 1] = (int64_t)sw.size() / 4;
+    }
+    const int64_t nsw = (int64_t)sw.size() / 4;
+    // per-window stream sizes
+    std::vector<int64_t> wnear(nw + 1, 0), wfar(nw + 1, 0);
+    {
+        std::vector<int64_t> kn(nw), kf(nw);
+        amgh::parallel_rows(nw, amgh::setup_threads(), [&](int, int64_t w0, int64_t w1) {
+            for (int64_t w = w0; w < w1; ++w) {
+                const int64_t s = swof[w], b = wblk[w];
+                const int64_t lo = bst[b] + sw[4 * s + 2], hi = bst[b] + sw[4 * s + 3];
+                int64_t a = 0, f = 0;
+                for (int64_t i = wrow[w]; i < wend[w]; ++i) {
+                    int64_t nn, nf;
+                    counts(i, w, lo, hi, nn, nf);
+                    a = std::max(a, nn);
+                    f = std::max(f, nf);
+                }
+                kn[w] = a;
+                kf[w] = f;
+            }
+        });
+        for (int64_t w = 0; w < nw; ++w) {
+            wnear[w + 1] = wnear[w] + kn[w] * 64;
+            wfar[w + 1] = wfar[w] + kf[w] * 64;
+        }
+    }
+    std::vector<int32_t> ncol(std::max<int64_t>(wnear[nw], 1), 0), fcol(std::max<int64_t>(wfar[nw], 1), 0);
+    std::vector<double> nval(ncol.size(), 0.0), fval(fcol.size(), 0.0), tinv((size_t)std::max<int64_t>(nw, 1) * TRI, 0.0);
+    amgh::parallel_rows(nw, amgh::setup_threads(), [&](int, int64_t w0, int64_t w1) {
+        std::vector<double> T(64 * 64), X(64 * 64);
+        for (int64_t w = w0; w < w1; ++w) {
+            const int64_t s = swof[w], b = wblk[w], base = bst[b];
+            const int64_t lo = base + sw[4 * s + 2], hi = base + sw[4 * s + 3];
+            const int64_t r0 = wrow[w], m = wend[w] - r0;
+            std::fill(T.begin(), T.end(), 0.0);
+            for (int64_t i = r0; i < wend[w]; ++i) {
+                const int lane = (int)(i - r0);
+                int64_t s0, s1, qn = 0, qf = 0;
+                side(i, s0, s1);
+                if (!upper) T[lane * 64 + lane] = 1.0;
+                for (int64_t k = s0; k < s1; ++k) {
+                    const int64_t cc = ci[k];
+                    if (cc >= r0 && cc < wend[w]) {
+                        T[lane * 64 + (cc - r0)] = fv[k];
+                    } else if (cc >= lo && cc < hi) {
+                        ncol[wnear[w] + qn * 64 + lane] = (int32_t)(cc - lo);
+                        nval[wnear[w] + qn * 64 + lane] = fv[k];
+                        ++qn;
+                    } else {
+                        fcol[wfar[w] + qf * 64 + lane] = (int32_t)(cc - base);
+                        fval[wfar[w] + qf * 64 + lane] = fv[k];
+                        ++qf;
+                    }
+                }
+                if (upper) T[lane * 64 + lane] = fv[dg[i]];
+            }
+            std::fill(X.begin(), X.end(), 0.0);
+            if (!upper) {  // X = T^-1, T unit lower
+                for (int64_t i = 0; i < m; ++i) {
+                    X[i * 64 + i] = 1.0;
+                    for (int64_t j = 0; j < i; ++j) {
+                        double acc = 0.0;
+                        for (int64_t k = j; k < i; ++k) acc += T[i * 64 + k] * X[k * 64 + j];
+                        X[i * 64 + j] = -acc;
+                    }
+                }
+            } else {  // T upper with its diagonal
+                for (int64_t i = m - 1; i >= 0; --i) {
+                    const double d = T[i * 64 + i];
+                    X[i * 64 + i] = 1.0 / d;
+                    for (int64_t j = i + 1; j < m; ++j) {
+                        double acc = 0.0;
+                        for (int64_t k = i + 1; k <= j; ++k) acc += T[i * 64 + k] * X[k * 64 + j];
+                        X[i * 64 + j] = -acc / d;
+                    }
+                }
+            }
+            // packed by column k: L -- rows k..63 at 64k - k(k-1)/2 + (row - k); U -- rows 0..k at k(k+1)/2 + row
+            double *t = &tinv[(size_t)w * TRI];
+            for (int64_t k = 0; k < 64; ++k) {
+                if (!upper)
+                    for (int64_t i = k; i < 64; ++i) t[64 * k - k * (k - 1) / 2 + (i - k)] = X[i * 64 + k];
+                else
+                    for (int64_t i = 0; i <= k; ++i) t[k * (k + 1) / 2 + i] = X[i * 64 + k];
+            }
+        }
+    });
+    auto up = [&](auto &d, const auto &v) {
+        d.alloc(std::max<size_t>(v.size(), 1));
+        if (!v.empty()) HIPCHK(hipMemcpyAsync(d.p, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice, c.st));
+    };
+    up(W.bsw, bsw);
+    up(W.sw, sw);
+    up(W.wnear, wnear);
+    up(W.wfar, wfar);
+    up(W.ncol, ncol);
+    up(W.nval, nval);
+    up(W.fcol, fcol);
+    up(W.fval, fval);
+    up(W.tinv, tinv);
+    c.sync();
+    W.nwin = nw;
+    W.nsw = nsw;
+    W.lds_bytes = 576 * 8 + max_stage;  // (the kernel's rows + broadcast slots, then the staged data)
+}
+
 static int64_t build_chain_tri(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
                                const std::vector<int32_t> &ci, const std::vector<int64_t> &dg,
                                const std::vector<double> &fv, const std::vector<double> &dinv,
@@ -1517,8 +1712,25 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         nlev_U = (int64_t)gU.size() - 1;
         use_lds = (allow_lds && fits_lds) || gmem;
         lds_gmem = gmem;
+        // the super-window sweep: y-resident blocks (pls.sweep_swin; default where
+        // the ring sweep would run)
+        if (gmem && c.sweep_swin != 0 && (c.sweep_swin == 1 || ring_mode != 0)) {
+            const std::vector<int64_t> bst = block_starts(n, nblocks, bnd);
+            std::vector<double> fv(F.nnz);
+            if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
+            c.sync();
+            build_swin_tri(nblocks, bst, rp, ci, dg, fv, false, Lsw, c);
+            build_swin_tri(nblocks, bst, rp, ci, dg, fv, true, Usw, c);
+            std::vector<int64_t> wf(nblocks + 1, 0);
+            for (int64_t b = 0; b < nblocks; ++b) wf[b + 1] = wf[b] + (bst[b + 1] - bst[b] + 63) / 64;
+            wstart.alloc(nblocks + 1);
+            HIPCHK(hipMemcpyAsync(wstart.p, wf.data(), sizeof(int64_t) * (nblocks + 1), hipMemcpyHostToDevice, c.st));
+            c.sync();
+            swin = true;
+            mark("super-window tables");
+        }
         // the ring sweep: y-resident blocks whose every level fits one chunk
-        if (gmem && ring_mode != 0) {
+        if (gmem && ring_mode != 0 && !swin) {
             int64_t wmax = 0;
             for (const auto *g : {&gL, &gU})
                 for (size_t k = 0; k + 1 < g->size(); ++k) wmax = std::max<int64_t>(wmax, (*g)[k + 1] - (*g)[k]);
@@ -1566,7 +1778,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                 build_chain_tri(nblocks, bst, rp, ci, dg, fv, dv, oU, gU, fU, true, &Uc, c);
             }
         }
-        if (use_lds && !chain && !window) {
+        if (use_lds && !chain && !window && !swin) {
             const int max_lpr = gmem ? (ring ? 32 : 16) : 4;
             std::vector<int32_t> pL, pU, loL, loU, nlL, nlU;
             if (ring) {
@@ -1647,16 +1859,18 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                 sweep_kind());
 }
 
-void PCILU::apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64_t b_hi, int rr_group) {
+void PCILU::apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64_t b_hi, int rr_group, int tpb,
+                         int depth, int64_t *prof) {
     if (!can_apply_blocks()) throw Error("PCILU: block subsets need the LDS sweep");
     const int rr = rr_group > 0 ? rr_group : (lds_rr ? 1 : 0);
     launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
-                          Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, nullptr, false, lds_tpb, rr,
-                          bstart_h.empty() ? nullptr : bstart.p, max_len, b_lo, b_hi);
+                          Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof, false,
+                          tpb > 0 ? tpb : lds_tpb, rr, bstart_h.empty() ? nullptr : bstart.p, max_len, b_lo, b_hi, depth);
 }
 
 const char *PCILU::sweep_kind() const {
     if (!use_lds) return csr_levels ? "levels-csr" : "levels";
+    if (swin) return "swin";
     if (ring) return "ring";
     if (window) return "window";
     if (chain) return "chain";
@@ -1664,6 +1878,13 @@ const char *PCILU::sweep_kind() const {
 }
 
 void PCILU::apply(const double *x, double *y, Ctx &c) {
+    if (use_lds && swin) {
+        launch_ilu_blocks_swin(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lsw.bsw.p, Lsw.sw.p,
+                               Lsw.wnear.p, Lsw.ncol.p, Lsw.nval.p, Lsw.wfar.p, Lsw.fcol.p, Lsw.fval.p, Lsw.tinv.p,
+                               Usw.bsw.p, Usw.sw.p, Usw.wnear.p, Usw.ncol.p, Usw.nval.p, Usw.wfar.p, Usw.fcol.p,
+                               Usw.fval.p, Usw.tinv.p, x, y, std::max(Lsw.lds_bytes, Usw.lds_bytes), c.st);
+        return;
+    }
     if (use_lds && ring) {
         auto &sc = ring_scratch[c.st];  // per stream: the concurrent 3-way sweeps share this PC
         if (sc.first.n < (size_t)n) {
@@ -2280,6 +2501,7 @@ void KSP::solve(const double *b, double *x, Ctx &c) {
     stat_its += its;
     stat_max = std::max<int64_t>(stat_max, its);
     ++stat_solves;
+    stat_div += reason < 0 ? 1 : 0;
     c.check_bounds();
 }
 
@@ -2525,6 +2747,27 @@ void upload(const HostCSR &H, DevCSR &M, Ctx &c) {
 // pinned staging buffers, each chunk spread back by host threads (a pageable
 // hipMemcpy of the N=59 s block's 5.1 GB ran at ~5 GB/s)
 namespace {
+// pinned staging buffers and their events, released on every path (a HIPCHK
+// that throws mid-copy must not leak them: ADVICE r04)
+struct Staging {
+    void *buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    explicit Staging(size_t bytes) {
+        for (int b = 0; b < 2; ++b) {
+            HIPCHK(hipHostMalloc(&buf[b], bytes, hipHostMallocDefault));
+            HIPCHK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
+        }
+    }
+    ~Staging() {
+        for (int b = 0; b < 2; ++b) {
+            if (ev[b]) (void)hipEventDestroy(ev[b]);
+            if (buf[b]) (void)hipHostFree(buf[b]);
+        }
+    }
+    Staging(const Staging &) = delete;
+    Staging &operator=(const Staging &) = delete;
+};
+
 void d2h_staged(void *dst, const void *src, size_t bytes, Ctx &c) {
     const size_t CH = (size_t)64 << 20;
     if (bytes < 2 * CH) {
@@ -2532,35 +2775,26 @@ void d2h_staged(void *dst, const void *src, size_t bytes, Ctx &c) {
         c.sync();
         return;
     }
-    void *stg[2] = {nullptr, nullptr};
-    hipEvent_t ev[2];
-    for (int b = 0; b < 2; ++b) {
-        HIPCHK(hipHostMalloc(&stg[b], CH, hipHostMallocDefault));
-        HIPCHK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
-    }
+    Staging S(CH);
     const size_t nch = (bytes + CH - 1) / CH;
     auto issue = [&](size_t k) {
         const size_t off = k * CH, len = std::min(CH, bytes - off);
-        HIPCHK(hipMemcpyAsync(stg[k & 1], (const char *)src + off, len, hipMemcpyDeviceToHost, c.st));
-        HIPCHK(hipEventRecord(ev[k & 1], c.st));
+        HIPCHK(hipMemcpyAsync(S.buf[k & 1], (const char *)src + off, len, hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipEventRecord(S.ev[k & 1], c.st));
     };
     issue(0);
     const int T = 8;
     for (size_t k = 0; k < nch; ++k) {
         if (k + 1 < nch) issue(k + 1);  // (the other buffer: its copy-out finished below)
-        HIPCHK(hipEventSynchronize(ev[k & 1]));
+        HIPCHK(hipEventSynchronize(S.ev[k & 1]));
         const size_t off = k * CH, len = std::min(CH, bytes - off);
         std::vector<std::thread> th;
         for (int t = 0; t < T; ++t)
             th.emplace_back([&, t] {
                 const size_t a = len * t / T, b = len * (t + 1) / T;
-                std::memcpy((char *)dst + off + a, (const char *)stg[k & 1] + a, b - a);
+                std::memcpy((char *)dst + off + a, (const char *)S.buf[k & 1] + a, b - a);
             });
         for (auto &x : th) x.join();
-    }
-    for (int b = 0; b < 2; ++b) {
-        HIPCHK(hipEventDestroy(ev[b]));
-        HIPCHK(hipHostFree(stg[b]));
     }
 }
 }  // namespace
@@ -2569,12 +2803,20 @@ HostCSR download(const DevCSR &M, Ctx &c) {
     HostCSR H;
     H.nrows = M.nrows;
     H.ncols = M.ncols;
-    std::thread tci([&] { H.ci.resize(M.nnz); }), tv([&] { H.v.resize(M.nnz); });
     H.rp.resize(M.nrows + 1);
-    HIPCHK(hipMemcpyAsync(H.rp.data(), M.rp.p, sizeof(int64_t) * (M.nrows + 1), hipMemcpyDeviceToHost, c.st));
-    c.sync();
-    tci.join();
-    tv.join();
+    {
+        // (joined on every path: a HIPCHK that throws below must not destroy joinable threads)
+        std::thread tci([&] { H.ci.resize(M.nnz); }), tv([&] { H.v.resize(M.nnz); });
+        struct Join {
+            std::thread &a, &b;
+            ~Join() {
+                if (a.joinable()) a.join();
+                if (b.joinable()) b.join();
+            }
+        } join{tci, tv};
+        HIPCHK(hipMemcpyAsync(H.rp.data(), M.rp.p, sizeof(int64_t) * (M.nrows + 1), hipMemcpyDeviceToHost, c.st));
+        c.sync();
+    }
     if (M.nnz) {
         d2h_staged(H.ci.data(), M.ci.p, sizeof(int32_t) * M.nnz, c);
         d2h_staged(H.v.data(), M.val.p, sizeof(double) * M.nnz, c);

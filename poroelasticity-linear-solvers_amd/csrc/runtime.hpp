@@ -83,6 +83,8 @@ struct Ctx {
     int sweep_window = -1;        // ... in 64-row windows with inverted window triangles (k_ilu_blocks_window):
                                   // -1 where the chain sweep would be chosen, 0 never, 1 whenever rows fit
     int ilu_view = 0;             // print every ILU / Gauss-Seidel PC's sweep choice to stderr (pls.ilu_view)
+    int sweep_swin = -1;          // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin):
+                                  // -1 where the ring sweep would run, 0 never, 1 whenever the block is y-resident
     double amg_csr_below = 16.0;  // AMG operators with fewer entries per row than this stay CSR (pls.amg_csr_below)
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)
@@ -193,7 +195,7 @@ void classify_halo_slices(DevCSR &M, Ctx &c);
 void spmv(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha = 1.0, double beta = 0.0,
           const double *z = nullptr);
 void spmv_slices(const DevCSR &M, const double *x, double *y, Ctx &c, double alpha, double beta, const double *z,
-                 const int32_t *slist, int64_t count);
+                 const int32_t *slist, int64_t count, size_t lds_reserve = 0);
 
 // Host copy of a CSR matrix (setup-time algebra: fieldsplit blocks, AMG hierarchy).
 // std::allocator whose value-initialisation is default-initialisation: a
@@ -360,8 +362,23 @@ struct WinTri {
     DBuf<double> val, tinv;  // tinv: per window the 64 x 64 inverse of its diagonal block, [k][lane]
     int64_t nwin = 0;
 };
+// Super-window sweep tables of one triangle (kernels.hip, k_ilu_blocks_swin):
+// blocks too long for LDS, in windows of 64 rows grouped into super-windows
+// whose window inverses and near streams fit LDS (see build_swin_tri)
+struct SwinTri {
+    DBuf<int64_t> bsw;         // per block: first super-window (nblocks + 1), in processing order
+    DBuf<int64_t> sw;          // per super-window: first window (global), windows, first row, end row (block-local)
+    DBuf<int64_t> wnear, wfar;  // per window: near / far SELL offsets (nwin + 1)
+    DBuf<int32_t> ncol, fcol;  // near: row - super-window's first row (LDS index); far: block-local row
+    DBuf<double> nval, fval;
+    DBuf<double> tinv;  // per window the packed triangle of the window inverse (2080 doubles)
+    int64_t lds_bytes = 0, nwin = 0, nsw = 0;
+};
 struct PCILU : PC {
     int64_t nblocks = 1;
+    // super-window sweep (Ctx::sweep_swin): blocks too long for LDS
+    bool swin = false;
+    SwinTri Lsw, Usw;
     // window sweep (Ctx::sweep_window): LDS-resident blocks in 64-row windows with
     // explicit inverses of the windows' triangles (one GEMV per window)
     bool window = false;
@@ -415,10 +432,12 @@ struct PCILU : PC {
     // first row of every block, host copies made at setup
     std::vector<int64_t> block_levels_h, block_start_h, block_maxsl_h;  // maxsl: most slices of any level
     bool can_apply_blocks() const {
-        return use_lds && !ring && !window && !chain && !lds_gmem && profile_tag.empty() && !exact && !sgs;
+        return use_lds && !ring && !window && !chain && !swin && !lds_gmem && profile_tag.empty() && !exact && !sgs;
     }
     // rr_group > 0: the round-robin sweep with groups of that many waves per level (a power of two)
-    void apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64_t b_hi, int rr_group = 0);
+    // tpb > 0: threads per workgroup for this launch; depth: levels of factor data in flight (2, or 6 with tpb <= 512)
+    void apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64_t b_hi, int rr_group = 0, int tpb = 0,
+                      int depth = 2, int64_t *prof = nullptr);  // prof: nblocks x 8 wall-clock records (diagnostics)
 };
 // Exact LU of a block small enough for a dense inverse (dense.hip): K^-1 is
 // formed once (blocked Gauss-Jordan, no pivoting, like the sparse path) and
@@ -495,7 +514,7 @@ struct KSP {
     bool monitor = false;
     // pls.ksp_stats: iteration totals printed when the KSP is destroyed (diagnostics)
     bool stats = false;
-    int64_t stat_its = 0, stat_max = 0, stat_solves = 0;
+    int64_t stat_its = 0, stat_max = 0, stat_solves = 0, stat_div = 0;  // stat_div: solves with reason < 0
     KSP() = default;
     KSP(const KSP &) = delete;
     ~KSP();

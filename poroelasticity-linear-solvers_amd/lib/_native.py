@@ -47,6 +47,7 @@ EXPORTS = [
     "pls_comm_destroy", "pls_create_synthetic_dist", "pls_spmv_layout", "pls_update_matrices",
     "pls_bench_copy", "pls_create_dist", "pls_bench_global_sum", "pls_anderson_create",
     "pls_anderson_next", "pls_anderson_destroy", "pls_boomeramg_host_level", "pls_sparse_lu_analyze",
+    "pls_get_ksp_stats",
 ]
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p)
@@ -86,6 +87,7 @@ def lib():
     L.pls_get_result.argtypes = [vp, C.POINTER(pls_result)]
     L.pls_get_history.argtypes = [vp, vp, i32]
     L.pls_get_timings.argtypes = [vp, C.POINTER(pls_timings)]
+    L.pls_get_ksp_stats.argtypes = [vp, C.c_char_p, vp]
     L.pls_export_matrix.argtypes = [vp, C.c_int, C.POINTER(i64), C.POINTER(i64), vp, vp, vp]
     L.pls_get_permutation.argtypes = [vp, vp]
     L.pls_bench_spmv.argtypes = [vp, vp, vp, i32, C.POINTER(C.c_double)]

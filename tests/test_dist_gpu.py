@@ -159,6 +159,29 @@ FE_CASES = [
 ]
 
 
+# G = 4 and 8 ranks (the north star's bar is its-exact at 8 GPUs;
+# paper-scripts/robustness_2d.sh:9,29 runs mpirun -np 8): BJACOBI 2-way,
+# BoomerAMG's np = G hierarchy (C/F relaxation, 3-way), AAR m = 5, and the
+# bench's --inner hypre shape (BoomerAMG on the s block, BJACOBI on fp) at
+# 3-D N = 10, whose coarsest levels leave ranks without rows
+_HYPRE_INEXACT = {"ksp_type": "preonly", "pc_type": "hypre", "pc_hypre_boomeramg_P_max": "4",
+                  "pc_hypre_boomeramg_agg_nl": "1", "pc_hypre_boomeramg_agg_num_paths": "2"}
+BIG_CASES = [
+    {"name": "big_twoway_3d", "dim": 3, "N": 6, "params": BASE, "db": _db({"s_": 8, "fp_": 8})},
+    {"name": "big_hypre_cf_3way_3d", "dim": 3, "N": 4, "params": dict(BASE, **{"pc type": "diagonal 3-way"}),
+     "pc_tol": 1e-12, "db": dict({"global_ksp_type": "gmres", "global_ksp_pc_side": "right"},
+                                 **{pre + k: v for pre in ("s_", "f_", "p_", "diff_") for k, v in _HYPRE_INEXACT.items()})},
+    {"name": "big_aar_m5_3d", "dim": 3, "N": 6,
+     "params": dict(BASE, **{"solver type": "aar", "solver maxiter": 200, "AAR order": 5, "AAR p": 5}),
+     "db": _db({"s_": 8, "fp_": 8})},
+    {"name": "big_hypre_s_bjacobi_fp_3d", "dim": 3, "N": 10, "pc_tol": 1e-12,
+     "params": dict(BASE, **{"solver rtol": 1e-6, "solver atol": 1e-8}),
+     "db": dict({"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "fp_ksp_type": "preonly",
+                 "fp_pc_type": "bjacobi", "fp_pc_bjacobi_blocks": "16"},
+                **{"s_" + k: v for k, v in dict(_HYPRE_INEXACT, pc_hypre_boomeramg_no_CF="true").items()})},
+]
+
+
 def _oracle(case, G):
     spec = S.SynthSpec(case["dim"], case["N"])
     A, P, Pd = S.matrix(spec, 0), S.matrix(spec, 1), S.matrix(spec, 2)
@@ -174,8 +197,23 @@ def ranks(request, tmp_path_factory):
     return G, launch("gpu", CASES + FE_CASES, G, str(tmp_path_factory.mktemp(f"dist{G}")), timeout=900)
 
 
+@pytest.fixture(scope="module", params=[4, 8])
+def ranks_big(request, tmp_path_factory):
+    G = request.param
+    return G, launch("gpu", BIG_CASES, G, str(tmp_path_factory.mktemp(f"distbig{G}")), timeout=900)
+
+
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_dist_solve(ranks, case):
+    _check_dist_solve(ranks, case)
+
+
+@pytest.mark.parametrize("case", BIG_CASES, ids=[c["name"] for c in BIG_CASES])
+def test_dist_solve_g4_g8(ranks_big, case):
+    _check_dist_solve(ranks_big, case)
+
+
+def _check_dist_solve(ranks, case):
     G, res = ranks
     parts = res[case["name"]]
     spec, A, o = _oracle(case, G)

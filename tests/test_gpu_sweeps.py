@@ -129,3 +129,54 @@ def test_fp_pipeline_bitwise(gpu, capfd, N, blocks):
     assert np.array_equal(a[1], b_[1])
     assert a[2] == b_[2] and a[3] == b_[3]
     assert np.array_equal(a[4], b_[4])
+
+
+def _fe_apply(s, two_way, extra):
+    from lib.handle import Handle, params_to_options
+    params = dict(PARAMS, **{"pc type": "diagonal" if two_way else "diagonal 3-way"})
+    db = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "pls.ilu_view": "1"}
+    for pre in (("s_", "fp_") if two_way else ("s_", "f_", "p_", "diff_")):
+        db[pre + "ksp_type"] = "preonly"
+        db[pre + "pc_type"] = "ilu"
+    opts = dict(db, **extra)
+    opts.update(params_to_options(params))
+    h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    x = np.random.default_rng(8).standard_normal(s.A.shape[0])
+    y = h.pc_apply(x)
+    h.destroy()
+    o = OracleSolver(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, params,
+                     {k: v for k, v in db.items() if not k.startswith("pls.")}, s.bcs_sub_pressure)
+    return y, o.block_pc.apply(x)
+
+
+@pytest.mark.parametrize("N,gmem", [(4, "1"), (12, "0")])
+def test_swin_sweep_matches_oracle(gpu, capfd, N, gmem):
+    """Whole-block ILU(0) on assembled 3-D swelling blocks through the super-
+    window sweep (pls.sweep_swin 1: 64-row windows with explicit inverses,
+    near terms from LDS, far terms from the block solution in global memory;
+    lib/Preconditioner.py:94-100's ILU).  N = 4 with every block forced
+    y-resident (pls.ilu_gmem 1), N = 12 at its size (s 46,875 / fp 49,072
+    rows, beyond LDS).  Bar: the window inverses reassociate the sums, <= 1e-12
+    of max |y| against the oracle; the ring sweep (pls.sweep_swin 0) on the
+    same blocks as a second reference."""
+    from lib.fe_swelling import assemble_swelling
+    s = assemble_swelling(3, N, "diagonal")
+    capfd.readouterr()
+    ysw, yo = _fe_apply(s, True, {"pls.sweep_swin": "1", "pls.ilu_gmem": gmem})
+    err = capfd.readouterr().err
+    kinds = [ln for ln in err.splitlines() if ln.startswith("[pls ilu]")]
+    assert kinds and all("sweep swin" in ln for ln in kinds), kinds
+    yr, _ = _fe_apply(s, True, {"pls.sweep_swin": "0", "pls.ilu_gmem": gmem})
+    scale = np.max(np.abs(yo))
+    assert np.max(np.abs(ysw - yo)) <= 1e-12 * scale
+    assert np.max(np.abs(ysw - yr)) <= 1e-12 * scale
+
+
+def test_swin_sweep_three_way(gpu, capfd):
+    """3-way (FS and DIFF sweeps on two streams share the s / f PCs: the super-
+    window sweep must be reentrant) on the 3-D N=4 system, every block forced
+    y-resident."""
+    from lib.fe_swelling import assemble_swelling
+    s = assemble_swelling(3, 4, "diagonal 3-way")
+    ysw, yo = _fe_apply(s, False, {"pls.sweep_swin": "1", "pls.ilu_gmem": "1"})
+    assert np.max(np.abs(ysw - yo)) <= 1e-12 * np.max(np.abs(yo))
