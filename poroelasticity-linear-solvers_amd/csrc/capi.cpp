@@ -542,6 +542,7 @@ struct Handle {
         ctx.d16_segs = (int)opt.integer("pls.d16_segs", D16_SEG);  // 8: force the halo layout (tests)
         if (ctx.d16_segs != D16_SEG && ctx.d16_segs != D16_SEG_MAX) throw Error("pls.d16_segs must be 4 or 8");
         set_d16_xcd((int)opt.integer("pls.d16_xcd", 0));  // process-wide (tuning)
+        set_spmv_short_rows(opt.flag("pls.spmv_short", true));  // process-wide
         if (opt.integer("pls.ring_probe", 0)) set_ring_probe((int)opt.integer("pls.ring_probe", 0));  // diagnostics
         ctx.d16_sigma = (int)opt.integer("pls.d16_sigma", 1024);
         if (ctx.d16_sigma < 0 || ctx.d16_sigma % 64) throw Error("pls.d16_sigma must be a multiple of 64 (0: off)");

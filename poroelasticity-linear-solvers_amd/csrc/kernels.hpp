@@ -48,6 +48,7 @@ void launch_extract_fill(const int64_t *rp, const int32_t *ci, const double *val
                          int32_t *out_ci, double *out_val, hipStream_t st);
 
 // y = alpha * (M x) + beta * z     (z may be null when beta == 0)
+void set_spmv_short_rows(bool on);  // CSR rows of < 12 entries: one lane per row (default on; pls.spmv_short)
 void launch_spmv(int64_t nrows, int64_t nnz, const int64_t *rp, const int32_t *ci,
                  const double *val, const double *x, double *y, double alpha, double beta,
                  const double *z, hipStream_t st);

@@ -2476,13 +2476,16 @@ void KSP::ensure_work(Ctx &c) {
 }
 
 int KSP::converged(int it, double r) {
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     if (it == 0) {
         rnorm0 = r;
         ttol = std::max(rtol * rnorm0, atol);
+        if (time_limit > 0) t_start = now();
     }
     if (std::isnan(r) || std::isinf(r)) return DIVERGED_NANORINF;
     if (r <= ttol) return r < atol ? CONVERGED_ATOL : CONVERGED_RTOL;
     if (r >= dtol * rnorm0) return DIVERGED_DTOL;
+    if (time_limit > 0 && it > 0 && now() - t_start > time_limit) return DIVERGED_TIME_LIMIT;
     return CONVERGED_ITERATING;
 }
 
@@ -2716,6 +2719,7 @@ std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const
     k->restart = o.integer(prefix + "ksp_gmres_restart", restart);
     k->monitor = o.has(prefix + "ksp_monitor");
     k->stats = o.flag("pls.ksp_stats", false);
+    if (prefix == "global_") k->time_limit = o.num("pls.solver_time_limit", 0.0);
     if (o.has(prefix + "ksp_gmres_modifiedgramschmidt") && k->type == "gmres")
         throw Error(prefix + "ksp_gmres_modifiedgramschmidt: only classical Gram-Schmidt is implemented");
     k->resolve_side_norm(o.str(prefix + "ksp_pc_side", ""), o.str(prefix + "ksp_norm_type", ""));

@@ -492,7 +492,8 @@ void boomeramg_host_level(const HostCSR &A, const Options &o, const std::string 
 enum Reason {
     CONVERGED_ITERATING = 0, CONVERGED_RTOL = 2, CONVERGED_ATOL = 3, CONVERGED_ITS = 4,
     DIVERGED_NULL = -2, DIVERGED_ITS = -3, DIVERGED_DTOL = -4, DIVERGED_BREAKDOWN = -5,
-    DIVERGED_INDEFINITE_PC = -8, DIVERGED_NANORINF = -9, DIVERGED_INDEFINITE_MAT = -10  // petscksp.h
+    DIVERGED_INDEFINITE_PC = -8, DIVERGED_NANORINF = -9, DIVERGED_INDEFINITE_MAT = -10,  // petscksp.h
+    DIVERGED_TIME_LIMIT = -100  // libpls diagnostic (pls.solver_time_limit), not a PETSc reason
 };
 
 struct KSP {
@@ -514,6 +515,8 @@ struct KSP {
     bool monitor = false;
     // pls.ksp_stats: iteration totals printed when the KSP is destroyed (diagnostics)
     bool stats = false;
+    double time_limit = 0;  // seconds (pls.solver_time_limit, the outer solver only; 0: none)
+    double t_start = 0;
     int64_t stat_its = 0, stat_max = 0, stat_solves = 0, stat_div = 0;  // stat_div: solves with reason < 0
     KSP() = default;
     KSP(const KSP &) = delete;

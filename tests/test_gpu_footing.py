@@ -109,7 +109,8 @@ def test_footing_full_solve_properties(gpu):
     estimate (a linear PC).  footing.py's own AMG set is parity-tested at
     N = 8 above; at N = 32 its device solve exceeded the test budget (the
     classical AMG's latency-bound level sweeps), and configs[2]'s
-    N = 128 is bench-only (setup 263 s)."""
+    N = 128 is bench-only (setup ~18 s since round 4; a solve to 500 its
+    takes ~270 s)."""
     from lib.handle import Handle, params_to_options
     s = FF.assemble_footing(32, "undrained")
     assert s.A.shape[0] == 79_104

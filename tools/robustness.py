@@ -80,7 +80,7 @@ def assemble(problem: str, N: int, pc: str):
 
 
 def run_case(problem: str, N: int, pc: str, optset: str, nranks: int, extra: dict | None = None,
-             oracle: bool = False) -> dict:
+             oracle: bool = False, history: bool = False) -> dict:
     from lib import options as popts
     from lib.IndexSet import IndexSet
     from lib.Preconditioner import Preconditioner
@@ -106,7 +106,21 @@ def run_case(problem: str, N: int, pc: str, optset: str, nranks: int, extra: dic
     t_setup = time.time() - t1
     x = np.zeros_like(b)
     t2 = time.time()
-    solver.solve(b, x)
+    # heartbeat while the library solves (ctypes releases the GIL): long cases
+    # must keep writing or the GPU harness takes them for hung
+    import threading
+    done = threading.Event()
+
+    def beat():
+        while not done.wait(30):
+            print(f"[robustness] {problem} N={N} '{pc}' {optset}: solving, {time.time() - t2:.0f} s", flush=True)
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        solver.solve(b, x)
+    finally:
+        done.set()
+        th.join()
     t_solve = time.time() - t2
     h = pcobj.handle
     inner = {}
@@ -123,6 +137,8 @@ def run_case(problem: str, N: int, pc: str, optset: str, nranks: int, extra: dic
            "rnorm0": float(hist[0]) if hist.size else None, "rnorm": float(hist[-1]) if hist.size else None,
            "assembly_s": round(t_asm, 2), "setup_s": round(t_setup, 2), "solve_s": round(t_solve, 3),
            "inner": inner, "extra": extra or {}}
+    if history:
+        out["history"] = [float(v) for v in hist]
     h.destroy()
     if oracle:
         from oracle.solver import OracleSolver
@@ -146,11 +162,14 @@ def main():
     ap.add_argument("--np", type=int, default=8)
     ap.add_argument("--opt", action="append", default=[], help="extra library option key=value")
     ap.add_argument("--oracle", action="store_true")
+    ap.add_argument("--monitor", action="store_true", help="print every outer iteration's residual (-global_ksp_monitor)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "robustness.jsonl"))
     a = ap.parse_args()
     import lib._native as Nat
     Nat.check(Nat.lib().pls_set_device(0))
     extra = dict(kv.split("=", 1) for kv in a.opt)
+    if a.monitor:
+        extra["global_ksp_monitor"] = None
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     for optset in a.set:
         for N in a.N:
