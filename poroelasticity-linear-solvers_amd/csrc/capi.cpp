@@ -542,7 +542,7 @@ struct Handle {
         ctx.d16_segs = (int)opt.integer("pls.d16_segs", D16_SEG);  // 8: force the halo layout (tests)
         if (ctx.d16_segs != D16_SEG && ctx.d16_segs != D16_SEG_MAX) throw Error("pls.d16_segs must be 4 or 8");
         set_d16_xcd((int)opt.integer("pls.d16_xcd", 0));  // process-wide (tuning)
-        set_spmv_short_rows(opt.flag("pls.spmv_short", true));  // process-wide
+        set_spmv_short_rows(opt.flag("pls.spmv_short", false));  // process-wide (measured slower for the AMG's P)
         if (opt.integer("pls.ring_probe", 0)) set_ring_probe((int)opt.integer("pls.ring_probe", 0));  // diagnostics
         ctx.d16_sigma = (int)opt.integer("pls.d16_sigma", 1024);
         if (ctx.d16_sigma < 0 || ctx.d16_sigma % 64) throw Error("pls.d16_sigma must be a multiple of 64 (0: off)");
@@ -747,8 +747,16 @@ static void upload_permuted(const pls_csr *M, Handle &H, const std::vector<int64
 static void setup_fp_pipeline(Handle &H) {
     auto &F = H.fpp;
     F.on = false;
-    if (H.three_way || H.distributed || !H.opt.flag("pls.fp_pipeline", true)) return;
+    // pls.fp_pipeline: 1 always, 0 never, -1 (default) when the s block's PC is an
+    // ILU / BJACOBI sweep too.  Measured (MI355X, N=59, same box, A/B x 3): the
+    // BJACOBI headline 168.4 -> 169.8 it/s; with BoomerAMG on the s block 120 ->
+    // 114 it/s -- with the CU-masked queues present every kernel of the V-cycle's
+    // ~40 per iteration ran slower (small ones ~2-10x), which the pipeline's
+    // ~90 us per iteration does not repay
+    const int64_t mode = H.opt.integer("pls.fp_pipeline", -1);
+    if (H.three_way || H.distributed || mode == 0) return;
     if (!H.ksp_fp || H.ksp_fp->type != "preonly" || H.mixer.order > 0) return;
+    if (mode < 0 && !(H.ksp_s && H.ksp_s->type == "preonly" && dynamic_cast<PCILU *>(H.ksp_s->pc))) return;
     PCILU *pc = dynamic_cast<PCILU *>(H.ksp_fp->pc);
     if (!pc || !pc->can_apply_blocks() || pc->nblocks < 8 || pc->block_levels_h.size() != (size_t)pc->nblocks) return;
     const DevCSR &M = H.Mfp_s;

@@ -335,11 +335,12 @@ __global__ __launch_bounds__(TPB) void k_spmv(int64_t nrows, const int64_t *__re
     }
 }
 
-// Short rows (mean < 12 nnz: AMG interpolation P, ~7 per row): one lane per
-// row, entries in CSR order (scipy's per-row order), eight loads of each kind
-// issued before the x gathers.  With 8 lanes per row (k_spmv<8>) a wave held
-// only ~0.7 KB of loads behind three dependent round trips (row_ptr, then
-// entries, then x): the level-0 prolongation P e at N=59 ran at ~1.3 TB/s.
+// Short rows (mean < 12 nnz: AMG interpolation P, ~7 per row), opt-in
+// (pls.spmv_short 1): one lane per row, entries in CSR order (scipy's per-row
+// order), eight loads of each kind issued before the x gathers.  Measured
+// slower than 8 lanes per row (k_spmv<8>) on the N=59 level-0 prolongation
+// P e (561-596 vs ~400 us): a load instruction touches 64 rows' k-th entries,
+// ~84 cache lines, and the texture path issues them a few lanes per cycle.
 __global__ __launch_bounds__(TPB) void k_spmv_short(int64_t nrows, const int64_t *__restrict__ rp,
                                                     const int32_t *__restrict__ ci, const double *__restrict__ val,
                                                     const double *__restrict__ x, double *__restrict__ y,
@@ -471,7 +472,7 @@ __global__ __launch_bounds__(TPB) void k_spmv_wg(int64_t nrows, const int64_t *_
     }
 }
 
-static bool spmv_short_rows = true;
+static bool spmv_short_rows = false;
 void set_spmv_short_rows(bool on) { spmv_short_rows = on; }
 
 void launch_spmv(int64_t nrows, int64_t nnz, const int64_t *rp, const int32_t *ci, const double *val,
@@ -1058,7 +1059,7 @@ static constexpr int ILU0_STAGE = 4096;  // staged upper-part entries per row (4
 __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ rows, const int64_t *__restrict__ rp,
                                                    const int32_t *__restrict__ ci, double *__restrict__ lu,
                                                    const int64_t *__restrict__ diag, double *__restrict__ dinv,
-                                                   int32_t *fail, int max_row, int stage) {
+                                                   int32_t *fail, int max_row, int stage, int hbits) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x;
     const int64_t i = rows[blockIdx.x];
@@ -1072,9 +1073,25 @@ __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ r
     int32_t *sc = rc + max_row;
     int32_t *so = sc + stage;
     double *sd = reinterpret_cast<double *>(((uintptr_t)(so + max_row + 1) + 7) & ~(uintptr_t)7);
+    int64_t *su = reinterpret_cast<int64_t *>(sd + max_row);  // per pivot: first entry of its upper part
+    // column -> position hash of the row (open addressing, 2^hbits slots; hbits 0: binary search)
+    int32_t *hk = reinterpret_cast<int32_t *>(su + max_row);
+    int32_t *hp = hk + (1 << hbits);
+    const uint32_t hmask = (1u << hbits) - 1;
+    auto hslot = [&](int32_t c) { return ((uint32_t)c * 2654435761u) >> (32 - hbits); };
     for (int t = lane; t < len; t += 64) {
         rv[t] = lu[s + t];
         rc[t] = ci[s + t];
+    }
+    if (hbits > 0) {
+        for (int h = lane; h <= (int)hmask; h += 64) hk[h] = -1;
+        __syncthreads();
+        for (int t = lane; t < len; t += 64) {
+            const int32_t c = rc[t];
+            uint32_t h = hslot(c);
+            while (atomicCAS(&hk[h], -1, c) != -1) h = (h + 1) & hmask;
+            hp[h] = t;
+        }
     }
     __syncthreads();
     const int dl = (int)(diag[i] - s);
@@ -1084,9 +1101,11 @@ __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ r
         const int t = t0 + lane;
         int cnt = 0;
         double dv = 0.0;
+        int64_t u0 = 0;
         if (t < dl) {
             const int64_t r = rc[t];
-            cnt = (int)(rp[r + 1] - diag[r] - 1);
+            u0 = diag[r] + 1;
+            cnt = (int)(rp[r + 1] - u0);
             dv = dinv[r];
         }
         // inclusive wave scan of cnt
@@ -1099,6 +1118,7 @@ __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ r
         if (t < dl) {
             so[t] = total + inc - cnt;
             sd[t] = dv;
+            su[t] = u0;
         }
         total += __shfl(inc, 63);
     }
@@ -1106,20 +1126,41 @@ __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ r
     if (lane == 0 && stage > 0) so[dl] = total;
     __syncthreads();
     if (staged) {
-        for (int t = 0; t < dl; ++t) {
-            const int64_t r = rc[t];
-            const int64_t us = diag[r] + 1;
-            const int o = so[t], m = so[t + 1] - o;
-            for (int k = lane; k < m; k += 64) {
-                sc[o + k] = ci[us + k];
-                sv[o + k] = lu[us + k];
+        // every staged entry's source, eight per lane in flight: entry q belongs to
+        // the pivot t with so[t] <= q < so[t + 1] (binary search in LDS)
+        for (int q0 = 0; q0 < total; q0 += 8 * 64) {
+            int64_t src[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = q0 + u * 64 + lane;
+                int lo = 0, hi = dl;  // last t with so[t] <= q
+                while (hi - lo > 1) {
+                    const int m = (lo + hi) >> 1;
+                    if (so[m] <= q) lo = m; else hi = m;
+                }
+                src[u] = q < total ? su[lo] + (q - so[lo]) : su[0];
+            }
+            int32_t cv[8];
+            double vv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cv[u] = ci[src[u]];
+                vv[u] = lu[src[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = q0 + u * 64 + lane;
+                if (q < total) {
+                    sc[q] = cv[u];
+                    sv[q] = vv[u];
+                }
             }
         }
         __syncthreads();
     }
+    // (one wave: its LDS accesses complete in order, so no barrier between pivots)
     for (int t = 0; t < dl; ++t) {
         const double pc = rv[t];
-        __syncthreads();
         if (pc != 0.0) {
             const int64_t r = rc[t];
             const double mult = pc * (staged ? sd[t] : dinv[r]);
@@ -1127,17 +1168,29 @@ __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ r
             const int64_t us = staged ? so[t] : diag[r] + 1, ue = staged ? so[t + 1] : rp[r + 1];
             for (int64_t kk = us + lane; kk < ue; kk += 64) {
                 const int32_t j = staged ? sc[kk] : ci[kk];
-                // search j in rc[t+1, len)
-                int lo = t + 1, hi = len;
-                while (lo < hi) {
-                    const int m = (lo + hi) >> 1;
-                    if (rc[m] < j) lo = m + 1; else hi = m;
+                int lo = len;
+                if (hbits > 0) {  // the column's position in the row (hash)
+                    uint32_t h = hslot(j);
+                    int32_t key = hk[h];
+                    while (key != j && key != -1) {
+                        h = (h + 1) & hmask;
+                        key = hk[h];
+                    }
+                    if (key == j) lo = hp[h];
+                } else {  // search j in rc[t+1, len)
+                    int a = t + 1, b = len;
+                    while (a < b) {
+                        const int m = (a + b) >> 1;
+                        if (rc[m] < j) a = m + 1; else b = m;
+                    }
+                    if (a < len && rc[a] == j) lo = a;
                 }
-                if (lo < len && rc[lo] == j) rv[lo] = rv[lo] - mult * (staged ? sv[kk] : lu[kk]);
+                if (lo < len) rv[lo] = rv[lo] - mult * (staged ? sv[kk] : lu[kk]);
             }
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
     }
+    __syncthreads();
     for (int t = lane; t < len; t += 64) lu[s + t] = rv[t];
     if (lane == 0) {
         const double piv = rv[dl];
@@ -1151,17 +1204,24 @@ __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ r
 }
 #pragma clang fp contract(on)
 
-// the LDS the level kernel takes for rows of up to max_row entries and `stage` staged entries
-static size_t ilu0_lds_bytes(int64_t max_row, int64_t stage) {
+// the LDS the level kernel takes for rows of up to max_row entries, `stage` staged entries and a
+// 2^hbits-slot column hash
+static size_t ilu0_lds_bytes(int64_t max_row, int64_t stage, int hbits) {
     const int64_t m = max_row < 1 ? 1 : max_row;
-    const int64_t extra = stage > 0 ? (m + 1) * 4 + 8 + m * 8 : 0;
+    const int64_t extra = (m + 1) * 4 + 8 + m * 16 + (hbits > 0 ? (int64_t)8 << hbits : 0);
     return (size_t)(((m * 12 + stage * 12 + extra) + 15) & ~(int64_t)15);
 }
-// staged entries for rows of up to max_row entries: ILU0_STAGE where it fits next to the row, else none
-static int ilu0_stage(int64_t max_row) {
+// hash slots (at least twice the longest row) and staged entries that fit the LDS; 0 = none
+static void ilu0_plan(int64_t max_row, int &stage, int &hbits) {
+    hbits = 7;
+    while ((int64_t)1 << hbits < 2 * max_row) ++hbits;
+    if (ilu0_lds_bytes(max_row, 0, hbits) > 163840) hbits = 0;
+    stage = 0;
     for (int64_t st = ILU0_STAGE; st >= 256; st /= 2)
-        if (ilu0_lds_bytes(max_row, st) <= 163840) return (int)st;
-    return 0;
+        if (ilu0_lds_bytes(max_row, st, hbits) <= 163840) {
+            stage = (int)st;
+            break;
+        }
 }
 int ilu0_max_row() { return 163840 / 12; }
 void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
@@ -1174,9 +1234,10 @@ void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *
                                   (int)163840);
         attr = true;
     }
-    const int stage = ilu0_stage(max_row);
-    k_ilu0_level<<<(unsigned)nrows_level, 64, ilu0_lds_bytes(max_row, stage), st>>>(
-        rows, rp, ci, lu, diag, dinv, fail, (int)(max_row < 1 ? 1 : max_row), stage);
+    int stage = 0, hbits = 0;
+    ilu0_plan(max_row, stage, hbits);
+    k_ilu0_level<<<(unsigned)nrows_level, 64, ilu0_lds_bytes(max_row, stage, hbits), st>>>(
+        rows, rp, ci, lu, diag, dinv, fail, (int)(max_row < 1 ? 1 : max_row), stage, hbits);
 }
 
 __global__ __launch_bounds__(TPB) void k_lvl_count(int64_t n, const int32_t *order, const int64_t *rp,

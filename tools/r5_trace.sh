@@ -9,6 +9,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$out" -o run 
 rc=$?
 echo "rc=$rc"
 f=$(find "$out" -name '*kernel_trace.csv' | head -1)
-python3 "$REPO/tools/trace_window.py" "$f" > "$out/window.txt" && rm -f "$f"
+python3 "$REPO/tools/trace_window.py" "$f" "${ANCHOR:-k_ilu_blocks_lds}" "${SKIP:-100}" "${COUNT:-24}" "${BEFORE:-4}" > "$out/window.txt" && rm -f "$f"
 cat "$out/window.txt" | head -60
 exit $rc

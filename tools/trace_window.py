@@ -11,9 +11,10 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 hits = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
 if len(hits) <= skip:
     skip = len(hits) // 2
-i0 = max(0, hits[skip] - 4)
+before = int(sys.argv[5]) if len(sys.argv) > 5 else 4
+i0 = max(0, hits[skip] - before)
 t0 = int(rows[i0]["Start_Timestamp"])
-for r in rows[i0:i0 + 24]:
+for r in rows[i0:i0 + (int(sys.argv[4]) if len(sys.argv) > 4 else 24)]:
     s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
     q = r.get("Queue_Id", r.get("Stream_Id", "?"))
     print(f"{s / 1e3:9.1f} {e / 1e3:9.1f} {(e - s) / 1e3:8.1f}  q{q}  {r['Kernel_Name'][:90]}")
