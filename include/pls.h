@@ -194,8 +194,8 @@ int pls_reset_timings(pls_handle *h);
  * stats[0] solves, [1] iterations, [2] most iterations of one solve, [3] solves
  * that ended with a negative KSPConvergedReason (PETSc's -ksp_converged_reason
  * per solve, summed; the reference's own output is the outer count only,
- * lib/AbstractPhysics.py:77-78).                                              */
-int pls_get_ksp_stats(pls_handle *h, const char *prefix, int64_t stats[4]);
+ * lib/AbstractPhysics.py:77-78), [4] the most recent such reason (0: none).  */
+int pls_get_ksp_stats(pls_handle *h, const char *prefix, int64_t stats[5]);
 
 /* Export a device matrix of the handle to host CSR (tests / parity):
  * which: 0 = A, 1 = P, 2 = P_diff (field-major order).  Call once with

@@ -543,6 +543,7 @@ struct Handle {
         if (ctx.d16_segs != D16_SEG && ctx.d16_segs != D16_SEG_MAX) throw Error("pls.d16_segs must be 4 or 8");
         set_d16_xcd((int)opt.integer("pls.d16_xcd", 0));  // process-wide (tuning)
         set_spmv_short_rows(opt.flag("pls.spmv_short", false));  // process-wide (measured slower for the AMG's P)
+        if (opt.integer("pls.ilu0_probe", 0)) set_ilu0_probe((int)opt.integer("pls.ilu0_probe", 0));  // diagnostics
         if (opt.integer("pls.ring_probe", 0)) set_ring_probe((int)opt.integer("pls.ring_probe", 0));  // diagnostics
         ctx.d16_sigma = (int)opt.integer("pls.d16_sigma", 1024);
         if (ctx.d16_sigma < 0 || ctx.d16_sigma % 64) throw Error("pls.d16_sigma must be a multiple of 64 (0: off)");
@@ -552,6 +553,7 @@ struct Handle {
         ctx.spmv_rcm = (int)opt.integer("pls.spmv_rcm", -1);
         ctx.sweep_chain = (int)opt.integer("pls.sweep_chain", -1);
         ctx.sweep_window = (int)opt.integer("pls.sweep_window", -1);
+        ctx.ilu_factor_dep = (int)opt.integer("pls.ilu_factor_dep", 1);
         ctx.ilu_view = (int)opt.integer("pls.ilu_view", 0);
         ctx.sweep_swin = (int)opt.integer("pls.sweep_swin", 0);
         ctx.amg_csr_below = opt.num("pls.amg_csr_below", 16.0);
@@ -1717,6 +1719,7 @@ int pls_get_ksp_stats(pls_handle *hh, const char *prefix, int64_t *stats) {
         stats[1] = found->stat_its;
         stats[2] = found->stat_max;
         stats[3] = found->stat_div;
+        stats[4] = found->stat_last_neg;
     })
 }
 int pls_reset_timings(pls_handle *hh) { PLS_TRY(reinterpret_cast<Handle *>(hh)->timers.reset()) }

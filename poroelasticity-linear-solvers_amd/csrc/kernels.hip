@@ -1043,50 +1043,86 @@ void launch_sgs_factor(int64_t n, const int64_t *rp, const int32_t *ci, double *
     k_sgs_scale<<<grid_for(n, TPB), TPB, 0, st>>>(n, rp, ci, lu, diag, dinv);
 }
 
-// One 64-lane wave per row; the row is staged in LDS (cols + values), the
-// IKJ elimination runs over its strict-lower entries in column order, each
-// step updating the row's pattern positions that match row r's upper part
-// (binary search in LDS).  Rounds as the CPU restatement (no contraction).
-// Round 5: the upper parts of every row r the elimination visits (final: r is
-// in an earlier level) and their 1/u_rr are staged in LDS first -- all their
-// loads in flight at once -- so the elimination loop reads no global memory;
-// it had waited ~1-2 us per pivot for row r's entries (FE 3-D N=12: 145 us
-// per level, 2,878 levels).  Rows whose staged data exceeds ILU0_STAGE keep
-// the global loads.  Same operations in the same order: bitwise the same
-// factors.
-static constexpr int ILU0_STAGE = 4096;  // staged upper-part entries per row (48 KiB)
+// ILU(0) numeric factorization, one workgroup (ILU0_TPB threads) per row.
+// The row is staged in LDS (values, columns and a column -> position hash);
+// the upper parts of its pivot rows (rows r of earlier levels, final) and
+// their 1/u_rr are staged in LDS too, in segments of at most ILU0_STAGE
+// entries -- all four waves' loads in flight at once -- and every staged
+// entry's position in the row is resolved while staging (the hash probes do
+// not depend on the elimination).  Wave 0 then runs the IKJ elimination over
+// the row's strict-lower entries in column order with the next pivot's
+// positions and values prefetched, so a pivot step is one LDS round trip
+// (rv[t] and the entries it updates) plus the update.  A pivot whose upper
+// part alone exceeds the stage reads global memory.  Same operations in the
+// same order as the CPU restatement (no contraction): bitwise the same
+// factors whatever the path.
+// DEP (k_ilu0_dep): one persistent launch -- rows are drawn from a counter in
+// level order and each waits for its pivot rows' completion flags.  Pivot
+// data written by other workgroups is read with agent-coherent (sc1) loads
+// and the row's results are written with agent-coherent stores, so neither
+// side needs the L2 write-back / invalidate of a release / acquire fence
+// (one per row measured ~1.8x slower rows: every row's fence emptied the
+// XCD's L2 for all the others).
+static constexpr int ILU0_TPB = 256;
+static constexpr int ILU0_STAGE = 8192;  // staged upper-part entries per segment (96 KiB)
+__constant__ int ilu0_probe;  // diagnostics (pls.ilu0_probe N): phase times of every N-th row to stdout
+void set_ilu0_probe(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(ilu0_probe), &v, sizeof(int)); }
+static constexpr int64_t ILU0_SPIN_MAX = 1ll << 24;  // dependency polls before a row gives up (never expected)
+static constexpr int ILU0_LDS = 163840 - 64;          // dynamic LDS budget (beside ilu0_ctl)
+__shared__ int32_t ilu0_ctl[4];                       // [0] drawn row (DEP), [1] abort
+
+template <bool COH>
+__device__ __forceinline__ double ilu0_ld(const double *p) {
+    if (COH)
+        return __longlong_as_double((long long)__hip_atomic_load(
+            reinterpret_cast<uint64_t *>(const_cast<double *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void ilu0_st(double *p, double v) {
+    if (COH)
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *p = v;
+}
+
 #pragma clang fp contract(off)
-__global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ rows, const int64_t *__restrict__ rp,
-                                                   const int32_t *__restrict__ ci, double *__restrict__ lu,
-                                                   const int64_t *__restrict__ diag, double *__restrict__ dinv,
-                                                   int32_t *fail, int max_row, int stage, int hbits) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x;
-    const int64_t i = rows[blockIdx.x];
+// returns false when the launch aborts (DEP: a dependency wait exceeded its bound)
+template <bool DEP>
+__device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                         double *lu, const int64_t *__restrict__ diag, double *dinv, int32_t *fail,
+                                         int max_row, int stage, int hbits, char *smem, int32_t *done,
+                                         int32_t *abortf) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool w0 = tid < 64;
     const int64_t s = rp[i], e = rp[i + 1];
     const int len = (int)(e - s);
-    // LDS: row values [max_row] | staged values [stage] | row cols [max_row] | staged cols [stage]
-    //      | per-pivot staged offsets [max_row + 1] | per-pivot 1/u_rr [max_row]   (stage 0: no staging)
+    const int probe = __builtin_amdgcn_readfirstlane(ilu0_probe);
+    const bool pr = probe > 0 && i % probe == 0;
+    uint64_t tp[5] = {pr ? (uint64_t)wall_clock64() : 0ull, 0, 0, 0, 0}, t_stage = 0, t_elim = 0, tq = 0;
+    // LDS: row values [max_row] | staged values [stage] | row cols [max_row] | staged positions [stage]
+    //      | per-pivot staged offsets [max_row + 1] | per-pivot 1/u_rr [max_row] | per-pivot first
+    //      upper entry [max_row] | hash keys, positions [2^hbits each]
     double *rv = reinterpret_cast<double *>(smem);
     double *sv = rv + max_row;
     int32_t *rc = reinterpret_cast<int32_t *>(sv + stage);
     int32_t *sc = rc + max_row;
     int32_t *so = sc + stage;
     double *sd = reinterpret_cast<double *>(((uintptr_t)(so + max_row + 1) + 7) & ~(uintptr_t)7);
-    int64_t *su = reinterpret_cast<int64_t *>(sd + max_row);  // per pivot: first entry of its upper part
-    // column -> position hash of the row (open addressing, 2^hbits slots; hbits 0: binary search)
+    int64_t *su = reinterpret_cast<int64_t *>(sd + max_row);
     int32_t *hk = reinterpret_cast<int32_t *>(su + max_row);
-    int32_t *hp = hk + (1 << hbits);
+    int32_t *hp = hk + (hbits > 0 ? 1 << hbits : 0);
     const uint32_t hmask = (1u << hbits) - 1;
     auto hslot = [&](int32_t c) { return ((uint32_t)c * 2654435761u) >> (32 - hbits); };
-    for (int t = lane; t < len; t += 64) {
-        rv[t] = lu[s + t];
+    for (int t = tid; t < len; t += ILU0_TPB) {
+        rv[t] = lu[s + t];  // (the row's own entries: written by no other row)
         rc[t] = ci[s + t];
     }
     if (hbits > 0) {
-        for (int h = lane; h <= (int)hmask; h += 64) hk[h] = -1;
+        for (int h = tid; h <= (int)hmask; h += ILU0_TPB) hk[h] = -1;
         __syncthreads();
-        for (int t = lane; t < len; t += 64) {
+        for (int t = tid; t < len; t += ILU0_TPB) {
             const int32_t c = rc[t];
             uint32_t h = hslot(c);
             while (atomicCAS(&hk[h], -1, c) != -1) h = (h + 1) & hmask;
@@ -1095,117 +1131,272 @@ __global__ __launch_bounds__(64) void k_ilu0_level(const int32_t *__restrict__ r
     }
     __syncthreads();
     const int dl = (int)(diag[i] - s);
-    // stage: pivot t's upper part (row rc[t]) at so[t] .. so[t + 1]
-    int total = 0;
-    for (int t0 = 0; t0 < (stage > 0 ? dl : 0); t0 += 64) {
-        const int t = t0 + lane;
-        int cnt = 0;
-        double dv = 0.0;
-        int64_t u0 = 0;
-        if (t < dl) {
-            const int64_t r = rc[t];
-            u0 = diag[r] + 1;
-            cnt = (int)(rp[r + 1] - u0);
-            dv = dinv[r];
-        }
-        // inclusive wave scan of cnt
-        int inc = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(inc, o);
-            if (lane >= o) inc += v;
-        }
-        if (t < dl) {
-            so[t] = total + inc - cnt;
-            sd[t] = dv;
-            su[t] = u0;
-        }
-        total += __shfl(inc, 63);
-    }
-    const bool staged = stage > 0 && total <= stage;
-    if (lane == 0 && stage > 0) so[dl] = total;
-    __syncthreads();
-    if (staged) {
-        // every staged entry's source, eight per lane in flight: entry q belongs to
-        // the pivot t with so[t] <= q < so[t + 1] (binary search in LDS)
-        for (int q0 = 0; q0 < total; q0 += 8 * 64) {
-            int64_t src[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int q = q0 + u * 64 + lane;
-                int lo = 0, hi = dl;  // last t with so[t] <= q
-                while (hi - lo > 1) {
-                    const int m = (lo + hi) >> 1;
-                    if (so[m] <= q) lo = m; else hi = m;
-                }
-                src[u] = q < total ? su[lo] + (q - so[lo]) : su[0];
-            }
-            int32_t cv[8];
-            double vv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                cv[u] = ci[src[u]];
-                vv[u] = lu[src[u]];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int q = q0 + u * 64 + lane;
-                if (q < total) {
-                    sc[q] = cv[u];
-                    sv[q] = vv[u];
+    if (pr) tp[1] = wall_clock64();
+    if (DEP) {  // every pivot row (an earlier level: already drawn) finished
+        if (w0) {
+            int ab = 0;
+            for (int t0 = 0; t0 < dl && !ab; t0 += 64) {
+                const int t = t0 + lane;
+                const int32_t k = t < dl ? rc[t] : -1;
+                for (int64_t spins = 0;; ++spins) {
+                    const bool ok = k < 0 || __hip_atomic_load(done + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    if (__all(ok)) break;
+                    if ((spins & 63) == 63 && __hip_atomic_load(abortf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        ab = 1;
+                        break;
+                    }
+                    if (spins > ILU0_SPIN_MAX) {  // report instead of hanging: every row then stops
+                        if (lane == 0) {
+                            atomicMax(fail, 3);
+                            __hip_atomic_store(abortf, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                        ab = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
             }
+            if (lane == 0) ilu0_ctl[1] = ab;
         }
         __syncthreads();
+        if (ilu0_ctl[1]) return false;
     }
-    // (one wave: its LDS accesses complete in order, so no barrier between pivots)
-    for (int t = 0; t < dl; ++t) {
-        const double pc = rv[t];
-        if (pc != 0.0) {
-            const int64_t r = rc[t];
-            const double mult = pc * (staged ? sd[t] : dinv[r]);
-            if (lane == 0) rv[t] = mult;
-            const int64_t us = staged ? so[t] : diag[r] + 1, ue = staged ? so[t + 1] : rp[r + 1];
-            for (int64_t kk = us + lane; kk < ue; kk += 64) {
-                const int32_t j = staged ? sc[kk] : ci[kk];
-                int lo = len;
-                if (hbits > 0) {  // the column's position in the row (hash)
-                    uint32_t h = hslot(j);
-                    int32_t key = hk[h];
-                    while (key != j && key != -1) {
-                        h = (h + 1) & hmask;
-                        key = hk[h];
-                    }
-                    if (key == j) lo = hp[h];
-                } else {  // search j in rc[t+1, len)
-                    int a = t + 1, b = len;
-                    while (a < b) {
-                        const int m = (a + b) >> 1;
-                        if (rc[m] < j) a = m + 1; else b = m;
-                    }
-                    if (a < len && rc[a] == j) lo = a;
-                }
-                if (lo < len) rv[lo] = rv[lo] - mult * (staged ? sv[kk] : lu[kk]);
+    if (pr) tp[2] = wall_clock64();
+    // pivot t's upper part (row rc[t]) goes to so[t] .. so[t + 1] (wave 0 scans)
+    if (w0 && stage > 0) {
+        int total = 0;
+        for (int t0 = 0; t0 < dl; t0 += 64) {
+            const int t = t0 + lane;
+            int cnt = 0;
+            double dv = 0.0;
+            int64_t u0 = 0;
+            if (t < dl) {
+                const int64_t r = rc[t];
+                u0 = diag[r] + 1;
+                cnt = (int)(rp[r + 1] - u0);
+                dv = ilu0_ld<DEP>(dinv + r);
             }
+            int inc = cnt;  // inclusive wave scan
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(inc, o);
+                if (lane >= o) inc += v;
+            }
+            if (t < dl) {
+                so[t] = total + inc - cnt;
+                sd[t] = dv;
+                su[t] = u0;
+            }
+            total += __shfl(inc, 63);
         }
-        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) so[dl] = total;
     }
     __syncthreads();
-    for (int t = lane; t < len; t += 64) lu[s + t] = rv[t];
-    if (lane == 0) {
-        const double piv = rv[dl];
-        if (piv == 0.0) {
-            atomicMax(fail, 2);
-            dinv[i] = 0.0;
-        } else {
-            dinv[i] = 1.0 / piv;
+    if (pr) tp[3] = wall_clock64();
+    int nseg = 0, nglob = 0;
+    // pivots in segments [ta, tb) whose upper parts fit the stage together; a
+    // pivot whose part alone does not (or no stage) goes through global memory
+    for (int ta = 0; ta < dl;) {
+        int tb = ta;
+        const int base = stage > 0 ? so[ta] : 0;
+        if (stage > 0) {  // the last tb with so[tb] - base <= stage
+            int hi = dl;
+            while (tb < hi) {
+                const int m = (tb + hi + 1) >> 1;
+                if (so[m] - base <= stage) tb = m; else hi = m - 1;
+            }
         }
+        if (tb > ta) {
+            if (pr) tq = wall_clock64();
+            const int cnt = so[tb] - base;
+            // every staged entry's source, eight per thread in flight: entry q belongs to
+            // the pivot t with so[t] <= base + q < so[t + 1] (binary search in LDS)
+            for (int q0 = 0; q0 < cnt; q0 += 8 * ILU0_TPB) {
+                int64_t src[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int q = base + q0 + u * ILU0_TPB + tid;
+                    int lo = ta, hi = tb;  // last t with so[t] <= q
+                    while (hi - lo > 1) {
+                        const int m = (lo + hi) >> 1;
+                        if (so[m] <= q) lo = m; else hi = m;
+                    }
+                    src[u] = q < base + cnt ? su[lo] + (q - so[lo]) : su[ta];
+                }
+                int32_t cv[8];
+                double vv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    cv[u] = ci[src[u]];
+                    vv[u] = ilu0_ld<DEP>(lu + src[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int q = q0 + u * ILU0_TPB + tid;
+                    if (q < cnt) {
+                        // the column's position in the row (len: not in the pattern)
+                        const int32_t j = cv[u];
+                        int lo = len;
+                        if (hbits > 0) {
+                            uint32_t h = hslot(j);
+                            int32_t key = hk[h];
+                            while (key != j && key != -1) {
+                                h = (h + 1) & hmask;
+                                key = hk[h];
+                            }
+                            if (key == j) lo = hp[h];
+                        } else {
+                            int a = 0, b = len;
+                            while (a < b) {
+                                const int m = (a + b) >> 1;
+                                if (rc[m] < j) a = m + 1; else b = m;
+                            }
+                            if (a < len && rc[a] == j) lo = a;
+                        }
+                        sc[q] = lo;
+                        sv[q] = vv[u];
+                    }
+                }
+            }
+            __syncthreads();
+            if (pr) {
+                const uint64_t now = wall_clock64();
+                t_stage += now - tq;
+                tq = now;
+            }
+            if (w0) {
+                // (one wave: its LDS accesses complete in order, so no barrier between pivots;
+                // pivot t + 1's first entries and 1/u_rr are read before pivot t's updates --
+                // the staged arrays are not written here)
+                int k0 = so[ta] - base + lane, e0 = so[ta + 1] - base;
+                int lon = k0 < e0 ? sc[k0] : len;
+                double vn = k0 < e0 ? sv[k0] : 0.0, dn = sd[ta];
+                for (int t = ta; t < tb; ++t) {
+                    const int lo0 = lon, kc = k0, ec = e0;
+                    const double v0 = vn, dc = dn;
+                    if (t + 1 < tb) {
+                        k0 = so[t + 1] - base + lane;
+                        e0 = so[t + 2] - base;
+                        lon = k0 < e0 ? sc[k0] : len;
+                        vn = k0 < e0 ? sv[k0] : 0.0;
+                        dn = sd[t + 1];
+                    }
+                    const double pc = rv[t];
+                    if (pc != 0.0) {
+                        const double mult = pc * dc;
+                        if (lane == 0) rv[t] = mult;
+                        if (lo0 < len) rv[lo0] = rv[lo0] - mult * v0;
+                        for (int kk = kc + 64; kk < ec; kk += 64) {
+                            const int lo = sc[kk];
+                            if (lo < len) rv[lo] = rv[lo] - mult * sv[kk];
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            __syncthreads();  // (the next segment overwrites the stage)
+            if (pr) t_elim += wall_clock64() - tq;
+            ta = tb;
+            ++nseg;
+            continue;
+        }
+        const int t = ta++;
+        ++nglob;
+        if (w0) {
+            const double pc = rv[t];
+            if (pc != 0.0) {
+                const int64_t r = rc[t];
+                const double mult = pc * ilu0_ld<DEP>(dinv + r);
+                if (lane == 0) rv[t] = mult;
+                const int64_t us = diag[r] + 1, ue = rp[r + 1];
+                for (int64_t kk = us + lane; kk < ue; kk += 64) {
+                    const int32_t j = ci[kk];
+                    int lo = len;
+                    if (hbits > 0) {  // the column's position in the row (hash)
+                        uint32_t h = hslot(j);
+                        int32_t key = hk[h];
+                        while (key != j && key != -1) {
+                            h = (h + 1) & hmask;
+                            key = hk[h];
+                        }
+                        if (key == j) lo = hp[h];
+                    } else {  // search j in rc[t+1, len)
+                        int a = t + 1, b = len;
+                        while (a < b) {
+                            const int m = (a + b) >> 1;
+                            if (rc[m] < j) a = m + 1; else b = m;
+                        }
+                        if (a < len && rc[a] == j) lo = a;
+                    }
+                    if (lo < len) rv[lo] = rv[lo] - mult * ilu0_ld<DEP>(lu + kk);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __syncthreads();
+    if (pr) tp[4] = wall_clock64();
+    for (int t = tid; t < len; t += ILU0_TPB) ilu0_st<DEP>(lu + s + t, rv[t]);
+    if (tid == 0) {
+        const double piv = rv[dl];
+        if (piv == 0.0) atomicMax(fail, 2);
+        ilu0_st<DEP>(dinv + i, piv == 0.0 ? 0.0 : 1.0 / piv);
+    }
+    if (DEP) {  // publish: the row's coherent stores complete, then its flag
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(done + i, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (pr && tid == 0) {
+        const uint64_t t5 = wall_clock64();
+        printf("[ilu0 row] %ld len %d dl %d staged %d seg %d glob %d | t %lu load %lu wait %lu scan %lu stage %lu "
+               "elim %lu rest %lu out %lu\n",
+               (long)i, len, dl, stage > 0 ? so[dl] : 0, nseg, nglob, (unsigned long)tp[0],
+               (unsigned long)(tp[1] - tp[0]), (unsigned long)(tp[2] - tp[1]), (unsigned long)(tp[3] - tp[2]),
+               (unsigned long)t_stage, (unsigned long)t_elim, (unsigned long)(tp[4] - tp[3] - t_stage - t_elim),
+               (unsigned long)(t5 - tp[4]));
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(ILU0_TPB) void k_ilu0_level(const int32_t *__restrict__ rows,
+                                                         const int64_t *__restrict__ rp,
+                                                         const int32_t *__restrict__ ci, double *__restrict__ lu,
+                                                         const int64_t *__restrict__ diag, double *__restrict__ dinv,
+                                                         int32_t *fail, int max_row, int stage, int hbits) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    (void)ilu0_row<false>(rows[blockIdx.x], rp, ci, lu, diag, dinv, fail, max_row, stage, hbits, smem, nullptr,
+                          nullptr);
+}
+
+// all levels in one launch: ctr[0] draws rows (rows: level order, so every
+// pivot row was drawn earlier -- by a running workgroup -- and the lowest
+// unfinished drawn row always has its pivots done: no deadlock); ctr[1] =
+// abort flag; done[n] zeroed by the caller
+__global__ __launch_bounds__(ILU0_TPB) void k_ilu0_dep(int64_t n, const int32_t *__restrict__ rows,
+                                                       const int64_t *__restrict__ rp, const int32_t *__restrict__ ci,
+                                                       double *lu, const int64_t *__restrict__ diag, double *dinv,
+                                                       int32_t *fail, int max_row, int stage, int hbits,
+                                                       int32_t *done, int32_t *ctr) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const int q = atomicAdd(ctr, 1);
+            ilu0_ctl[0] = (q >= n || __hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ? -1 : q;
+        }
+        __syncthreads();
+        const int q = ilu0_ctl[0];
+        __syncthreads();
+        if (q < 0) return;
+        if (!ilu0_row<true>(rows[q], rp, ci, lu, diag, dinv, fail, max_row, stage, hbits, smem, done, ctr + 1))
+            return;
+        __syncthreads();
     }
 }
 #pragma clang fp contract(on)
 
-// the LDS the level kernel takes for rows of up to max_row entries, `stage` staged entries and a
-// 2^hbits-slot column hash
+// the LDS the factorization kernels take for rows of up to max_row entries, `stage` staged
+// entries and a 2^hbits-slot column hash
 static size_t ilu0_lds_bytes(int64_t max_row, int64_t stage, int hbits) {
     const int64_t m = max_row < 1 ? 1 : max_row;
     const int64_t extra = (m + 1) * 4 + 8 + m * 16 + (hbits > 0 ? (int64_t)8 << hbits : 0);
@@ -1215,28 +1406,47 @@ static size_t ilu0_lds_bytes(int64_t max_row, int64_t stage, int hbits) {
 static void ilu0_plan(int64_t max_row, int &stage, int &hbits) {
     hbits = 7;
     while ((int64_t)1 << hbits < 2 * max_row) ++hbits;
-    if (ilu0_lds_bytes(max_row, 0, hbits) > 163840) hbits = 0;
+    if (ilu0_lds_bytes(max_row, 0, hbits) > ILU0_LDS) hbits = 0;
     stage = 0;
     for (int64_t st = ILU0_STAGE; st >= 256; st /= 2)
-        if (ilu0_lds_bytes(max_row, st, hbits) <= 163840) {
+        if (ilu0_lds_bytes(max_row, st, hbits) <= ILU0_LDS) {
             stage = (int)st;
             break;
         }
 }
-int ilu0_max_row() { return 163840 / 12; }
+int ilu0_max_row() { return (ILU0_LDS - 16) / 32; }  // (row values, columns, offsets, 1/u_rr, first entries)
+void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
+                     const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int32_t *done, int32_t *ctr,
+                     hipStream_t st) {
+    if (n <= 0) return;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void *)k_ilu0_dep, hipFuncAttributeMaxDynamicSharedMemorySize, ILU0_LDS);
+        attr = true;
+    }
+    int stage = 0, hbits = 0;
+    ilu0_plan(max_row, stage, hbits);
+    const size_t lds = ilu0_lds_bytes(max_row, stage, hbits);
+    (void)hipMemsetAsync(done, 0, sizeof(int32_t) * n, st);
+    (void)hipMemsetAsync(ctr, 0, sizeof(int32_t) * 2, st);
+    // persistent: the workgroups that fit (4 per CU at most), never more than rows
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(4, 163840 / (int64_t)(lds + 64)));
+    const int64_t grid = std::min<int64_t>(n, 256 * per_cu);
+    k_ilu0_dep<<<(unsigned)grid, ILU0_TPB, lds, st>>>(n, rows, rp, ci, lu, diag, dinv, fail,
+                                                       (int)(max_row < 1 ? 1 : max_row), stage, hbits, done, ctr);
+}
 void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
                        const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, hipStream_t st) {
     // caller guarantees max_row <= ilu0_max_row(); LDS sized to the longest row (occupancy for short rows)
     if (nrows_level <= 0) return;
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void *)k_ilu0_level, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)163840);
+        (void)hipFuncSetAttribute((const void *)k_ilu0_level, hipFuncAttributeMaxDynamicSharedMemorySize, ILU0_LDS);
         attr = true;
     }
     int stage = 0, hbits = 0;
     ilu0_plan(max_row, stage, hbits);
-    k_ilu0_level<<<(unsigned)nrows_level, 64, ilu0_lds_bytes(max_row, stage, hbits), st>>>(
+    k_ilu0_level<<<(unsigned)nrows_level, ILU0_TPB, ilu0_lds_bytes(max_row, stage, hbits), st>>>(
         rows, rp, ci, lu, diag, dinv, fail, (int)(max_row < 1 ? 1 : max_row), stage, hbits);
 }
 

@@ -99,6 +99,10 @@ int ilu0_max_row();
 void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp,
                        const int32_t *ci, double *lu, const int64_t *diag, double *dinv,
                        int32_t *fail, int64_t max_row, hipStream_t st);
+// all levels in one launch (rows in level order; done: n flags, ctr: 2 ints -- scratch)
+void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
+                     const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int32_t *done, int32_t *ctr,
+                     hipStream_t st);
 void launch_find_diag(int64_t n, const int64_t *rp, const int32_t *ci, int64_t *diag, int32_t *fail,
                       hipStream_t st);
 // Symmetric Gauss-Seidel "factors" in ILU(0) storage (hypre relax type 6 as a
@@ -243,6 +247,7 @@ void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart,
 // (position -> row), mapUL (U position -> yL index), scratch yL / yU (n each).
 int ilu_ring_slots();
 int ilu_ring_lane_entries();  // factor entries per lane per pipeline slot of the ring sweep
+void set_ilu0_probe(int v);  // diagnostics only (pls.ilu0_probe)
 void set_ring_probe(int v);  // diagnostics only (pls.ring_probe)
 int ilu_ring_chunk();
 void launch_ilu_blocks_ring(int64_t n, int64_t nblocks, const int64_t *Lgoff, const int64_t *Lgslice,

@@ -1675,13 +1675,22 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
     } else {
         DBuf<int32_t> rowsL(std::max<int64_t>(n, 1));
         HIPCHK(hipMemcpyAsync(rowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
-        for (int64_t l = 0; l < nlev_L; ++l)
-            launch_ilu0_level(Lptr[l + 1] - Lptr[l], rowsL.p + Lptr[l], F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p,
-                              fail.p, F.max_row, c.st);
+        if (c.ilu_factor_dep && nlev_L > 1) {  // one launch; rows wait on their pivot rows' flags
+            DBuf<int32_t> done(std::max<int64_t>(n, 1)), ctr(2);
+            launch_ilu0_dep(n, rowsL.p, F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p, fail.p, F.max_row, done.p, ctr.p,
+                            c.st);
+            HIPCHK(hipGetLastError());
+            c.sync();  // (done / ctr freed below)
+        } else {
+            for (int64_t l = 0; l < nlev_L; ++l)
+                launch_ilu0_level(Lptr[l + 1] - Lptr[l], rowsL.p + Lptr[l], F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p,
+                                  fail.p, F.max_row, c.st);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
         c.sync();
     }
+    if (hfail == 3) throw Error("ILU(0): dependency wait exceeded its bound (set pls.ilu_factor_dep 0)");
     if (hfail) throw Error("ILU(0): zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
     int64_t blen = n / nblocks + 1;
     if (bnd)
@@ -2505,6 +2514,7 @@ void KSP::solve(const double *b, double *x, Ctx &c) {
     stat_max = std::max<int64_t>(stat_max, its);
     ++stat_solves;
     stat_div += reason < 0 ? 1 : 0;
+    if (reason < 0) stat_last_neg = reason;
     c.check_bounds();
 }
 

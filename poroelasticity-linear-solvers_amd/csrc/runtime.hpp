@@ -82,6 +82,7 @@ struct Ctx {
                                   // -1 where the level DAG is deep and narrow, 0 never, 1 whenever rows fit
     int sweep_window = -1;        // ... in 64-row windows with inverted window triangles (k_ilu_blocks_window):
                                   // -1 where the chain sweep would be chosen, 0 never, 1 whenever rows fit
+    int ilu_factor_dep = 1;       // ILU(0) numeric factorization in one dependency-driven launch (pls.ilu_factor_dep)
     int ilu_view = 0;             // print every ILU / Gauss-Seidel PC's sweep choice to stderr (pls.ilu_view)
     int sweep_swin = -1;          // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin):
                                   // -1 where the ring sweep would run, 0 never, 1 whenever the block is y-resident
@@ -518,6 +519,7 @@ struct KSP {
     double time_limit = 0;  // seconds (pls.solver_time_limit, the outer solver only; 0: none)
     double t_start = 0;
     int64_t stat_its = 0, stat_max = 0, stat_solves = 0, stat_div = 0;  // stat_div: solves with reason < 0
+    int64_t stat_last_neg = 0;  // the most recent negative reason
     KSP() = default;
     KSP(const KSP &) = delete;
     ~KSP();

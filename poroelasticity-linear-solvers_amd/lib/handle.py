@@ -219,9 +219,10 @@ class Handle:
         return {f: getattr(t, f) for f, _ in t._fields_}
 
     def ksp_stats(self, prefix):
-        """(solves, iterations, most iterations of one solve, solves with a negative reason)
-        of the inner solver with this options prefix (pls_get_ksp_stats)."""
-        s = np.zeros(4, dtype=np.int64)
+        """(solves, iterations, most iterations of one solve, solves with a negative reason,
+        the most recent negative reason) of the inner solver with this options prefix
+        (pls_get_ksp_stats)."""
+        s = np.zeros(5, dtype=np.int64)
         N.check(N.lib().pls_get_ksp_stats(self.ptr, prefix.encode(), N.ptr(s)))
         return tuple(int(v) for v in s)
 

@@ -371,3 +371,22 @@ def test_ring_sweep_equals_y_resident(gpu, dim, N, blocks):
     assert np.array_equal(hr.pc_apply(x), yr)  # repeatable (scratch reuse)
     hr.destroy()
     hy.destroy()
+
+
+@pytest.mark.parametrize("dim,N", [(3, 12), (2, 24)])
+def test_ilu_factor_dep_bitwise(gpu, dim, N):
+    """The one-launch ILU(0) factorization (k_ilu0_dep: rows drawn in level
+    order, each waiting on its pivot rows' flags) gives the same factors as
+    one launch per level (pls.ilu_factor_dep 0): PC applies bitwise equal."""
+    from lib.handle import Handle, params_to_options
+    s = F.assemble_swelling(dim, N, "diagonal")
+    opts = dict(_db("ilu"))
+    opts.update(params_to_options(dict(BASE, **{"pc type": "diagonal"})))
+    x = np.random.default_rng(9).standard_normal(s.A.shape[0])
+    ys = []
+    for dep in ("1", "0"):
+        h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure,
+                            dict(opts, **{"pls.ilu_factor_dep": dep}))
+        ys.append(h.pc_apply(x))
+        h.destroy()
+    assert np.array_equal(ys[0], ys[1])

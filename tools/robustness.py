@@ -130,7 +130,8 @@ def run_case(problem: str, N: int, pc: str, optset: str, nranks: int, extra: dic
         except RuntimeError:
             continue
         if st[0]:
-            inner[pre] = {"solves": st[0], "its": st[1], "max": st[2], "negative_reason": st[3]}
+            inner[pre] = {"solves": st[0], "its": st[1], "max": st[2], "negative_reason": st[3],
+                          "last_negative": st[4]}
     hist = solver.history
     out = {"problem": problem, "N": N, "pc_type": pc, "options": optset, "np": nranks, "dofs": int(s.A.shape[0]),
            "nnz": int(s.A.nnz), "its": int(solver.getIterationNumber()), "reason": int(solver.getConvergedReason()),

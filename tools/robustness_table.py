@@ -6,7 +6,8 @@ Later lines for the same (problem, N, pc type, option set) replace earlier ones.
 import json
 import sys
 
-REASON = {2: "rtol", 3: "atol", -3: "max its", -100: "time limit", -8: "indefinite PC", -9: "nan/inf"}
+REASON = {2: "rtol", 3: "atol", -3: "max its", -100: "time limit", -4: "dtol", -5: "breakdown", -8: "indefinite PC",
+          -9: "nan/inf", -11: "PC failed"}
 
 
 def main(paths):
@@ -25,7 +26,9 @@ def main(paths):
         inner = []
         for pre, v in d["inner"].items():
             if v["its"] > v["solves"]:  # skip PREONLY (one "iteration" per solve)
-                neg = f", {v['negative_reason']} diverged" if v["negative_reason"] else ""
+                last = REASON.get(v.get("last_negative"), v.get("last_negative"))
+                neg = f", {v['negative_reason']} diverged" + (f": {last}" if v.get("last_negative") else "") \
+                    if v["negative_reason"] else ""
                 inner.append(f"{pre.rstrip('_')} {v['its']} ({v['its'] / v['solves']:.0f} / {v['max']}{neg})")
         red = (d["rnorm"] / d["rnorm0"]) if d.get("rnorm0") else float("nan")
         print(f"| {d['problem']} | {d['options']} | {d['pc_type']} | {d['N']} | {d['dofs']:,} | {d['its']} | "
