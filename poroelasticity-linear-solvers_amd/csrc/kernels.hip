@@ -1087,6 +1087,66 @@ __device__ __forceinline__ void ilu0_st(double *p, double v) {
         *p = v;
 }
 
+// stage pivots [ta, tb)'s upper parts (entries so[t] - base ..): POS their
+// positions in the row (sc), VAL their values (sv); eight loads per thread in
+// flight, entry q's pivot found by binary search over so
+template <bool COH, bool POS, bool VAL>
+__device__ __forceinline__ void ilu0_stage_part(int ta, int tb, int base, int cnt, const int64_t *__restrict__ rp,
+                                                const int32_t *__restrict__ ci, const double *lu, int len, int hbits,
+                                                const int32_t *rc, const int32_t *so, const int64_t *su, int32_t *sc,
+                                                double *sv, const int32_t *hk, const int32_t *hp) {
+    const int tid = threadIdx.x;
+    const uint32_t hmask = (1u << hbits) - 1;
+    for (int q0 = 0; q0 < cnt; q0 += 8 * ILU0_TPB) {
+        int64_t src[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = base + q0 + u * ILU0_TPB + tid;
+            int lo = ta, hi = tb;  // last t with so[t] <= q
+            while (hi - lo > 1) {
+                const int m = (lo + hi) >> 1;
+                if (so[m] <= q) lo = m; else hi = m;
+            }
+            src[u] = q < base + cnt ? su[lo] + (q - so[lo]) : su[ta];
+        }
+        int32_t cv[8];
+        double vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (POS) cv[u] = ci[src[u]];
+            if (VAL) vv[u] = ilu0_ld<COH>(lu + src[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + u * ILU0_TPB + tid;
+            if (q < cnt) {
+                if (POS) {  // the column's position in the row (len: not in the pattern)
+                    const int32_t j = cv[u];
+                    int lo = len;
+                    if (hbits > 0) {
+                        uint32_t h = ((uint32_t)j * 2654435761u) >> (32 - hbits);
+                        int32_t key = hk[h];
+                        while (key != j && key != -1) {
+                            h = (h + 1) & hmask;
+                            key = hk[h];
+                        }
+                        if (key == j) lo = hp[h];
+                    } else {
+                        int a = 0, b = len;
+                        while (a < b) {
+                            const int m = (a + b) >> 1;
+                            if (rc[m] < j) a = m + 1; else b = m;
+                        }
+                        if (a < len && rc[a] == j) lo = a;
+                    }
+                    sc[q] = lo;
+                }
+                if (VAL) sv[q] = vv[u];
+            }
+        }
+    }
+}
+
 #pragma clang fp contract(off)
 // returns false when the launch aborts (DEP: a dependency wait exceeded its bound)
 template <bool DEP>
@@ -1132,14 +1192,49 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
     __syncthreads();
     const int dl = (int)(diag[i] - s);
     if (pr) tp[1] = wall_clock64();
+    // pivot t's upper part (row rc[t]) goes to so[t] .. so[t + 1] (wave 0 scans)
+    if (w0 && stage > 0) {
+        int total = 0;
+        for (int t0 = 0; t0 < dl; t0 += 64) {
+            const int t = t0 + lane;
+            int cnt = 0;
+            int64_t u0 = 0;
+            if (t < dl) {
+                const int64_t r = rc[t];
+                u0 = diag[r] + 1;
+                cnt = (int)(rp[r + 1] - u0);
+            }
+            int inc = cnt;  // inclusive wave scan
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(inc, o);
+                if (lane >= o) inc += v;
+            }
+            if (t < dl) {
+                so[t] = total + inc - cnt;
+                su[t] = u0;
+            }
+            total += __shfl(inc, 63);
+        }
+        if (lane == 0) so[dl] = total;
+    }
+    __syncthreads();
+    // the staged entries' positions depend on the pattern only: with one segment
+    // they are resolved before the wait (DEP), off the dependency chain
+    const bool pre = DEP && stage > 0 && so[dl] <= stage;
+    if (pre) ilu0_stage_part<DEP, true, false>(0, dl, 0, so[dl], rp, ci, lu, len, hbits, rc, so, su, sc, sv, hk, hp);
+    if (pr) tp[2] = wall_clock64();
     if (DEP) {  // every pivot row (an earlier level: already drawn) finished
         if (w0) {
             int ab = 0;
             for (int t0 = 0; t0 < dl && !ab; t0 += 64) {
                 const int t = t0 + lane;
                 const int32_t k = t < dl ? rc[t] : -1;
+                bool ok = k < 0;
                 for (int64_t spins = 0;; ++spins) {
-                    const bool ok = k < 0 || __hip_atomic_load(done + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    // (only the flags not yet seen are polled: 64 scattered loads per poll from
+                    // ~250 waiting rows measured ~30x slower staging for every row)
+                    if (!ok) ok = __hip_atomic_load(done + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
                     if (__all(ok)) break;
                     if ((spins & 63) == 63 && __hip_atomic_load(abortf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                         ab = 1;
@@ -1153,7 +1248,7 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
                         ab = 1;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(4);
                 }
             }
             if (lane == 0) ilu0_ctl[1] = ab;
@@ -1161,36 +1256,7 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
         __syncthreads();
         if (ilu0_ctl[1]) return false;
     }
-    if (pr) tp[2] = wall_clock64();
-    // pivot t's upper part (row rc[t]) goes to so[t] .. so[t + 1] (wave 0 scans)
-    if (w0 && stage > 0) {
-        int total = 0;
-        for (int t0 = 0; t0 < dl; t0 += 64) {
-            const int t = t0 + lane;
-            int cnt = 0;
-            double dv = 0.0;
-            int64_t u0 = 0;
-            if (t < dl) {
-                const int64_t r = rc[t];
-                u0 = diag[r] + 1;
-                cnt = (int)(rp[r + 1] - u0);
-                dv = ilu0_ld<DEP>(dinv + r);
-            }
-            int inc = cnt;  // inclusive wave scan
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(inc, o);
-                if (lane >= o) inc += v;
-            }
-            if (t < dl) {
-                so[t] = total + inc - cnt;
-                sd[t] = dv;
-                su[t] = u0;
-            }
-            total += __shfl(inc, 63);
-        }
-        if (lane == 0) so[dl] = total;
-    }
+    for (int t = tid; t < dl; t += ILU0_TPB) sd[t] = ilu0_ld<DEP>(dinv + rc[t]);
     __syncthreads();
     if (pr) tp[3] = wall_clock64();
     int nseg = 0, nglob = 0;
@@ -1209,55 +1275,10 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
         if (tb > ta) {
             if (pr) tq = wall_clock64();
             const int cnt = so[tb] - base;
-            // every staged entry's source, eight per thread in flight: entry q belongs to
-            // the pivot t with so[t] <= base + q < so[t + 1] (binary search in LDS)
-            for (int q0 = 0; q0 < cnt; q0 += 8 * ILU0_TPB) {
-                int64_t src[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int q = base + q0 + u * ILU0_TPB + tid;
-                    int lo = ta, hi = tb;  // last t with so[t] <= q
-                    while (hi - lo > 1) {
-                        const int m = (lo + hi) >> 1;
-                        if (so[m] <= q) lo = m; else hi = m;
-                    }
-                    src[u] = q < base + cnt ? su[lo] + (q - so[lo]) : su[ta];
-                }
-                int32_t cv[8];
-                double vv[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    cv[u] = ci[src[u]];
-                    vv[u] = ilu0_ld<DEP>(lu + src[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int q = q0 + u * ILU0_TPB + tid;
-                    if (q < cnt) {
-                        // the column's position in the row (len: not in the pattern)
-                        const int32_t j = cv[u];
-                        int lo = len;
-                        if (hbits > 0) {
-                            uint32_t h = hslot(j);
-                            int32_t key = hk[h];
-                            while (key != j && key != -1) {
-                                h = (h + 1) & hmask;
-                                key = hk[h];
-                            }
-                            if (key == j) lo = hp[h];
-                        } else {
-                            int a = 0, b = len;
-                            while (a < b) {
-                                const int m = (a + b) >> 1;
-                                if (rc[m] < j) a = m + 1; else b = m;
-                            }
-                            if (a < len && rc[a] == j) lo = a;
-                        }
-                        sc[q] = lo;
-                        sv[q] = vv[u];
-                    }
-                }
-            }
+            if (pre)
+                ilu0_stage_part<DEP, false, true>(ta, tb, base, cnt, rp, ci, lu, len, hbits, rc, so, su, sc, sv, hk, hp);
+            else
+                ilu0_stage_part<DEP, true, true>(ta, tb, base, cnt, rp, ci, lu, len, hbits, rc, so, su, sc, sv, hk, hp);
             __syncthreads();
             if (pr) {
                 const uint64_t now = wall_clock64();
@@ -1402,13 +1423,15 @@ static size_t ilu0_lds_bytes(int64_t max_row, int64_t stage, int hbits) {
     const int64_t extra = (m + 1) * 4 + 8 + m * 16 + (hbits > 0 ? (int64_t)8 << hbits : 0);
     return (size_t)(((m * 12 + stage * 12 + extra) + 15) & ~(int64_t)15);
 }
-// hash slots (at least twice the longest row) and staged entries that fit the LDS; 0 = none
-static void ilu0_plan(int64_t max_row, int &stage, int &hbits) {
+// hash slots (at least twice the longest row) and staged entries (the most one
+// row needs, at most ILU0_STAGE) that fit the LDS; 0 = none
+static void ilu0_plan(int64_t max_row, int64_t max_staged, int &stage, int &hbits) {
     hbits = 7;
     while ((int64_t)1 << hbits < 2 * max_row) ++hbits;
     if (ilu0_lds_bytes(max_row, 0, hbits) > ILU0_LDS) hbits = 0;
     stage = 0;
-    for (int64_t st = ILU0_STAGE; st >= 256; st /= 2)
+    const int64_t want = std::min<int64_t>(ILU0_STAGE, std::max<int64_t>(256, (max_staged + 63) & ~(int64_t)63));
+    for (int64_t st = want; st >= 256; st /= 2)
         if (ilu0_lds_bytes(max_row, st, hbits) <= ILU0_LDS) {
             stage = (int)st;
             break;
@@ -1416,8 +1439,8 @@ static void ilu0_plan(int64_t max_row, int &stage, int &hbits) {
 }
 int ilu0_max_row() { return (ILU0_LDS - 16) / 32; }  // (row values, columns, offsets, 1/u_rr, first entries)
 void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
-                     const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int32_t *done, int32_t *ctr,
-                     hipStream_t st) {
+                     const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int64_t max_staged,
+                     int32_t *done, int32_t *ctr, hipStream_t st) {
     if (n <= 0) return;
     static bool attr = false;
     if (!attr) {
@@ -1425,7 +1448,7 @@ void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const in
         attr = true;
     }
     int stage = 0, hbits = 0;
-    ilu0_plan(max_row, stage, hbits);
+    ilu0_plan(max_row, max_staged, stage, hbits);
     const size_t lds = ilu0_lds_bytes(max_row, stage, hbits);
     (void)hipMemsetAsync(done, 0, sizeof(int32_t) * n, st);
     (void)hipMemsetAsync(ctr, 0, sizeof(int32_t) * 2, st);
@@ -1436,7 +1459,8 @@ void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const in
                                                        (int)(max_row < 1 ? 1 : max_row), stage, hbits, done, ctr);
 }
 void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
-                       const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, hipStream_t st) {
+                       const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int64_t max_staged,
+                       hipStream_t st) {
     // caller guarantees max_row <= ilu0_max_row(); LDS sized to the longest row (occupancy for short rows)
     if (nrows_level <= 0) return;
     static bool attr = false;
@@ -1445,7 +1469,7 @@ void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *
         attr = true;
     }
     int stage = 0, hbits = 0;
-    ilu0_plan(max_row, stage, hbits);
+    ilu0_plan(max_row, max_staged, stage, hbits);
     k_ilu0_level<<<(unsigned)nrows_level, ILU0_TPB, ilu0_lds_bytes(max_row, stage, hbits), st>>>(
         rows, rp, ci, lu, diag, dinv, fail, (int)(max_row < 1 ? 1 : max_row), stage, hbits);
 }

@@ -96,13 +96,14 @@ void launch_tsqr(int64_t n, int m, const double *const *cols_dev, double *Rout, 
 // Factor the rows of one level in place (original CSR): lu, diag pos, dinv.
 // max_row: longest row of the matrix (<= ilu0_max_row(); staged in LDS).
 int ilu0_max_row();
+// max_staged: the most upper-part entries of one row's pivots (LDS sizing)
 void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *rp,
                        const int32_t *ci, double *lu, const int64_t *diag, double *dinv,
-                       int32_t *fail, int64_t max_row, hipStream_t st);
+                       int32_t *fail, int64_t max_row, int64_t max_staged, hipStream_t st);
 // all levels in one launch (rows in level order; done: n flags, ctr: 2 ints -- scratch)
 void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
-                     const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int32_t *done, int32_t *ctr,
-                     hipStream_t st);
+                     const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int64_t max_staged,
+                     int32_t *done, int32_t *ctr, hipStream_t st);
 void launch_find_diag(int64_t n, const int64_t *rp, const int32_t *ci, int64_t *diag, int32_t *fail,
                       hipStream_t st);
 // Symmetric Gauss-Seidel "factors" in ILU(0) storage (hypre relax type 6 as a

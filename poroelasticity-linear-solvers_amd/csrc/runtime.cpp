@@ -1673,18 +1673,39 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
         c.sync();
     } else {
+        // LDS sizing: the most staged entries one row needs
+        int64_t max_staged = 0;
+        {
+            const int T = (int)std::max<int64_t>(1, std::min<int64_t>(16, n / 65536));
+            std::vector<int64_t> ms(T, 0);
+            std::vector<std::thread> th;
+            for (int w = 0; w < T; ++w)
+                th.emplace_back([&, w] {
+                    for (int64_t i = n * w / T; i < n * (w + 1) / T; ++i) {
+                        int64_t tot = 0;
+                        for (int64_t k = rp[i]; k < dg[i]; ++k) tot += rp[ci[k] + 1] - dg[ci[k]] - 1;
+                        ms[w] = std::max(ms[w], tot);
+                    }
+                });
+            for (auto &x : th) x.join();
+            for (int w = 0; w < T; ++w) max_staged = std::max(max_staged, ms[w]);
+        }
         DBuf<int32_t> rowsL(std::max<int64_t>(n, 1));
         HIPCHK(hipMemcpyAsync(rowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
-        if (c.ilu_factor_dep && nlev_L > 1) {  // one launch; rows wait on their pivot rows' flags
+        // one launch where levels are narrow (FE blocks: ~30 rows per level); wide levels
+        // (BJACOBI on the headline: thousands of rows per level) keep a launch per level,
+        // which there costs less than the per-row flags (setup 1.42 vs 1.73 s at N = 59)
+        const bool dep = c.ilu_factor_dep == 1 ? nlev_L > 1 && n / nlev_L <= 2048 : c.ilu_factor_dep == 2;
+        if (dep) {  // one launch; rows wait on their pivot rows' flags
             DBuf<int32_t> done(std::max<int64_t>(n, 1)), ctr(2);
-            launch_ilu0_dep(n, rowsL.p, F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p, fail.p, F.max_row, done.p, ctr.p,
-                            c.st);
+            launch_ilu0_dep(n, rowsL.p, F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p, fail.p, F.max_row, max_staged,
+                            done.p, ctr.p, c.st);
             HIPCHK(hipGetLastError());
             c.sync();  // (done / ctr freed below)
         } else {
             for (int64_t l = 0; l < nlev_L; ++l)
                 launch_ilu0_level(Lptr[l + 1] - Lptr[l], rowsL.p + Lptr[l], F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p,
-                                  fail.p, F.max_row, c.st);
+                                  fail.p, F.max_row, max_staged, c.st);
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));

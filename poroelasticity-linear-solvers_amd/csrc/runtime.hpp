@@ -82,7 +82,7 @@ struct Ctx {
                                   // -1 where the level DAG is deep and narrow, 0 never, 1 whenever rows fit
     int sweep_window = -1;        // ... in 64-row windows with inverted window triangles (k_ilu_blocks_window):
                                   // -1 where the chain sweep would be chosen, 0 never, 1 whenever rows fit
-    int ilu_factor_dep = 1;       // ILU(0) numeric factorization in one dependency-driven launch (pls.ilu_factor_dep)
+    int ilu_factor_dep = 1;       // ILU(0) factorization in one dependency-driven launch: 1 narrow levels, 2 always, 0 never
     int ilu_view = 0;             // print every ILU / Gauss-Seidel PC's sweep choice to stderr (pls.ilu_view)
     int sweep_swin = -1;          // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin):
                                   // -1 where the ring sweep would run, 0 never, 1 whenever the block is y-resident

@@ -384,7 +384,7 @@ def test_ilu_factor_dep_bitwise(gpu, dim, N):
     opts.update(params_to_options(dict(BASE, **{"pc type": "diagonal"})))
     x = np.random.default_rng(9).standard_normal(s.A.shape[0])
     ys = []
-    for dep in ("1", "0"):
+    for dep in ("2", "0"):
         h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure,
                             dict(opts, **{"pls.ilu_factor_dep": dep}))
         ys.append(h.pc_apply(x))
