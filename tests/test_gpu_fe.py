@@ -390,3 +390,4 @@ def test_ilu_factor_dep_bitwise(gpu, dim, N):
         ys.append(h.pc_apply(x))
         h.destroy()
     assert np.array_equal(ys[0], ys[1])
+
