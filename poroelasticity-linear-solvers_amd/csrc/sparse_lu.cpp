@@ -190,6 +190,7 @@ struct PCSparseLU : PC {
     double setup_s[4] = {0, 0, 0, 0};  // ordering, symbolic, factorization, total
     double factor_gb = 0;
     int static_pivots = 0;
+    double tau_used = 0.0;  // the static pivoting threshold applied
 
     PCSparseLU(const DevCSR &M, const Options &o, Ctx &c) {
         type = "lu";
@@ -276,6 +277,7 @@ struct PCSparseLU : PC {
         double amax = 0.0;
         for (double v : A.v) amax = std::max(amax, std::fabs(v));
         const double tau = o.num("pls.lu_static_pivot", 64 * 2.220446049250313e-16) * amax;
+        tau_used = tau;
         double *Wcur = Wa.p, *Wprev = Wb.p;
         std::vector<int64_t> prev_ws;  // workspace offsets of the previous (deeper) level's fronts
         constexpr int CH = 32768;      // fronts per batched launch (grid z / y limit)
@@ -419,6 +421,13 @@ struct PCSparseLU : PC {
         setup_s[1] = t2 - t1;
         setup_s[2] = t3 - t2;
         setup_s[3] = now_s() - t0;
+        // perturbed pivots are reported always (MUMPS reports its own as warnings, INFO(1) > 0;
+        // not only under pls.lu_view)
+        if (static_pivots > 0 && !o.flag("pls.lu_view", false))
+            fprintf(stderr,
+                    "[sparse lu] n %lld: %d pivots below %.1e perturbed (static pivoting, pls.lu_static_pivot); "
+                    "%d refinement steps per solve\n",
+                    (long long)n, static_pivots, tau_used, refine);
         if (o.flag("pls.lu_view", false)) {
             int64_t maxf = 0;
             for (int32_t f : post) maxf = std::max(maxf, p[f] + q[f]);
