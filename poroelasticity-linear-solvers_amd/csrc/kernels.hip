@@ -1302,11 +1302,15 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
                         vn = k0 < e0 ? sv[k0] : 0.0;
                         dn = sd[t + 1];
                     }
+                    // rv[t] and the first entry the pivot updates are read together (one LDS
+                    // round trip per pivot on the chain): positions of pivot t's upper part
+                    // are > t and distinct, so nothing writes rv[lo0] in between
                     const double pc = rv[t];
+                    const double r0 = rv[lo0 < len ? lo0 : t];
                     if (pc != 0.0) {
                         const double mult = pc * dc;
                         if (lane == 0) rv[t] = mult;
-                        if (lo0 < len) rv[lo0] = rv[lo0] - mult * v0;
+                        if (lo0 < len) rv[lo0] = r0 - mult * v0;
                         for (int kk = kc + 64; kk < ec; kk += 64) {
                             const int lo = sc[kk];
                             if (lo < len) rv[lo] = rv[lo] - mult * sv[kk];
