@@ -1068,8 +1068,9 @@ static constexpr int ILU0_STAGE = 8192;  // staged upper-part entries per segmen
 __constant__ int ilu0_probe;  // diagnostics (pls.ilu0_probe N): phase times of every N-th row to stdout
 void set_ilu0_probe(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(ilu0_probe), &v, sizeof(int)); }
 static constexpr int64_t ILU0_SPIN_MAX = 1ll << 24;  // dependency polls before a row gives up (never expected)
-static constexpr int ILU0_LDS = 163840 - 64;          // dynamic LDS budget (beside ilu0_ctl)
+static constexpr int ILU0_LDS = 163840 - 512;         // dynamic LDS budget (beside ilu0_ctl, ilu0_cnt)
 __shared__ int32_t ilu0_ctl[4];                       // [0] drawn row (DEP), [1] abort
+__shared__ int32_t ilu0_cnt[64];                      // per pivot chunk: staging waves done (DEP)
 
 template <bool COH>
 __device__ __forceinline__ double ilu0_ld(const double *p) {
@@ -1094,14 +1095,16 @@ template <bool COH, bool POS, bool VAL>
 __device__ __forceinline__ void ilu0_stage_part(int ta, int tb, int base, int cnt, const int64_t *__restrict__ rp,
                                                 const int32_t *__restrict__ ci, const double *lu, int len, int hbits,
                                                 const int32_t *rc, const int32_t *so, const int64_t *su, int32_t *sc,
-                                                double *sv, const int32_t *hk, const int32_t *hp) {
-    const int tid = threadIdx.x;
+                                                double *sv, const int32_t *hk, const int32_t *hp, int wbase = 0,
+                                                int tid_ = -1, int nthr = ILU0_TPB) {
+    // (entry base + q is written at wbase + q; threads tid_ of nthr, default all)
+    const int tid = tid_ < 0 ? (int)threadIdx.x : tid_;
     const uint32_t hmask = (1u << hbits) - 1;
-    for (int q0 = 0; q0 < cnt; q0 += 8 * ILU0_TPB) {
+    for (int q0 = 0; q0 < cnt; q0 += 8 * nthr) {
         int64_t src[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int q = base + q0 + u * ILU0_TPB + tid;
+            const int q = base + q0 + u * nthr + tid;
             int lo = ta, hi = tb;  // last t with so[t] <= q
             while (hi - lo > 1) {
                 const int m = (lo + hi) >> 1;
@@ -1118,7 +1121,7 @@ __device__ __forceinline__ void ilu0_stage_part(int ta, int tb, int base, int cn
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int q = q0 + u * ILU0_TPB + tid;
+            const int q = q0 + u * nthr + tid;
             if (q < cnt) {
                 if (POS) {  // the column's position in the row (len: not in the pattern)
                     const int32_t j = cv[u];
@@ -1139,9 +1142,9 @@ __device__ __forceinline__ void ilu0_stage_part(int ta, int tb, int base, int cn
                         }
                         if (a < len && rc[a] == j) lo = a;
                     }
-                    sc[q] = lo;
+                    sc[wbase + q] = lo;
                 }
-                if (VAL) sv[q] = vv[u];
+                if (VAL) sv[wbase + q] = vv[u];
             }
         }
     }
@@ -1271,6 +1274,70 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
                 const int m = (tb + hi + 1) >> 1;
                 if (so[m] - base <= stage) tb = m; else hi = m - 1;
             }
+        }
+        if (tb > ta && pre) {
+            // DEP, one segment: waves 1-3 stage the values chunk by chunk (CH pivots)
+            // while wave 0 eliminates, waiting only for the chunk it needs next
+            // (values ~5 us, elimination ~9 us per row: the row's time after its
+            // pivots finish is the dependency chain's step)
+            if (pr) tq = wall_clock64();
+            const int CH = dl > 512 ? (dl + 63) / 64 : 8, nch = (dl + CH - 1) / CH;
+            if (tid < 64) ilu0_cnt[tid] = 0;
+            __syncthreads();
+            if (!w0) {
+                for (int cc = 0; cc < nch; ++cc) {
+                    const int t0 = cc * CH, t1 = min(dl, t0 + CH);
+                    ilu0_stage_part<DEP, false, true>(t0, t1, so[t0], so[t1] - so[t0], rp, ci, lu, len, hbits, rc, so,
+                                                      su, sc, sv, hk, hp, so[t0], tid - 64, ILU0_TPB - 64);
+                    if (lane == 0) __hip_atomic_fetch_add(ilu0_cnt + cc, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            } else {
+                auto wait_chunk = [&](int cc) {
+                    for (int64_t spins = 0;
+                         __hip_atomic_load(ilu0_cnt + cc, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                         ILU0_TPB / 64 - 1;
+                         ++spins) {
+                        if (spins > ILU0_SPIN_MAX) {  // never expected: report, do not hang
+                            if (lane == 0) atomicMax(fail, 3);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                };
+                wait_chunk(0);
+                int k0 = so[0] + lane, e0 = so[1];
+                int lon = k0 < e0 ? sc[k0] : len;
+                double vn = k0 < e0 ? sv[k0] : 0.0, dn = sd[0];
+                for (int t = 0; t < dl; ++t) {
+                    const int lo0 = lon, kc = k0, ec = e0;
+                    const double v0 = vn, dc = dn;
+                    if (t + 1 < dl) {
+                        if ((t + 1) % CH == 0) wait_chunk((t + 1) / CH);
+                        k0 = so[t + 1] + lane;
+                        e0 = so[t + 2];
+                        lon = k0 < e0 ? sc[k0] : len;
+                        vn = k0 < e0 ? sv[k0] : 0.0;
+                        dn = sd[t + 1];
+                    }
+                    const double pc = rv[t];
+                    const double r0 = rv[lo0 < len ? lo0 : t];
+                    if (pc != 0.0) {
+                        const double mult = pc * dc;
+                        if (lane == 0) rv[t] = mult;
+                        if (lo0 < len) rv[lo0] = r0 - mult * v0;
+                        for (int kk = kc + 64; kk < ec; kk += 64) {
+                            const int lo = sc[kk];
+                            if (lo < len) rv[lo] = rv[lo] - mult * sv[kk];
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            __syncthreads();
+            if (pr) t_elim += wall_clock64() - tq;
+            ta = tb;
+            ++nseg;
+            continue;
         }
         if (tb > ta) {
             if (pr) tq = wall_clock64();
@@ -1457,7 +1524,7 @@ void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const in
     (void)hipMemsetAsync(done, 0, sizeof(int32_t) * n, st);
     (void)hipMemsetAsync(ctr, 0, sizeof(int32_t) * 2, st);
     // persistent: the workgroups that fit (4 per CU at most), never more than rows
-    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(4, 163840 / (int64_t)(lds + 64)));
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(4, 163840 / (int64_t)(lds + 512)));
     const int64_t grid = std::min<int64_t>(n, 256 * per_cu);
     k_ilu0_dep<<<(unsigned)grid, ILU0_TPB, lds, st>>>(n, rows, rp, ci, lu, diag, dinv, fail,
                                                        (int)(max_row < 1 ? 1 : max_row), stage, hbits, done, ctr);
