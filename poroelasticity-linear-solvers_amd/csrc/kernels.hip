@@ -1304,23 +1304,29 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
                         __builtin_amdgcn_s_sleep(1);
                     }
                 };
+                // software pipeline: pivot t computes while pivot t + 1's first entries
+                // and pivot t + 2's offsets are in flight; rv[t] and the first update
+                // target are read first, so the chain waits for one LDS round trip
                 wait_chunk(0);
-                int k0 = so[0] + lane, e0 = so[1];
-                int lon = k0 < e0 ? sc[k0] : len;
-                double vn = k0 < e0 ? sv[k0] : 0.0, dn = sd[0];
+                int kn = so[0] + lane, en = so[1];
+                int lon = kn < en ? sc[kn] : len;
+                double vn = kn < en ? sv[kn] : 0.0, dn = sd[0];
+                int s2a = dl > 1 ? so[1] : 0, s2b = dl > 1 ? so[2] : 0;  // pivot t + 1's range (next)
                 for (int t = 0; t < dl; ++t) {
-                    const int lo0 = lon, kc = k0, ec = e0;
+                    const int lo0 = lon, kc = kn, ec = en;
                     const double v0 = vn, dc = dn;
-                    if (t + 1 < dl) {
-                        if ((t + 1) % CH == 0) wait_chunk((t + 1) / CH);
-                        k0 = so[t + 1] + lane;
-                        e0 = so[t + 2];
-                        lon = k0 < e0 ? sc[k0] : len;
-                        vn = k0 < e0 ? sv[k0] : 0.0;
-                        dn = sd[t + 1];
-                    }
                     const double pc = rv[t];
                     const double r0 = rv[lo0 < len ? lo0 : t];
+                    if (t + 1 < dl) {
+                        if ((t + 1) % CH == 0) wait_chunk((t + 1) / CH);
+                        kn = s2a + lane;
+                        en = s2b;
+                        lon = kn < en ? sc[kn] : len;
+                        vn = kn < en ? sv[kn] : 0.0;
+                        dn = sd[t + 1];
+                        s2a = s2b;
+                        s2b = t + 3 <= dl ? so[t + 3] : s2b;
+                    }
                     if (pc != 0.0) {
                         const double mult = pc * dc;
                         if (lane == 0) rv[t] = mult;
