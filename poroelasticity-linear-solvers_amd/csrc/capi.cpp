@@ -555,6 +555,9 @@ struct Handle {
         ctx.sweep_window = (int)opt.integer("pls.sweep_window", -1);
         ctx.ilu_factor_dep = (int)opt.integer("pls.ilu_factor_dep", 1);
         ctx.ilu_view = (int)opt.integer("pls.ilu_view", 0);
+        // test knobs of the ILU(0) factorization: staged-entry cap, persistent grid cap
+        ctx.ilu0_stage_cap = (int)opt.integer("pls.ilu0_stage", -1);
+        ctx.ilu_dep_grid = (int)opt.integer("pls.ilu_dep_grid", 0);
         ctx.sweep_swin = (int)opt.integer("pls.sweep_swin", 0);
         ctx.amg_csr_below = opt.num("pls.amg_csr_below", 16.0);
         if (opt.flag("pls.debug_bounds", false) || opt.integer("pls.debug_partial_cap", 0) > 0)
@@ -624,6 +627,7 @@ void BlockPC::apply(const double *x, double *y, Ctx &c) {
                 span(0, F.b_split, "light");
             }
             H.ksp_fp->note_preonly();
+            c.check_bounds();  // (what KSP::solve does after a solve; pls.debug_bounds)
         } else {
             // t = x_fp - P_fp,s y_s   (Preconditioner.py:232-233, fused)
             spmv(H.Mfp_s, y, H.t_fp.p, c, -1.0, 1.0, x + ns);
@@ -758,6 +762,7 @@ static void setup_fp_pipeline(Handle &H) {
     const int64_t mode = H.opt.integer("pls.fp_pipeline", -1);
     if (H.three_way || H.distributed || mode == 0) return;
     if (!H.ksp_fp || H.ksp_fp->type != "preonly" || H.mixer.order > 0) return;
+    if (H.ksp_fp->monitor) return;  // -fp_ksp_monitor: the plain path's KSP::solve prints it
     if (mode < 0 && !(H.ksp_s && H.ksp_s->type == "preonly" && dynamic_cast<PCILU *>(H.ksp_s->pc))) return;
     PCILU *pc = dynamic_cast<PCILU *>(H.ksp_fp->pc);
     if (!pc || !pc->can_apply_blocks() || pc->nblocks < 8 || pc->block_levels_h.size() != (size_t)pc->nblocks) return;
@@ -788,24 +793,21 @@ static void setup_fp_pipeline(Handle &H) {
     if (!H.ctx2) H.ctx2 = std::make_unique<Ctx>();
     if (!F.ev_t) HIPCHK(hipEventCreateWithFlags(&F.ev_t, hipEventDisableTiming));
     if (!F.ev_p) HIPCHK(hipEventCreateWithFlags(&F.ev_p, hipEventDisableTiming));
-    // the heavy blocks' levels hold a few slices each: waves in groups of the
-    // next power of two >= the most slices of any of their levels own the
-    // levels round robin, so factor data is requested (waves / group) levels
-    // ahead -- under the concurrent product's HBM traffic the two-level
-    // pipeline of the plain sweep exposed the load latency (measured: the 11
-    // pressure blocks took 1.24 ms beside the product, ~0.5 ms alone)
+    // Experimental variants for the heavy sweep (both measured no faster, kept
+    // opt-in): round-robin wave groups owning whole levels
+    // (pls.fp_pipeline_rr g) and 6 levels of factor data in flight on 8 waves
+    // (pls.fp_pipeline_depth 6, levels of <= 8 slices) -- meant for the
+    // concurrent product's HBM traffic, which stretches a load's latency past
+    // the plain sweep's two levels (the 11 pressure blocks: 1.24 ms beside the
+    // unmasked product, ~0.5 ms alone)
     int64_t msl = 0;
     for (int64_t k = b; k < nb; ++k) msl = std::max(msl, pc->block_maxsl_h.empty() ? 16 : pc->block_maxsl_h[k]);
-    int grp = 1;
-    while (grp < msl) grp *= 2;
-    const int64_t rr_opt = H.opt.integer("pls.fp_pipeline_rr", -1);  // -1 auto, 0 off, a group size forced
+    // pls.fp_pipeline_rr (experimental, measured no faster): 0 / -1 off (default), or a forced group size
+    const int64_t rr_opt = H.opt.integer("pls.fp_pipeline_rr", 0);
     if (rr_opt > 16 || (rr_opt > 0 && (rr_opt & (rr_opt - 1))))
-        throw Error("pls.fp_pipeline_rr must be -1 (auto), 0 or a power of two <= 16");
-    // default: 8 waves (levels of <= 8 slices need no more) with 6 levels of
-    // factor data in flight -- the heavy blocks sweep beside the product, whose
-    // HBM traffic stretches a load's latency past the plain sweep's two levels
+        throw Error("pls.fp_pipeline_rr must be 0 (off) or a power of two <= 16");
     const bool deep = msl <= 8 && H.opt.integer("pls.fp_pipeline_depth", 2) == 6;
-    F.rr = rr_opt >= 0 ? (int)rr_opt : 0;
+    F.rr = rr_opt > 0 ? (int)rr_opt : 0;
     F.tpb = deep && F.rr == 0 ? 512 : 0;
     F.depth = deep && F.rr == 0 ? 6 : 2;
     // the sweep holds max_len * 8 bytes of the CU's 160 KiB: reserve more than what is left

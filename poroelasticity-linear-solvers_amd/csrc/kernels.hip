@@ -1167,6 +1167,8 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
     // LDS: row values [max_row] | staged values [stage] | row cols [max_row] | staged positions [stage]
     //      | per-pivot staged offsets [max_row + 1] | per-pivot 1/u_rr [max_row] | per-pivot first
     //      upper entry [max_row] | hash keys, positions [2^hbits each]
+    // (stage == 0: no staged arrays -- every pivot goes through global memory
+    // and reads 1/u_rr there -- so rows of up to ~13.6k entries fit, ilu0_max_row)
     double *rv = reinterpret_cast<double *>(smem);
     double *sv = rv + max_row;
     int32_t *rc = reinterpret_cast<int32_t *>(sv + stage);
@@ -1174,7 +1176,7 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
     int32_t *so = sc + stage;
     double *sd = reinterpret_cast<double *>(((uintptr_t)(so + max_row + 1) + 7) & ~(uintptr_t)7);
     int64_t *su = reinterpret_cast<int64_t *>(sd + max_row);
-    int32_t *hk = reinterpret_cast<int32_t *>(su + max_row);
+    int32_t *hk = stage > 0 ? reinterpret_cast<int32_t *>(su + max_row) : so;
     int32_t *hp = hk + (hbits > 0 ? 1 << hbits : 0);
     const uint32_t hmask = (1u << hbits) - 1;
     auto hslot = [&](int32_t c) { return ((uint32_t)c * 2654435761u) >> (32 - hbits); };
@@ -1259,7 +1261,8 @@ __device__ __forceinline__ bool ilu0_row(int64_t i, const int64_t *__restrict__ 
         __syncthreads();
         if (ilu0_ctl[1]) return false;
     }
-    for (int t = tid; t < dl; t += ILU0_TPB) sd[t] = ilu0_ld<DEP>(dinv + rc[t]);
+    if (stage > 0)
+        for (int t = tid; t < dl; t += ILU0_TPB) sd[t] = ilu0_ld<DEP>(dinv + rc[t]);
     __syncthreads();
     if (pr) tp[3] = wall_clock64();
     int nseg = 0, nglob = 0;
@@ -1497,8 +1500,19 @@ __global__ __launch_bounds__(ILU0_TPB) void k_ilu0_dep(int64_t n, const int32_t 
 // entries and a 2^hbits-slot column hash
 static size_t ilu0_lds_bytes(int64_t max_row, int64_t stage, int hbits) {
     const int64_t m = max_row < 1 ? 1 : max_row;
-    const int64_t extra = (m + 1) * 4 + 8 + m * 16 + (hbits > 0 ? (int64_t)8 << hbits : 0);
+    // the per-pivot arrays (offsets, 1/u_rr, first entries) exist only with a stage
+    const int64_t extra = (stage > 0 ? (m + 1) * 4 + 8 + m * 16 : 0) + (hbits > 0 ? (int64_t)8 << hbits : 0);
     return (size_t)(((m * 12 + stage * 12 + extra) + 15) & ~(int64_t)15);
+}
+// test knobs (process-wide, pls.ilu0_stage / pls.ilu_dep_grid): a cap on the
+// staged entries (0: none staged, every pivot through global memory; small
+// values force the segmented path) and on the persistent launch's grid (1: one
+// workgroup takes the rows in draw order -- a draw order that is not a
+// topological order of the pivot DAG would then stop at the bounded wait)
+static int ilu0_stage_cap = -1, ilu0_grid_cap = 0;
+void set_ilu0_test_caps(int stage_cap, int grid_cap) {
+    ilu0_stage_cap = stage_cap;
+    ilu0_grid_cap = grid_cap;
 }
 // hash slots (at least twice the longest row) and staged entries (the most one
 // row needs, at most ILU0_STAGE) that fit the LDS; 0 = none
@@ -1507,14 +1521,16 @@ static void ilu0_plan(int64_t max_row, int64_t max_staged, int &stage, int &hbit
     while ((int64_t)1 << hbits < 2 * max_row) ++hbits;
     if (ilu0_lds_bytes(max_row, 0, hbits) > ILU0_LDS) hbits = 0;
     stage = 0;
-    const int64_t want = std::min<int64_t>(ILU0_STAGE, std::max<int64_t>(256, (max_staged + 63) & ~(int64_t)63));
-    for (int64_t st = want; st >= 256; st /= 2)
+    int64_t want = std::min<int64_t>(ILU0_STAGE, std::max<int64_t>(256, (max_staged + 63) & ~(int64_t)63));
+    if (ilu0_stage_cap >= 0) want = std::min<int64_t>(want, ilu0_stage_cap);
+    for (int64_t st = want; st >= std::min<int64_t>(want, 256) && st > 0; st /= 2)
         if (ilu0_lds_bytes(max_row, st, hbits) <= ILU0_LDS) {
             stage = (int)st;
             break;
         }
 }
-int ilu0_max_row() { return (ILU0_LDS - 16) / 32; }  // (row values, columns, offsets, 1/u_rr, first entries)
+// the longest row with no stage: row values and columns (12 bytes per entry)
+int ilu0_max_row() { return (ILU0_LDS - 16) / 12; }
 void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
                      const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int64_t max_staged,
                      int32_t *done, int32_t *ctr, hipStream_t st) {
@@ -1531,7 +1547,8 @@ void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const in
     (void)hipMemsetAsync(ctr, 0, sizeof(int32_t) * 2, st);
     // persistent: the workgroups that fit (4 per CU at most), never more than rows
     const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(4, 163840 / (int64_t)(lds + 512)));
-    const int64_t grid = std::min<int64_t>(n, 256 * per_cu);
+    int64_t grid = std::min<int64_t>(n, 256 * per_cu);
+    if (ilu0_grid_cap > 0) grid = std::min<int64_t>(grid, ilu0_grid_cap);
     k_ilu0_dep<<<(unsigned)grid, ILU0_TPB, lds, st>>>(n, rows, rp, ci, lu, diag, dinv, fail,
                                                        (int)(max_row < 1 ? 1 : max_row), stage, hbits, done, ctr);
 }

@@ -48,7 +48,7 @@ void launch_extract_fill(const int64_t *rp, const int32_t *ci, const double *val
                          int32_t *out_ci, double *out_val, hipStream_t st);
 
 // y = alpha * (M x) + beta * z     (z may be null when beta == 0)
-void set_spmv_short_rows(bool on);  // CSR rows of < 12 entries: one lane per row (default on; pls.spmv_short)
+void set_spmv_short_rows(bool on);  // CSR rows of < 12 entries: one lane per row (default off; pls.spmv_short 1, opt-in)
 void launch_spmv(int64_t nrows, int64_t nnz, const int64_t *rp, const int32_t *ci,
                  const double *val, const double *x, double *y, double alpha, double beta,
                  const double *z, hipStream_t st);
@@ -104,6 +104,10 @@ void launch_ilu0_level(int64_t nrows_level, const int32_t *rows, const int64_t *
 void launch_ilu0_dep(int64_t n, const int32_t *rows, const int64_t *rp, const int32_t *ci, double *lu,
                      const int64_t *diag, double *dinv, int32_t *fail, int64_t max_row, int64_t max_staged,
                      int32_t *done, int32_t *ctr, hipStream_t st);
+// test knobs (process-wide; pls.ilu0_stage, pls.ilu_dep_grid): stage_cap < 0 default,
+// 0 no staged pivots, > 0 at most that many staged entries; grid_cap > 0 caps
+// k_ilu0_dep's persistent grid (1: one workgroup)
+void set_ilu0_test_caps(int stage_cap, int grid_cap);
 void launch_find_diag(int64_t n, const int64_t *rp, const int32_t *ci, int64_t *diag, int32_t *fail,
                       hipStream_t st);
 // Symmetric Gauss-Seidel "factors" in ILU(0) storage (hypre relax type 6 as a
@@ -215,7 +219,7 @@ void launch_ilu_blocks_swin(int64_t n, int64_t nblocks, const int64_t *bstart, c
                             const int32_t *Uncol, const double *Unval, const int64_t *Uwfar, const int32_t *Ufcol,
                             const double *Ufval, const double *Utinv, const double *x, double *y, int64_t lds_bytes,
                             hipStream_t st);
-int ilu_swin_lds_budget();  // bytes of LDS a super-window's staged inverses + near streams may take  // factor entries per lane the LDS sweep keeps in registers
+int ilu_swin_lds_budget();  // bytes of LDS a super-window's staged inverses + near streams may take
 // The chain sweep (kernels.hip, k_ilu_blocks_chain): one wave per LDS-resident
 // block walks its slices in order with ilu_chain_depth() slices in flight
 // (deep, narrow level DAGs).  Per triangle and block: first slice's entry

@@ -1692,11 +1692,24 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         }
         DBuf<int32_t> rowsL(std::max<int64_t>(n, 1));
         HIPCHK(hipMemcpyAsync(rowsL.p, ordL.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+        set_ilu0_test_caps(c.ilu0_stage_cap, c.ilu_dep_grid);  // (process-wide: set per factorization)
         // one launch where levels are narrow (FE blocks: ~30 rows per level); wide levels
         // (BJACOBI on the headline: thousands of rows per level) keep a launch per level,
         // which there costs less than the per-row flags (setup 1.42 vs 1.73 s at N = 59)
         const bool dep = c.ilu_factor_dep == 1 ? nlev_L > 1 && n / nlev_L <= 2048 : c.ilu_factor_dep == 2;
         if (dep) {  // one launch; rows wait on their pivot rows' flags
+            // the launch is deadlock-free only if the draw order is a topological
+            // order of the pivot DAG (every pivot row r < i with l_ir != 0 drawn
+            // before row i): the lowest unfinished drawn row then always has its
+            // pivots done.  level_order gives one by construction; checked here
+            // (O(nnz)) so that a wrong order is an error, not a bounded wait
+            std::vector<int32_t> pos(n);
+            for (int64_t q = 0; q < n; ++q) pos[ordL[q]] = (int32_t)q;
+            for (int64_t i = 0; i < n; ++i)
+                for (int64_t k = rp[i]; k < dg[i]; ++k)
+                    if (pos[ci[k]] >= pos[i])
+                        throw Error("ILU(0): factorization draw order is not topological (row " +
+                                    std::to_string(i) + " before its pivot row " + std::to_string(ci[k]) + ")");
             DBuf<int32_t> done(std::max<int64_t>(n, 1)), ctr(2);
             launch_ilu0_dep(n, rowsL.p, F.rp.p, F.ci.p, F.val.p, diag.p, dinv.p, fail.p, F.max_row, max_staged,
                             done.p, ctr.p, c.st);
@@ -1708,6 +1721,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                                   fail.p, F.max_row, max_staged, c.st);
         }
         HIPCHK(hipGetLastError());
+        set_ilu0_test_caps(-1, 0);  // (launches above are enqueued with their plan: knobs off for other users)
         HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
         c.sync();
     }

@@ -84,8 +84,11 @@ struct Ctx {
                                   // -1 where the chain sweep would be chosen, 0 never, 1 whenever rows fit
     int ilu_factor_dep = 1;       // ILU(0) factorization in one dependency-driven launch: 1 narrow levels, 2 always, 0 never
     int ilu_view = 0;             // print every ILU / Gauss-Seidel PC's sweep choice to stderr (pls.ilu_view)
-    int sweep_swin = -1;          // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin):
-                                  // -1 where the ring sweep would run, 0 never, 1 whenever the block is y-resident
+    int ilu0_stage_cap = -1;      // test knob (pls.ilu0_stage): staged entries of the ILU(0) factorization, -1 default
+    int ilu_dep_grid = 0;         // test knob (pls.ilu_dep_grid): k_ilu0_dep's persistent grid capped (0: none)
+    int sweep_swin = 0;           // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin, experimental,
+                                  // measured slower than the ring sweep): 0 never (default, capi), -1 where the ring
+                                  // sweep would run, 1 whenever the block is y-resident
     double amg_csr_below = 16.0;  // AMG operators with fewer entries per row than this stay CSR (pls.amg_csr_below)
     bool halo_overlap = true;     // distributed SpMV: interior slices overlap the halo exchange (pls.halo_overlap)
     hipStream_t st_comm = nullptr;  // stream of the overlapped halo exchange (created on first use)

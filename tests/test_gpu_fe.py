@@ -391,3 +391,78 @@ def test_ilu_factor_dep_bitwise(gpu, dim, N):
         h.destroy()
     assert np.array_equal(ys[0], ys[1])
 
+
+
+def _dep_pair(s, a_opts, b_opts, x):
+    from lib.handle import Handle, params_to_options
+    opts = dict(_db("ilu"))
+    opts.update(params_to_options(dict(BASE, **{"pc type": "diagonal"})))
+    ys = []
+    for extra in (a_opts, b_opts):
+        h = Handle.from_csr(s.A, s.P, s.P_diff, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, dict(opts, **extra))
+        ys.append(h.pc_apply(x))
+        h.destroy()
+    return ys
+
+
+@pytest.mark.parametrize("dim,N", [(2, 24), (3, 4)])
+def test_ilu_factor_dep_one_workgroup(gpu, dim, N):
+    """k_ilu0_dep on a one-workgroup grid
+    (pls.ilu_dep_grid 1).  That workgroup takes the rows in draw order, one
+    after the other, so the launch completes only if the draw order is a
+    topological order of the pivot DAG -- a row whose pivot row is drawn
+    later would wait at the bounded poll and the setup would raise ("wait
+    exceeded its bound").  Factors bitwise the per-level launches'."""
+    s = F.assemble_swelling(dim, N, "diagonal")
+    x = np.random.default_rng(5).standard_normal(s.A.shape[0])
+    ya, yb = _dep_pair(s, {"pls.ilu_factor_dep": "2", "pls.ilu_dep_grid": "1"}, {"pls.ilu_factor_dep": "0"}, x)
+    assert np.all(np.isfinite(ya))
+    assert np.array_equal(ya, yb)
+
+
+@pytest.mark.parametrize("stage", ["0", "64", "256"])
+def test_ilu_factor_dep_stage_paths(gpu, stage):
+    """the DEP factorization's other two pivot paths, bitwise the
+    per-level launches with the default stage.  pls.ilu0_stage 0: no pivot
+    staged, every pivot row's upper part and 1/u_rr read from global memory
+    with agent-coherent loads; 64 / 256: a row's pivots span several stage
+    segments (the segmented staging path with coherent loads).  3-D N=6 FE
+    blocks: the pivots' upper parts of one row total up to 6,048 entries."""
+    s = F.assemble_swelling(3, 6, "diagonal")
+    x = np.random.default_rng(6).standard_normal(s.A.shape[0])
+    ya, yb = _dep_pair(s, {"pls.ilu_factor_dep": "2", "pls.ilu0_stage": stage}, {"pls.ilu_factor_dep": "0"}, x)
+    assert np.all(np.isfinite(ya))
+    assert np.array_equal(ya, yb)
+    # the per-level launches take the same paths (stage cap applies to both kernels)
+    yc, yd = _dep_pair(s, {"pls.ilu_factor_dep": "0", "pls.ilu0_stage": stage}, {"pls.ilu_factor_dep": "0"}, x)
+    assert np.array_equal(yc, yd)
+
+
+def test_ilu0_row_longer_than_the_staged_layout(gpu):
+    """a row of 6,000 entries (past the 5,103 the staged LDS layout
+    holds; the unstaged layout takes ~13,600) in the solid block of a 2-D N=40
+    system, factorized (no stage: pivots through global memory) and swept;
+    the PC apply against the CPU oracle's ILU(0)."""
+    import scipy.sparse as sp
+    from lib.handle import Handle, params_to_options
+    s = F.assemble_swelling(2, 40, "diagonal")
+    is_s = np.asarray(s.is_s)
+    r = int(is_s[-1])
+    cols = is_s[np.linspace(0, is_s.size - 2, 6000).astype(np.int64)]
+    P = s.P.tolil(copy=True)
+    for c in cols.tolist():
+        P[r, c] = P[r, c] + 1e-7
+    P = sp.csr_matrix(P)
+    P.sort_indices()
+    assert P.indptr[r + 1] - P.indptr[r] >= 6000
+    params = dict(BASE, **{"pc type": "diagonal"})
+    db = _db("ilu")
+    opts = dict(db)
+    opts.update(params_to_options(params))
+    h = Handle.from_csr(s.A, P, None, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    o = OracleSolver(s.A, P, None, s.is_s, s.is_f, s.is_p, params, db, s.bcs_sub_pressure)
+    x = np.random.default_rng(7).standard_normal(s.A.shape[0])
+    y = h.pc_apply(x)
+    yo = o.block_pc.apply(x)
+    h.destroy()
+    assert np.max(np.abs(y - yo)) <= 1e-12 * np.max(np.abs(yo))

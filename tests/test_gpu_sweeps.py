@@ -96,13 +96,20 @@ def test_window_sweep_long_block_matches_workgroup_sweep(gpu, capfd):
     assert np.max(np.abs(yw - yl)) <= 1e-12 * scale
 
 
-@pytest.mark.parametrize("N,blocks", [(16, 24)])
-def test_fp_pipeline_bitwise(gpu, capfd, N, blocks):
+@pytest.mark.parametrize("N,blocks,variant", [
+    (16, 24, {}),
+    (16, 24, {"pls.fp_pipeline_depth": "6"}),
+    (16, 24, {"pls.fp_pipeline_rr": "2"}),
+    (16, 24, {"pls.fp_pipeline_rr": "4"}),
+])
+def test_fp_pipeline_bitwise(gpu, capfd, N, blocks, variant):
     """The 2-way PC's pressure-first pipeline (pls.fp_pipeline, capi.cpp
     setup_fp_pipeline): the heavy pressure BJACOBI blocks of the fp block get
     their rows of t = x_fp - P_fp,s y_s first and sweep on a second stream.
     Same per-row sums and per-block sweeps as the plain path: PC applies and
-    whole solves bitwise equal, and the pipeline must have engaged."""
+    whole solves bitwise equal, and the pipeline must have engaged.  Also the
+    experimental heavy-sweep variants: 6 levels in flight on 8
+    waves (sweep2_deep) and round-robin wave groups of 2 / 4 (sweep_rr)."""
     from lib.handle import Handle, params_to_options
     from oracle import synthetic as S
     spec = S.SynthSpec(3, N)
@@ -112,7 +119,7 @@ def test_fp_pipeline_bitwise(gpu, capfd, N, blocks):
           "fp_pc_bjacobi_blocks": str(blocks), "pls.ilu_view": "1"}
     out = {}
     for pipe in ("1", "0"):
-        opts = dict(db, **{"pls.fp_pipeline": pipe})
+        opts = dict(db, **{"pls.fp_pipeline": pipe}, **(variant if pipe == "1" else {}))
         opts.update(params_to_options(params))
         capfd.readouterr()
         h = Handle.synthetic(spec.dim, spec.N, spec.seed, spec.delta, opts)
