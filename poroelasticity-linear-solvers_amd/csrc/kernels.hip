@@ -505,7 +505,13 @@ __global__ __launch_bounds__(TPB) void k_set(int64_t n, double a, double *y) {
 __global__ __launch_bounds__(TPB) void k_scale(int64_t n, double a, double *y) {
     for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) y[i] *= a;
 }
-__global__ __launch_bounds__(TPB) void k_axpby(int64_t n, double a, const double *x, double b, double *y) {
+// (pa / pb: the scalars read from device memory instead, skip: no-op when *skip
+// -- the device-resident CG; one kernel body, so both paths round alike)
+__global__ __launch_bounds__(TPB) void k_axpby(int64_t n, double a, const double *x, double b, double *y,
+                                               const double *pa, const double *pb, const int64_t *skip) {
+    if (skip && *skip) return;
+    if (pa) a = *pa;
+    if (pb) b = *pb;
     for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
         y[i] = a * x[i] + b * y[i];
 }
@@ -594,7 +600,70 @@ void launch_scale(int64_t n, double a, double *y, hipStream_t st) {
     if (n > 0) k_scale<<<stream_grid(n), TPB, 0, st>>>(n, a, y);
 }
 void launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st) {
-    if (n > 0) k_axpby<<<stream_grid(n), TPB, 0, st>>>(n, a, x, b, y);
+    if (n > 0) k_axpby<<<stream_grid(n), TPB, 0, st>>>(n, a, x, b, y, nullptr, nullptr, nullptr);
+}
+void launch_axpby_dev(int64_t n, const double *pa, const double *x, const double *pb, double *y, const int64_t *skip,
+                      hipStream_t st) {
+    if (n > 0) k_axpby<<<stream_grid(n), TPB, 0, st>>>(n, 0.0, x, 0.0, y, pa, pb, skip);
+}
+
+// ------------------------------------------------ device-resident CG state --
+// KSPSolve_CG's scalar recurrences (runtime.cpp KSP::solve_cg) on the device,
+// one thread, so the host enqueues iterations without reading a scalar back:
+// every phase returns at once when the solve has ended (I[CG_DONE]); the
+// vector updates that follow check the same flag.  Same operations as the host
+// loop (IEEE division and square root): bitwise the same iterates.
+__device__ int cg_conv(const CgParams &p, double r, double rnorm0, double ttol) {
+    if (isnan(r) || isinf(r)) return p.r_nan;
+    if (r <= ttol) return r < p.atol ? p.r_atol : p.r_rtol;
+    if (r >= p.dtol * rnorm0) return p.r_dtol;
+    return 0;
+}
+__global__ void k_cg_state(int phase, int64_t i, double *S, int64_t *I, double *hist, CgParams p) {
+    if (threadIdx.x != 0 || I[CG_DONE]) return;
+    auto stop = [&](int reason) {
+        I[CG_REASON] = reason;
+        I[CG_DONE] = 1;
+    };
+    switch (phase) {
+        case CG_TOP: {  // loop head of iteration i (beta = (z, r) of the previous step)
+            I[CG_ITS] = i + 1;
+            const double beta = S[CG_BETA], betaold = S[CG_BETAOLD];
+            if (beta == 0.0) return stop(p.r_atol);
+            if (i > 0 && beta * betaold < 0.0) return stop(p.r_indef_pc);
+            if (i > 0) S[CG_BB] = beta / betaold;
+            return;
+        }
+        case CG_MID: {  // dpi = (p, A p) in S[CG_SLOT]
+            const double dpiold = S[CG_DPI], dpi = S[CG_SLOT];
+            S[CG_DPI] = dpi;
+            S[CG_BETAOLD] = S[CG_BETA];
+            const int sd = (dpi > 0) - (dpi < 0), so = (dpiold > 0) - (dpiold < 0);
+            if (dpi == 0.0 || (i > 0 && sd * so < 0)) return stop(p.r_indef_mat);
+            const double a = S[CG_BETA] / dpi;
+            S[CG_A] = a;
+            S[CG_NEGA] = -a;
+            return;
+        }
+        case CG_POST: {  // the residual norm's square (or 0) in S[CG_SLOT]
+            const double dp = p.norm ? sqrt(S[CG_SLOT]) : 0.0;
+            S[CG_RNORM] = dp;
+            hist[I[CG_HCOUNT]++] = dp;
+            if (p.norm) {
+                const int r = cg_conv(p, dp, S[CG_RNORM0], S[CG_TTOL]);
+                if (r) return stop(r);
+            }
+            return;
+        }
+        case CG_END: {  // beta = (z, r) in S[CG_SLOT2]; i counts this iteration
+            S[CG_BETA] = S[CG_SLOT2];
+            if (i + 1 >= p.maxit) return stop(p.r_its);
+            return;
+        }
+    }
+}
+void launch_cg_state(int phase, int64_t i, double *S, int64_t *I, double *hist, const CgParams &p, hipStream_t st) {
+    k_cg_state<<<1, 64, 0, st>>>(phase, i, S, I, hist, p);
 }
 void launch_waxpby(int64_t n, double a, const double *x, double b, const double *y, double *w, hipStream_t st) {
     if (n > 0) k_waxpby<<<stream_grid(n), TPB, 0, st>>>(n, a, x, b, y, w);
@@ -3099,6 +3168,25 @@ void launch_ilu_blocks_lds(int64_t n, int64_t nblocks, const int64_t *Lgoff, con
         return;
     }
     const size_t bytes = (size_t)(max_len > 0 ? max_len : n / nblocks + 1) * 8;
+    if ((depth == 3 || depth == 4) && rr == 0) {  // 3 / 4 levels in flight on up to 16 waves (pls.sweep_depth)
+        static bool conf34 = false;
+        if (!conf34) {
+            (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds<false, 3, 1024>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)163840);
+            (void)hipFuncSetAttribute((const void *)k_ilu_blocks_lds<false, 4, 1024>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)163840);
+            conf34 = true;
+        }
+        if (depth == 3)
+            k_ilu_blocks_lds<false, 3, 1024><<<grid, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval,
+                                                                       Llpr, Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr,
+                                                                       x, y, prof, rr, bstart, blk_hi);
+        else
+            k_ilu_blocks_lds<false, 4, 1024><<<grid, tpb, bytes, st>>>(n, nblocks, Lgoff, Lgslice, Lsptr, Lcol, Lval,
+                                                                       Llpr, Ugoff, Ugslice, Usptr, Ucol, Uval, Ulpr,
+                                                                       x, y, prof, rr, bstart, blk_hi);
+        return;
+    }
     if (depth == 6 && tpb <= 512 && rr == 0) {  // 6 levels in flight, at most 8 waves (register room)
         static bool conf6 = false;
         if (!conf6) {

@@ -60,6 +60,21 @@ void launch_set(int64_t n, double a, double *y, hipStream_t st);
 void launch_scale(int64_t n, double a, double *y, hipStream_t st);
 // y = a*x + b*y
 void launch_axpby(int64_t n, double a, const double *x, double b, double *y, hipStream_t st);
+// the same with a = *pa, b = *pb read on the device; a no-op when *skip (device-resident CG)
+void launch_axpby_dev(int64_t n, const double *pa, const double *x, const double *pb, double *y, const int64_t *skip,
+                      hipStream_t st);
+// device-resident CG (KSP::solve_cg_dev): scalar state S (doubles) / I (ints) and its phases
+enum CgS { CG_BETA, CG_BETAOLD, CG_DPI, CG_A, CG_NEGA, CG_BB, CG_ONE, CG_RNORM, CG_RNORM0, CG_TTOL, CG_SLOT, CG_SLOT2,
+           CG_NS = 16 };
+enum CgI { CG_DONE, CG_ITS, CG_REASON, CG_HCOUNT, CG_NI = 8 };
+enum CgPhase { CG_TOP, CG_MID, CG_POST, CG_END };
+struct CgParams {
+    double rtol, atol, dtol;
+    int64_t maxit;
+    int norm;  // 0 none, else the norm of S[CG_SLOT] is the residual norm
+    int r_rtol, r_atol, r_dtol, r_nan, r_its, r_indef_pc, r_indef_mat;  // the KSPConvergedReason codes
+};
+void launch_cg_state(int phase, int64_t i, double *S, int64_t *I, double *hist, const CgParams &p, hipStream_t st);
 // w = a*x + b*y  (out of place)
 void launch_waxpby(int64_t n, double a, const double *x, double b, const double *y, double *w,
                    hipStream_t st);

@@ -22,6 +22,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstring>
 #include <sstream>
 
 namespace pls {
@@ -1795,8 +1796,17 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             const bool deep = sL >= 0 && sU >= 0 && 2 * (sL + sU) <= 7 * lev;
             chain = c.sweep_chain != 0 && sL >= 0 && sU >= 0 && (c.sweep_chain == 1 || deep);
             // the window sweep where the chain would run (or forced): a block's
-            // dependent chain becomes its len / 64 windows
-            window = (c.sweep_window == 1 || (c.sweep_window == -1 && c.sweep_chain != 1 && deep)) &&
+            // dependent chain becomes its len / 64 windows.  Also where the levels
+            // outnumber the windows 2:1 (<= 32 rows per level): the classical AMG's
+            // level-0 hybrid Gauss-Seidel chunks under mpirun -np 8 semantics
+            // (swelling N=80: 8 chunks of 6,481 rows, ~700 levels per chunk over both
+            // triangles) took 790 us per sweep in the workgroup sweep (~1.1 us per
+            // level), 745 us in the chain sweep, ~250 us in the window sweep (~1.2 us
+            // per window)
+            int64_t nwin = 0;
+            for (int64_t b = 0; b < nblocks; ++b) nwin += 2 * ((bst[b + 1] - bst[b] + 63) / 64);
+            const bool many_levels = lev >= 2 * nwin;
+            window = (c.sweep_window == 1 || (c.sweep_window == -1 && c.sweep_chain != 1 && (deep || many_levels))) &&
                      blen <= ilu_window_max_rows() &&
                      window_max_entries(nblocks, bst, rp, ci, dg) <= ilu_window_max_entries();
             if (window) {
@@ -1909,7 +1919,8 @@ void PCILU::apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64
     const int rr = rr_group > 0 ? rr_group : (lds_rr ? 1 : 0);
     launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
                           Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof, false,
-                          tpb > 0 ? tpb : lds_tpb, rr, bstart_h.empty() ? nullptr : bstart.p, max_len, b_lo, b_hi, depth);
+                          tpb > 0 ? tpb : lds_tpb, rr, bstart_h.empty() ? nullptr : bstart.p, max_len, b_lo, b_hi,
+                          depth == 2 ? lds_depth : depth);
 }
 
 const char *PCILU::sweep_kind() const {
@@ -1958,7 +1969,8 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
         if (!profile_tag.empty()) prof.alloc(nblocks * 8);
         launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, Uf.goff.p,
                               Us.gslice.p, Us.sptr.p, Us.col.p, Us.val.p, Us.lpr.p, x, y, c.st, prof.p, lds_gmem,
-                              lds_tpb, lds_rr ? 1 : 0, bstart_h.empty() ? nullptr : bstart.p, max_len);
+                              lds_tpb, lds_rr ? 1 : 0, bstart_h.empty() ? nullptr : bstart.p, max_len, -1, -1,
+                              lds_gmem ? 2 : lds_depth);
         if (!profile_tag.empty()) {
             // diagnostics: per-block sweep times (100 MHz wall clock), slowest first
             std::vector<int64_t> h(nblocks * 8);
@@ -2387,6 +2399,15 @@ std::unique_ptr<PC> make_redundant(const std::string &type, const DevCSR &M, Ctx
     return std::make_unique<PCRedundant>(type, M, c, factory, prefix, pre);
 }
 
+// levels of factor data the LDS sweep keeps in flight: pls.sweep_depth (or
+// <prefix>pls_sweep_depth for one PC) 2 (default), 3 or 4 -- bitwise the same sweep
+static int sweep_depth_opt(const Options &o, const std::string &prefix) {
+    const std::string k = o.has(prefix + "pls_sweep_depth") ? prefix + "pls_sweep_depth" : "pls.sweep_depth";
+    const int d = (int)o.integer(k, 2);
+    if (d < 2 || d > 4) throw Error(k + " must be 2, 3 or 4");
+    return d;
+}
+
 std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Options &o, const std::string &prefix,
                             Ctx &c) {
     if (type == "none") return std::make_unique<PCNone>(M.nrows);
@@ -2421,6 +2442,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
         auto pc = std::make_unique<PCILU>(M, 1, c, false, o.flag("pls.ilu_lds", true), 0,
                                           (int)o.integer("pls.ilu_gmem", 0), (int)o.integer("pls.ilu_ring", 1));
         if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+        pc->lds_depth = sweep_depth_opt(o, prefix);
         if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
         return pc;
     }
@@ -2440,6 +2462,7 @@ std::unique_ptr<PC> make_pc(const std::string &type, const DevCSR &M, const Opti
                                               (int)o.integer("pls.ilu_ring", 1));
             if (o.flag("pls.sweep_profile", false)) pc->profile_tag = prefix;
             if (o.has("pls.sweep_tpb")) pc->lds_tpb = (int)o.integer("pls.sweep_tpb", 1024);
+            pc->lds_depth = sweep_depth_opt(o, prefix);
             if (o.has("pls.sweep_rr")) pc->lds_rr = o.flag("pls.sweep_rr", false) && pc->use_lds && !pc->ring;
             return pc;
         }
@@ -2542,7 +2565,11 @@ void KSP::solve(const double *b, double *x, Ctx &c) {
     } else {
         ensure_work(c);
         if (type == "gmres") solve_gmres(b, x, c);
-        else if (type == "cg") solve_cg(b, x, c);
+        else if (type == "cg") {
+            // the device-resident loop unless something needs each iteration on the host
+            if (cg_device && !monitor && time_limit <= 0 && maxit > 0 && maxit <= 10000000) solve_cg_dev(b, x, c);
+            else solve_cg(b, x, c);
+        }
         else throw Error("KSP type " + type + " not available");
     }
     stat_its += its;
@@ -2751,6 +2778,99 @@ void KSP::solve_cg(const double *b, double *x, Ctx &c) {
     if (i >= maxit && !reason) reason = DIVERGED_ITS;
 }
 
+// KSPSolve_CG with its scalar recurrences on the device (k_cg_state): the
+// start (||r0||, the convergence test's reference, (z, r)) as in solve_cg,
+// then iterations enqueued in batches -- 1 per read-back for the first 32,
+// growing to 8 -- with one read-back of (done, its, reason) per batch instead
+// of three scalar read-backs per iteration.  Iterations enqueued after the
+// solve ended run their products and PC applies on frozen vectors (the vector
+// updates and every state phase check the done flag): x, the iteration count,
+// the reason and the history are those of solve_cg, bit for bit.
+void KSP::solve_cg_dev(const double *b, double *x, Ctx &c) {
+    double *r = t1.p, *z = t2.p, *p = t3.p, *w = t4.p;
+    launch_set(n, 0.0, x, c.st);
+    launch_copy(n, b, r, c.st);
+    double dp = 0.0;
+    if (norm == "preconditioned") {
+        pc->apply(r, z, c);
+        dp = c.norm2(n, z);
+    } else if (norm == "unpreconditioned") {
+        dp = c.norm2(n, r);
+    }
+    history.push_back(dp);
+    if (monitor) printf("  %3d KSP Residual norm %.12e\n", 0, dp);
+    rnorm = dp;
+    its = 0;
+    reason = (norm != "none") ? converged(0, dp) : 0;
+    if (reason) return;
+    if (norm != "preconditioned") pc->apply(r, z, c);
+    const double beta0 = c.dot(n, z, r);
+    if (cgS.n < (size_t)CG_NS) cgS.alloc(CG_NS);
+    if (cgI.n < (size_t)CG_NI) cgI.alloc(CG_NI);
+    if (cghist.n < (size_t)(maxit + 2)) cghist.alloc(maxit + 2);
+    std::vector<double> hs(CG_NS, 0.0);
+    hs[CG_BETA] = beta0;
+    hs[CG_ONE] = 1.0;
+    hs[CG_RNORM0] = rnorm0;
+    hs[CG_TTOL] = ttol;
+    std::vector<int64_t> hi(CG_NI, 0);
+    HIPCHK(hipMemcpyAsync(cgS.p, hs.data(), sizeof(double) * CG_NS, hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(cgI.p, hi.data(), sizeof(int64_t) * CG_NI, hipMemcpyHostToDevice, c.st));
+    c.sync();  // (the host vectors above go out of scope only after the copies)
+    const CgParams prm{rtol, atol, dtol, maxit, norm != "none" ? 1 : 0, CONVERGED_RTOL, CONVERGED_ATOL, DIVERGED_DTOL,
+                       DIVERGED_NANORINF, DIVERGED_ITS, DIVERGED_INDEFINITE_PC, DIVERGED_INDEFINITE_MAT};
+    double *S = cgS.p;
+    int64_t *I = cgI.p;
+    const int64_t *done = I + CG_DONE;
+    auto sum_into = [&](const double *u, const double *v, double *slot) {
+        launch_dot(n, u, v, c.partials(n, 1), slot, c.st);
+        c.comm->global_sum_dev(slot, 1, c.st);
+    };
+    double *hb = c.host_scalars(CG_NI);
+    int64_t i = 0;
+    while (i < maxit) {
+        // (at most 8 per batch: iterations enqueued past the end are wasted work --
+        // batches of 32 cost more than the read-backs they saved, swelling N=80)
+        const int64_t B = std::min<int64_t>(std::clamp<int64_t>(i / 16, 1, 8), maxit - i);
+        for (int64_t k = 0; k < B; ++k, ++i) {
+            launch_cg_state(CG_TOP, i, S, I, cghist.p, prm, c.st);
+            if (i == 0) launch_copy(n, z, p, c.st);
+            else launch_axpby_dev(n, S + CG_ONE, z, S + CG_BB, p, done, c.st);  // p = z + (beta / betaold) p
+            A->apply(p, w, c);
+            sum_into(p, w, S + CG_SLOT);
+            launch_cg_state(CG_MID, i, S, I, cghist.p, prm, c.st);
+            launch_axpby_dev(n, S + CG_A, p, S + CG_ONE, x, done, c.st);     // x += a p
+            launch_axpby_dev(n, S + CG_NEGA, w, S + CG_ONE, r, done, c.st);  // r -= a w
+            if (norm == "preconditioned") {
+                pc->apply(r, z, c);
+                sum_into(z, z, S + CG_SLOT);
+            } else if (norm == "unpreconditioned") {
+                sum_into(r, r, S + CG_SLOT);
+            }
+            launch_cg_state(CG_POST, i, S, I, cghist.p, prm, c.st);
+            if (norm != "preconditioned") pc->apply(r, z, c);
+            sum_into(z, r, S + CG_SLOT2);
+            launch_cg_state(CG_END, i, S, I, cghist.p, prm, c.st);
+        }
+        HIPCHK(hipMemcpyAsync(hb, I, sizeof(int64_t) * CG_NI, hipMemcpyDeviceToHost, c.st));
+        c.sync();
+        int64_t d = 0;
+        std::memcpy(&d, hb + CG_DONE, sizeof(d));
+        if (d) break;
+    }
+    int64_t st[CG_NI];
+    std::memcpy(st, hb, sizeof(st));
+    its = (int)st[CG_ITS];
+    reason = (int)st[CG_REASON];
+    if (st[CG_HCOUNT] > 0) {
+        std::vector<double> hh(st[CG_HCOUNT]);
+        HIPCHK(hipMemcpyAsync(hh.data(), cghist.p, sizeof(double) * hh.size(), hipMemcpyDeviceToHost, c.st));
+        c.sync();
+        history.insert(history.end(), hh.begin(), hh.end());
+        rnorm = hh.back();
+    }
+}
+
 std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const DevCSR *Amat, const DevCSR *Pmat,
                               const std::string &default_ksp, const std::string &default_pc, Ctx &c, double rtol,
                               double atol, double dtol, int64_t maxit, int64_t restart, PC *external_pc) {
@@ -2764,6 +2884,7 @@ std::unique_ptr<KSP> make_ksp(const std::string &prefix, const Options &o, const
     k->restart = o.integer(prefix + "ksp_gmres_restart", restart);
     k->monitor = o.has(prefix + "ksp_monitor");
     k->stats = o.flag("pls.ksp_stats", false);
+    k->cg_device = o.flag("pls.cg_device", true);
     if (prefix == "global_") k->time_limit = o.num("pls.solver_time_limit", 0.0);
     if (o.has(prefix + "ksp_gmres_modifiedgramschmidt") && k->type == "gmres")
         throw Error(prefix + "ksp_gmres_modifiedgramschmidt: only classical Gram-Schmidt is implemented");

@@ -405,6 +405,7 @@ struct PCILU : PC {
     bool use_lds = false;  // one workgroup per block sweeps (k_ilu_blocks_lds)
     bool lds_gmem = false;  // ... with the block solution kept in y (blocks too long for LDS)
     int lds_tpb = 1024;     // threads per workgroup of the LDS sweep (set from the widest level; pls.sweep_tpb)
+    int lds_depth = 2;      // levels of factor data in flight in the LDS sweep (pls.sweep_depth 2 / 3 / 4)
     bool lds_rr = false;    // round-robin level sweep (deep DAGs of ~one slice per level; pls.sweep_rr)
     int64_t nlev_L = 0, nlev_U = 0;
     bool allow_lds = true;  // block solution resident in LDS when it fits
@@ -530,6 +531,9 @@ struct KSP {
     DBuf<double> V, w, t1, t2, t3, t4;
     int64_t ldv = 0;  // column stride of the Krylov basis V
     DBuf<double> dh;  // device Hessenberg column / coefficients
+    DBuf<double> cgS, cghist;  // device-resident CG: scalar state, residual history
+    DBuf<int64_t> cgI;
+    bool cg_device = true;     // pls.cg_device: CG's recurrences on the device (no read-back per iteration)
     int64_t allocated_k = -1;
     void set_type_defaults();
     void resolve_side_norm(const std::string &side, const std::string &nt);
@@ -547,6 +551,7 @@ struct KSP {
     void ensure_work(Ctx &c);
     void solve_gmres(const double *b, double *x, Ctx &c);
     void solve_cg(const double *b, double *x, Ctx &c);
+    void solve_cg_dev(const double *b, double *x, Ctx &c);
     int converged(int it, double r);
     double rnorm0 = 0, ttol = 0;
 };
