@@ -558,6 +558,8 @@ struct Handle {
         // test knobs of the ILU(0) factorization: staged-entry cap, persistent grid cap
         ctx.ilu0_stage_cap = (int)opt.integer("pls.ilu0_stage", -1);
         ctx.ilu_dep_grid = (int)opt.integer("pls.ilu_dep_grid", 0);
+        ctx.window_depth = (int)opt.integer("pls.window_depth", 2);
+        if (ctx.window_depth != 2 && ctx.window_depth != 3) throw Error("pls.window_depth must be 2 or 3");
         ctx.sweep_swin = (int)opt.integer("pls.sweep_swin", 0);
         ctx.amg_csr_below = opt.num("pls.amg_csr_below", 16.0);
         if (opt.flag("pls.debug_bounds", false) || opt.integer("pls.debug_partial_cap", 0) > 0)

@@ -3477,7 +3477,7 @@ __device__ __forceinline__ void win_wait(WinBuf &B) {  // vmcnt(N), B's register
     for (int u = 0; u < WIN_KPW; ++u) asm volatile("" : "+v"(B.sv[u]), "+v"(B.sc[u]));
 }
 
-template <bool UP>
+template <bool UP, int WD = 2>
 __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t *__restrict__ woff,
                                           const int32_t *__restrict__ col, const double *__restrict__ val,
                                           const double *__restrict__ tinv, double *ys, double *part, int lane,
@@ -3538,6 +3538,29 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         ys[act ? r : len + lane] = yr;  // every wave writes the same value (its own later reads see it)
         __syncthreads();                // part[] free for the next window
     };
+    if (WD == 3) {
+        // three windows of data in flight: the oldest window's WIN_LOADS loads are
+        // followed by 2 x WIN_LOADS = 64 younger ones, more than vmcnt counts (63);
+        // waiting for <= 63 outstanding waits for one load of the next window too
+        static_assert(2 * WIN_LOADS >= 63, "vmcnt(63) must cover the oldest window");
+        WinBuf A, B, C;
+        issue(0, A);
+        issue(1, B);
+        issue(2, C);
+        for (int64_t ww = 0; ww < nw; ww += 3) {
+            win_wait<63>(A);
+            compute(ww, A);
+            issue(ww + 3, A);
+            win_wait<63>(B);
+            compute(ww + 1, B);
+            issue(ww + 4, B);
+            win_wait<63>(C);
+            compute(ww + 2, C);
+            issue(ww + 5, C);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
     WinBuf A, B;
     issue(0, A);
     issue(1, B);
@@ -3552,6 +3575,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the prefetches past the block: nothing in range)
 }
 
+template <int WD>
 __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart,
                                                            const int64_t *__restrict__ wstart,
                                                            const int64_t *__restrict__ Lwoff, const int32_t *__restrict__ Lcol,
@@ -3577,8 +3601,8 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
     };
     len = uni(len);
     const int64_t w0 = uni(wstart[blk]);
-    win_sweep<false>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q);
-    win_sweep<true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q);
+    win_sweep<false, WD>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q);
+    win_sweep<true, WD>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q);
     __syncthreads();
     for (int64_t t = threadIdx.x; t < len; t += 256) y[b0 + t] = ys[t];
 }
@@ -3591,16 +3615,22 @@ int ilu_window_max_entries() { return WIN_KP; }
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
                               const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,
-                              const double *x, double *y, int64_t max_len, hipStream_t st) {
+                              const double *x, double *y, int64_t max_len, hipStream_t st, int depth) {
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_window, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_window<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)163840);
+        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_window<3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)163840);
         configured = true;
     }
     const size_t bytes = (size_t)(256 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
-    k_ilu_blocks_window<<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv,
-                                                              Uwoff, Ucol, Uval, Utinv, x, y);
+    if (depth == 3)
+        k_ilu_blocks_window<3><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval,
+                                                                      Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
+    else
+        k_ilu_blocks_window<2><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval,
+                                                                      Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
 }
 
 // ======================================================= super-window sweep ==

@@ -1955,7 +1955,8 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
     }
     if (use_lds && window) {
         launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.col.p,
-                                 Lw.val.p, Lw.tinv.p, Uw.woff.p, Uw.col.p, Uw.val.p, Uw.tinv.p, x, y, max_len, c.st);
+                                 Lw.val.p, Lw.tinv.p, Uw.woff.p, Uw.col.p, Uw.val.p, Uw.tinv.p, x, y, max_len, c.st,
+                                 c.window_depth);
         return;
     }
     if (use_lds && chain) {
@@ -2318,6 +2319,7 @@ std::unique_ptr<Ctx> layout_ctx(const Ctx &c) {
     self->spmv_rcm = c.spmv_rcm;
     self->sweep_chain = c.sweep_chain;
     self->sweep_window = c.sweep_window;
+    self->window_depth = c.window_depth;
     self->amg_csr_below = c.amg_csr_below;
     return self;
 }

@@ -86,6 +86,7 @@ struct Ctx {
     int ilu_view = 0;             // print every ILU / Gauss-Seidel PC's sweep choice to stderr (pls.ilu_view)
     int ilu0_stage_cap = -1;      // test knob (pls.ilu0_stage): staged entries of the ILU(0) factorization, -1 default
     int ilu_dep_grid = 0;         // test knob (pls.ilu_dep_grid): k_ilu0_dep's persistent grid capped (0: none)
+    int window_depth = 2;         // window sweep: windows of data in flight, 2 or 3 (pls.window_depth)
     int sweep_swin = 0;           // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin, experimental,
                                   // measured slower than the ring sweep): 0 never (default, capi), -1 where the ring
                                   // sweep would run, 1 whenever the block is y-resident
