@@ -79,6 +79,126 @@ __global__ __launch_bounds__(DTPB) void k_gj_diag(int64_t ld, int64_t k, const d
 }
 #pragma clang fp contract(on)
 
+// ---------------------------------------------- threshold partial pivoting --
+// MUMPS's pivot rule (CNTL(1) = u, 0.01 for unsymmetric matrices) before the
+// Gauss-Jordan step k of a front (or of the dense block): the 64 pivots of tile
+// column k are chosen among the front's remaining fully-summed rows [r0, r0 + m)
+// -- not only the tile's own 64 -- by an LU with threshold partial pivoting of
+// that panel (a scratch copy P, with the q update rows below it as the
+// threshold's reference: they are eliminated too but never chosen): column j
+// keeps its diagonal row while |a_jj| >= u max_i |a_ij| over the candidates,
+// else takes the largest (ties: the smaller row).  The chosen rows are then
+// swapped into the tile's positions in W -- whole rows, every column -- and in
+// rowperm (front-local original row of each position), so the elimination
+// that follows factors Pi F; the solves permute the right-hand side alike.
+// stats[0]: rows exchanged, [1]: pivots below u x the column's largest entry
+// over the candidates and the update rows (the pivots MUMPS would delay to the
+// parent; here the best candidate is used), [2]: columns with no nonzero
+// candidate (singular fully-summed block).
+__device__ void panel_pivot(double *W, int64_t ld, int64_t r0, int m, int64_t ur0, int q, double *P,
+                            int32_t *rowperm, int32_t *stats, double u) {
+    __shared__ double rv[DTPB], rc[DTPB];
+    __shared__ int ri[DTPB];
+    __shared__ int swp[DB];
+    const int tid = threadIdx.x;
+    const int nr = m + q, nc = m < DB ? m : DB;
+    for (int64_t t = tid; t < (int64_t)nr * DB; t += DTPB) {
+        const int64_t i = t >> 6, c = t & 63;
+        const int64_t row = i < m ? r0 + i : ur0 + (i - m);
+        P[t] = W[row * ld + r0 + c];
+    }
+    __syncthreads();
+    for (int j = 0; j < nc; ++j) {
+        double bv = -1.0, cv = 0.0;
+        int bi = m;
+        for (int i = j + tid; i < m; i += DTPB) {  // ascending per thread: a tie keeps the smaller row
+            const double v = fabs(P[(int64_t)i * DB + j]);
+            if (v > bv) {
+                bv = v;
+                bi = i;
+            }
+        }
+        for (int i = m + tid; i < nr; i += DTPB) cv = fmax(cv, fabs(P[(int64_t)i * DB + j]));
+        rv[tid] = bv;
+        ri[tid] = bi;
+        rc[tid] = cv;
+        __syncthreads();
+        for (int o = DTPB / 2; o > 0; o >>= 1) {
+            if (tid < o) {
+                const double v2 = rv[tid + o];
+                const int i2 = ri[tid + o];
+                if (v2 > rv[tid] || (v2 == rv[tid] && i2 < ri[tid])) {
+                    rv[tid] = v2;
+                    ri[tid] = i2;
+                }
+                rc[tid] = fmax(rc[tid], rc[tid + o]);
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            const double amax = rv[0], dj = fabs(P[(int64_t)j * DB + j]);
+            const int sel = (amax > 0.0 && dj < u * amax) ? ri[0] : j;
+            if (sel != j) atomicAdd(stats, 1);
+            if (amax < u * fmax(amax, rc[0])) atomicAdd(stats + 1, 1);
+            if (amax == 0.0) atomicAdd(stats + 2, 1);
+            swp[j] = sel;
+        }
+        __syncthreads();
+        const int sel = swp[j];
+        if (sel != j && tid < DB) {
+            const double t0 = P[(int64_t)j * DB + tid];
+            P[(int64_t)j * DB + tid] = P[(int64_t)sel * DB + tid];
+            P[(int64_t)sel * DB + tid] = t0;
+        }
+        __syncthreads();
+        const double d = P[(int64_t)j * DB + j];
+        if (d != 0.0)
+            for (int i = j + 1 + tid; i < nr; i += DTPB) {
+                double *pi = P + (int64_t)i * DB;
+                const double l = pi[j] / d;
+                pi[j] = l;
+                for (int c = j + 1; c < DB; ++c) pi[c] = pi[c] - l * P[(int64_t)j * DB + c];
+            }
+        __syncthreads();
+    }
+    for (int j = 0; j < nc; ++j) {  // the exchanges, in order, on whole rows of W
+        const int sel = swp[j];
+        if (sel == j) continue;
+        double *a = W + (r0 + j) * ld, *b = W + (r0 + sel) * ld;
+        for (int64_t c = tid; c < ld; c += DTPB) {
+            const double t0 = a[c];
+            a[c] = b[c];
+            b[c] = t0;
+        }
+        if (tid == 0) {
+            const int32_t t0 = rowperm[r0 + j];
+            rowperm[r0 + j] = rowperm[r0 + sel];
+            rowperm[r0 + sel] = t0;
+        }
+        __syncthreads();
+    }
+}
+
+// dense block (PCDenseLU): candidates rows [64 k, n), no update rows
+__global__ __launch_bounds__(DTPB) void k_dense_panel_pivot(int64_t n, int64_t ld, int64_t k, double *M, double *P,
+                                                            int32_t *rowperm, int32_t *stats, double u) {
+    const int64_t r0 = k * DB;
+    if (r0 >= n) return;
+    panel_pivot(M, ld, r0, (int)(n - r0), 0, 0, P, rowperm, stats, u);
+}
+// fronts (blockIdx.x): candidates rows [64 k, p), update rows [64 pt, 64 pt + q);
+// P + soff[f]: (p + q) x 64 scratch; rowperm + pst[f]: the front's pivot rows
+__global__ __launch_bounds__(DTPB) void k_mf_panel_pivot(const MFront *F, const int64_t *pst, const int64_t *soff,
+                                                         int k, double *W, double *P, int32_t *rowperm,
+                                                         int32_t *stats, double u) {
+    const MFront f = F[blockIdx.x];
+    const int64_t r0 = (int64_t)k * DB;
+    if (k >= f.pt || r0 >= f.p || f.p - r0 < 2) return;
+    const int64_t ld = (int64_t)f.ldt * DB;
+    panel_pivot(W + f.ws, ld, r0, (int)(f.p - r0), (int64_t)f.pt * DB, f.q, P + soff[blockIdx.x], rowperm + pst[blockIdx.x],
+                stats, u);
+}
+
 // C (64 x 64 tile, leading dimension ld) := alpha * op: tile-by-tile products
 // with 4 x 4 outputs per thread; A^T staged in LDS so the A reads broadcast.
 __device__ __forceinline__ void tile_load(const double *src, int64_t ld, double (*dst)[DB + 1], bool transpose) {
@@ -182,9 +302,11 @@ __global__ __launch_bounds__(DTPB) void k_gj_colpanel(int64_t ld, int64_t k, con
         for (int q = 0; q < 4; ++q) C[(int64_t)(ty + 16 * r) * ld + tx + 16 * q] = -acc[r][q];
 }
 
-void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStream_t st) {
+void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStream_t st, int64_t n, double *P,
+                         int32_t *rowperm, int32_t *stats, double u) {
     const int64_t nb = ld / DB;
     for (int64_t k = 0; k < nb; ++k) {
+        if (u > 0.0 && P) k_dense_panel_pivot<<<1, DTPB, 0, st>>>(n, ld, k, M, P, rowperm, stats, u);
         k_gj_diag<<<1, DTPB, 0, st>>>(ld, k, M, D, fail);
         k_gj_rowpanel<<<(unsigned)nb, DTPB, 0, st>>>(ld, k, D, M);
         if (nb > 1) {
@@ -197,26 +319,30 @@ void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStr
 // y = alpha * M x + beta * y over the leading n x n block: one wave per row,
 // 16-byte loads of the row (ld is a multiple of 64 doubles), x from L2.
 typedef double dn_d2 __attribute__((ext_vector_type(2)));
+// (xp: x permuted, xp[c] = x[rowperm[c]] -- the threshold-pivoted inverse is (Pi M)^-1)
 __global__ __launch_bounds__(256) void k_dense_gemv(int64_t n, int64_t ld, const double *__restrict__ M,
-                                                    const double *__restrict__ x, double *__restrict__ y) {
+                                                    const double *__restrict__ x, double *__restrict__ y,
+                                                    const int32_t *__restrict__ rowperm) {
     const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= n) return;
     const int lane = threadIdx.x & 63;
     const double *row = M + i * ld;
     double acc = 0.0;
     const int64_t n2 = n & ~(int64_t)1;
+    auto xa = [&](int64_t c) { return rowperm ? x[rowperm[c]] : x[c]; };
     for (int64_t c = 2 * lane; c < n2; c += 128) {
         const dn_d2 m = __builtin_nontemporal_load(reinterpret_cast<const dn_d2 *>(row + c));
-        acc += m.x * x[c];
-        acc += m.y * x[c + 1];
+        acc += m.x * xa(c);
+        acc += m.y * xa(c + 1);
     }
-    if ((n & 1) && lane == 0) acc += row[n - 1] * x[n - 1];
+    if ((n & 1) && lane == 0) acc += row[n - 1] * xa(n - 1);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) y[i] = acc;
 }
-void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, double *y, hipStream_t st) {
-    if (n > 0) k_dense_gemv<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(n, ld, M, x, y);
+void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, double *y, hipStream_t st,
+                       const int32_t *rowperm) {
+    if (n > 0) k_dense_gemv<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(n, ld, M, x, y, rowperm);
 }
 
 // Block-diagonal GEMV: one wave per row, the row of its chunk's block.
@@ -518,6 +644,10 @@ __global__ __launch_bounds__(DTPB) void k_mf_gj_colpanel(const MFront *F, int k,
         for (int q = 0; q < 4; ++q) C[(int64_t)(ty + 16 * r) * ld + tx + 16 * q] = -acc[r][q];
 }
 
+void launch_mf_panel_pivot(int nf, const MFront *F, const int64_t *pst, const int64_t *soff, int k, double *W,
+                           double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st) {
+    if (nf > 0 && u > 0.0) k_mf_panel_pivot<<<(unsigned)nf, DTPB, 0, st>>>(F, pst, soff, k, W, P, rowperm, stats, u);
+}
 void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, double *D, int32_t *fail,
                        double tau, hipStream_t st) {
     if (nf <= 0 || max_ldt <= 0) return;

@@ -298,11 +298,16 @@ void launch_unpack(int64_t m, const int32_t *idx, const double *buf, double *x, 
 // M: ld x ld row-major (ld = 64 * ceil(n / 64)); pads are identity rows.
 void launch_dense_from_csr(int64_t n, int64_t ld, const int64_t *rp, const int32_t *ci, const double *val, double *M,
                            hipStream_t st);
-// In place M := M^-1 by blocked Gauss-Jordan (no pivoting); D: 64 x 64 scratch;
-// *fail |= 1 on a zero pivot.
-void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStream_t st);
-// y = M[:n, :n] x
-void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, double *y, hipStream_t st);
+// In place M := M^-1 by blocked Gauss-Jordan; D: 64 x 64 scratch; *fail |= 1 on
+// a zero pivot.  With u > 0 and P (n x 64 scratch) each tile column's pivots are
+// chosen over rows [64 k, n) by threshold partial pivoting (MUMPS CNTL(1) = u),
+// the rows exchanged in M and rowperm (initialised to the identity): M := (Pi M)^-1;
+// stats[3] as launch_mf_panel_pivot.  u = 0: no pivoting (rounds 1-5).
+void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStream_t st, int64_t n = 0,
+                         double *P = nullptr, int32_t *rowperm = nullptr, int32_t *stats = nullptr, double u = 0.0);
+// y = M[:n, :n] x  (rowperm: y = M xp, xp[c] = x[rowperm[c]])
+void launch_dense_gemv(int64_t n, int64_t ld, const double *M, const double *x, double *y, hipStream_t st,
+                       const int32_t *rowperm = nullptr);
 // Block-diagonal dense operators (hybrid Gauss-Seidel chunks of the AMG): chunk
 // c holds rows [cptr[c], cptr[c+1]) and its ld x ld row-major block at
 // M + c ld^2; cof[i] = chunk of row i.  y = blockdiag(M_c) x.
@@ -341,6 +346,13 @@ void launch_mf_extend(int nc, const MChild *C, int max_q, const int32_t *maps, c
 // pivoting); with tau = 0 an exact zero pivot sets fail[0] instead.
 void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, double *D, int32_t *fail,
                        double tau, hipStream_t st);
+// Threshold partial pivoting (MUMPS CNTL(1) = u) before step k: front f's tile-k
+// pivots chosen among its fully-summed rows [64 k, p) (update rows the threshold's
+// reference), rows exchanged in W and in rowperm + pst[f] (front-local original
+// row per position); P + soff[f]: (p + q) x 64 scratch.  stats: [0] rows
+// exchanged, [1] pivots below u x column max (MUMPS would delay them), [2] zero columns.
+void launch_mf_panel_pivot(int nf, const MFront *F, const int64_t *pst, const int64_t *soff, int k, double *W,
+                           double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st);
 // Persistent factors: rows [0, 64 pt) of the front (U part, ld wide) to U + uoff
 // and rows [64 pt, 64 pt + q) x columns [0, 64 pt) (X part) to X + xoff.
 struct MStore {

@@ -2014,25 +2014,38 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
     Uf.apply(y, y, c);
 }
 
-PCDenseLU::PCDenseLU(const DevCSR &M, Ctx &c) {
+PCDenseLU::PCDenseLU(const DevCSR &M, Ctx &c, double u) {
     type = "lu";
     n = M.nrows;
     if (M.ncols != n) throw Error("lu: block is not square");
     ld = std::max<int64_t>(64, (n + 63) / 64 * 64);
     inv.alloc(ld * ld);
     launch_dense_from_csr(n, ld, M.rp.p, M.ci.p, M.val.p, inv.p, c.st);
-    DBuf<double> D(64 * 64);
-    DBuf<int32_t> fail(1);
+    DBuf<double> D(64 * 64), P;
+    DBuf<int32_t> fail(1), st;
     HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t), c.st));
-    launch_dense_invert(ld, inv.p, D.p, fail.p, c.st);
+    if (u > 0.0 && n > 1) {  // MUMPS-style threshold partial pivoting over every remaining row
+        std::vector<int32_t> id(n);
+        std::iota(id.begin(), id.end(), 0);
+        rowperm.alloc(n);
+        HIPCHK(hipMemcpyAsync(rowperm.p, id.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
+        P.alloc((size_t)n * 64);
+        st.alloc(3);
+        HIPCHK(hipMemsetAsync(st.p, 0, sizeof(int32_t) * 3, c.st));
+        c.sync();  // (id)
+    }
+    launch_dense_invert(ld, inv.p, D.p, fail.p, c.st, n, P.p, rowperm.p, st.p, rowperm.p ? u : 0.0);
     HIPCHK(hipGetLastError());
     int32_t hfail = 0;
     HIPCHK(hipMemcpyAsync(&hfail, fail.p, sizeof(int32_t), hipMemcpyDeviceToHost, c.st));
+    if (st.p) HIPCHK(hipMemcpyAsync(piv_stats, st.p, sizeof(int32_t) * 3, hipMemcpyDeviceToHost, c.st));
     c.sync();
     if (hfail) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
 }
 
-void PCDenseLU::apply(const double *x, double *y, Ctx &c) { launch_dense_gemv(n, ld, inv.p, x, y, c.st); }
+void PCDenseLU::apply(const double *x, double *y, Ctx &c) {
+    launch_dense_gemv(n, ld, inv.p, x, y, c.st, rowperm.p);
+}
 
 void csr_bandwidths(const DevCSR &M, int64_t &kl, int64_t &ku, Ctx &c) {
     const int64_t n = M.nrows;
@@ -2122,8 +2135,14 @@ std::unique_ptr<PC> make_lu(const DevCSR &M, const Options &o, Ctx &c) {
     const std::string path = o.str("pls.lu_path", "auto");
     if (path != "auto" && path != "dense" && path != "sparse" && path != "band" && path != "envelope")
         throw Error("pls.lu_path " + path + " (auto, dense, sparse, band, envelope)");
-    if (path == "dense" || (path == "auto" && M.nrows <= o.integer("pls.lu_dense_max", 32768)))
-        return std::make_unique<PCDenseLU>(M, c);
+    if (path == "dense" || (path == "auto" && M.nrows <= o.integer("pls.lu_dense_max", 32768))) {
+        auto pc = std::make_unique<PCDenseLU>(M, c, o.num("pls.lu_pivot_threshold", 0.01));
+        if (o.flag("pls.lu_view", false))
+            fprintf(stderr, "[dense lu] n %lld: threshold pivoting u = %g: %d rows exchanged, %d pivots below u x "
+                    "column max (delayed by MUMPS), %d zero columns\n", (long long)M.nrows,
+                    o.num("pls.lu_pivot_threshold", 0.01), pc->piv_stats[0], pc->piv_stats[1], pc->piv_stats[2]);
+        return pc;
+    }
     // larger blocks: nested dissection + multifrontal LU (the MUMPS stand-in)
     if (path == "sparse" || path == "auto") return make_sparse_lu(M, o, c);
     if (path == "band") {

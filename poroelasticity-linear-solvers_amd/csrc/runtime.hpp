@@ -451,7 +451,10 @@ struct PCILU : PC {
 struct PCDenseLU : PC {
     int64_t ld = 0;
     DBuf<double> inv;
-    PCDenseLU(const DevCSR &M, Ctx &c);
+    DBuf<int32_t> rowperm;  // threshold pivoting's row order (empty: none); inv = (Pi M)^-1
+    int32_t piv_stats[3] = {0, 0, 0};  // rows exchanged, pivots below u x column max, zero columns
+    // u: MUMPS's relative pivot threshold CNTL(1) (pls.lu_pivot_threshold, default 0.01; 0 = no pivoting)
+    PCDenseLU(const DevCSR &M, Ctx &c, double u = 0.0);
     bool reentrant() const override { return true; }
     void apply(const double *x, double *y, Ctx &c) override;
 };

@@ -177,7 +177,10 @@ void sparse_lu_analyze(const HostCSR &A, const Options &o, double *stats, int64_
 
 struct PCSparseLU : PC {
     int64_t nfront = 0, nlevels = 0;
-    DBuf<int32_t> perm;  // ND position -> row of M
+    DBuf<int32_t> perm;   // ND position -> unknown (column) of M: the solution's scatter
+    DBuf<int32_t> rperm;  // ND position -> equation (row) of M after threshold pivoting: the right-hand side's gather
+    int32_t piv_stats[3] = {0, 0, 0};  // rows exchanged, pivots below u x column max, zero columns
+    double piv_u = 0.0;
     DBuf<double> U, X;   // factors (per front: U part pp x ld, X part q x pp)
     DBuf<MSolve> S;
     DBuf<int32_t> slist;
@@ -273,11 +276,25 @@ struct PCSparseLU : PC {
         DBuf<int32_t> dmaps(maps.size()), fail(2);
         HIPCHK(hipMemcpyAsync(dmaps.p, maps.data(), sizeof(int32_t) * maps.size(), hipMemcpyHostToDevice, c.st));
         HIPCHK(hipMemsetAsync(fail.p, 0, sizeof(int32_t) * 2, c.st));
-        // static pivoting threshold: pls.lu_static_pivot x max |a_ij| (0: a zero pivot is an error)
+        // static pivoting threshold: pls.lu_static_pivot x max |a_ij|; 0 (default, MUMPS's
+        // CNTL(4) <= 0): off, an exactly zero pivot is an error
         double amax = 0.0;
         for (double v : A.v) amax = std::max(amax, std::fabs(v));
-        const double tau = o.num("pls.lu_static_pivot", 64 * 2.220446049250313e-16) * amax;
+        const double tau = o.num("pls.lu_static_pivot", 0.0) * amax;
         tau_used = tau;
+        // threshold partial pivoting over each front's fully-summed rows (MUMPS CNTL(1) = u,
+        // pls.lu_pivot_threshold, default 0.01; 0: pivots only inside each 64 x 64 tile)
+        const double u = o.num("pls.lu_pivot_threshold", 0.01);
+        piv_u = u;
+        DBuf<int32_t> drowp(std::max<int64_t>(n, 1)), pstats(3);
+        {
+            std::vector<int32_t> lid(std::max<int64_t>(n, 1), 0);
+            for (int32_t f : post)
+                for (int64_t r = 0; r < p[f]; ++r) lid[pstart[f] + r] = (int32_t)r;
+            HIPCHK(hipMemcpyAsync(drowp.p, lid.data(), sizeof(int32_t) * lid.size(), hipMemcpyHostToDevice, c.st));
+            HIPCHK(hipMemsetAsync(pstats.p, 0, sizeof(int32_t) * 3, c.st));
+            c.sync();
+        }
         double *Wcur = Wa.p, *Wprev = Wb.p;
         std::vector<int64_t> prev_ws;  // workspace offsets of the previous (deeper) level's fronts
         constexpr int CH = 32768;      // fronts per batched launch (grid z / y limit)
@@ -303,6 +320,20 @@ struct PCSparseLU : PC {
                 DBuf<double> Dt(hf.size() * 4096);
                 HIPCHK(hipMemcpyAsync(dF.p, hf.data(), sizeof(MFront) * hf.size(), hipMemcpyHostToDevice, c.st));
                 HIPCHK(hipMemcpyAsync(dS.p, hs.data(), sizeof(MStore) * hs.size(), hipMemcpyHostToDevice, c.st));
+                // threshold pivoting: per front its pivot rows' offset in rowperm and a (p + q) x 64 panel scratch
+                std::vector<int64_t> hpst, hsoff;
+                int64_t pscr = 0;
+                for (size_t t = c0; t < c1; ++t) {
+                    const int32_t f = fl[t];
+                    hpst.push_back(pstart[f]);
+                    hsoff.push_back(pscr);
+                    pscr += (p[f] > 1 ? p[f] + q[f] : 0) * 64;
+                }
+                DBuf<int64_t> dpst(hpst.size()), dsoff(hsoff.size());
+                DBuf<double> Pscr(u > 0.0 ? std::max<int64_t>(pscr, 1) : 1);
+                HIPCHK(hipMemcpyAsync(dpst.p, hpst.data(), sizeof(int64_t) * hpst.size(), hipMemcpyHostToDevice, c.st));
+                HIPCHK(hipMemcpyAsync(dsoff.p, hsoff.data(), sizeof(int64_t) * hsoff.size(), hipMemcpyHostToDevice,
+                                      c.st));
                 launch_mf_pad((int)hf.size(), dF.p, max_pad, Wcur, c.st);
                 if (c0 == 0) {  // the level's original entries (all of its fronts)
                     DBuf<int64_t> dd(std::max<size_t>(sc_dst[d].size(), 1)), ds(std::max<size_t>(sc_src[d].size(), 1));
@@ -336,7 +367,11 @@ struct PCSparseLU : PC {
                         }
                     }
                 }
-                for (int k = 0; k < max_pt; ++k) launch_mf_gj_step((int)hf.size(), dF.p, max_ldt, k, Wcur, Dt.p, fail.p, tau, c.st);
+                for (int k = 0; k < max_pt; ++k) {
+                    launch_mf_panel_pivot((int)hf.size(), dF.p, dpst.p, dsoff.p, k, Wcur, Pscr.p, drowp.p, pstats.p, u,
+                                          c.st);
+                    launch_mf_gj_step((int)hf.size(), dF.p, max_ldt, k, Wcur, Dt.p, fail.p, tau, c.st);
+                }
                 launch_mf_store((int)hf.size(), dF.p, dS.p, max_rows, Wcur, U.p, X.p, c.st);
                 HIPCHK(hipGetLastError());
                 c.sync();
@@ -347,8 +382,14 @@ struct PCSparseLU : PC {
         }
         int32_t hfail[2] = {0, 0};
         HIPCHK(hipMemcpyAsync(hfail, fail.p, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, c.st));
+        std::vector<int32_t> rowp(std::max<int64_t>(n, 1));
+        HIPCHK(hipMemcpyAsync(rowp.data(), drowp.p, sizeof(int32_t) * rowp.size(), hipMemcpyDeviceToHost, c.st));
+        HIPCHK(hipMemcpyAsync(piv_stats, pstats.p, sizeof(int32_t) * 3, hipMemcpyDeviceToHost, c.st));
         c.sync();
         if (hfail[0]) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
+        // the equations' order after the exchanges: ND position -> row of M
+        std::vector<int32_t> rpermh(std::max<int64_t>(n, 1));
+        for (int64_t i = 0; i < n; ++i) rpermh[i] = permh[pstart[front_of[i]] + rowp[i]];
         static_pivots = hfail[1];
         const double t3 = now_s();
         // ---- solve tables
@@ -377,7 +418,10 @@ struct PCSparseLU : PC {
                 for (int64_t r = 0; r < p[f] + q[f]; ++r) {
                     hrf.push_back(f);
                     hrl.push_back((int32_t)r);
-                    hci.insert(hci.end(), contrib[r].begin(), contrib[r].end());
+                    // a pivot position holds the equation rowp[.] of the front after the exchanges:
+                    // its children's contributions follow it
+                    const int64_t src = r < p[f] ? rowp[pstart[f] + r] : r;
+                    hci.insert(hci.end(), contrib[src].begin(), contrib[src].end());
                     hcp.push_back((int64_t)hci.size());
                 }
                 for (int64_t k = 0; k < q[f]; ++k) {
@@ -401,6 +445,7 @@ struct PCSparseLU : PC {
         up(S, hS);
         up(slist, hsl);
         up(perm, permh);
+        up(rperm, rpermh);
         up(rf, hrf);
         up(rl, hrl);
         up(qf, hqf);
@@ -433,10 +478,12 @@ struct PCSparseLU : PC {
             for (int32_t f : post) maxf = std::max(maxf, p[f] + q[f]);
             fprintf(stderr,
                     "[sparse lu] n %lld: %lld fronts, %lld levels, largest front %lld, factors %.2f GB, %d static "
-                    "pivots, refinement steps %d; setup: ordering %.2f s, symbolic %.2f s, factorization %.2f s, "
-                    "total %.2f s\n",
+                    "pivots, refinement steps %d; threshold pivoting u = %g: %d rows exchanged, %d pivots below u x "
+                    "column max (delayed by MUMPS), %d zero columns; setup: ordering %.2f s, symbolic %.2f s, "
+                    "factorization %.2f s, total %.2f s\n",
                     (long long)n, (long long)nfront, (long long)nlevels, (long long)maxf, factor_gb, static_pivots,
-                    refine, setup_s[0], setup_s[1], setup_s[2], setup_s[3]);
+                    refine, piv_u, piv_stats[0], piv_stats[1], piv_stats[2], setup_s[0], setup_s[1], setup_s[2],
+                    setup_s[3]);
         }
     }
 
@@ -463,7 +510,7 @@ struct PCSparseLU : PC {
 
     void solve(const double *xin, double *y, DBuf<double> &w, Ctx &c) {
         double *bp = w.p, *z = bp + n, *x = z + n, *cu = x + n, *acc = cu + std::max<int64_t>(nq, 1);
-        launch_gather_i32(n, perm.p, xin, bp, c.st);
+        launch_gather_i32(n, rperm.p, xin, bp, c.st);
         for (int64_t d = nlevels - 1; d >= 0; --d) {
             launch_mf_fwd_gather(lr_off[d + 1] - lr_off[d], rf.p + lr_off[d], rl.p + lr_off[d], S.p,
                                  cptr.p + lr_off[d], cidx.p, bp, cu, z, acc, c.st);

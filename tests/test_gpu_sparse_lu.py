@@ -9,9 +9,12 @@
   level: dense partial-pivoting LU (scipy lu_factor + lu_solve) leaves
   4.1e-11 (N=8) .. 4.7e-11 (N=16) on it, so unrefined <= 1e-9, refined
   <= 2e-10; the fp block is well conditioned: <= 1e-12 either way;
-* static pivoting: a block with an exactly singular pivot (a zeroed row and
-  column) factors with the pivot replaced by tau (the apply is finite), and
-  pls.lu_static_pivot 0 restores PETSc's MAT_FACTOR_NUMERIC_ZEROPIVOT error.
+* static pivoting (opt-in since round 6, MUMPS's CNTL(4) default): a block
+  with an exactly singular pivot (a zeroed row and column) factors with the
+  pivot replaced by tau when pls.lu_static_pivot is set (the apply is
+  finite), and is PETSc's MAT_FACTOR_NUMERIC_ZEROPIVOT error by default;
+* threshold partial pivoting over each front's fully-summed rows (MUMPS
+  CNTL(1) = 0.01): a block whose leading tile is exactly zero.
 """
 import numpy as np
 import pytest
@@ -76,13 +79,70 @@ def test_sparse_lu_static_pivot(gpu):
     rows = np.repeat(np.arange(P.shape[0]), np.diff(P.indptr))
     P.data[(rows == z) | (P.indices == z)] = 0.0  # row and column z zero, structure (and its diagonal) kept
     x = np.random.default_rng(6).standard_normal(s.A.shape[0])
-    h = _handle(s, {}, P=P)
+    h = _handle(s, {"pls.lu_static_pivot": str(64 * 2.220446049250313e-16)}, P=P)  # opt-in (MUMPS CNTL(4) > 0)
     y = h.pc_apply(x)
     h.destroy()
     assert np.all(np.isfinite(y))
     with pytest.raises(RuntimeError, match="zero pivot"):
-        h = _handle(s, {"pls.lu_static_pivot": "0"}, P=P)
+        h = _handle(s, {}, P=P)  # default: off, an exactly singular block is an error (MUMPS: INFO(1) = -10)
         try:
             h.pc_apply(x)
         finally:
             h.destroy()
+
+
+def _swap_system(n2=64, eps=0.05):
+    """A 3-field system whose solid block K = [[0, B], [B^T, 0]] (B = I + eps
+    tridiag, 2 n2 rows) has an exactly zero leading 64 x 64 tile: LU without
+    pivoting fails at its first pivot, LU with row exchanges does not (K is
+    nonsingular, det = det(B)^2 up to sign).  Fluid and pressure blocks:
+    identity, no coupling -- the 2-way PC's y is [K^-1 x_s, x_fp]."""
+    import types
+    B = sp.eye(n2) + eps * sp.diags([np.ones(n2 - 1), np.ones(n2 - 1)], [-1, 1])
+    K = sp.bmat([[None, B], [B.T, None]]).tocsr()
+    ns, nf, npr = 2 * n2, 32, 32
+    P = sp.block_diag([K, sp.eye(nf), sp.eye(npr)]).tocsr()
+    P.sort_indices()
+    n = P.shape[0]
+    s = types.SimpleNamespace(A=P, P=P, P_diff=None, is_s=np.arange(ns, dtype=np.int32),
+                              is_f=np.arange(ns, ns + nf, dtype=np.int32),
+                              is_p=np.arange(ns + nf, n, dtype=np.int32), bcs_sub_pressure=[])
+    return s, K
+
+
+def _swap_apply(s, extra):
+    from lib.handle import Handle, params_to_options
+    opts = {"global_ksp_type": "gmres", "global_ksp_pc_side": "right", "s_ksp_type": "preonly", "s_pc_type": "lu",
+            "fp_ksp_type": "preonly", "fp_pc_type": "lu", "pls.lu_view": "1"}
+    opts.update(extra)
+    opts.update(params_to_options(BASE))
+    h = Handle.from_csr(s.A, s.P, None, s.is_s, s.is_f, s.is_p, s.bcs_sub_pressure, opts)
+    try:
+        x = np.random.default_rng(8).standard_normal(s.A.shape[0])
+        return x, h.pc_apply(x)
+    finally:
+        h.destroy()
+
+
+@pytest.mark.parametrize("path", ["dense", "sparse"])
+def test_lu_threshold_pivoting_zero_leading_tile(gpu, capfd, path):
+    """MUMPS's threshold partial pivoting (CNTL(1) = u = 0.01, pls.lu_pivot_threshold):
+    each 64 x 64 tile's pivots are chosen over all the front's remaining
+    fully-summed rows (the dense path: all remaining rows), so the zero leading
+    tile takes its pivots from the other half; the exact solve against numpy.
+    Without it (u = 0) the same block is a zero pivot -- static pivoting is off
+    by default as in MUMPS (CNTL(4) <= 0)."""
+    import scipy.sparse.linalg as spla
+    s, K = _swap_system()
+    extra = {"pls.lu_path": path, "pls.lu_nd_leaf": "256", "pls.lu_nd_compress": "0"}
+    capfd.readouterr()
+    x, y = _swap_apply(s, extra)
+    err = capfd.readouterr().err
+    ns = K.shape[0]
+    ys = spla.spsolve(K.tocsc(), x[:ns])
+    assert np.max(np.abs(y[:ns] - ys)) <= 1e-12 * np.max(np.abs(ys))
+    assert np.array_equal(y[ns:], x[ns:])
+    line = [l for l in err.splitlines() if ("[sparse lu] n %d" % ns if path == "sparse" else "[dense lu] n %d" % ns) in l]
+    assert line and " 0 rows exchanged" not in line[0], err
+    with pytest.raises(RuntimeError, match="zero pivot"):
+        _swap_apply(s, dict(extra, **{"pls.lu_pivot_threshold": "0"}))
