@@ -96,7 +96,7 @@ __global__ __launch_bounds__(DTPB) void k_gj_diag(int64_t ld, int64_t k, const d
 // parent; here the best candidate is used), [2]: columns with no nonzero
 // candidate (singular fully-summed block).
 __device__ void panel_pivot(double *W, int64_t ld, int64_t r0, int m, int64_t ur0, int q, double *P,
-                            int32_t *rowperm, int32_t *stats, double u) {
+                            int32_t *rowperm, int32_t *stats, double u, int32_t *dflag = nullptr) {
     __shared__ double rv[DTPB], rc[DTPB];
     __shared__ int ri[DTPB];
     __shared__ int swp[DB];
@@ -139,7 +139,10 @@ __device__ void panel_pivot(double *W, int64_t ld, int64_t r0, int m, int64_t ur
             const double amax = rv[0], dj = fabs(P[(int64_t)j * DB + j]);
             const int sel = (amax > 0.0 && dj < u * amax) ? ri[0] : j;
             if (sel != j) atomicAdd(stats, 1);
-            if (amax < u * fmax(amax, rc[0])) atomicAdd(stats + 1, 1);
+            if (amax < u * fmax(amax, rc[0])) {
+                atomicAdd(stats + 1, 1);
+                if (dflag) dflag[r0 + j] = 1;  // column (unknown) r0 + j of the front: MUMPS would delay it
+            }
             if (amax == 0.0) atomicAdd(stats + 2, 1);
             swp[j] = sel;
         }
@@ -190,13 +193,13 @@ __global__ __launch_bounds__(DTPB) void k_dense_panel_pivot(int64_t n, int64_t l
 // P + soff[f]: (p + q) x 64 scratch; rowperm + pst[f]: the front's pivot rows
 __global__ __launch_bounds__(DTPB) void k_mf_panel_pivot(const MFront *F, const int64_t *pst, const int64_t *soff,
                                                          int k, double *W, double *P, int32_t *rowperm,
-                                                         int32_t *stats, double u) {
+                                                         int32_t *stats, double u, int32_t *dflag) {
     const MFront f = F[blockIdx.x];
     const int64_t r0 = (int64_t)k * DB;
-    if (k >= f.pt || r0 >= f.p || f.p - r0 < 2) return;
+    if (k >= f.pt || r0 >= f.p || (f.p - r0 < 2 && f.q == 0)) return;
     const int64_t ld = (int64_t)f.ldt * DB;
     panel_pivot(W + f.ws, ld, r0, (int)(f.p - r0), (int64_t)f.pt * DB, f.q, P + soff[blockIdx.x], rowperm + pst[blockIdx.x],
-                stats, u);
+                stats, u, dflag ? dflag + pst[blockIdx.x] : nullptr);
 }
 
 // C (64 x 64 tile, leading dimension ld) := alpha * op: tile-by-tile products
@@ -645,8 +648,9 @@ __global__ __launch_bounds__(DTPB) void k_mf_gj_colpanel(const MFront *F, int k,
 }
 
 void launch_mf_panel_pivot(int nf, const MFront *F, const int64_t *pst, const int64_t *soff, int k, double *W,
-                           double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st) {
-    if (nf > 0 && u > 0.0) k_mf_panel_pivot<<<(unsigned)nf, DTPB, 0, st>>>(F, pst, soff, k, W, P, rowperm, stats, u);
+                           double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st, int32_t *dflag) {
+    if (nf > 0 && u > 0.0)
+        k_mf_panel_pivot<<<(unsigned)nf, DTPB, 0, st>>>(F, pst, soff, k, W, P, rowperm, stats, u, dflag);
 }
 void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, double *D, int32_t *fail,
                        double tau, hipStream_t st) {

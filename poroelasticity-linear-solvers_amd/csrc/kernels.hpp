@@ -350,9 +350,11 @@ void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, d
 // pivots chosen among its fully-summed rows [64 k, p) (update rows the threshold's
 // reference), rows exchanged in W and in rowperm + pst[f] (front-local original
 // row per position); P + soff[f]: (p + q) x 64 scratch.  stats: [0] rows
-// exchanged, [1] pivots below u x column max (MUMPS would delay them), [2] zero columns.
+// exchanged, [1] pivots below u x column max (MUMPS would delay them; dflag + pst[f]:
+// 1 at those columns), [2] zero columns.
 void launch_mf_panel_pivot(int nf, const MFront *F, const int64_t *pst, const int64_t *soff, int k, double *W,
-                           double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st);
+                           double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st,
+                           int32_t *dflag = nullptr);
 // Persistent factors: rows [0, 64 pt) of the front (U part, ld wide) to U + uoff
 // and rows [64 pt, 64 pt + q) x columns [0, 64 pt) (X part) to X + xoff.
 struct MStore {

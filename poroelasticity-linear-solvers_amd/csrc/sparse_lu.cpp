@@ -76,6 +76,50 @@ double now_s() {
 
 }  // namespace
 
+// ND positions, pivot ranges and update rows of every front from the tree's
+// pivot sets (Y.T.piv) in postorder; re-run after delayed pivots moved
+// variables to their parents' fronts
+void lu_structure(LUSymbolic &Y) {
+    const NDTree &T = Y.T;
+    const int64_t n = (int64_t)Y.pos.size();
+    const double t1 = now_s();
+    Y.pstart.assign(Y.nfront, 0);
+    {
+        int64_t k = 0;
+        for (int32_t f : Y.post) {
+            Y.pstart[f] = k;
+            for (int32_t v : T.piv[f]) {
+                Y.pos[v] = (int32_t)k;
+                Y.permh[k] = v;
+                Y.front_of[k] = f;
+                ++k;
+            }
+        }
+        if (k != n) throw Error("lu: the dissection does not cover every row");
+    }
+    // update rows (ND positions, ascending) of every front
+    Y.st.assign(Y.nfront, {});
+    {
+        std::vector<int32_t> mark(n, -1);
+        for (int32_t f : Y.post) {
+            const int64_t pend = Y.pstart[f] + (int64_t)T.piv[f].size();
+            std::vector<int32_t> &s = Y.st[f];
+            auto add = [&](int32_t p) {
+                if (p >= pend && mark[p] != f) {
+                    mark[p] = f;
+                    s.push_back(p);
+                }
+            };
+            for (int32_t cch : T.ch[f])
+                for (int32_t p : Y.st[cch]) add(p);
+            for (int32_t v : T.piv[f])
+                for (int64_t k = Y.gp[v]; k < Y.gp[v + 1]; ++k) add(Y.pos[Y.gi[k]]);
+            std::sort(s.begin(), s.end());
+        }
+    }
+    Y.t_symbolic += now_s() - t1;
+}
+
 LUSymbolic lu_symbolic(const HostCSR &A, const Options &o) {
     LUSymbolic Y;
     const int64_t n = A.nrows;
@@ -102,46 +146,12 @@ LUSymbolic lu_symbolic(const HostCSR &A, const Options &o) {
     Y.pos.assign(n, 0);
     Y.permh.assign(n, 0);
     Y.front_of.assign(n, 0);
-    Y.pstart.assign(Y.nfront, 0);
-    {
-        int64_t k = 0;
-        for (int32_t f : Y.post) {
-            Y.pstart[f] = k;
-            for (int32_t v : T.piv[f]) {
-                Y.pos[v] = (int32_t)k;
-                Y.permh[k] = v;
-                Y.front_of[k] = f;
-                ++k;
-            }
-        }
-        if (k != n) throw Error("lu: the dissection does not cover every row");
-    }
-    const double t1 = now_s();
-    // update rows (ND positions, ascending) of every front
-    Y.st.assign(Y.nfront, {});
-    {
-        std::vector<int32_t> mark(n, -1);
-        for (int32_t f : Y.post) {
-            const int64_t pend = Y.pstart[f] + (int64_t)T.piv[f].size();
-            std::vector<int32_t> &s = Y.st[f];
-            auto add = [&](int32_t p) {
-                if (p >= pend && mark[p] != f) {
-                    mark[p] = f;
-                    s.push_back(p);
-                }
-            };
-            for (int32_t cch : T.ch[f])
-                for (int32_t p : Y.st[cch]) add(p);
-            for (int32_t v : T.piv[f])
-                for (int64_t k = Y.gp[v]; k < Y.gp[v + 1]; ++k) add(Y.pos[Y.gi[k]]);
-            std::sort(s.begin(), s.end());
-        }
-    }
+    Y.t_order = now_s() - t0;
+    Y.t_symbolic = 0;
+    lu_structure(Y);
     int32_t maxd = 0;
     for (int32_t d : T.depth) maxd = std::max(maxd, d);
     Y.nlevels = maxd + 1;
-    Y.t_order = t1 - t0;
-    Y.t_symbolic = now_s() - t1;
     return Y;
 }
 
@@ -195,6 +205,9 @@ struct PCSparseLU : PC {
     int static_pivots = 0;
     double tau_used = 0.0;  // the static pivoting threshold applied
 
+    int delayed = 0, delay_rounds = 0;  // variables moved to their parents' fronts, re-analyses
+    int64_t maxf = 0;                   // largest front (p + q)
+
     PCSparseLU(const DevCSR &M, const Options &o, Ctx &c) {
         type = "lu";
         n = M.nrows;
@@ -202,6 +215,48 @@ struct PCSparseLU : PC {
         const double t0 = now_s();
         const HostCSR A = download(M, c);
         LUSymbolic Y = lu_symbolic(A, o);
+        // Delayed pivots (MUMPS): a column whose best fully-summed candidate is below
+        // u x its largest entry over the front (update rows included) is not
+        // eliminated in this front but in its parent's, where the rows that made it
+        // small are fully summed too.  Here that is a re-analysis: the flagged
+        // variables move to their parents' pivot sets, the structure is recomputed
+        // and the factorization re-run (pls.lu_delay_rounds times at most; 0: off,
+        // the best candidate is used as it is).  The root's columns cannot move.
+        const int64_t rounds = o.integer("pls.lu_delay_rounds", 8);
+        for (int round = 0;; ++round) {
+            std::vector<int32_t> dfl;
+            factor(M, A, Y, o, c, t0, round < rounds ? &dfl : nullptr);
+            int moved = 0;
+            for (int64_t i = 0; i < (int64_t)dfl.size(); ++i) {
+                if (!dfl[i]) continue;
+                const int32_t f = Y.front_of[i], g = Y.T.parent[f], v = Y.permh[i];
+                if (g < 0) continue;
+                auto &pf = Y.T.piv[f];
+                pf.erase(std::find(pf.begin(), pf.end(), v));
+                Y.T.piv[g].push_back(v);
+                ++moved;
+            }
+            if (!moved) break;
+            delayed += moved;
+            ++delay_rounds;
+            lu_structure(Y);
+        }
+        setup_s[3] = now_s() - t0;
+        if (o.flag("pls.lu_view", false))
+            fprintf(stderr,
+                    "[sparse lu] n %lld: %lld fronts, %lld levels, largest front %lld, factors %.2f GB, %d static "
+                    "pivots, refinement steps %d; threshold pivoting u = %g: %d rows exchanged, %d pivots below u x "
+                    "column max, %d zero columns; %d delayed pivots (%d re-analyses); setup: ordering %.2f s, "
+                    "symbolic %.2f s, factorization %.2f s, total %.2f s\n",
+                    (long long)n, (long long)nfront, (long long)nlevels, (long long)maxf, factor_gb, static_pivots,
+                    refine, piv_u, piv_stats[0], piv_stats[1], piv_stats[2], delayed, delay_rounds, setup_s[0],
+                    setup_s[1], setup_s[2], setup_s[3]);
+    }
+
+    // numeric factorization and solve tables for the structure Y; dfl (if given):
+    // per ND position 1 where the column's pivot fell below the threshold
+    void factor(const DevCSR &M, const HostCSR &A, LUSymbolic &Y, const Options &o, Ctx &c, double t0,
+                std::vector<int32_t> *dfl) {
         const NDTree &T = Y.T;
         nfront = Y.nfront;
         const std::vector<int32_t> &post = Y.post, &pos = Y.pos, &permh = Y.permh, &front_of = Y.front_of;
@@ -286,7 +341,8 @@ struct PCSparseLU : PC {
         // pls.lu_pivot_threshold, default 0.01; 0: pivots only inside each 64 x 64 tile)
         const double u = o.num("pls.lu_pivot_threshold", 0.01);
         piv_u = u;
-        DBuf<int32_t> drowp(std::max<int64_t>(n, 1)), pstats(3);
+        DBuf<int32_t> drowp(std::max<int64_t>(n, 1)), pstats(3), dflag(dfl ? std::max<int64_t>(n, 1) : 0);
+        if (dfl) HIPCHK(hipMemsetAsync(dflag.p, 0, sizeof(int32_t) * std::max<int64_t>(n, 1), c.st));
         {
             std::vector<int32_t> lid(std::max<int64_t>(n, 1), 0);
             for (int32_t f : post)
@@ -327,7 +383,7 @@ struct PCSparseLU : PC {
                     const int32_t f = fl[t];
                     hpst.push_back(pstart[f]);
                     hsoff.push_back(pscr);
-                    pscr += (p[f] > 1 ? p[f] + q[f] : 0) * 64;
+                    pscr += (p[f] > 1 || (p[f] == 1 && q[f] > 0) ? p[f] + q[f] : 0) * 64;
                 }
                 DBuf<int64_t> dpst(hpst.size()), dsoff(hsoff.size());
                 DBuf<double> Pscr(u > 0.0 ? std::max<int64_t>(pscr, 1) : 1);
@@ -369,7 +425,7 @@ struct PCSparseLU : PC {
                 }
                 for (int k = 0; k < max_pt; ++k) {
                     launch_mf_panel_pivot((int)hf.size(), dF.p, dpst.p, dsoff.p, k, Wcur, Pscr.p, drowp.p, pstats.p, u,
-                                          c.st);
+                                          c.st, dflag.p);
                     launch_mf_gj_step((int)hf.size(), dF.p, max_ldt, k, Wcur, Dt.p, fail.p, tau, c.st);
                 }
                 launch_mf_store((int)hf.size(), dF.p, dS.p, max_rows, Wcur, U.p, X.p, c.st);
@@ -385,7 +441,16 @@ struct PCSparseLU : PC {
         std::vector<int32_t> rowp(std::max<int64_t>(n, 1));
         HIPCHK(hipMemcpyAsync(rowp.data(), drowp.p, sizeof(int32_t) * rowp.size(), hipMemcpyDeviceToHost, c.st));
         HIPCHK(hipMemcpyAsync(piv_stats, pstats.p, sizeof(int32_t) * 3, hipMemcpyDeviceToHost, c.st));
+        if (dfl) {
+            dfl->assign(std::max<int64_t>(n, 1), 0);
+            HIPCHK(hipMemcpyAsync(dfl->data(), dflag.p, sizeof(int32_t) * dfl->size(), hipMemcpyDeviceToHost, c.st));
+        }
         c.sync();
+        if (dfl) {  // delays pending: this factorization is replaced; a zero pivot here is not final
+            bool any = false;
+            for (int64_t i = 0; i < n && !any; ++i) any = (*dfl)[i] && T.parent[Y.front_of[i]] >= 0;
+            if (any) return;
+        }
         if (hfail[0]) throw Error("LU: zero pivot (PETSc: MAT_FACTOR_NUMERIC_ZEROPIVOT)");
         // the equations' order after the exchanges: ND position -> row of M
         std::vector<int32_t> rpermh(std::max<int64_t>(n, 1));
@@ -473,18 +538,8 @@ struct PCSparseLU : PC {
                     "[sparse lu] n %lld: %d pivots below %.1e perturbed (static pivoting, pls.lu_static_pivot); "
                     "%d refinement steps per solve\n",
                     (long long)n, static_pivots, tau_used, refine);
-        if (o.flag("pls.lu_view", false)) {
-            int64_t maxf = 0;
-            for (int32_t f : post) maxf = std::max(maxf, p[f] + q[f]);
-            fprintf(stderr,
-                    "[sparse lu] n %lld: %lld fronts, %lld levels, largest front %lld, factors %.2f GB, %d static "
-                    "pivots, refinement steps %d; threshold pivoting u = %g: %d rows exchanged, %d pivots below u x "
-                    "column max (delayed by MUMPS), %d zero columns; setup: ordering %.2f s, symbolic %.2f s, "
-                    "factorization %.2f s, total %.2f s\n",
-                    (long long)n, (long long)nfront, (long long)nlevels, (long long)maxf, factor_gb, static_pivots,
-                    refine, piv_u, piv_stats[0], piv_stats[1], piv_stats[2], setup_s[0], setup_s[1], setup_s[2],
-                    setup_s[3]);
-        }
+        maxf = 0;
+        for (int32_t f : post) maxf = std::max(maxf, p[f] + q[f]);
     }
 
     bool reentrant() const override { return true; }
