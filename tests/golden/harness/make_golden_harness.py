@@ -18,7 +18,10 @@ MUMPS and the device LU are (tests/test_gpu_fe.py _lu_swap_floor).  Stored:
 * ``first_dev``: per perturbation run (eps seeds, then LU swaps), the first
   iteration whose residual deviates from the unperturbed history by more than
   1e-10 relative (its length when none does); the device history is held to
-  1e-10 up to the smallest of them on the cases whose count moves.
+  1e-10 up to the smallest of them on the cases whose count moves -- on the
+  exact set to 10x ``lu_swap_prefix_floor``, the LU-swap runs' largest
+  relative deviation over that prefix, if larger (the device LU is a third
+  backward-stable LU: it moves the history as much as the swaps do).
 
 usage: python tests/golden/harness/make_golden_harness.py  (writes n10.json)
 """
@@ -96,11 +99,19 @@ def main():
         for q in swaps:
             if q.its == o.its:
                 floor = max(floor, float(np.max(np.abs(np.asarray(q.history) - ho) / ho)))
+        k = min(first_dev(q.history, ho) for q in runs + swaps)
+        pfloor = 0.0
+        for q in swaps:
+            hq = np.asarray(q.history)
+            m = min(k, hq.size, ho.size)
+            if m:
+                pfloor = max(pfloor, float(np.max(np.abs(hq[:m] - ho[:m]) / ho[:m])))
         key = f"{prob}|{pc}|{optset}"
         out[key] = {"its": int(o.its), "reason": int(o.reason), "history": [float(v) for v in o.history],
                     "perturbed_its": [int(q.its) for q in runs],
                     "lu_swap_its": [int(q.its) for q in swaps],
                     "lu_swap_floor": floor,
+                    "lu_swap_prefix_floor": pfloor,
                     "first_dev": [first_dev(q.history, ho) for q in runs + swaps]}
         print(key, o.its, out[key]["perturbed_its"], out[key]["lu_swap_its"], floor, out[key]["first_dev"],
               flush=True)
