@@ -149,33 +149,39 @@ def test_lu_threshold_pivoting_zero_leading_tile(gpu, capfd, path):
 
 
 def test_lu_delayed_pivot(gpu, capfd):
-    """A pivot MUMPS must delay (petsc-options-exact:11-35's LU): 8 disjoint
-    paths a - s - b, K = [[eps, 1, 0], [1, 2, 1], [0, 1, 2]] each (nonsingular,
-    det -2 + O(eps)), eps = 1e-14.  With leaves of one vertex the dissection
-    cuts every path at s: the leaf front {a} has the single fully-summed entry
-    eps against the update row's 1 -- below u = 0.01 of its column, so the
-    column is delayed to the parent front {s}, where rows s and a are both fully
-    summed and the exchange picks s.  Solved to rounding against numpy; with the
-    delays off (pls.lu_delay_rounds 0) the eps pivot is used and the solve loses
-    ~eps^-1 x 1e-16 of its accuracy."""
+    """A pivot MUMPS must delay (petsc-options-exact:11-35's LU): 4 disjoint
+    stars, center s (diagonal 4) coupled by 1 to leaves a1 (diagonal 1e-14)
+    and a2, a3, a4 (diagonal 2) -- nonsingular.  The dissection (leaves of one
+    vertex, ``sparse_lu_analyze``) puts {a1, a3} in one leaf front and s in its
+    parent: a1's column has the fully-summed entry 1e-14 against the update
+    row's 1, below u = 0.01 of the column, so it is delayed to the parent
+    front, where rows s and a1 are both fully summed and the exchange picks s.
+    Solved to rounding against numpy; with the delays off
+    (pls.lu_delay_rounds 0) the 1e-14 pivot is used and the solve loses
+    ~1e14 x 1e-16 of its accuracy."""
     import types
 
     import scipy.sparse.linalg as spla
-    blk = sp.csr_matrix(np.array([[1e-14, 1.0, 0.0], [1.0, 2.0, 1.0], [0.0, 1.0, 2.0]]))
-    K = sp.block_diag([blk] * 8).tocsr()
+    from lib.handle import sparse_lu_analyze
+    star = np.array([[4, 1, 1, 1, 1], [1, 1e-14, 0, 0, 0], [1, 0, 2, 0, 0], [1, 0, 0, 2, 0], [1, 0, 0, 0, 2]], float)
+    K = sp.block_diag([sp.csr_matrix(star)] * 4).tocsr()
+    nd = {"pls.lu_nd_leaf": "1", "pls.lu_nd_compress": "0"}
+    _, perm, front_of, parent = sparse_lu_analyze(K, nd, tree=True)
+    pos = {int(v): k for k, v in enumerate(perm)}
+    assert front_of[pos[1]] != front_of[pos[0]] and parent[front_of[pos[1]]] == front_of[pos[0]]  # a1 below s
     ns, nf, npr = K.shape[0], 8, 8
     P = sp.block_diag([K, sp.eye(nf), sp.eye(npr)]).tocsr()
     P.sort_indices()
     s = types.SimpleNamespace(A=P, P=P, P_diff=None, is_s=np.arange(ns, dtype=np.int32),
                               is_f=np.arange(ns, ns + nf, dtype=np.int32),
                               is_p=np.arange(ns + nf, P.shape[0], dtype=np.int32), bcs_sub_pressure=[])
-    extra = {"pls.lu_path": "sparse", "pls.lu_nd_leaf": "1", "pls.lu_nd_compress": "0"}
+    extra = dict(nd, **{"pls.lu_path": "sparse"})
     capfd.readouterr()
     x, y = _swap_apply(s, extra)
     err = capfd.readouterr().err
     ys = spla.spsolve(K.tocsc(), x[:ns])
     assert np.max(np.abs(y[:ns] - ys)) <= 1e-12 * np.max(np.abs(ys)), np.max(np.abs(y[:ns] - ys))
     line = [l for l in err.splitlines() if "[sparse lu] n %d" % ns in l]
-    assert line and " 8 delayed pivots" in line[0], err
+    assert line and " 4 delayed pivots" in line[0], err
     x2, y2 = _swap_apply(s, dict(extra, **{"pls.lu_delay_rounds": "0"}))
-    assert np.max(np.abs(y2[:ns] - ys)) > 1e-8 * np.max(np.abs(ys))  # the eps pivot, undelayed
+    assert np.max(np.abs(y2[:ns] - ys)) > 1e-8 * np.max(np.abs(ys))  # the 1e-14 pivot, undelayed
