@@ -182,24 +182,193 @@ __device__ void panel_pivot(double *W, int64_t ld, int64_t r0, int m, int64_t ur
     }
 }
 
+// The panel's common case, in parallel: the diagonal row kept in every column.
+// Then the panel's elimination is the unpivoted one, a_ij at step j is l_ij u_jj
+// with L = A U11^-1 (U11: the tile's unpivoted LU), and the rule above reads
+//   exchange in column j   <=>  u x max_{candidates i > j} |l_ij| > 1,
+//   below u x column max   <=>  max(1, max_cand |l_ij|) < u x max_{update rows} |l_ij|.
+// k_panel_tile (one workgroup per panel) factors the tile, k_panel_rows (a
+// thread per row below it, many workgroups) forms the rows of L by the same
+// right-looking updates as panel_pivot and takes the column maxima; the
+// per-panel workgroup (k_*_panel_pivot) then sets the statistics and the delay
+// flags from them, or -- on an exchange, a zero or a non-finite entry -- runs
+// panel_pivot itself.  Rounds 1-6's one-workgroup panel alone took ~23 s of
+// the 30 s setup at footing N = 80 (inexact; a 29,988-row dense block), with
+// no exchange at all.
+// Per-panel scratch (PANEL_FAST doubles): U11 [64][64], then the column maxima
+// of |l| over candidates (64) and update rows (64) as the bits of non-negative
+// doubles (ordered as unsigned integers), then a flag (bad entry).
+static constexpr int PANEL_FAST = 4096 + 192;
+struct PanelRef {
+    double *W;
+    int64_t ld, r0, ur0;
+    int m, q;  // candidates [r0, r0 + m), update rows [ur0, ur0 + q)
+};
+__device__ __forceinline__ bool mf_panel_ref(const MFront &f, int k, double *W, PanelRef &p) {
+    p.r0 = (int64_t)k * DB;
+    // nothing to choose and nothing to compare with: every candidate is in the tile, whose own
+    // partial pivoting (k_mf_gj_diag) takes the same rows, and no update rows
+    if (k >= f.pt || p.r0 >= f.p || (f.p - p.r0 <= DB && f.q == 0)) return false;
+    p.W = W + f.ws;
+    p.ld = (int64_t)f.ldt * DB;
+    p.ur0 = (int64_t)f.pt * DB;
+    p.m = (int)(f.p - p.r0);
+    p.q = f.q;
+    return true;
+}
+__device__ __forceinline__ bool dense_panel_ref(int64_t n, int64_t ld, int64_t k, double *M, PanelRef &p) {
+    p.r0 = k * DB;
+    if (p.r0 >= n) return false;
+    p.W = M;
+    p.ld = ld;
+    p.ur0 = 0;
+    p.m = (int)(n - p.r0);
+    p.q = 0;
+    return true;
+}
+__device__ __forceinline__ const double *panel_row(const PanelRef &p, int i) {  // panel row i, column r0
+    return p.W + (i < p.m ? p.r0 + i : p.ur0 + (i - p.m)) * p.ld + p.r0;
+}
+__device__ __forceinline__ uint64_t dbits(double v) { return (uint64_t)__double_as_longlong(v); }
+
+__device__ void panel_tile(const PanelRef &p, double *S) {
+    __shared__ double T[DB][DB + 1];
+    __shared__ int sbad;
+    const int tid = threadIdx.x, nc = p.m < DB ? p.m : DB;
+    if (tid == 0) sbad = 0;
+    for (int t = tid; t < DB * DB; t += DTPB) {
+        const int i = t >> 6, c = t & 63;
+        T[i][c] = i < nc ? panel_row(p, i)[c] : 0.0;
+    }
+    __syncthreads();
+    const int i = tid >> 2, c0 = (tid & 3) * 16;  // row i, columns [c0, c0 + 16)
+    bool bad = false;
+    for (int j = 0; j < nc; ++j) {
+        const double d = T[j][j];
+        bad = bad || d == 0.0 || !(fabs(d) <= 1.7976931348623157e308);
+        const double l = (i > j && i < nc) ? T[i][j] / d : 0.0;
+        __syncthreads();
+        if (i > j && i < nc) {
+            for (int c = c0 > j + 1 ? c0 : j + 1; c < c0 + 16; ++c) T[i][c] = T[i][c] - l * T[j][c];
+            if (c0 == 0) T[i][j] = l;
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < DB * DB; t += DTPB) S[t] = T[t >> 6][t & 63];
+    uint64_t *mx = reinterpret_cast<uint64_t *>(S + 4096);
+    if (tid < DB) {
+        double mc = 0.0;
+        for (int r = tid + 1; r < nc; ++r) mc = fmax(mc, fabs(T[r][tid]));
+        if (!(mc <= 1.7976931348623157e308)) bad = true;
+        mx[tid] = dbits(mc);
+        mx[64 + tid] = 0;
+    }
+    if (bad) sbad = 1;
+    __syncthreads();
+    if (tid == 0) mx[128] = sbad;
+}
+static constexpr int PRTPB = 128;  // k_panel_rows: rows per workgroup (a thread each; LDS: the rows + U11)
+__device__ void panel_rows(const PanelRef &p, const double *S) {
+    __shared__ double U[DB][DB + 1];
+    __shared__ double A[DB][PRTPB];  // A[c][t]: column c of the workgroup's row t
+    const int tid = threadIdx.x, lane = tid & 63, nc = p.m < DB ? p.m : DB;
+    const int i0 = nc + (int)blockIdx.x * PRTPB, nr = p.m + p.q;
+    for (int t = tid; t < DB * DB; t += PRTPB) U[t >> 6][t & 63] = S[t];
+    for (int t = tid; t < DB * PRTPB; t += PRTPB) {  // (coalesced: 64 threads per row)
+        const int r = t >> 6, c = t & 63;
+        A[c][r] = i0 + r < nr && c < nc ? panel_row(p, i0 + r)[c] : 0.0;
+    }
+    __syncthreads();
+    const int i = i0 + tid;  // panel row (below the tile)
+    const bool act = i < nr;
+    bool bad = false;
+    uint64_t *mx = reinterpret_cast<uint64_t *>(const_cast<double *>(S) + 4096);
+    uint64_t myc = 0, myu = 0;
+    // the right-looking updates of panel_pivot, row by row: bitwise its l
+    for (int j = 0; j < nc; ++j) {
+        const double l = A[j][tid] / U[j][j];
+        for (int c = j + 1; c < DB; ++c) A[c][tid] = A[c][tid] - l * U[j][c];
+        const double al = act ? fabs(l) : 0.0;
+        bad = bad || !(al <= 1.7976931348623157e308);
+        double vc = i < p.m ? al : 0.0, vu = i < p.m ? 0.0 : al;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            vc = fmax(vc, __shfl_xor(vc, o));
+            vu = fmax(vu, __shfl_xor(vu, o));
+        }
+        if (lane == j) {
+            myc = dbits(vc);
+            myu = dbits(vu);
+        }
+    }
+    if (lane < nc) {
+        if (myc) atomicMax(reinterpret_cast<unsigned long long *>(mx + lane), (unsigned long long)myc);
+        if (myu) atomicMax(reinterpret_cast<unsigned long long *>(mx + 64 + lane), (unsigned long long)myu);
+    }
+    if (bad) atomicMax(reinterpret_cast<unsigned long long *>(mx + 128), 1ull);
+}
+// true: the fast path holds for this panel (statistics and flags set)
+__device__ bool panel_fast_done(const PanelRef &p, const double *S, int32_t *stats, double u, int32_t *dflag) {
+    __shared__ int slow;
+    const int tid = threadIdx.x, nc = p.m < DB ? p.m : DB;
+    const uint64_t *mx = reinterpret_cast<const uint64_t *>(S + 4096);
+    if (tid == 0) slow = mx[128] != 0;
+    __syncthreads();
+    if (tid < nc && u * __longlong_as_double((long long)mx[tid]) > 1.0) slow = 1;
+    __syncthreads();
+    const bool s = slow;
+    __syncthreads();  // (slow is read by every thread before the next panel's use)
+    if (s) return false;
+    if (tid < nc) {
+        const double mc = __longlong_as_double((long long)mx[tid]), mu = __longlong_as_double((long long)mx[64 + tid]);
+        if (fmax(1.0, mc) < u * mu) {
+            atomicAdd(stats + 1, 1);
+            if (dflag) dflag[p.r0 + tid] = 1;
+        }
+    }
+    return true;
+}
+
+template <bool MF>
+__global__ __launch_bounds__(DTPB) void k_panel_tile(const MFront *F, int64_t n, int64_t ld, int k, double *W,
+                                                     double *S) {
+    PanelRef p;
+    if (!(MF ? mf_panel_ref(F[blockIdx.x], k, W, p) : dense_panel_ref(n, ld, k, W, p))) return;
+    panel_tile(p, S + (int64_t)blockIdx.x * PANEL_FAST);
+}
+template <bool MF>
+__global__ __launch_bounds__(PRTPB) void k_panel_rows(const MFront *F, int64_t n, int64_t ld, int k, double *W,
+                                                      double *S) {
+    PanelRef p;
+    if (!(MF ? mf_panel_ref(F[blockIdx.y], k, W, p) : dense_panel_ref(n, ld, k, W, p))) return;
+    const int nc = p.m < DB ? p.m : DB;
+    if (nc + (int64_t)blockIdx.x * PRTPB >= p.m + p.q) return;  // (uniform: no row of this panel here)
+    panel_rows(p, S + (int64_t)blockIdx.y * PANEL_FAST);
+}
+
 // dense block (PCDenseLU): candidates rows [64 k, n), no update rows
 __global__ __launch_bounds__(DTPB) void k_dense_panel_pivot(int64_t n, int64_t ld, int64_t k, double *M, double *P,
-                                                            int32_t *rowperm, int32_t *stats, double u) {
-    const int64_t r0 = k * DB;
-    if (r0 >= n) return;
-    panel_pivot(M, ld, r0, (int)(n - r0), 0, 0, P, rowperm, stats, u);
+                                                            int32_t *rowperm, int32_t *stats, double u,
+                                                            const double *S) {
+    PanelRef p;
+    if (!dense_panel_ref(n, ld, k, M, p)) return;
+    if (S && panel_fast_done(p, S, stats, u, nullptr)) return;
+    panel_pivot(M, ld, p.r0, p.m, 0, 0, P, rowperm, stats, u);
 }
 // fronts (blockIdx.x): candidates rows [64 k, p), update rows [64 pt, 64 pt + q);
 // P + soff[f]: (p + q) x 64 scratch; rowperm + pst[f]: the front's pivot rows
+static constexpr int PANEL_LDS_ROWS = 160;  // panels of up to this many rows stay in LDS (80 KiB)
 __global__ __launch_bounds__(DTPB) void k_mf_panel_pivot(const MFront *F, const int64_t *pst, const int64_t *soff,
                                                          int k, double *W, double *P, int32_t *rowperm,
-                                                         int32_t *stats, double u, int32_t *dflag) {
-    const MFront f = F[blockIdx.x];
-    const int64_t r0 = (int64_t)k * DB;
-    if (k >= f.pt || r0 >= f.p || (f.p - r0 < 2 && f.q == 0)) return;
-    const int64_t ld = (int64_t)f.ldt * DB;
-    panel_pivot(W + f.ws, ld, r0, (int)(f.p - r0), (int64_t)f.pt * DB, f.q, P + soff[blockIdx.x], rowperm + pst[blockIdx.x],
-                stats, u, dflag ? dflag + pst[blockIdx.x] : nullptr);
+                                                         int32_t *stats, double u, int32_t *dflag, const double *S) {
+    __shared__ double Pl[PANEL_LDS_ROWS * DB];
+    PanelRef p;
+    if (!mf_panel_ref(F[blockIdx.x], k, W, p)) return;
+    int32_t *df = dflag ? dflag + pst[blockIdx.x] : nullptr;
+    if (S && panel_fast_done(p, S + (int64_t)blockIdx.x * PANEL_FAST, stats, u, df)) return;
+    const int nr = p.m + p.q;
+    panel_pivot(p.W, p.ld, p.r0, p.m, p.ur0, p.q, nr <= PANEL_LDS_ROWS ? Pl : P + soff[blockIdx.x],
+                rowperm + pst[blockIdx.x], stats, u, df);
 }
 
 // C (64 x 64 tile, leading dimension ld) := alpha * op: tile-by-tile products
@@ -309,7 +478,15 @@ void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStr
                          int32_t *rowperm, int32_t *stats, double u) {
     const int64_t nb = ld / DB;
     for (int64_t k = 0; k < nb; ++k) {
-        if (u > 0.0 && P) k_dense_panel_pivot<<<1, DTPB, 0, st>>>(n, ld, k, M, P, rowperm, stats, u);
+        if (u > 0.0 && P) {  // (P: n x 64 for the panel, then PANEL_FAST for the fast path)
+            double *S = P + n * DB;
+            const int64_t rows = n - k * DB - DB;  // below the tile
+            k_panel_tile<false><<<1, DTPB, 0, st>>>(nullptr, n, ld, (int)k, M, S);
+            if (rows > 0)
+                k_panel_rows<false><<<dim3((unsigned)((rows + PRTPB - 1) / PRTPB), 1), PRTPB, 0, st>>>(nullptr, n, ld,
+                                                                                                     (int)k, M, S);
+            k_dense_panel_pivot<<<1, DTPB, 0, st>>>(n, ld, k, M, P, rowperm, stats, u, S);
+        }
         k_gj_diag<<<1, DTPB, 0, st>>>(ld, k, M, D, fail);
         k_gj_rowpanel<<<(unsigned)nb, DTPB, 0, st>>>(ld, k, D, M);
         if (nb > 1) {
@@ -648,10 +825,19 @@ __global__ __launch_bounds__(DTPB) void k_mf_gj_colpanel(const MFront *F, int k,
 }
 
 void launch_mf_panel_pivot(int nf, const MFront *F, const int64_t *pst, const int64_t *soff, int k, double *W,
-                           double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st, int32_t *dflag) {
-    if (nf > 0 && u > 0.0)
-        k_mf_panel_pivot<<<(unsigned)nf, DTPB, 0, st>>>(F, pst, soff, k, W, P, rowperm, stats, u, dflag);
+                           double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st, int32_t *dflag,
+                           double *S, int64_t max_rows) {
+    if (nf <= 0 || u <= 0.0) return;
+    if (S) {
+        k_panel_tile<true><<<(unsigned)nf, DTPB, 0, st>>>(F, 0, 0, k, W, S);
+        const int64_t rows = max_rows - (int64_t)k * DB;  // (bound on every front's panel rows at step k)
+        if (rows > 0)
+            k_panel_rows<true><<<dim3((unsigned)((rows + PRTPB - 1) / PRTPB), (unsigned)nf), PRTPB, 0, st>>>(F, 0, 0, k,
+                                                                                                           W, S);
+    }
+    k_mf_panel_pivot<<<(unsigned)nf, DTPB, 0, st>>>(F, pst, soff, k, W, P, rowperm, stats, u, dflag, S);
 }
+int panel_fast_doubles() { return PANEL_FAST; }
 void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, double *D, int32_t *fail,
                        double tau, hipStream_t st) {
     if (nf <= 0 || max_ldt <= 0) return;

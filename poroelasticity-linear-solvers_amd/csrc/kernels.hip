@@ -3421,13 +3421,16 @@ static constexpr int WIN_KP = WIN_NW * WIN_KPW;  // stream entries per row (ever
 // (WIN_OFFR registers hold 64 * WIN_OFFR offsets: every window of a block up to
 // ilu_window_max_rows() rows plus the end offset -- 316 for 20,160 rows)
 static constexpr int WIN_OFFR = 5;
+// the ring variant (blocks longer than LDS): 16 registers, 1,023 windows
+static constexpr int WIN_OFFR_RING = 16, WIN_RING = 16384;
+template <int R>
 struct WinOff {
-    int64_t r[WIN_OFFR];
-    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: WIN_OFFR readlanes, scalar selects
+    int64_t r[R];
+    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: R readlanes, scalar selects
         const int j = (int)(w >> 6), l = (int)(w & 63);
         int64_t v = readlane64(r[0], l);
 #pragma unroll
-        for (int k = 1; k < WIN_OFFR; ++k) {
+        for (int k = 1; k < R; ++k) {
             const int64_t t = readlane64(r[k], l);
             v = j == k ? t : v;
         }
@@ -3450,6 +3453,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t win_rsrc(const void *base, int
 struct WinBuf {  // one wave's share of a window's data in registers
     double tv[16], sv[WIN_KPW];
     int32_t sc[WIN_KPW];
+    double rx;  // (ring variant) the window's input rows, from global memory
 };
 
 // Range-checked buffer loads issued through inline asm: the compiler does not
@@ -3458,6 +3462,8 @@ struct WinBuf {  // one wave's share of a window's data in registers
 // window issues WIN_LOADS of them -- and win_wait ties the registers to the
 // wait (no use or copy can move above it).
 static constexpr int WIN_LOADS = 16 + 2 * WIN_KPW;
+template <bool RING>
+constexpr int win_loads() { return WIN_LOADS + (RING ? 1 : 0); }
 __device__ __forceinline__ double win_ld64(__amdgpu_buffer_rsrc_t r, int off) {
     double v;
     asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
@@ -3468,26 +3474,37 @@ __device__ __forceinline__ int32_t win_ld32(__amdgpu_buffer_rsrc_t r, int off) {
     asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
     return v;
 }
-template <int N>
+__device__ __forceinline__ void win_st64(__amdgpu_buffer_rsrc_t r, int off, double v) {
+    asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
+}
+template <int N, bool RING = false>
 __device__ __forceinline__ void win_wait(WinBuf &B) {  // vmcnt(N), B's registers pinned to it
     asm volatile("s_waitcnt vmcnt(%c0)" ::"n"(N) : "memory");
 #pragma unroll
     for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(B.tv[k]));
 #pragma unroll
     for (int u = 0; u < WIN_KPW; ++u) asm volatile("" : "+v"(B.sv[u]), "+v"(B.sc[u]));
+    if (RING) asm volatile("" : "+v"(B.rx));
 }
 
-template <bool UP, int WD = 2>
+// RING: ys is a ring of WIN_RING rows (row r in slot r mod WIN_RING; the setup
+// checks that no row depends on one more than WIN_RING - 64 rows away), the
+// window's input rows come from global memory (in, prefetched with the window's
+// data) and its solution goes to global memory (out) as well as to the ring
+template <bool UP, int WD = 2, bool RING = false>
 __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t *__restrict__ woff,
                                           const int32_t *__restrict__ col, const double *__restrict__ val,
                                           const double *__restrict__ tinv, double *ys, double *part, int lane,
-                                          int q) {
+                                          int q, const double *in = nullptr, double *out = nullptr) {
+    constexpr int R = RING ? WIN_OFFR_RING : WIN_OFFR, NL = win_loads<RING>();
+    constexpr int64_t RM = WIN_RING - 1;
     const int64_t nw = (len + 63) >> 6;
     if (nw == 0) return;
-    WinOff wo;
+    WinOff<R> wo;
 #pragma unroll
-    for (int j = 0; j < WIN_OFFR; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
+    for (int j = 0; j < R; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the offsets (ordinary loads) before the counted ones
+    const auto rin = win_rsrc(in, RING ? len * 8 : 0), rout = win_rsrc(out, RING ? len * 8 : 0);
     auto wi = [&](int64_t ww) { return UP ? nw - 1 - ww : ww; };
     // T^-1[k][lane] is zero above (L) / below (U) the diagonal: those lanes read out of range
     auto toff = [&](int k) { return (UP ? k >= lane : k <= lane) ? (k * 64 + lane) * 8 : 0x40000000; };
@@ -3507,6 +3524,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) B.tv[k] = win_ld64(rt, toff(16 * q + k));
+        if (RING) B.rx = win_ld64(rin, (int)(ok * (w * 64 + lane) * 8 + (1 - ok) * 0x40000000));
     };
     // one window, branch-free (a window past the block computes zeros into a dummy slot)
     auto compute = [&](int64_t ww, const WinBuf &B) {
@@ -3515,13 +3533,13 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         const bool act = ww < nw && r < len;
         double d[WIN_KPW];
 #pragma unroll
-        for (int u = 0; u < WIN_KPW; ++u) d[u] = ys[B.sc[u]];
+        for (int u = 0; u < WIN_KPW; ++u) d[u] = ys[RING ? (B.sc[u] & RM) : B.sc[u]];
         double acc = 0.0;
 #pragma unroll
         for (int u = 0; u < WIN_KPW; ++u) acc += __dmul_rn(B.sv[u], d[u]);
         part[q * 64 + lane] = acc;
         __syncthreads();
-        const double rhs = ys[act ? r : 0];
+        const double rhs = RING ? B.rx : ys[act ? r : 0];
         const double t = act ? rhs - (((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane]) : 0.0;
         const int tlo = __double2loint(t), thi = __double2hiint(t);
         double out = 0.0;
@@ -3535,47 +3553,58 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         part[q * 64 + lane] = out;
         __syncthreads();
         const double yr = ((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane];
-        ys[act ? r : len + lane] = yr;  // every wave writes the same value (its own later reads see it)
-        __syncthreads();                // part[] free for the next window
+        if (RING) {
+            // every wave stores the window (the same values): one counted store per
+            // wave and window, issued after the window's loads
+            ys[act ? (r & RM) : WIN_RING + lane] = yr;
+            win_st64(rout, act ? (int)(r * 8) : 0x40000000, yr);
+        } else {
+            ys[act ? r : len + lane] = yr;  // every wave writes the same value (its own later reads see it)
+        }
+        __syncthreads();  // part[] free for the next window
     };
-    if (WD == 3) {
-        // three windows of data in flight: the oldest window's WIN_LOADS loads are
-        // followed by 2 x WIN_LOADS = 64 younger ones, more than vmcnt counts (63);
+    if (WD == 3 && !RING) {
+        // three windows of data in flight: the oldest window's NL loads are
+        // followed by 2 x NL >= 64 younger ones, more than vmcnt counts (63);
         // waiting for <= 63 outstanding waits for one load of the next window too
-        static_assert(2 * WIN_LOADS >= 63, "vmcnt(63) must cover the oldest window");
+        static_assert(2 * NL >= 63, "vmcnt(63) must cover the oldest window");
         WinBuf A, B, C;
         issue(0, A);
         issue(1, B);
         issue(2, C);
         for (int64_t ww = 0; ww < nw; ww += 3) {
-            win_wait<63>(A);
+            win_wait<63, RING>(A);
             compute(ww, A);
             issue(ww + 3, A);
-            win_wait<63>(B);
+            win_wait<63, RING>(B);
             compute(ww + 1, B);
             issue(ww + 4, B);
-            win_wait<63>(C);
+            win_wait<63, RING>(C);
             compute(ww + 2, C);
             issue(ww + 5, C);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         return;
     }
+    // (ring: a window's store sits between its successor's loads and the next
+    // issue; vector memory completes in issue order, so one more may be pending)
+    constexpr int WT = RING ? NL + 1 : NL;
     WinBuf A, B;
     issue(0, A);
     issue(1, B);
+    if (RING) win_wait<NL, RING>(A);  // (no store yet between A and B)
     for (int64_t ww = 0; ww < nw; ww += 2) {  // two windows per trip: loads of window ww + 2 fly during ww + 1
-        win_wait<WIN_LOADS>(A);               // A's loads are older than B's WIN_LOADS
+        win_wait<WT, RING>(A);               // A's loads are older than B's NL (and a store)
         compute(ww, A);
         issue(ww + 2, A);
-        win_wait<WIN_LOADS>(B);
+        win_wait<WT, RING>(B);
         compute(ww + 1, B);
         issue(ww + 3, B);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the prefetches past the block: nothing in range)
 }
 
-template <int WD>
+template <int WD, bool RING>
 __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart,
                                                            const int64_t *__restrict__ wstart,
                                                            const int64_t *__restrict__ Lwoff, const int32_t *__restrict__ Lcol,
@@ -3591,7 +3620,10 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
     block_range(blk, n, nblocks, bstart, b0, len);
     const int lane = threadIdx.x & 63;
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (v_readlane's lane is a scalar)
-    for (int64_t t = threadIdx.x; t < len; t += 256) ys[t] = x[b0 + t];
+    if (RING)  // (padding entries read slot 0 with value 0: every slot finite)
+        for (int64_t t = threadIdx.x; t < WIN_RING; t += 256) ys[t] = 0.0;
+    else
+        for (int64_t t = threadIdx.x; t < len; t += 256) ys[t] = x[b0 + t];
     __syncthreads();
     // block bounds as scalars (buffer resources built from them must live in SGPRs)
     auto uni = [](int64_t v) {
@@ -3601,6 +3633,15 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
     };
     len = uni(len);
     const int64_t w0 = uni(wstart[blk]);
+    if (RING) {
+        // L: x -> y (global and the ring); U: y -> y in place, its input rows read
+        // from global memory after every wave's L stores completed (win_sweep ends
+        // with vmcnt(0); the barrier orders them before U's first loads)
+        win_sweep<false, 2, true>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q, x + b0, y + b0);
+        __syncthreads();
+        win_sweep<true, 2, true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q, y + b0, y + b0);
+        return;
+    }
     win_sweep<false, WD>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q);
     win_sweep<true, WD>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q);
     __syncthreads();
@@ -3609,28 +3650,36 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
 
 int ilu_window_max_rows() { return 163840 / 8 - 256 - 64; }  // LDS: partial sums, the block, a dummy slot per lane
 static_assert((163840 / 8 - 256 - 64 + 63) / 64 + 1 <= 64 * WIN_OFFR, "window offsets exceed WinOff's registers");
+int ilu_window_ring_rows() { return WIN_RING; }
+int64_t ilu_window_ring_max_rows() { return (int64_t)(64 * WIN_OFFR_RING - 1) * 64; }
+static_assert(256 + WIN_RING + 64 <= 163840 / 8, "the ring exceeds LDS");
 int ilu_window_stream_pad() { return 0; }
 int ilu_window_max_entries() { return WIN_KP; }
 
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
                               const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,
-                              const double *x, double *y, int64_t max_len, hipStream_t st, int depth) {
+                              const double *x, double *y, int64_t max_len, hipStream_t st, int depth, bool ring) {
     static bool configured = false;
     if (!configured) {
-        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_window<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)163840);
-        (void)hipFuncSetAttribute((const void *)k_ilu_blocks_window<3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)163840);
+        for (const void *k : {(const void *)k_ilu_blocks_window<2, false>, (const void *)k_ilu_blocks_window<3, false>,
+                              (const void *)k_ilu_blocks_window<2, true>})
+            (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)163840);
         configured = true;
+    }
+    if (ring) {  // (x may be y: a window's input rows are read before its solution is stored)
+        const size_t bytes = (size_t)(256 + WIN_RING + 64) * 8;
+        k_ilu_blocks_window<2, true><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol,
+                                                                            Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
+        return;
     }
     const size_t bytes = (size_t)(256 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
     if (depth == 3)
-        k_ilu_blocks_window<3><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval,
-                                                                      Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
+        k_ilu_blocks_window<3, false><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol,
+                                                                             Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
     else
-        k_ilu_blocks_window<2><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol, Lval,
-                                                                      Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
+        k_ilu_blocks_window<2, false><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol,
+                                                                             Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
 }
 
 // ======================================================= super-window sweep ==

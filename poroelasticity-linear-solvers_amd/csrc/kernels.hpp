@@ -257,11 +257,18 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
 int ilu_window_max_rows();
 int ilu_window_stream_pad();
 int ilu_window_max_entries();  // off-window entries per row the kernel handles
+// The ring variant (ring = true): blocks longer than LDS, up to
+// ilu_window_ring_max_rows() rows, y as the block solution and an LDS ring of
+// ilu_window_ring_rows() rows for the off-window terms -- no row may depend on
+// one more than ilu_window_ring_rows() - 64 rows away (the caller checks)
+int ilu_window_ring_rows();
+int64_t ilu_window_ring_max_rows();
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
                               const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,
-                              const double *x, double *y, int64_t max_len, hipStream_t st, int depth = 2);
-// (depth: windows of data in flight, 2 or 3; pls.window_depth)
+                              const double *x, double *y, int64_t max_len, hipStream_t st, int depth = 2,
+                              bool ring = false);
+// (depth: windows of data in flight, 2 or 3; pls.window_depth; the ring variant: 2)
 // The ring sweep (kernels.hip, k_ilu_blocks_ring): blocks of narrow levels whose
 // every level has <= ilu_ring_chunk() rows; per triangle chunk tables (coff per
 // block, cg first level, cp [start, end) positions), level orders ordL / ordU
@@ -300,7 +307,8 @@ void launch_dense_from_csr(int64_t n, int64_t ld, const int64_t *rp, const int32
                            hipStream_t st);
 // In place M := M^-1 by blocked Gauss-Jordan; D: 64 x 64 scratch; *fail |= 1 on
 // a zero pivot.  With u > 0 and P (n x 64 scratch) each tile column's pivots are
-// chosen over rows [64 k, n) by threshold partial pivoting (MUMPS CNTL(1) = u),
+// chosen over rows [64 k, n) by threshold partial pivoting (MUMPS CNTL(1) = u;
+// P then holds n x 64 + panel_fast_doubles(): the panel and the fast path's scratch),
 // the rows exchanged in M and rowperm (initialised to the identity): M := (Pi M)^-1;
 // stats[3] as launch_mf_panel_pivot.  u = 0: no pivoting (rounds 1-5).
 void launch_dense_invert(int64_t ld, double *M, double *D, int32_t *fail, hipStream_t st, int64_t n = 0,
@@ -351,10 +359,14 @@ void launch_mf_gj_step(int nf, const MFront *F, int max_ldt, int k, double *W, d
 // reference), rows exchanged in W and in rowperm + pst[f] (front-local original
 // row per position); P + soff[f]: (p + q) x 64 scratch.  stats: [0] rows
 // exchanged, [1] pivots below u x column max (MUMPS would delay them; dflag + pst[f]:
-// 1 at those columns), [2] zero columns.
+// 1 at those columns), [2] zero columns.  S (nf x panel_fast_doubles() scratch;
+// max_rows >= every front's p + q): the parallel fast path for panels that keep
+// every diagonal pivot (dense.hip k_panel_tile / k_panel_rows); the one-workgroup
+// panel runs only where it does not hold.
 void launch_mf_panel_pivot(int nf, const MFront *F, const int64_t *pst, const int64_t *soff, int k, double *W,
                            double *P, int32_t *rowperm, int32_t *stats, double u, hipStream_t st,
-                           int32_t *dflag = nullptr);
+                           int32_t *dflag = nullptr, double *S = nullptr, int64_t max_rows = 0);
+int panel_fast_doubles();
 // Persistent factors: rows [0, 64 pt) of the front (U part, ld wide) to U + uoff
 // and rows [64 pt, 64 pt + q) x columns [0, 64 pt) (X part) to X + xoff.
 struct MStore {

@@ -1234,6 +1234,14 @@ static int64_t window_max_entries(int64_t nblk, const std::vector<int64_t> &bst,
         }
     return kmax;
 }
+// Farthest dependency of a row in rows (|i - c| over the off-diagonal entries;
+// the ring variant's limit: ilu_window_ring_rows() - 64)
+static int64_t window_max_reach(int64_t n, const std::vector<int64_t> &rp, const std::vector<int32_t> &ci) {
+    int64_t r = 0;
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = rp[i]; k < rp[i + 1]; ++k) r = std::max<int64_t>(r, std::abs(i - (int64_t)ci[k]));
+    return r;
+}
 
 static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
                              const std::vector<int32_t> &ci, const std::vector<int64_t> &dg,
@@ -1774,8 +1782,42 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             swin = true;
             mark("super-window tables");
         }
+        auto build_windows = [&](const std::vector<int64_t> &bst) {
+            std::vector<double> fv(F.nnz);
+            if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
+            c.sync();
+            build_window_tri(nblocks, bst, rp, ci, dg, fv, false, Lw, c);
+            build_window_tri(nblocks, bst, rp, ci, dg, fv, true, Uw, c);
+            mark("window triangles");
+            std::vector<int64_t> wf(nblocks + 1, 0);
+            for (int64_t b = 0; b < nblocks; ++b) wf[b + 1] = wf[b] + (bst[b + 1] - bst[b] + 63) / 64;
+            wstart.alloc(nblocks + 1);
+            HIPCHK(hipMemcpyAsync(wstart.p, wf.data(), sizeof(int64_t) * (nblocks + 1), hipMemcpyHostToDevice, c.st));
+            c.sync();
+        };
+        const int64_t lev = (int64_t)gL.size() - 1 + (int64_t)gU.size() - 1;
+        auto window_count = [&](const std::vector<int64_t> &bst) {
+            int64_t nwin = 0;
+            for (int64_t b = 0; b < nblocks; ++b) nwin += 2 * ((bst[b + 1] - bst[b] + 63) / 64);
+            return nwin;
+        };
+        auto ring_fits = [&] {
+            return c.window_ring != 0 && blen <= ilu_window_ring_max_rows() &&
+                   window_max_reach(n, rp, ci) <= ilu_window_ring_rows() - 64;
+        };
+        // the window sweep's ring variant on blocks too long for LDS, where the
+        // levels outnumber the windows 2:1 (the classical AMG's np=8 hybrid
+        // Gauss-Seidel chunks beyond 20,160 rows: swelling N=160, footing N=80)
+        if (gmem && !swin && c.sweep_window != 0 && ring_fits()) {
+            const std::vector<int64_t> bst = block_starts(n, nblocks, bnd);
+            if ((c.sweep_window == 1 || lev >= 2 * window_count(bst)) &&
+                window_max_entries(nblocks, bst, rp, ci, dg) <= ilu_window_max_entries()) {
+                build_windows(bst);
+                window = window_ring = true;
+            }
+        }
         // the ring sweep: y-resident blocks whose every level fits one chunk
-        if (gmem && ring_mode != 0 && !swin) {
+        if (gmem && ring_mode != 0 && !swin && !window) {
             int64_t wmax = 0;
             for (const auto *g : {&gL, &gU})
                 for (size_t k = 0; k + 1 < g->size(); ++k) wmax = std::max<int64_t>(wmax, (*g)[k + 1] - (*g)[k]);
@@ -1792,7 +1834,6 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             const int64_t sL = build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oL, gL, fL, false, nullptr, c);
             const int64_t sU = sL < 0 ? -1 : build_chain_tri(nblocks, bst, rp, ci, dg, none, none, oU, gU, fU, true, nullptr, c);
             mark("chain plan");
-            const int64_t lev = (int64_t)gL.size() - 1 + (int64_t)gU.size() - 1;
             const bool deep = sL >= 0 && sU >= 0 && 2 * (sL + sU) <= 7 * lev;
             chain = c.sweep_chain != 0 && sL >= 0 && sU >= 0 && (c.sweep_chain == 1 || deep);
             // the window sweep where the chain would run (or forced): a block's
@@ -1803,25 +1844,14 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             // triangles) took 790 us per sweep in the workgroup sweep (~1.1 us per
             // level), 745 us in the chain sweep, ~250 us in the window sweep (~1.2 us
             // per window)
-            int64_t nwin = 0;
-            for (int64_t b = 0; b < nblocks; ++b) nwin += 2 * ((bst[b + 1] - bst[b] + 63) / 64);
-            const bool many_levels = lev >= 2 * nwin;
+            const bool many_levels = lev >= 2 * window_count(bst);
             window = (c.sweep_window == 1 || (c.sweep_window == -1 && c.sweep_chain != 1 && (deep || many_levels))) &&
                      blen <= ilu_window_max_rows() &&
                      window_max_entries(nblocks, bst, rp, ci, dg) <= ilu_window_max_entries();
             if (window) {
                 chain = false;
-                std::vector<double> fv(F.nnz);
-                if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
-                c.sync();
-                build_window_tri(nblocks, bst, rp, ci, dg, fv, false, Lw, c);
-                build_window_tri(nblocks, bst, rp, ci, dg, fv, true, Uw, c);
-                mark("window triangles");
-                std::vector<int64_t> wf(nblocks + 1, 0);
-                for (int64_t b = 0; b < nblocks; ++b) wf[b + 1] = wf[b] + (bst[b + 1] - bst[b] + 63) / 64;
-                wstart.alloc(nblocks + 1);
-                HIPCHK(hipMemcpyAsync(wstart.p, wf.data(), sizeof(int64_t) * (nblocks + 1), hipMemcpyHostToDevice, c.st));
-                c.sync();
+                build_windows(bst);
+                window_ring = c.window_ring == 1 && ring_fits();  // (forced: tests compare it with the LDS variant)
             }
             if (chain) {
                 std::vector<double> fv(F.nnz), dv(n);
@@ -1927,7 +1957,7 @@ const char *PCILU::sweep_kind() const {
     if (!use_lds) return csr_levels ? "levels-csr" : "levels";
     if (swin) return "swin";
     if (ring) return "ring";
-    if (window) return "window";
+    if (window) return window_ring ? "window-ring" : "window";
     if (chain) return "chain";
     return lds_gmem ? "gmem" : "lds";
 }
@@ -1956,7 +1986,7 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
     if (use_lds && window) {
         launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.col.p,
                                  Lw.val.p, Lw.tinv.p, Uw.woff.p, Uw.col.p, Uw.val.p, Uw.tinv.p, x, y, max_len, c.st,
-                                 c.window_depth);
+                                 c.window_depth, window_ring);
         return;
     }
     if (use_lds && chain) {
@@ -2029,7 +2059,7 @@ PCDenseLU::PCDenseLU(const DevCSR &M, Ctx &c, double u) {
         std::iota(id.begin(), id.end(), 0);
         rowperm.alloc(n);
         HIPCHK(hipMemcpyAsync(rowperm.p, id.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c.st));
-        P.alloc((size_t)n * 64);
+        P.alloc((size_t)n * 64 + panel_fast_doubles());
         st.alloc(3);
         HIPCHK(hipMemsetAsync(st.p, 0, sizeof(int32_t) * 3, c.st));
         c.sync();  // (id)
@@ -2339,6 +2369,7 @@ std::unique_ptr<Ctx> layout_ctx(const Ctx &c) {
     self->sweep_chain = c.sweep_chain;
     self->sweep_window = c.sweep_window;
     self->window_depth = c.window_depth;
+    self->window_ring = c.window_ring;
     self->amg_csr_below = c.amg_csr_below;
     return self;
 }

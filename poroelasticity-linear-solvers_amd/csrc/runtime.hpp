@@ -87,6 +87,8 @@ struct Ctx {
     int ilu0_stage_cap = -1;      // test knob (pls.ilu0_stage): staged entries of the ILU(0) factorization, -1 default
     int ilu_dep_grid = 0;         // test knob (pls.ilu_dep_grid): k_ilu0_dep's persistent grid capped (0: none)
     int window_depth = 2;         // window sweep: windows of data in flight, 2 or 3 (pls.window_depth)
+    int window_ring = -1;         // ... its ring variant for blocks longer than LDS (pls.window_ring: -1 where the
+                                  // window sweep's level test holds, 0 off, 1 also forced on LDS-resident blocks)
     int sweep_swin = 0;           // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin, experimental,
                                   // measured slower than the ring sweep): 0 never (default, capi), -1 where the ring
                                   // sweep would run, 1 whenever the block is y-resident
@@ -387,6 +389,7 @@ struct PCILU : PC {
     // window sweep (Ctx::sweep_window): LDS-resident blocks in 64-row windows with
     // explicit inverses of the windows' triangles (one GEMV per window)
     bool window = false;
+    bool window_ring = false;  // (the ring variant: y-resident, an LDS ring of the recent rows)
     WinTri Lw, Uw;
     DBuf<int64_t> wstart;  // per block: its first window
     // chain sweep (Ctx::sweep_chain): LDS-resident blocks of deep, narrow level DAGs

@@ -386,7 +386,10 @@ struct PCSparseLU : PC {
                     pscr += (p[f] > 1 || (p[f] == 1 && q[f] > 0) ? p[f] + q[f] : 0) * 64;
                 }
                 DBuf<int64_t> dpst(hpst.size()), dsoff(hsoff.size());
-                DBuf<double> Pscr(u > 0.0 ? std::max<int64_t>(pscr, 1) : 1);
+                int64_t max_pq = 0;
+                for (size_t t = c0; t < c1; ++t) max_pq = std::max<int64_t>(max_pq, p[fl[t]] + q[fl[t]]);
+                // (then the panels' fast-path scratch, one per front)
+                DBuf<double> Pscr(u > 0.0 ? pscr + (int64_t)(c1 - c0) * panel_fast_doubles() : 1);
                 HIPCHK(hipMemcpyAsync(dpst.p, hpst.data(), sizeof(int64_t) * hpst.size(), hipMemcpyHostToDevice, c.st));
                 HIPCHK(hipMemcpyAsync(dsoff.p, hsoff.data(), sizeof(int64_t) * hsoff.size(), hipMemcpyHostToDevice,
                                       c.st));
@@ -425,7 +428,7 @@ struct PCSparseLU : PC {
                 }
                 for (int k = 0; k < max_pt; ++k) {
                     launch_mf_panel_pivot((int)hf.size(), dF.p, dpst.p, dsoff.p, k, Wcur, Pscr.p, drowp.p, pstats.p, u,
-                                          c.st, dflag.p);
+                                          c.st, dflag.p, u > 0.0 ? Pscr.p + pscr : nullptr, max_pq);
                     launch_mf_gj_step((int)hf.size(), dF.p, max_ldt, k, Wcur, Dt.p, fail.p, tau, c.st);
                 }
                 launch_mf_store((int)hf.size(), dF.p, dS.p, max_rows, Wcur, U.p, X.p, c.st);

@@ -96,6 +96,56 @@ def test_window_sweep_long_block_matches_workgroup_sweep(gpu, capfd):
     assert np.max(np.abs(yw - yl)) <= 1e-12 * scale
 
 
+def _sweeps(err):
+    return [ln for ln in err.splitlines() if ln.startswith("[pls ilu]")]
+
+
+def test_window_ring_matches_window_sweep(gpu, capfd):
+    """The window sweep's ring variant (blocks longer than LDS: y as the block
+    solution, an LDS ring of the last 16,384 rows for the off-window terms,
+    input rows prefetched from global memory with the window's data) forced on
+    the LDS-resident blocks above: the same sums in the same order, so bitwise
+    the LDS variant."""
+    A, is_s, is_f, is_p = _system()
+    x = np.random.default_rng(3).standard_normal(A.shape[0])
+    capfd.readouterr()
+    yw = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "1"})
+    assert not any("window-ring" in ln for ln in _sweeps(capfd.readouterr().err))
+    yr = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "1", "pls.window_ring": "1"})
+    lines = _sweeps(capfd.readouterr().err)
+    assert any("n 19880 " in ln and "sweep window-ring" in ln for ln in lines), lines
+    assert np.array_equal(yr, yw)
+
+
+def test_window_ring_long_block(gpu, capfd):
+    """A 36,000-row block (563 windows, beyond the 20,160-row LDS window): the
+    ring variant against the oracle and against the one-workgroup GMEM sweep
+    that ran there before (1e-12: the window inverses reassociate the sums)."""
+    rng = np.random.default_rng(5)
+    Ks = _grid_block(200, 180, rng)
+    Kf = _grid_block(40, 40, rng)
+    Kp = _grid_block(30, 30, rng)
+    ns, nf, npr = Ks.shape[0], Kf.shape[0], Kp.shape[0]
+    A = sp.block_diag([Ks, Kf, Kp], format="csr")
+    A.sort_indices()
+    is_s = np.arange(ns, dtype=np.int32)
+    is_f = np.arange(ns, ns + nf, dtype=np.int32)
+    is_p = np.arange(ns + nf, ns + nf + npr, dtype=np.int32)
+    x = np.random.default_rng(4).standard_normal(A.shape[0])
+    capfd.readouterr()
+    yr = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "1"})
+    lines = _sweeps(capfd.readouterr().err)
+    assert any("n 36000 " in ln and "sweep window-ring" in ln for ln in lines), lines
+    yg = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "0", "pls.window_ring": "0"})
+    lines = _sweeps(capfd.readouterr().err)
+    assert any("n 36000 " in ln and "window" not in ln for ln in lines), lines
+    o = OracleSolver(A, A, None, is_s, is_f, is_p, PARAMS, {k: v for k, v in DB.items() if not k.startswith("pls.")}, [])
+    yo = o.block_pc.apply(x)
+    scale = np.max(np.abs(yo))
+    assert np.max(np.abs(yr - yo)) <= 1e-12 * scale
+    assert np.max(np.abs(yg - yo)) <= 1e-13 * scale
+
+
 @pytest.mark.parametrize("N,blocks,variant", [
     (16, 24, {}),
     (16, 24, {"pls.fp_pipeline_depth": "6"}),
