@@ -561,6 +561,7 @@ struct Handle {
         ctx.window_depth = (int)opt.integer("pls.window_depth", 2);
         if (ctx.window_depth != 2 && ctx.window_depth != 3) throw Error("pls.window_depth must be 2 or 3");
         ctx.window_ring = (int)opt.integer("pls.window_ring", -1);
+        ctx.window_mixed = (int)opt.integer("pls.window_mixed", -1);
         ctx.sweep_swin = (int)opt.integer("pls.sweep_swin", 0);
         ctx.amg_csr_below = opt.num("pls.amg_csr_below", 16.0);
         if (opt.flag("pls.debug_bounds", false) || opt.integer("pls.debug_partial_cap", 0) > 0)

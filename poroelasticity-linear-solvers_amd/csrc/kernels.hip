@@ -3505,6 +3505,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     for (int j = 0; j < R; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the offsets (ordinary loads) before the counted ones
     const auto rin = win_rsrc(in, RING ? len * 8 : 0), rout = win_rsrc(out, RING ? len * 8 : 0);
+    const int probe = RING ? __builtin_amdgcn_readfirstlane(ring_probe) : 0;
     auto wi = [&](int64_t ww) { return UP ? nw - 1 - ww : ww; };
     // T^-1[k][lane] is zero above (L) / below (U) the diagonal: those lanes read out of range
     auto toff = [&](int k) { return (UP ? k >= lane : k <= lane) ? (k * 64 + lane) * 8 : 0x40000000; };
@@ -3514,9 +3515,10 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         const int64_t ok = ww < nw ? 1 : 0;
         const int64_t w = wi(ww < nw ? ww : 0);
         const int64_t s0 = wo.at(w), s1 = wo.at(w + 1);
-        const auto rt = win_rsrc(tinv + (w0 + w) * 4096, ok * 32768);
-        const auto rc = win_rsrc(col + s0, ok * (s1 - s0) * 4);
-        const auto rv = win_rsrc(val + s0, ok * (s1 - s0) * 8);
+        // (pls.ring_probe 8192: no inverse loads, 16384: no stream loads -- ring variant, timing only)
+        const auto rt = win_rsrc(tinv + (w0 + w) * 4096, (probe & 8192) ? 0 : ok * 32768);
+        const auto rc = win_rsrc(col + s0, (probe & 16384) ? 0 : ok * (s1 - s0) * 4);
+        const auto rv = win_rsrc(val + s0, (probe & 16384) ? 0 : ok * (s1 - s0) * 8);
 #pragma unroll
         for (int u = 0; u < WIN_KPW; ++u) {
             B.sc[u] = win_ld32(rc, sk(u) * 4);
@@ -3557,16 +3559,20 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
             // every wave stores the window (the same values): one counted store per
             // wave and window, issued after the window's loads
             ys[act ? (r & RM) : WIN_RING + lane] = yr;
-            win_st64(rout, act ? (int)(r * 8) : 0x40000000, yr);
+            // (pls.ring_probe 2048: no store, 4096: stores out of range -- timing only, wrong results)
+            if (!(probe & 2048)) win_st64(rout, act && !(probe & 4096) ? (int)(r * 8) : 0x40000000, yr);
         } else {
             ys[act ? r : len + lane] = yr;  // every wave writes the same value (its own later reads see it)
         }
         __syncthreads();  // part[] free for the next window
+        // (measured: double-buffering part[] to drop this barrier and the one above
+        // was no faster -- 1,612 against 1,531 us per swelling N=160 chunk sweep)
     };
-    if (WD == 3 && !RING) {
+    if (WD == 3) {
         // three windows of data in flight: the oldest window's NL loads are
-        // followed by 2 x NL >= 64 younger ones, more than vmcnt counts (63);
-        // waiting for <= 63 outstanding waits for one load of the next window too
+        // followed by 2 x NL >= 64 younger ones (and the ring's stores), more than
+        // vmcnt counts (63); waiting for <= 63 outstanding waits for a few loads of
+        // the next window too
         static_assert(2 * NL >= 63, "vmcnt(63) must cover the oldest window");
         WinBuf A, B, C;
         issue(0, A);
@@ -3611,7 +3617,7 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
                                                            const double *__restrict__ Lval, const double *__restrict__ Ltinv,
                                                            const int64_t *__restrict__ Uwoff, const int32_t *__restrict__ Ucol,
                                                            const double *__restrict__ Uval, const double *__restrict__ Utinv,
-                                                           const double *x, double *y) {
+                                                           const double *x, double *y, int tri) {
     // one dynamic LDS array: the partial sums (4 x 64), then the block solution
     extern __shared__ __attribute__((aligned(16))) double lds_win[];
     double *part = lds_win, *ys = lds_win + 256;
@@ -3637,9 +3643,10 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
         // L: x -> y (global and the ring); U: y -> y in place, its input rows read
         // from global memory after every wave's L stores completed (win_sweep ends
         // with vmcnt(0); the barrier orders them before U's first loads)
-        win_sweep<false, 2, true>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q, x + b0, y + b0);
+        // (tri: 1 L, 2 U -- y already holds L's solution, the ring then only U's rows -- 3 both)
+        if (tri & 1) win_sweep<false, WD, true>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q, x + b0, y + b0);
         __syncthreads();
-        win_sweep<true, 2, true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q, y + b0, y + b0);
+        if (tri & 2) win_sweep<true, WD, true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q, y + b0, y + b0);
         return;
     }
     win_sweep<false, WD>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q);
@@ -3659,27 +3666,32 @@ int ilu_window_max_entries() { return WIN_KP; }
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
                               const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,
-                              const double *x, double *y, int64_t max_len, hipStream_t st, int depth, bool ring) {
+                              const double *x, double *y, int64_t max_len, hipStream_t st, int depth, bool ring,
+                              int tri) {
     static bool configured = false;
     if (!configured) {
         for (const void *k : {(const void *)k_ilu_blocks_window<2, false>, (const void *)k_ilu_blocks_window<3, false>,
-                              (const void *)k_ilu_blocks_window<2, true>})
+                              (const void *)k_ilu_blocks_window<2, true>, (const void *)k_ilu_blocks_window<3, true>})
             (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)163840);
         configured = true;
     }
     if (ring) {  // (x may be y: a window's input rows are read before its solution is stored)
         const size_t bytes = (size_t)(256 + WIN_RING + 64) * 8;
-        k_ilu_blocks_window<2, true><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol,
-                                                                            Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
+        if (depth == 3)
+            k_ilu_blocks_window<3, true><<<(unsigned)nblocks, 256, bytes, st>>>(
+                n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y, tri);
+        else
+            k_ilu_blocks_window<2, true><<<(unsigned)nblocks, 256, bytes, st>>>(
+                n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y, tri);
         return;
     }
     const size_t bytes = (size_t)(256 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
     if (depth == 3)
         k_ilu_blocks_window<3, false><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol,
-                                                                             Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
+                                                                             Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y, 3);
     else
         k_ilu_blocks_window<2, false><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol,
-                                                                             Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y);
+                                                                             Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y, 3);
 }
 
 // ======================================================= super-window sweep ==

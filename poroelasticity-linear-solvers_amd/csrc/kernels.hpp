@@ -267,8 +267,9 @@ void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart,
                               const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
                               const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,
                               const double *x, double *y, int64_t max_len, hipStream_t st, int depth = 2,
-                              bool ring = false);
-// (depth: windows of data in flight, 2 or 3; pls.window_depth; the ring variant: 2)
+                              bool ring = false, int tri = 3);
+// (depth: windows of data in flight, 2 or 3; pls.window_depth;
+// tri (ring variant): 1 the L sweep, 2 the U sweep on y (holding L's solution), 3 both)
 // The ring sweep (kernels.hip, k_ilu_blocks_ring): blocks of narrow levels whose
 // every level has <= ilu_ring_chunk() rows; per triangle chunk tables (coff per
 // block, cg first level, cp [start, end) positions), level orders ordL / ordU

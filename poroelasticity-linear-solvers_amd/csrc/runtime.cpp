@@ -1805,15 +1805,39 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             return c.window_ring != 0 && blen <= ilu_window_ring_max_rows() &&
                    window_max_reach(n, rp, ci) <= ilu_window_ring_rows() - 64;
         };
-        // the window sweep's ring variant on blocks too long for LDS, where the
-        // levels outnumber the windows 2:1 (the classical AMG's np=8 hybrid
-        // Gauss-Seidel chunks beyond 20,160 rows: swelling N=160, footing N=80)
+        // the window sweep's ring variant on blocks too long for LDS (the classical
+        // AMG's np=8 hybrid Gauss-Seidel chunks beyond 20,160 rows: swelling N=160,
+        // footing N=80), optionally with the L triangle by levels (the y-resident
+        // workgroup sweep; pls.window_mixed).  Cost model, a level ~ a window
+        // (measured ~2.4 and ~1.9 us on those chunks): both triangles by levels (the
+        // ring sweep) levL + levU, both by windows 2 nw, mixed levL + nw; windows
+        // where they save a fifth.  Swelling N=160 (per chunk): L 110 levels, U 666,
+        // 403 windows per triangle -- mixed; footing N=80: L 154, U 1,034, 467.
         if (gmem && !swin && c.sweep_window != 0 && ring_fits()) {
             const std::vector<int64_t> bst = block_starts(n, nblocks, bnd);
-            if ((c.sweep_window == 1 || lev >= 2 * window_count(bst)) &&
+            const int64_t nw = window_count(bst) / 2, levL = (int64_t)gL.size() - 1;
+            const int64_t cost_lev = lev, cost_win = 2 * nw, cost_mix = levL + nw;
+            const bool mix = c.window_mixed == 1 || (c.window_mixed == -1 && cost_mix < cost_win);
+            if ((c.sweep_window == 1 || 5 * (mix ? cost_mix : cost_win) <= 4 * cost_lev) &&
                 window_max_entries(nblocks, bst, rp, ci, dg) <= ilu_window_max_entries()) {
                 build_windows(bst);
                 window = window_ring = true;
+                if (mix) {
+                    build_lds_tri(*this, n, nblocks, force_lpr, 16, rp, dg, oL, gL, fL, false, Ls, c, nullptr, nullptr,
+                                  nullptr, &block_maxsl_h);
+                    int64_t wmax = 1;
+                    for (size_t k = 0; k + 1 < gL.size(); ++k) wmax = std::max<int64_t>(wmax, gL[k + 1] - gL[k]);
+                    std::vector<int32_t> hl(nblocks);
+                    HIPCHK(hipMemcpyAsync(hl.data(), Ls.lpr.p, sizeof(int32_t) * nblocks, hipMemcpyDeviceToHost, c.st));
+                    c.sync();
+                    int lmax = 1;
+                    for (int64_t b = 0; b < nblocks; ++b) lmax = std::max(lmax, hl[b]);
+                    const int64_t slices = (wmax * lmax + 63) / 64;
+                    lds_tpb = slices <= 1 ? 64 : slices <= 4 ? 256 : 1024;
+                    zgoff.alloc(nblocks + 1);
+                    HIPCHK(hipMemsetAsync(zgoff.p, 0, sizeof(int64_t) * (nblocks + 1), c.st));
+                    window_mixed = true;
+                }
             }
         }
         // the ring sweep: y-resident blocks whose every level fits one chunk
@@ -1957,7 +1981,7 @@ const char *PCILU::sweep_kind() const {
     if (!use_lds) return csr_levels ? "levels-csr" : "levels";
     if (swin) return "swin";
     if (ring) return "ring";
-    if (window) return window_ring ? "window-ring" : "window";
+    if (window) return window_mixed ? "levels+window-ring" : window_ring ? "window-ring" : "window";
     if (chain) return "chain";
     return lds_gmem ? "gmem" : "lds";
 }
@@ -1981,6 +2005,15 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
                                Ur.coff.p, Ur.cg.p, Ur.cp.p, Lr.ord.p, mapUL.p, Ur.ord.p, Lr.frp.p, Lr.fcol.p,
                                Lr.fval.p, Ur.frp.p, Ur.fcol.p, Ur.fval.p, x, y, sc.first.p, sc.second.p, c.st,
                                lds_tpb, bstart_h.empty() ? nullptr : bstart.p);
+        return;
+    }
+    if (use_lds && window && window_mixed) {  // L: the y-resident level sweep; U: the ring windows
+        launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, zgoff.p,
+                              Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, x, y, c.st, nullptr, true, lds_tpb,
+                              0, bstart_h.empty() ? nullptr : bstart.p, max_len, -1, -1, 2);
+        launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.col.p,
+                                 Lw.val.p, Lw.tinv.p, Uw.woff.p, Uw.col.p, Uw.val.p, Uw.tinv.p, y, y, max_len, c.st,
+                                 c.window_depth, true, 2);
         return;
     }
     if (use_lds && window) {
@@ -2370,6 +2403,7 @@ std::unique_ptr<Ctx> layout_ctx(const Ctx &c) {
     self->sweep_window = c.sweep_window;
     self->window_depth = c.window_depth;
     self->window_ring = c.window_ring;
+    self->window_mixed = c.window_mixed;
     self->amg_csr_below = c.amg_csr_below;
     return self;
 }

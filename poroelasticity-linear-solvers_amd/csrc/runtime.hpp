@@ -89,6 +89,8 @@ struct Ctx {
     int window_depth = 2;         // window sweep: windows of data in flight, 2 or 3 (pls.window_depth)
     int window_ring = -1;         // ... its ring variant for blocks longer than LDS (pls.window_ring: -1 where the
                                   // window sweep's level test holds, 0 off, 1 also forced on LDS-resident blocks)
+    int window_mixed = -1;        // ... its L triangle by levels (pls.window_mixed: -1 where L has no more levels
+                                  // than windows, 0 off, 1 forced)
     int sweep_swin = 0;           // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin, experimental,
                                   // measured slower than the ring sweep): 0 never (default, capi), -1 where the ring
                                   // sweep would run, 1 whenever the block is y-resident
@@ -390,6 +392,8 @@ struct PCILU : PC {
     // explicit inverses of the windows' triangles (one GEMV per window)
     bool window = false;
     bool window_ring = false;  // (the ring variant: y-resident, an LDS ring of the recent rows)
+    bool window_mixed = false; // (ring variant: L by the y-resident level sweep, U by windows)
+    DBuf<int64_t> zgoff;       // (no levels: the mixed sweep's empty U for the level launch)
     WinTri Lw, Uw;
     DBuf<int64_t> wstart;  // per block: its first window
     // chain sweep (Ctx::sweep_chain): LDS-resident blocks of deep, narrow level DAGs

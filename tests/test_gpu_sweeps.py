@@ -100,27 +100,31 @@ def _sweeps(err):
     return [ln for ln in err.splitlines() if ln.startswith("[pls ilu]")]
 
 
-def test_window_ring_matches_window_sweep(gpu, capfd):
+@pytest.mark.parametrize("depth", ["2", "3"])
+def test_window_ring_matches_window_sweep(gpu, capfd, depth):
     """The window sweep's ring variant (blocks longer than LDS: y as the block
     solution, an LDS ring of the last 16,384 rows for the off-window terms,
     input rows prefetched from global memory with the window's data) forced on
-    the LDS-resident blocks above: the same sums in the same order, so bitwise
-    the LDS variant."""
+    the LDS-resident blocks above, with 2 or 3 windows of data in flight: the
+    same sums in the same order, so bitwise the LDS variant."""
     A, is_s, is_f, is_p = _system()
     x = np.random.default_rng(3).standard_normal(A.shape[0])
     capfd.readouterr()
     yw = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "1"})
     assert not any("window-ring" in ln for ln in _sweeps(capfd.readouterr().err))
-    yr = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "1", "pls.window_ring": "1"})
+    yr = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "1", "pls.window_ring": "1", "pls.window_depth": depth})
     lines = _sweeps(capfd.readouterr().err)
     assert any("n 19880 " in ln and "sweep window-ring" in ln for ln in lines), lines
     assert np.array_equal(yr, yw)
 
 
-def test_window_ring_long_block(gpu, capfd):
+@pytest.mark.parametrize("mixed", ["0", "1"])
+def test_window_ring_long_block(gpu, capfd, mixed):
     """A 36,000-row block (563 windows, beyond the 20,160-row LDS window): the
-    ring variant against the oracle and against the one-workgroup GMEM sweep
-    that ran there before (1e-12: the window inverses reassociate the sums)."""
+    ring variant -- both triangles in windows, or (mixed) L by the y-resident
+    level sweep and U in windows -- against the oracle and against the
+    one-workgroup GMEM sweep that ran there before (1e-12: the window inverses
+    reassociate the sums)."""
     rng = np.random.default_rng(5)
     Ks = _grid_block(200, 180, rng)
     Kf = _grid_block(40, 40, rng)
@@ -133,9 +137,10 @@ def test_window_ring_long_block(gpu, capfd):
     is_p = np.arange(ns + nf, ns + nf + npr, dtype=np.int32)
     x = np.random.default_rng(4).standard_normal(A.shape[0])
     capfd.readouterr()
-    yr = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "1"})
+    yr = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "1", "pls.window_mixed": mixed})
     lines = _sweeps(capfd.readouterr().err)
-    assert any("n 36000 " in ln and "sweep window-ring" in ln for ln in lines), lines
+    kind = "sweep levels+window-ring" if mixed == "1" else "sweep window-ring"
+    assert any("n 36000 " in ln and kind in ln for ln in lines), lines
     yg = _apply(A, is_s, is_f, is_p, x, {"pls.sweep_window": "0", "pls.window_ring": "0"})
     lines = _sweeps(capfd.readouterr().err)
     assert any("n 36000 " in ln and "window" not in ln for ln in lines), lines
