@@ -544,7 +544,7 @@ struct Handle {
         set_d16_xcd((int)opt.integer("pls.d16_xcd", 0));  // process-wide (tuning)
         set_spmv_short_rows(opt.flag("pls.spmv_short", false));  // process-wide (measured slower for the AMG's P)
         if (opt.integer("pls.ilu0_probe", 0)) set_ilu0_probe((int)opt.integer("pls.ilu0_probe", 0));  // diagnostics
-        if (opt.integer("pls.ring_probe", 0)) set_ring_probe((int)opt.integer("pls.ring_probe", 0));  // diagnostics
+        set_ring_probe((int)opt.integer("pls.ring_probe", 0));  // diagnostics (every handle: its own setting)
         ctx.d16_sigma = (int)opt.integer("pls.d16_sigma", 1024);
         if (ctx.d16_sigma < 0 || ctx.d16_sigma % 64) throw Error("pls.d16_sigma must be a multiple of 64 (0: off)");
         ctx.d16_sigma_pad = opt.num("pls.d16_sigma_pad", 0.15);
@@ -562,6 +562,7 @@ struct Handle {
         if (ctx.window_depth != 2 && ctx.window_depth != 3) throw Error("pls.window_depth must be 2 or 3");
         ctx.window_ring = (int)opt.integer("pls.window_ring", -1);
         ctx.window_mixed = (int)opt.integer("pls.window_mixed", -1);
+        ctx.window_kpw = (int)opt.integer("pls.window_kpw", 0);
         ctx.sweep_swin = (int)opt.integer("pls.sweep_swin", 0);
         ctx.amg_csr_below = opt.num("pls.amg_csr_below", 16.0);
         if (opt.flag("pls.debug_bounds", false) || opt.integer("pls.debug_partial_cap", 0) > 0)

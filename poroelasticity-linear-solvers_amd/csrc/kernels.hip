@@ -3450,40 +3450,46 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t win_rsrc(const void *base, int
                                              __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
 
+typedef double win_d2 __attribute__((ext_vector_type(2)));
+template <int KPW>
 struct WinBuf {  // one wave's share of a window's data in registers
-    double tv[16], sv[WIN_KPW];
-    int32_t sc[WIN_KPW];
-    double rx;  // (ring variant) the window's input rows, from global memory
+    win_d2 tv[8];     // T^-1 columns 16 q + 2 j, + 1 of the lane's row
+    win_d2 sr[KPW];   // stream records: value, column (low word of .y)
+    double rx;            // (ring variant) the window's input rows, from global memory
 };
 
-// Range-checked buffer loads issued through inline asm: the compiler does not
-// track them, so it cannot drain them at the loop header (its waits for
-// loop-carried loads were vmcnt(0)); the sweep counts them itself -- every
+// Range-checked 16-byte buffer loads issued through inline asm: the compiler
+// does not track them, so it cannot drain them at the loop header (its waits
+// for loop-carried loads were vmcnt(0)); the sweep counts them itself -- every
 // window issues WIN_LOADS of them -- and win_wait ties the registers to the
-// wait (no use or copy can move above it).
-static constexpr int WIN_LOADS = 16 + 2 * WIN_KPW;
-template <bool RING>
-constexpr int win_loads() { return WIN_LOADS + (RING ? 1 : 0); }
+// wait (no use or copy can move above it).  (Round 6: 8-byte loads, two per
+// stream entry, were 33 instructions per wave and window, and the load
+// instructions -- not their bytes: out-of-range or exec-masked lanes cost the
+// same -- took ~1.1 of the ~1.9 us per window on the swelling N = 160 chunks.)
+// (KPW: stream records per wave and window -- 4 where no row has more than 16
+// off-window entries, else WIN_KPW)
+template <bool RING, int KPW>
+constexpr int win_loads() { return 8 + KPW + (RING ? 1 : 0); }
 __device__ __forceinline__ double win_ld64(__amdgpu_buffer_rsrc_t r, int off) {
     double v;
     asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
     return v;
 }
-__device__ __forceinline__ int32_t win_ld32(__amdgpu_buffer_rsrc_t r, int off) {
-    int32_t v;
-    asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+__device__ __forceinline__ win_d2 win_ld128(__amdgpu_buffer_rsrc_t r, int off) {
+    win_d2 v;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
     return v;
 }
 __device__ __forceinline__ void win_st64(__amdgpu_buffer_rsrc_t r, int off, double v) {
     asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen" ::"v"(v), "v"(off), "s"(r) : "memory");
 }
-template <int N, bool RING = false>
-__device__ __forceinline__ void win_wait(WinBuf &B) {  // vmcnt(N), B's registers pinned to it
+template <int N, bool RING, int KPW>
+__device__ __forceinline__ void win_wait(WinBuf<KPW> &B) {  // vmcnt(N), B's registers pinned to it
     asm volatile("s_waitcnt vmcnt(%c0)" ::"n"(N) : "memory");
 #pragma unroll
-    for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(B.tv[k]));
+    for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(B.tv[k]));
 #pragma unroll
-    for (int u = 0; u < WIN_KPW; ++u) asm volatile("" : "+v"(B.sv[u]), "+v"(B.sc[u]));
+    for (int u = 0; u < KPW; ++u) asm volatile("" : "+v"(B.sr[u]));
     if (RING) asm volatile("" : "+v"(B.rx));
 }
 
@@ -3491,12 +3497,12 @@ __device__ __forceinline__ void win_wait(WinBuf &B) {  // vmcnt(N), B's register
 // checks that no row depends on one more than WIN_RING - 64 rows away), the
 // window's input rows come from global memory (in, prefetched with the window's
 // data) and its solution goes to global memory (out) as well as to the ring
-template <bool UP, int WD = 2, bool RING = false>
+template <bool UP, int WD, bool RING, int KPW>
 __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t *__restrict__ woff,
-                                          const int32_t *__restrict__ col, const double *__restrict__ val,
-                                          const double *__restrict__ tinv, double *ys, double *part, int lane,
-                                          int q, const double *in = nullptr, double *out = nullptr) {
-    constexpr int R = RING ? WIN_OFFR_RING : WIN_OFFR, NL = win_loads<RING>();
+                                          const double *__restrict__ rec, const double *__restrict__ tinv, double *ys,
+                                          double *part, int lane, int q, const double *in = nullptr,
+                                          double *out = nullptr) {
+    constexpr int R = RING ? WIN_OFFR_RING : WIN_OFFR, NL = win_loads<RING, KPW>();
     constexpr int64_t RM = WIN_RING - 1;
     const int64_t nw = (len + 63) >> 6;
     if (nw == 0) return;
@@ -3505,40 +3511,44 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     for (int j = 0; j < R; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the offsets (ordinary loads) before the counted ones
     const auto rin = win_rsrc(in, RING ? len * 8 : 0), rout = win_rsrc(out, RING ? len * 8 : 0);
+    // (pls.ring_probe, ring variant, timing only -- results wrong: 2048 no stores,
+    // 32768 no loads after the first two windows)
     const int probe = RING ? __builtin_amdgcn_readfirstlane(ring_probe) : 0;
     auto wi = [&](int64_t ww) { return UP ? nw - 1 - ww : ww; };
-    // T^-1[k][lane] is zero above (L) / below (U) the diagonal: those lanes read out of range
-    auto toff = [&](int k) { return (UP ? k >= lane : k <= lane) ? (k * 64 + lane) * 8 : 0x40000000; };
+    // T^-1[lane][k], T^-1[lane][k + 1] (k even): both zero above (L) / below (U)
+    // the diagonal -- those lanes read out of range
+    auto toff = [&](int k) {
+        return (UP ? k + 1 >= lane : k <= lane) ? (k >> 1) * 1024 + lane * 16 : 0x40000000;
+    };
     auto sk = [&](int u) { return (u * WIN_NW + q) * 64 + lane; };  // this wave's u-th stream slot
-    // every window's loads, WIN_LOADS in one fixed order (past the block: 0 bytes in range, no traffic)
-    auto issue = [&](int64_t ww, WinBuf &B) {
+    // every window's loads, NL in one fixed order (past the block: 0 bytes in range, no traffic)
+    auto issue = [&](int64_t ww, WinBuf<KPW> &B) {
+        if ((probe & 32768) && ww >= 2) return;
         const int64_t ok = ww < nw ? 1 : 0;
         const int64_t w = wi(ww < nw ? ww : 0);
         const int64_t s0 = wo.at(w), s1 = wo.at(w + 1);
-        // (pls.ring_probe 8192: no inverse loads, 16384: no stream loads -- ring variant, timing only)
-        const auto rt = win_rsrc(tinv + (w0 + w) * 4096, (probe & 8192) ? 0 : ok * 32768);
-        const auto rc = win_rsrc(col + s0, (probe & 16384) ? 0 : ok * (s1 - s0) * 4);
-        const auto rv = win_rsrc(val + s0, (probe & 16384) ? 0 : ok * (s1 - s0) * 8);
+        const auto rt = win_rsrc(tinv + (w0 + w) * 4096, ok * 32768);
+        const auto rs = win_rsrc(rec + 2 * s0, ok * (s1 - s0) * 16);
 #pragma unroll
-        for (int u = 0; u < WIN_KPW; ++u) {
-            B.sc[u] = win_ld32(rc, sk(u) * 4);
-            B.sv[u] = win_ld64(rv, sk(u) * 8);
-        }
+        for (int u = 0; u < KPW; ++u) B.sr[u] = win_ld128(rs, sk(u) * 16);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) B.tv[k] = win_ld64(rt, toff(16 * q + k));
+        for (int j = 0; j < 8; ++j) B.tv[j] = win_ld128(rt, toff(16 * q + 2 * j));
         if (RING) B.rx = win_ld64(rin, (int)(ok * (w * 64 + lane) * 8 + (1 - ok) * 0x40000000));
     };
     // one window, branch-free (a window past the block computes zeros into a dummy slot)
-    auto compute = [&](int64_t ww, const WinBuf &B) {
+    auto compute = [&](int64_t ww, const WinBuf<KPW> &B) {
         const int64_t w = wi(ww < nw ? ww : 0);
         const int64_t r = w * 64 + lane;
         const bool act = ww < nw && r < len;
-        double d[WIN_KPW];
+        double d[KPW];
 #pragma unroll
-        for (int u = 0; u < WIN_KPW; ++u) d[u] = ys[RING ? (B.sc[u] & RM) : B.sc[u]];
+        for (int u = 0; u < KPW; ++u) {
+            const int32_t c = __double2loint(B.sr[u].y);
+            d[u] = ys[RING ? (c & RM) : c];
+        }
         double acc = 0.0;
 #pragma unroll
-        for (int u = 0; u < WIN_KPW; ++u) acc += __dmul_rn(B.sv[u], d[u]);
+        for (int u = 0; u < KPW; ++u) acc += __dmul_rn(B.sr[u].x, d[u]);
         part[q * 64 + lane] = acc;
         __syncthreads();
         const double rhs = RING ? B.rx : ys[act ? r : 0];
@@ -3549,7 +3559,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         for (int k = 0; k < 16; ++k) {
             const int kk = 16 * q + k;
             const double tk = __hiloint2double(__builtin_amdgcn_readlane(thi, kk), __builtin_amdgcn_readlane(tlo, kk));
-            out += __dmul_rn(B.tv[k], tk);
+            out += __dmul_rn((k & 1) ? B.tv[k >> 1].y : B.tv[k >> 1].x, tk);
         }
         __syncthreads();  // every wave has read part[] (t) before it is overwritten
         part[q * 64 + lane] = out;
@@ -3559,8 +3569,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
             // every wave stores the window (the same values): one counted store per
             // wave and window, issued after the window's loads
             ys[act ? (r & RM) : WIN_RING + lane] = yr;
-            // (pls.ring_probe 2048: no store, 4096: stores out of range -- timing only, wrong results)
-            if (!(probe & 2048)) win_st64(rout, act && !(probe & 4096) ? (int)(r * 8) : 0x40000000, yr);
+            if (!(probe & 2048)) win_st64(rout, act ? (int)(r * 8) : 0x40000000, yr);
         } else {
             ys[act ? r : len + lane] = yr;  // every wave writes the same value (its own later reads see it)
         }
@@ -3568,24 +3577,22 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         // (measured: double-buffering part[] to drop this barrier and the one above
         // was no faster -- 1,612 against 1,531 us per swelling N=160 chunk sweep)
     };
-    if (WD == 3) {
-        // three windows of data in flight: the oldest window's NL loads are
-        // followed by 2 x NL >= 64 younger ones (and the ring's stores), more than
-        // vmcnt counts (63); waiting for <= 63 outstanding waits for a few loads of
-        // the next window too
-        static_assert(2 * NL >= 63, "vmcnt(63) must cover the oldest window");
-        WinBuf A, B, C;
+    if (WD == 3 && !RING) {
+        // three windows of data in flight: the oldest window's loads are followed
+        // by exactly 2 NL younger ones
+        static_assert(2 * NL <= 63, "vmcnt counts 63");
+        WinBuf<KPW> A, B, C;
         issue(0, A);
         issue(1, B);
         issue(2, C);
         for (int64_t ww = 0; ww < nw; ww += 3) {
-            win_wait<63, RING>(A);
+            win_wait<2 * NL, false>(A);
             compute(ww, A);
             issue(ww + 3, A);
-            win_wait<63, RING>(B);
+            win_wait<2 * NL, false>(B);
             compute(ww + 1, B);
             issue(ww + 4, B);
-            win_wait<63, RING>(C);
+            win_wait<2 * NL, false>(C);
             compute(ww + 2, C);
             issue(ww + 5, C);
         }
@@ -3595,12 +3602,12 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     // (ring: a window's store sits between its successor's loads and the next
     // issue; vector memory completes in issue order, so one more may be pending)
     constexpr int WT = RING ? NL + 1 : NL;
-    WinBuf A, B;
+    WinBuf<KPW> A, B;
     issue(0, A);
     issue(1, B);
     if (RING) win_wait<NL, RING>(A);  // (no store yet between A and B)
     for (int64_t ww = 0; ww < nw; ww += 2) {  // two windows per trip: loads of window ww + 2 fly during ww + 1
-        win_wait<WT, RING>(A);               // A's loads are older than B's NL (and a store)
+        win_wait<WT, RING>(A);                // A's loads are older than B's NL (and a store)
         compute(ww, A);
         issue(ww + 2, A);
         win_wait<WT, RING>(B);
@@ -3610,14 +3617,14 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the prefetches past the block: nothing in range)
 }
 
-template <int WD, bool RING>
+template <int WD, bool RING, int KPW>
 __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart,
                                                            const int64_t *__restrict__ wstart,
-                                                           const int64_t *__restrict__ Lwoff, const int32_t *__restrict__ Lcol,
-                                                           const double *__restrict__ Lval, const double *__restrict__ Ltinv,
-                                                           const int64_t *__restrict__ Uwoff, const int32_t *__restrict__ Ucol,
-                                                           const double *__restrict__ Uval, const double *__restrict__ Utinv,
-                                                           const double *x, double *y, int tri) {
+                                                           const int64_t *__restrict__ Lwoff, const double *__restrict__ Lrec,
+                                                           const double *__restrict__ Ltinv,
+                                                           const int64_t *__restrict__ Uwoff, const double *__restrict__ Urec,
+                                                           const double *__restrict__ Utinv, const double *x, double *y,
+                                                           int tri) {
     // one dynamic LDS array: the partial sums (4 x 64), then the block solution
     extern __shared__ __attribute__((aligned(16))) double lds_win[];
     double *part = lds_win, *ys = lds_win + 256;
@@ -3644,13 +3651,13 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
         // from global memory after every wave's L stores completed (win_sweep ends
         // with vmcnt(0); the barrier orders them before U's first loads)
         // (tri: 1 L, 2 U -- y already holds L's solution, the ring then only U's rows -- 3 both)
-        if (tri & 1) win_sweep<false, WD, true>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q, x + b0, y + b0);
+        if (tri & 1) win_sweep<false, 2, true, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys, part, lane, q, x + b0, y + b0);
         __syncthreads();
-        if (tri & 2) win_sweep<true, WD, true>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q, y + b0, y + b0);
+        if (tri & 2) win_sweep<true, 2, true, KPW>(len, w0, Uwoff, Urec, Utinv, ys, part, lane, q, y + b0, y + b0);
         return;
     }
-    win_sweep<false, WD>(len, w0, Lwoff, Lcol, Lval, Ltinv, ys, part, lane, q);
-    win_sweep<true, WD>(len, w0, Uwoff, Ucol, Uval, Utinv, ys, part, lane, q);
+    win_sweep<false, WD, false, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys, part, lane, q);
+    win_sweep<true, WD, false, KPW>(len, w0, Uwoff, Urec, Utinv, ys, part, lane, q);
     __syncthreads();
     for (int64_t t = threadIdx.x; t < len; t += 256) y[b0 + t] = ys[t];
 }
@@ -3663,35 +3670,43 @@ static_assert(256 + WIN_RING + 64 <= 163840 / 8, "the ring exceeds LDS");
 int ilu_window_stream_pad() { return 0; }
 int ilu_window_max_entries() { return WIN_KP; }
 
-void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
-                              const int64_t *Lwoff, const int32_t *Lcol, const double *Lval, const double *Ltinv,
-                              const int64_t *Uwoff, const int32_t *Ucol, const double *Uval, const double *Utinv,
-                              const double *x, double *y, int64_t max_len, hipStream_t st, int depth, bool ring,
-                              int tri) {
+template <int KPW>
+static void window_launch(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
+                          const int64_t *Lwoff, const double *Lrec, const double *Ltinv, const int64_t *Uwoff,
+                          const double *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
+                          hipStream_t st, int depth, bool ring, int tri) {
     static bool configured = false;
     if (!configured) {
-        for (const void *k : {(const void *)k_ilu_blocks_window<2, false>, (const void *)k_ilu_blocks_window<3, false>,
-                              (const void *)k_ilu_blocks_window<2, true>, (const void *)k_ilu_blocks_window<3, true>})
+        for (const void *k : {(const void *)k_ilu_blocks_window<2, false, KPW>,
+                              (const void *)k_ilu_blocks_window<3, false, KPW>,
+                              (const void *)k_ilu_blocks_window<2, true, KPW>})
             (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)163840);
         configured = true;
     }
     if (ring) {  // (x may be y: a window's input rows are read before its solution is stored)
         const size_t bytes = (size_t)(256 + WIN_RING + 64) * 8;
-        if (depth == 3)
-            k_ilu_blocks_window<3, true><<<(unsigned)nblocks, 256, bytes, st>>>(
-                n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y, tri);
-        else
-            k_ilu_blocks_window<2, true><<<(unsigned)nblocks, 256, bytes, st>>>(
-                n, nblocks, bstart, wstart, Lwoff, Lcol, Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y, tri);
+        k_ilu_blocks_window<2, true, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
+            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, tri);
         return;
     }
     const size_t bytes = (size_t)(256 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
     if (depth == 3)
-        k_ilu_blocks_window<3, false><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol,
-                                                                             Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y, 3);
+        k_ilu_blocks_window<3, false, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
+            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3);
     else
-        k_ilu_blocks_window<2, false><<<(unsigned)nblocks, 256, bytes, st>>>(n, nblocks, bstart, wstart, Lwoff, Lcol,
-                                                                             Lval, Ltinv, Uwoff, Ucol, Uval, Utinv, x, y, 3);
+        k_ilu_blocks_window<2, false, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
+            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3);
+}
+void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
+                              const int64_t *Lwoff, const double *Lrec, const double *Ltinv, const int64_t *Uwoff,
+                              const double *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
+                              hipStream_t st, int depth, bool ring, int tri, int max_entries) {
+    if (max_entries <= 4 * WIN_NW)
+        window_launch<4>(n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st, depth,
+                         ring, tri);
+    else
+        window_launch<WIN_KPW>(n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st,
+                               depth, ring, tri);
 }
 
 // ======================================================= super-window sweep ==

@@ -1277,8 +1277,12 @@ static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, cons
         woff[w + 1] = woff[w] + K * 64;
     }
     // (the staging copies read a fixed number of entries past a window's start: padding at the end)
-    std::vector<int32_t> col(woff[nw] + ilu_window_stream_pad(), 0);
-    std::vector<double> val(woff[nw] + ilu_window_stream_pad(), 0.0), tinv((size_t)std::max<int64_t>(nw, 1) * 4096, 0.0);
+    std::vector<double> rec(2 * (woff[nw] + ilu_window_stream_pad()), 0.0), tinv((size_t)std::max<int64_t>(nw, 1) * 4096, 0.0);
+    auto put = [&](int64_t e, int32_t col, double v) {
+        rec[2 * e] = v;
+        const uint64_t bits = (uint64_t)(uint32_t)col;
+        std::memcpy(&rec[2 * e + 1], &bits, 8);
+    };
     amgh::parallel_rows(nw, amgh::setup_threads(), [&](int, int64_t w0, int64_t w1) {
         std::vector<double> T(64 * 64), X(64 * 64);
         for (int64_t w = w0; w < w1; ++w) {
@@ -1289,10 +1293,7 @@ static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, cons
                 const int lane = (int)(i - r0);
                 int64_t k0, k1;
                 off_range(i, w, k0, k1);
-                for (int64_t k = k0; k < k1; ++k) {
-                    col[woff[w] + (k - k0) * 64 + lane] = (int32_t)(ci[k] - base);
-                    val[woff[w] + (k - k0) * 64 + lane] = fv[k];
-                }
+                for (int64_t k = k0; k < k1; ++k) put(woff[w] + (k - k0) * 64 + lane, (int32_t)(ci[k] - base), fv[k]);
                 // the window's triangle, row-major T[i][j]
                 if (!upper) {
                     T[lane * 64 + lane] = 1.0;
@@ -1322,18 +1323,16 @@ static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, cons
                     }
                 }
             }
-            for (int64_t i = 0; i < 64; ++i)
-                for (int64_t k = 0; k < 64; ++k) tinv[(size_t)w * 4096 + k * 64 + i] = X[i * 64 + k];
+            for (int64_t i = 0; i < 64; ++i)  // column pairs: lane i loads X[i][k], X[i][k + 1] at once
+                for (int64_t k = 0; k < 64; ++k) tinv[(size_t)w * 4096 + (k >> 1) * 128 + i * 2 + (k & 1)] = X[i * 64 + k];
         }
     });
     W.nwin = nw;
     W.woff.alloc(nw + 1);
-    W.col.alloc(col.size());
-    W.val.alloc(val.size());
+    W.rec.alloc(rec.size());
     W.tinv.alloc(tinv.size());
     HIPCHK(hipMemcpyAsync(W.woff.p, woff.data(), sizeof(int64_t) * (nw + 1), hipMemcpyHostToDevice, c.st));
-    HIPCHK(hipMemcpyAsync(W.col.p, col.data(), sizeof(int32_t) * col.size(), hipMemcpyHostToDevice, c.st));
-    HIPCHK(hipMemcpyAsync(W.val.p, val.data(), sizeof(double) * val.size(), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(W.rec.p, rec.data(), sizeof(double) * rec.size(), hipMemcpyHostToDevice, c.st));
     HIPCHK(hipMemcpyAsync(W.tinv.p, tinv.data(), sizeof(double) * tinv.size(), hipMemcpyHostToDevice, c.st));
     c.sync();
 }
@@ -1783,6 +1782,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             mark("super-window tables");
         }
         auto build_windows = [&](const std::vector<int64_t> &bst) {
+            window_entries = c.window_kpw == 8 ? 32 : (int)window_max_entries(nblocks, bst, rp, ci, dg);
             std::vector<double> fv(F.nnz);
             if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
             c.sync();
@@ -1962,9 +1962,9 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
         }
     }
     if (c.ilu_view)
-        fprintf(stderr, "[pls ilu] type %s n %lld blocks %lld max_len %lld levels %lld/%lld sweep %s\n", type.c_str(),
+        fprintf(stderr, "[pls ilu] type %s n %lld blocks %lld max_len %lld levels %lld/%lld sweep %s%s\n", type.c_str(),
                 (long long)n, (long long)nblocks, (long long)max_len, (long long)nlev_L, (long long)nlev_U,
-                sweep_kind());
+                sweep_kind(), window ? (window_entries <= 16 ? " (4 records)" : " (8 records)") : "");
 }
 
 void PCILU::apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64_t b_hi, int rr_group, int tpb,
@@ -2011,15 +2011,15 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
         launch_ilu_blocks_lds(n, nblocks, Lf.goff.p, Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, zgoff.p,
                               Ls.gslice.p, Ls.sptr.p, Ls.col.p, Ls.val.p, Ls.lpr.p, x, y, c.st, nullptr, true, lds_tpb,
                               0, bstart_h.empty() ? nullptr : bstart.p, max_len, -1, -1, 2);
-        launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.col.p,
-                                 Lw.val.p, Lw.tinv.p, Uw.woff.p, Uw.col.p, Uw.val.p, Uw.tinv.p, y, y, max_len, c.st,
-                                 c.window_depth, true, 2);
+        launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.rec.p,
+                                 Lw.tinv.p, Uw.woff.p, Uw.rec.p, Uw.tinv.p, y, y, max_len, c.st,
+                                 c.window_depth, true, 2, window_entries);
         return;
     }
     if (use_lds && window) {
-        launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.col.p,
-                                 Lw.val.p, Lw.tinv.p, Uw.woff.p, Uw.col.p, Uw.val.p, Uw.tinv.p, x, y, max_len, c.st,
-                                 c.window_depth, window_ring);
+        launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.rec.p,
+                                 Lw.tinv.p, Uw.woff.p, Uw.rec.p, Uw.tinv.p, x, y, max_len, c.st,
+                                 c.window_depth, window_ring, 3, window_entries);
         return;
     }
     if (use_lds && chain) {
@@ -2404,6 +2404,7 @@ std::unique_ptr<Ctx> layout_ctx(const Ctx &c) {
     self->window_depth = c.window_depth;
     self->window_ring = c.window_ring;
     self->window_mixed = c.window_mixed;
+    self->window_kpw = c.window_kpw;
     self->amg_csr_below = c.amg_csr_below;
     return self;
 }

@@ -89,6 +89,7 @@ struct Ctx {
     int window_depth = 2;         // window sweep: windows of data in flight, 2 or 3 (pls.window_depth)
     int window_ring = -1;         // ... its ring variant for blocks longer than LDS (pls.window_ring: -1 where the
                                   // window sweep's level test holds, 0 off, 1 also forced on LDS-resident blocks)
+    int window_kpw = 0;           // window sweep: stream records per wave (pls.window_kpw: 0 by the rows, 8 forced)
     int window_mixed = -1;        // ... its L triangle by levels (pls.window_mixed: -1 where L has no more levels
                                   // than windows, 0 off, 1 forced)
     int sweep_swin = 0;           // blocks too long for LDS: the super-window sweep (k_ilu_blocks_swin, experimental,
@@ -367,8 +368,10 @@ struct ChainTri {
 // Window-sweep tables of one triangle (kernels.hip, k_ilu_blocks_window)
 struct WinTri {
     DBuf<int64_t> woff;  // per window: off-window stream offsets (nwin + 1)
-    DBuf<int32_t> col;
-    DBuf<double> val, tinv;  // tinv: per window the 64 x 64 inverse of its diagonal block, [k][lane]
+    // rec: per stream entry (value, block-local column in the low word of the
+    // second double) -- one 16-byte load each; tinv: per window the 64 x 64
+    // inverse of its diagonal block, column pairs [k / 2][lane][k % 2]
+    DBuf<double> rec, tinv;
     int64_t nwin = 0;
 };
 // Super-window sweep tables of one triangle (kernels.hip, k_ilu_blocks_swin):
@@ -392,6 +395,7 @@ struct PCILU : PC {
     // explicit inverses of the windows' triangles (one GEMV per window)
     bool window = false;
     bool window_ring = false;  // (the ring variant: y-resident, an LDS ring of the recent rows)
+    int window_entries = 32;   // (the rows' most off-window entries: <= 16 loads 4 stream records per wave)
     bool window_mixed = false; // (ring variant: L by the y-resident level sweep, U by windows)
     DBuf<int64_t> zgoff;       // (no levels: the mixed sweep's empty U for the level launch)
     WinTri Lw, Uw;

@@ -118,6 +118,22 @@ def test_window_ring_matches_window_sweep(gpu, capfd, depth):
     assert np.array_equal(yr, yw)
 
 
+@pytest.mark.parametrize("ring", ["0", "1"])
+def test_window_records_per_wave(gpu, capfd, ring):
+    """The window sweep loads 4 stream records per wave and window where no row
+    has more than 16 off-window entries (these 5-point blocks: 1), else 8
+    (pls.window_kpw 8 forces it): the same sums, bitwise."""
+    A, is_s, is_f, is_p = _system()
+    x = np.random.default_rng(3).standard_normal(A.shape[0])
+    capfd.readouterr()
+    base = {"pls.sweep_window": "1", "pls.window_ring": ring}
+    y4 = _apply(A, is_s, is_f, is_p, x, base)
+    assert any("n 19880 " in ln and "(4 records)" in ln for ln in _sweeps(capfd.readouterr().err))
+    y8 = _apply(A, is_s, is_f, is_p, x, dict(base, **{"pls.window_kpw": "8"}))
+    assert any("n 19880 " in ln and "(8 records)" in ln for ln in _sweeps(capfd.readouterr().err))
+    assert np.array_equal(y4, y8)
+
+
 @pytest.mark.parametrize("mixed", ["0", "1"])
 def test_window_ring_long_block(gpu, capfd, mixed):
     """A 36,000-row block (563 windows, beyond the 20,160-row LDS window): the
