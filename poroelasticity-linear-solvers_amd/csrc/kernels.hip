@@ -3467,7 +3467,10 @@ struct WinBuf {  // one wave's share of a window's data in registers
 // instructions -- not their bytes: out-of-range or exec-masked lanes cost the
 // same -- took ~1.1 of the ~1.9 us per window on the swelling N = 160 chunks.)
 // (KPW: stream records per wave and window -- 4 where no row has more than 16
-// off-window entries, else WIN_KPW)
+// off-window entries, else WIN_KPW.  Loading only the records inside each
+// window's stream -- a wave-uniform count, waited for through a switch of
+// vmcnt immediates -- was measured slower: 274 against 239 us per swelling
+// N = 80 level-0 sweep, 1,420 against 1,361 at N = 160)
 template <bool RING, int KPW>
 constexpr int win_loads() { return 8 + KPW + (RING ? 1 : 0); }
 __device__ __forceinline__ double win_ld64(__amdgpu_buffer_rsrc_t r, int off) {
