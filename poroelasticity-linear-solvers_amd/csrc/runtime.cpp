@@ -1818,7 +1818,9 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             const int64_t nw = window_count(bst) / 2, levL = (int64_t)gL.size() - 1;
             const int64_t cost_lev = lev, cost_win = 2 * nw, cost_mix = levL + nw;
             const bool mix = c.window_mixed == 1 || (c.window_mixed == -1 && cost_mix < cost_win);
-            if ((c.sweep_window == 1 || 5 * (mix ? cost_mix : cost_win) <= 4 * cost_lev) &&
+            // (pls.ilu_gmem 1 -- the y-resident workgroup sweep forced on blocks that fit
+            // LDS -- keeps that sweep unless the window sweep is forced too)
+            if ((c.sweep_window == 1 || (gmem_mode != 1 && 5 * (mix ? cost_mix : cost_win) <= 4 * cost_lev)) &&
                 window_max_entries(nblocks, bst, rp, ci, dg) <= ilu_window_max_entries()) {
                 build_windows(bst);
                 window = window_ring = true;
