@@ -3419,7 +3419,7 @@ static constexpr int WIN_KP = WIN_NW * WIN_KPW;  // stream entries per row (ever
 // a block's window stream offsets, 64 per vector register (lane l: window j * 64 + l),
 // picked with v_readlane: no scalar load (and its latency) per window
 // (WIN_OFFR registers hold 64 * WIN_OFFR offsets: every window of a block up to
-// ilu_window_max_rows() rows plus the end offset -- 316 for 20,160 rows)
+// ilu_window_max_rows() rows plus the end offset -- 312 for 19,904 rows)
 static constexpr int WIN_OFFR = 5;
 // the ring variant (blocks longer than LDS): 16 registers, 1,023 windows
 static constexpr int WIN_OFFR_RING = 16, WIN_RING = 16384;
@@ -3556,14 +3556,13 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         __syncthreads();
         const double rhs = RING ? B.rx : ys[act ? r : 0];
         const double t = act ? rhs - (((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane]) : 0.0;
-        const int tlo = __double2loint(t), thi = __double2hiint(t);
+        // t_k to every lane through the wave's own LDS slot (its own write: no
+        // barrier; same-address reads broadcast) -- 32 v_readlane before
+        double *tbq = part + 256 + q * 64;
+        tbq[lane] = t;
         double out = 0.0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int kk = 16 * q + k;
-            const double tk = __hiloint2double(__builtin_amdgcn_readlane(thi, kk), __builtin_amdgcn_readlane(tlo, kk));
-            out += __dmul_rn((k & 1) ? B.tv[k >> 1].y : B.tv[k >> 1].x, tk);
-        }
+        for (int k = 0; k < 16; ++k) out += __dmul_rn((k & 1) ? B.tv[k >> 1].y : B.tv[k >> 1].x, tbq[16 * q + k]);
         __syncthreads();  // every wave has read part[] (t) before it is overwritten
         part[q * 64 + lane] = out;
         __syncthreads();
@@ -3628,9 +3627,9 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
                                                            const int64_t *__restrict__ Uwoff, const double *__restrict__ Urec,
                                                            const double *__restrict__ Utinv, const double *x, double *y,
                                                            int tri) {
-    // one dynamic LDS array: the partial sums (4 x 64), then the block solution
+    // one dynamic LDS array: the partial sums (4 x 64), the waves' t (4 x 64), then the block solution
     extern __shared__ __attribute__((aligned(16))) double lds_win[];
-    double *part = lds_win, *ys = lds_win + 256;
+    double *part = lds_win, *ys = lds_win + 512;
     const int64_t blk = nblocks - 1 - (int64_t)blockIdx.x;
     int64_t b0, len;
     block_range(blk, n, nblocks, bstart, b0, len);
@@ -3665,11 +3664,11 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
     for (int64_t t = threadIdx.x; t < len; t += 256) y[b0 + t] = ys[t];
 }
 
-int ilu_window_max_rows() { return 163840 / 8 - 256 - 64; }  // LDS: partial sums, the block, a dummy slot per lane
-static_assert((163840 / 8 - 256 - 64 + 63) / 64 + 1 <= 64 * WIN_OFFR, "window offsets exceed WinOff's registers");
+int ilu_window_max_rows() { return 163840 / 8 - 512 - 64; }  // LDS: partial sums, t, the block, a dummy slot per lane
+static_assert((163840 / 8 - 512 - 64 + 63) / 64 + 1 <= 64 * WIN_OFFR, "window offsets exceed WinOff's registers");
 int ilu_window_ring_rows() { return WIN_RING; }
 int64_t ilu_window_ring_max_rows() { return (int64_t)(64 * WIN_OFFR_RING - 1) * 64; }
-static_assert(256 + WIN_RING + 64 <= 163840 / 8, "the ring exceeds LDS");
+static_assert(512 + WIN_RING + 64 <= 163840 / 8, "the ring exceeds LDS");
 int ilu_window_stream_pad() { return 0; }
 int ilu_window_max_entries() { return WIN_KP; }
 
@@ -3687,12 +3686,12 @@ static void window_launch(int64_t n, int64_t nblocks, const int64_t *bstart, con
         configured = true;
     }
     if (ring) {  // (x may be y: a window's input rows are read before its solution is stored)
-        const size_t bytes = (size_t)(256 + WIN_RING + 64) * 8;
+        const size_t bytes = (size_t)(512 + WIN_RING + 64) * 8;
         k_ilu_blocks_window<2, true, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
             n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, tri);
         return;
     }
-    const size_t bytes = (size_t)(256 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
+    const size_t bytes = (size_t)(512 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
     if (depth == 3)
         k_ilu_blocks_window<3, false, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
             n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3);

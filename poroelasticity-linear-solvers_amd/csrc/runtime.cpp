@@ -1806,7 +1806,7 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
                    window_max_reach(n, rp, ci) <= ilu_window_ring_rows() - 64;
         };
         // the window sweep's ring variant on blocks too long for LDS (the classical
-        // AMG's np=8 hybrid Gauss-Seidel chunks beyond 20,160 rows: swelling N=160,
+        // AMG's np=8 hybrid Gauss-Seidel chunks beyond 19,904 rows: swelling N=160,
         // footing N=80), optionally with the L triangle by levels (the y-resident
         // workgroup sweep; pls.window_mixed).  Cost model, a level ~ a window
         // (measured ~2.4 and ~1.9 us on those chunks): both triangles by levels (the

@@ -1,8 +1,8 @@
 """ILU(0) sweep kernels on blocks sized to their limits.
 
 The window sweep (k_ilu_blocks_window) keeps a block's per-window stream
-offsets in registers; blocks of up to ilu_window_max_rows() = 20,160 rows
-(315 windows) qualify.  Round 4 held only 192 offsets, so a block of more
+offsets in registers; blocks of up to ilu_window_max_rows() = 19,904 rows
+(311 windows) qualify.  Round 4 held only 192 offsets, so a block of more
 than 12,224 rows read wrong offsets.  Here a one-block ILU(0) on a 19,880-row
 s block (311 windows) and a 12,300-row fp block is forced onto the window
 sweep and compared against the workgroup sweep and the oracle
@@ -136,7 +136,7 @@ def test_window_records_per_wave(gpu, capfd, ring):
 
 @pytest.mark.parametrize("mixed", ["0", "1"])
 def test_window_ring_long_block(gpu, capfd, mixed):
-    """A 36,000-row block (563 windows, beyond the 20,160-row LDS window): the
+    """A 36,000-row block (563 windows, beyond the 19,904-row LDS window): the
     ring variant -- both triangles in windows, or (mixed) L by the y-resident
     level sweep and U in windows -- against the oracle and against the
     one-workgroup GMEM sweep that ran there before (1e-12: the window inverses
