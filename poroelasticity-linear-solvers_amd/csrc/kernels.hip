@@ -3426,15 +3426,12 @@ static constexpr int WIN_OFFR_RING = 16, WIN_RING = 16384;
 template <int R>
 struct WinOff {
     int64_t r[R];
-    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: R readlanes, scalar selects
+    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: R - 1 vector selects, one readlane
         const int j = (int)(w >> 6), l = (int)(w & 63);
-        int64_t v = readlane64(r[0], l);
+        int64_t v = r[0];
 #pragma unroll
-        for (int k = 1; k < R; ++k) {
-            const int64_t t = readlane64(r[k], l);
-            v = j == k ? t : v;
-        }
-        return v;
+        for (int k = 1; k < R; ++k) v = j == k ? r[k] : v;  // (j uniform: the register of window w)
+        return readlane64(v, l);
     }
 };
 
