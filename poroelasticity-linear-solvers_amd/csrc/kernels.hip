@@ -3448,21 +3448,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t win_rsrc(const void *base, int
 }
 
 typedef double win_d2 __attribute__((ext_vector_type(2)));
+typedef int win_i3 __attribute__((ext_vector_type(3)));  // a stream record: value (lo, hi), column
 template <int KPW>
 struct WinBuf {  // one wave's share of a window's data in registers
     win_d2 tv[8];     // T^-1 columns 16 q + 2 j, + 1 of the lane's row
-    win_d2 sr[KPW];   // stream records: value, column (low word of .y)
+    win_i3 sr[KPW];   // stream records: value (.x lo, .y hi), column (.z)
     double rx;            // (ring variant) the window's input rows, from global memory
 };
 
-// Range-checked 16-byte buffer loads issued through inline asm: the compiler
-// does not track them, so it cannot drain them at the loop header (its waits
-// for loop-carried loads were vmcnt(0)); the sweep counts them itself -- every
-// window issues WIN_LOADS of them -- and win_wait ties the registers to the
-// wait (no use or copy can move above it).  (Round 6: 8-byte loads, two per
-// stream entry, were 33 instructions per wave and window, and the load
-// instructions -- not their bytes: out-of-range or exec-masked lanes cost the
-// same -- took ~1.1 of the ~1.9 us per window on the swelling N = 160 chunks.)
+// Range-checked buffer loads (the inverse's column pairs 16 bytes, stream
+// records 12) issued through inline asm: the compiler does not track them, so
+// it cannot drain them at the loop header (its waits for loop-carried loads
+// were vmcnt(0)); the sweep counts them itself -- every window issues the same
+// number -- and win_wait ties the registers to the wait (no use or copy can
+// move above it).  (Round 6: 8-byte loads, two per stream entry, were 33
+// instructions per wave and window, and the loads -- whole wave-wide
+// transfers: out-of-range or exec-masked lanes cost the same -- took ~1.1 of
+// the ~1.9 us per window on the swelling N = 160 chunks.)
 // (KPW: stream records per wave and window -- 4 where no row has more than 16
 // off-window entries, else WIN_KPW.  Loading only the records inside each
 // window's stream -- a wave-uniform count, waited for through a switch of
@@ -3478,6 +3480,11 @@ __device__ __forceinline__ double win_ld64(__amdgpu_buffer_rsrc_t r, int off) {
 __device__ __forceinline__ win_d2 win_ld128(__amdgpu_buffer_rsrc_t r, int off) {
     win_d2 v;
     asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+    return v;
+}
+__device__ __forceinline__ win_i3 win_ld96(__amdgpu_buffer_rsrc_t r, int off) {
+    win_i3 v;
+    asm volatile("buffer_load_dwordx3 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
     return v;
 }
 __device__ __forceinline__ void win_st64(__amdgpu_buffer_rsrc_t r, int off, double v) {
@@ -3499,7 +3506,7 @@ __device__ __forceinline__ void win_wait(WinBuf<KPW> &B) {  // vmcnt(N), B's reg
 // data) and its solution goes to global memory (out) as well as to the ring
 template <bool UP, int WD, bool RING, int KPW>
 __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t *__restrict__ woff,
-                                          const double *__restrict__ rec, const double *__restrict__ tinv, double *ys,
+                                          const int32_t *__restrict__ rec, const double *__restrict__ tinv, double *ys,
                                           double *part, int lane, int q, const double *in = nullptr,
                                           double *out = nullptr) {
     constexpr int R = RING ? WIN_OFFR_RING : WIN_OFFR, NL = win_loads<RING, KPW>();
@@ -3528,9 +3535,9 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         const int64_t w = wi(ww < nw ? ww : 0);
         const int64_t s0 = wo.at(w), s1 = wo.at(w + 1);
         const auto rt = win_rsrc(tinv + (w0 + w) * 4096, ok * 32768);
-        const auto rs = win_rsrc(rec + 2 * s0, ok * (s1 - s0) * 16);
+        const auto rs = win_rsrc(rec + 3 * s0, ok * (s1 - s0) * 12);
 #pragma unroll
-        for (int u = 0; u < KPW; ++u) B.sr[u] = win_ld128(rs, sk(u) * 16);
+        for (int u = 0; u < KPW; ++u) B.sr[u] = win_ld96(rs, sk(u) * 12);
 #pragma unroll
         for (int j = 0; j < 8; ++j) B.tv[j] = win_ld128(rt, toff(16 * q + 2 * j));
         if (RING) B.rx = win_ld64(rin, (int)(ok * (w * 64 + lane) * 8 + (1 - ok) * 0x40000000));
@@ -3543,12 +3550,12 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         double d[KPW];
 #pragma unroll
         for (int u = 0; u < KPW; ++u) {
-            const int32_t c = __double2loint(B.sr[u].y);
+            const int32_t c = B.sr[u].z;
             d[u] = ys[RING ? (c & RM) : c];
         }
         double acc = 0.0;
 #pragma unroll
-        for (int u = 0; u < KPW; ++u) acc += __dmul_rn(B.sr[u].x, d[u]);
+        for (int u = 0; u < KPW; ++u) acc += __dmul_rn(__hiloint2double(B.sr[u].y, B.sr[u].x), d[u]);
         part[q * 64 + lane] = acc;
         __syncthreads();
         const double rhs = RING ? B.rx : ys[act ? r : 0];
@@ -3619,9 +3626,9 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
 template <int WD, bool RING, int KPW>
 __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart,
                                                            const int64_t *__restrict__ wstart,
-                                                           const int64_t *__restrict__ Lwoff, const double *__restrict__ Lrec,
+                                                           const int64_t *__restrict__ Lwoff, const int32_t *__restrict__ Lrec,
                                                            const double *__restrict__ Ltinv,
-                                                           const int64_t *__restrict__ Uwoff, const double *__restrict__ Urec,
+                                                           const int64_t *__restrict__ Uwoff, const int32_t *__restrict__ Urec,
                                                            const double *__restrict__ Utinv, const double *x, double *y,
                                                            int tri) {
     // one dynamic LDS array: the partial sums (4 x 64), the waves' t (4 x 64), then the block solution
@@ -3671,8 +3678,8 @@ int ilu_window_max_entries() { return WIN_KP; }
 
 template <int KPW>
 static void window_launch(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
-                          const int64_t *Lwoff, const double *Lrec, const double *Ltinv, const int64_t *Uwoff,
-                          const double *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
+                          const int64_t *Lwoff, const int32_t *Lrec, const double *Ltinv, const int64_t *Uwoff,
+                          const int32_t *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
                           hipStream_t st, int depth, bool ring, int tri) {
     static bool configured = false;
     if (!configured) {
@@ -3697,8 +3704,8 @@ static void window_launch(int64_t n, int64_t nblocks, const int64_t *bstart, con
             n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3);
 }
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
-                              const int64_t *Lwoff, const double *Lrec, const double *Ltinv, const int64_t *Uwoff,
-                              const double *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
+                              const int64_t *Lwoff, const int32_t *Lrec, const double *Ltinv, const int64_t *Uwoff,
+                              const int32_t *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
                               hipStream_t st, int depth, bool ring, int tri, int max_entries) {
     if (max_entries <= 4 * WIN_NW)
         window_launch<4>(n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st, depth,

@@ -250,8 +250,8 @@ void launch_ilu_blocks_chain(int64_t n, int64_t nblocks, const int64_t *bstart, 
 // The window sweep (kernels.hip, k_ilu_blocks_window): LDS-resident blocks in
 // windows of 64 rows; per block its first window wstart[b] (nblocks + 1); per
 // triangle and window the off-window stream [woff[w], woff[w + 1]) ([k][lane]
-// SELL of 16-byte records: value, block-local column in the low word of the
-// next double) and the window's inverse in column pairs,
+// SELL of 12-byte records: value, block-local column) and the window's
+// inverse in column pairs,
 // tinv[w * 4096 + (k / 2) * 128 + lane * 2 + k % 2].
 // The record streams carry ilu_window_stream_pad() entries of padding at
 // their end (the staging copies read a fixed count); blocks of at most
@@ -266,8 +266,8 @@ int ilu_window_max_entries();  // off-window entries per row the kernel handles
 int ilu_window_ring_rows();
 int64_t ilu_window_ring_max_rows();
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
-                              const int64_t *Lwoff, const double *Lrec, const double *Ltinv, const int64_t *Uwoff,
-                              const double *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
+                              const int64_t *Lwoff, const int32_t *Lrec, const double *Ltinv, const int64_t *Uwoff,
+                              const int32_t *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
                               hipStream_t st, int depth = 2, bool ring = false, int tri = 3,
                               int max_entries = 32);  // (the rows' most off-window entries, <= 32)
 // (depth: windows of data in flight, 2 or 3; pls.window_depth; the ring variant: 2;

@@ -1277,11 +1277,11 @@ static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, cons
         woff[w + 1] = woff[w] + K * 64;
     }
     // (the staging copies read a fixed number of entries past a window's start: padding at the end)
-    std::vector<double> rec(2 * (woff[nw] + ilu_window_stream_pad()), 0.0), tinv((size_t)std::max<int64_t>(nw, 1) * 4096, 0.0);
+    std::vector<int32_t> rec(3 * (woff[nw] + ilu_window_stream_pad()), 0);
+    std::vector<double> tinv((size_t)std::max<int64_t>(nw, 1) * 4096, 0.0);
     auto put = [&](int64_t e, int32_t col, double v) {
-        rec[2 * e] = v;
-        const uint64_t bits = (uint64_t)(uint32_t)col;
-        std::memcpy(&rec[2 * e + 1], &bits, 8);
+        std::memcpy(&rec[3 * e], &v, 8);
+        rec[3 * e + 2] = col;
     };
     amgh::parallel_rows(nw, amgh::setup_threads(), [&](int, int64_t w0, int64_t w1) {
         std::vector<double> T(64 * 64), X(64 * 64);
@@ -1332,7 +1332,7 @@ static void build_window_tri(int64_t nblk, const std::vector<int64_t> &bst, cons
     W.rec.alloc(rec.size());
     W.tinv.alloc(tinv.size());
     HIPCHK(hipMemcpyAsync(W.woff.p, woff.data(), sizeof(int64_t) * (nw + 1), hipMemcpyHostToDevice, c.st));
-    HIPCHK(hipMemcpyAsync(W.rec.p, rec.data(), sizeof(double) * rec.size(), hipMemcpyHostToDevice, c.st));
+    HIPCHK(hipMemcpyAsync(W.rec.p, rec.data(), sizeof(int32_t) * rec.size(), hipMemcpyHostToDevice, c.st));
     HIPCHK(hipMemcpyAsync(W.tinv.p, tinv.data(), sizeof(double) * tinv.size(), hipMemcpyHostToDevice, c.st));
     c.sync();
 }

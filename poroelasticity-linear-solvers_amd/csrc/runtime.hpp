@@ -368,10 +368,11 @@ struct ChainTri {
 // Window-sweep tables of one triangle (kernels.hip, k_ilu_blocks_window)
 struct WinTri {
     DBuf<int64_t> woff;  // per window: off-window stream offsets (nwin + 1)
-    // rec: per stream entry (value, block-local column in the low word of the
-    // second double) -- one 16-byte load each; tinv: per window the 64 x 64
-    // inverse of its diagonal block, column pairs [k / 2][lane][k % 2]
-    DBuf<double> rec, tinv;
+    // rec: per stream entry (value, block-local column) as 3 words -- one
+    // 12-byte load each; tinv: per window the 64 x 64 inverse of its diagonal
+    // block, column pairs [k / 2][lane][k % 2]
+    DBuf<int32_t> rec;
+    DBuf<double> tinv;
     int64_t nwin = 0;
 };
 // Super-window sweep tables of one triangle (kernels.hip, k_ilu_blocks_swin):
