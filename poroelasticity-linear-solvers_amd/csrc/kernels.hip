@@ -3421,17 +3421,23 @@ static constexpr int WIN_KP = WIN_NW * WIN_KPW;  // stream entries per row (ever
 // (WIN_OFFR registers hold 64 * WIN_OFFR offsets: every window of a block up to
 // ilu_window_max_rows() rows plus the end offset -- 312 for 19,904 rows)
 static constexpr int WIN_OFFR = 5;
-// the ring variant (blocks longer than LDS): 16 registers, 1,023 windows
+// the ring variant (blocks longer than LDS): offsets in LDS, up to 1,023 windows
 static constexpr int WIN_OFFR_RING = 16, WIN_RING = 16384;
 template <int R>
 struct WinOff {
     int64_t r[R];
-    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: R - 1 vector selects, one readlane
+    __device__ __forceinline__ int64_t at(int64_t w) const {  // branch-free: R readlanes, scalar selects
+        // (vector selects of the window's register and one readlane: the compiler
+        // turned r[] into a scratch array indexed per window, whose loads drain
+        // vmcnt -- the ring variant keeps its offsets in LDS instead)
         const int j = (int)(w >> 6), l = (int)(w & 63);
-        int64_t v = r[0];
+        int64_t v = readlane64(r[0], l);
 #pragma unroll
-        for (int k = 1; k < R; ++k) v = j == k ? r[k] : v;  // (j uniform: the register of window w)
-        return readlane64(v, l);
+        for (int k = 1; k < R; ++k) {
+            const int64_t t = readlane64(r[k], l);
+            v = j == k ? t : v;
+        }
+        return v;
     }
 };
 
@@ -3509,14 +3515,24 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
                                           const int32_t *__restrict__ rec, const double *__restrict__ tinv, double *ys,
                                           double *part, int lane, int q, const double *in = nullptr,
                                           double *out = nullptr) {
-    constexpr int R = RING ? WIN_OFFR_RING : WIN_OFFR, NL = win_loads<RING, KPW>();
+    constexpr int R = RING ? 1 : WIN_OFFR, NL = win_loads<RING, KPW>();  // (ring: offsets in LDS)
     constexpr int64_t RM = WIN_RING - 1;
     const int64_t nw = (len + 63) >> 6;
     if (nw == 0) return;
+    // the block's window stream offsets: registers (64 per register, picked by a
+    // vector select and one readlane), or -- ring variant -- LDS (part + 576,
+    // up to 1,024; a same-address read per window)
     WinOff<R> wo;
+    int64_t *lwo = reinterpret_cast<int64_t *>(part + 576);
+    if (RING) {
+        for (int64_t t = threadIdx.x; t <= nw; t += 256) lwo[t] = woff[w0 + t];
+        __syncthreads();
+    } else {
 #pragma unroll
-    for (int j = 0; j < R; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
+        for (int j = 0; j < R; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the offsets (ordinary loads) before the counted ones
+    auto at = [&](int64_t w) -> int64_t { return RING ? sgpr64(lwo[w]) : wo.at(w); };
     const auto rin = win_rsrc(in, RING ? len * 8 : 0), rout = win_rsrc(out, RING ? len * 8 : 0);
     // (pls.ring_probe, ring variant, timing only -- results wrong: 2048 no stores,
     // 32768 no loads after the first two windows)
@@ -3533,14 +3549,16 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         if ((probe & 32768) && ww >= 2) return;
         const int64_t ok = ww < nw ? 1 : 0;
         const int64_t w = wi(ww < nw ? ww : 0);
-        const int64_t s0 = wo.at(w), s1 = wo.at(w + 1);
+        const int64_t s0 = at(w), s1 = at(w + 1);
         const auto rt = win_rsrc(tinv + (w0 + w) * 4096, ok * 32768);
         const auto rs = win_rsrc(rec + 3 * s0, ok * (s1 - s0) * 12);
 #pragma unroll
         for (int u = 0; u < KPW; ++u) B.sr[u] = win_ld96(rs, sk(u) * 12);
 #pragma unroll
         for (int j = 0; j < 8; ++j) B.tv[j] = win_ld128(rt, toff(16 * q + 2 * j));
-        if (RING) B.rx = win_ld64(rin, (int)(ok * (w * 64 + lane) * 8 + (1 - ok) * 0x40000000));
+        // (ring: wave 0 alone loads the input rows and stores the solution -- the
+        // load instructions, not their lanes, are what a window costs)
+        if (RING && q == 0) B.rx = win_ld64(rin, (int)(ok * (w * 64 + lane) * 8 + (1 - ok) * 0x40000000));
     };
     // one window, branch-free (a window past the block computes zeros into a dummy slot)
     auto compute = [&](int64_t ww, const WinBuf<KPW> &B) {
@@ -3557,8 +3575,10 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
 #pragma unroll
         for (int u = 0; u < KPW; ++u) acc += __dmul_rn(__hiloint2double(B.sr[u].y, B.sr[u].x), d[u]);
         part[q * 64 + lane] = acc;
+        double *rxs = part + 512;  // (ring: wave 0's input rows for every wave)
+        if (RING && q == 0) rxs[lane] = B.rx;
         __syncthreads();
-        const double rhs = RING ? B.rx : ys[act ? r : 0];
+        const double rhs = RING ? rxs[lane] : ys[act ? r : 0];
         const double t = act ? rhs - (((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane]) : 0.0;
         // t_k to every lane through the wave's own LDS slot (its own write: no
         // barrier; same-address reads broadcast) -- 32 v_readlane before
@@ -3575,7 +3595,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
             // every wave stores the window (the same values): one counted store per
             // wave and window, issued after the window's loads
             ys[act ? (r & RM) : WIN_RING + lane] = yr;
-            if (!(probe & 2048)) win_st64(rout, act ? (int)(r * 8) : 0x40000000, yr);
+            if (q == 0 && !(probe & 2048)) win_st64(rout, act ? (int)(r * 8) : 0x40000000, yr);
         } else {
             ys[act ? r : len + lane] = yr;  // every wave writes the same value (its own later reads see it)
         }
@@ -3607,19 +3627,28 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     }
     // (ring: a window's store sits between its successor's loads and the next
     // issue; vector memory completes in issue order, so one more may be pending)
-    constexpr int WT = RING ? NL + 1 : NL;
-    WinBuf<KPW> A, B;
-    issue(0, A);
-    issue(1, B);
-    if (RING) win_wait<NL, RING>(A);  // (no store yet between A and B)
-    for (int64_t ww = 0; ww < nw; ww += 2) {  // two windows per trip: loads of window ww + 2 fly during ww + 1
-        win_wait<WT, RING>(A);                // A's loads are older than B's NL (and a store)
-        compute(ww, A);
-        issue(ww + 2, A);
-        win_wait<WT, RING>(B);
-        compute(ww + 1, B);
-        issue(ww + 3, B);
-    }
+    // (ring: only wave 0 has the input load and the store; the other waves
+    // count NL - 1 loads per window and no store)
+    auto run = [&](auto w0) {
+        constexpr bool S = RING && decltype(w0)::value;
+        constexpr int NLq = RING && !S ? NL - 1 : NL, WT = S ? NL + 1 : NLq;
+        WinBuf<KPW> A, B;
+        issue(0, A);
+        issue(1, B);
+        if (S) win_wait<NLq, RING>(A);  // (no store yet between A and B)
+        for (int64_t ww = 0; ww < nw; ww += 2) {  // two windows per trip: loads of window ww + 2 fly during ww + 1
+            win_wait<WT, RING>(A);                // A's loads are older than B's (and a store)
+            compute(ww, A);
+            issue(ww + 2, A);
+            win_wait<WT, RING>(B);
+            compute(ww + 1, B);
+            issue(ww + 3, B);
+        }
+    };
+    if (RING && q == 0)
+        run(std::integral_constant<bool, true>{});
+    else
+        run(std::integral_constant<bool, false>{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the prefetches past the block: nothing in range)
 }
 
@@ -3640,7 +3669,7 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
     const int lane = threadIdx.x & 63;
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (v_readlane's lane is a scalar)
     if (RING)  // (padding entries read slot 0 with value 0: every slot finite)
-        for (int64_t t = threadIdx.x; t < WIN_RING; t += 256) ys[t] = 0.0;
+        for (int64_t t = threadIdx.x; t < WIN_RING; t += 256) ys[1088 + t] = 0.0;  // (the ring: after rows, offsets)
     else
         for (int64_t t = threadIdx.x; t < len; t += 256) ys[t] = x[b0 + t];
     __syncthreads();
@@ -3657,9 +3686,11 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
         // from global memory after every wave's L stores completed (win_sweep ends
         // with vmcnt(0); the barrier orders them before U's first loads)
         // (tri: 1 L, 2 U -- y already holds L's solution, the ring then only U's rows -- 3 both)
-        if (tri & 1) win_sweep<false, 2, true, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys, part, lane, q, x + b0, y + b0);
+        // (ring layout: partial sums, t, wave 0's input rows (64), the window
+        // offsets (1,024), then the ring)
+        if (tri & 1) win_sweep<false, 2, true, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys + 1088, part, lane, q, x + b0, y + b0);
         __syncthreads();
-        if (tri & 2) win_sweep<true, 2, true, KPW>(len, w0, Uwoff, Urec, Utinv, ys, part, lane, q, y + b0, y + b0);
+        if (tri & 2) win_sweep<true, 2, true, KPW>(len, w0, Uwoff, Urec, Utinv, ys + 1088, part, lane, q, y + b0, y + b0);
         return;
     }
     win_sweep<false, WD, false, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys, part, lane, q);
@@ -3672,7 +3703,8 @@ int ilu_window_max_rows() { return 163840 / 8 - 512 - 64; }  // LDS: partial sum
 static_assert((163840 / 8 - 512 - 64 + 63) / 64 + 1 <= 64 * WIN_OFFR, "window offsets exceed WinOff's registers");
 int ilu_window_ring_rows() { return WIN_RING; }
 int64_t ilu_window_ring_max_rows() { return (int64_t)(64 * WIN_OFFR_RING - 1) * 64; }
-static_assert(512 + WIN_RING + 64 <= 163840 / 8, "the ring exceeds LDS");
+static_assert(1600 + WIN_RING + 64 <= 163840 / 8, "the ring exceeds LDS");
+static_assert(64 * WIN_OFFR_RING <= 1024, "the ring variant's window offsets exceed their LDS slots");
 int ilu_window_stream_pad() { return 0; }
 int ilu_window_max_entries() { return WIN_KP; }
 
@@ -3690,7 +3722,7 @@ static void window_launch(int64_t n, int64_t nblocks, const int64_t *bstart, con
         configured = true;
     }
     if (ring) {  // (x may be y: a window's input rows are read before its solution is stored)
-        const size_t bytes = (size_t)(512 + WIN_RING + 64) * 8;
+        const size_t bytes = (size_t)(1600 + WIN_RING + 64) * 8;
         k_ilu_blocks_window<2, true, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
             n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, tri);
         return;
