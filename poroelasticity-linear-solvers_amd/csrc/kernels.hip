@@ -3514,7 +3514,7 @@ template <bool UP, int WD, bool RING, int KPW>
 __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t *__restrict__ woff,
                                           const int32_t *__restrict__ rec, const double *__restrict__ tinv, double *ys,
                                           double *part, int lane, int q, const double *in = nullptr,
-                                          double *out = nullptr) {
+                                          double *out = nullptr, int64_t *lwo_lds = nullptr) {
     constexpr int R = RING ? 1 : WIN_OFFR, NL = win_loads<RING, KPW>();  // (ring: offsets in LDS)
     constexpr int64_t RM = WIN_RING - 1;
     const int64_t nw = (len + 63) >> 6;
@@ -3522,9 +3522,11 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     // the block's window stream offsets: registers (64 per register, picked by a
     // vector select and one readlane), or -- ring variant -- LDS (part + 576,
     // up to 1,024; a same-address read per window)
+    // (the LDS variant too where they fit after the block: lwo_lds)
     WinOff<R> wo;
-    int64_t *lwo = reinterpret_cast<int64_t *>(part + 576);
-    if (RING) {
+    int64_t *lwo = RING ? reinterpret_cast<int64_t *>(part + 576) : lwo_lds;
+    const bool in_lds = RING || lwo_lds != nullptr;  // (uniform)
+    if (in_lds) {
         for (int64_t t = threadIdx.x; t <= nw; t += 256) lwo[t] = woff[w0 + t];
         __syncthreads();
     } else {
@@ -3532,7 +3534,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
         for (int j = 0; j < R; ++j) wo.r[j] = j * 64 + lane <= nw ? woff[w0 + j * 64 + lane] : 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the offsets (ordinary loads) before the counted ones
-    auto at = [&](int64_t w) -> int64_t { return RING ? sgpr64(lwo[w]) : wo.at(w); };
+    auto at = [&](int64_t w) -> int64_t { return in_lds ? sgpr64(lwo[w]) : wo.at(w); };
     const auto rin = win_rsrc(in, RING ? len * 8 : 0), rout = win_rsrc(out, RING ? len * 8 : 0);
     // (pls.ring_probe, ring variant, timing only -- results wrong: 2048 no stores,
     // 32768 no loads after the first two windows)
@@ -3659,7 +3661,7 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
                                                            const double *__restrict__ Ltinv,
                                                            const int64_t *__restrict__ Uwoff, const int32_t *__restrict__ Urec,
                                                            const double *__restrict__ Utinv, const double *x, double *y,
-                                                           int tri) {
+                                                           int tri, int lwo_ok) {
     // one dynamic LDS array: the partial sums (4 x 64), the waves' t (4 x 64), then the block solution
     extern __shared__ __attribute__((aligned(16))) double lds_win[];
     double *part = lds_win, *ys = lds_win + 512;
@@ -3693,8 +3695,11 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
         if (tri & 2) win_sweep<true, 2, true, KPW>(len, w0, Uwoff, Urec, Utinv, ys + 1088, part, lane, q, y + b0, y + b0);
         return;
     }
-    win_sweep<false, WD, false, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys, part, lane, q);
-    win_sweep<true, WD, false, KPW>(len, w0, Uwoff, Urec, Utinv, ys, part, lane, q);
+    // (the window offsets after the block and its dummy slots, where the launch sized LDS for them)
+    int64_t *lwo = lwo_ok ? reinterpret_cast<int64_t *>(ys + len + 64) : nullptr;
+    win_sweep<false, WD, false, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys, part, lane, q, nullptr, nullptr, lwo);
+    __syncthreads();  // (L's last offset reads before U's fill)
+    win_sweep<true, WD, false, KPW>(len, w0, Uwoff, Urec, Utinv, ys, part, lane, q, nullptr, nullptr, lwo);
     __syncthreads();
     for (int64_t t = threadIdx.x; t < len; t += 256) y[b0 + t] = ys[t];
 }
@@ -3724,16 +3729,19 @@ static void window_launch(int64_t n, int64_t nblocks, const int64_t *bstart, con
     if (ring) {  // (x may be y: a window's input rows are read before its solution is stored)
         const size_t bytes = (size_t)(1600 + WIN_RING + 64) * 8;
         k_ilu_blocks_window<2, true, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
-            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, tri);
+            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, tri, 0);
         return;
     }
-    const size_t bytes = (size_t)(512 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
+    size_t bytes = (size_t)(512 + std::max<int64_t>(max_len, 1) + 64) * 8;  // + a dummy slot per lane
+    const size_t obytes = (size_t)((std::max<int64_t>(max_len, 1) + 63) / 64 + 1) * 8;  // the window offsets
+    const int lwo_ok = bytes + obytes <= 163840 ? 1 : 0;
+    if (lwo_ok) bytes += obytes;
     if (depth == 3)
         k_ilu_blocks_window<3, false, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
-            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3);
+            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3, lwo_ok);
     else
         k_ilu_blocks_window<2, false, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
-            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3);
+            n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3, lwo_ok);
 }
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lrec, const double *Ltinv, const int64_t *Uwoff,
