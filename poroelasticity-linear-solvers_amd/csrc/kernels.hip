@@ -3654,7 +3654,7 @@ __device__ __forceinline__ void win_sweep(int64_t len, int64_t w0, const int64_t
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the prefetches past the block: nothing in range)
 }
 
-template <int WD, bool RING, int KPW>
+template <int WD, bool RING, int KL, int KU>
 __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *__restrict__ bstart,
                                                            const int64_t *__restrict__ wstart,
                                                            const int64_t *__restrict__ Lwoff, const int32_t *__restrict__ Lrec,
@@ -3690,16 +3690,16 @@ __global__ __launch_bounds__(256) void k_ilu_blocks_window(int64_t n, int64_t nb
         // (tri: 1 L, 2 U -- y already holds L's solution, the ring then only U's rows -- 3 both)
         // (ring layout: partial sums, t, wave 0's input rows (64), the window
         // offsets (1,024), then the ring)
-        if (tri & 1) win_sweep<false, 2, true, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys + 1088, part, lane, q, x + b0, y + b0);
+        if (tri & 1) win_sweep<false, 2, true, KL>(len, w0, Lwoff, Lrec, Ltinv, ys + 1088, part, lane, q, x + b0, y + b0);
         __syncthreads();
-        if (tri & 2) win_sweep<true, 2, true, KPW>(len, w0, Uwoff, Urec, Utinv, ys + 1088, part, lane, q, y + b0, y + b0);
+        if (tri & 2) win_sweep<true, 2, true, KU>(len, w0, Uwoff, Urec, Utinv, ys + 1088, part, lane, q, y + b0, y + b0);
         return;
     }
     // (the window offsets after the block and its dummy slots, where the launch sized LDS for them)
     int64_t *lwo = lwo_ok ? reinterpret_cast<int64_t *>(ys + len + 64) : nullptr;
-    win_sweep<false, WD, false, KPW>(len, w0, Lwoff, Lrec, Ltinv, ys, part, lane, q, nullptr, nullptr, lwo);
+    win_sweep<false, WD, false, KL>(len, w0, Lwoff, Lrec, Ltinv, ys, part, lane, q, nullptr, nullptr, lwo);
     __syncthreads();  // (L's last offset reads before U's fill)
-    win_sweep<true, WD, false, KPW>(len, w0, Uwoff, Urec, Utinv, ys, part, lane, q, nullptr, nullptr, lwo);
+    win_sweep<true, WD, false, KU>(len, w0, Uwoff, Urec, Utinv, ys, part, lane, q, nullptr, nullptr, lwo);
     __syncthreads();
     for (int64_t t = threadIdx.x; t < len; t += 256) y[b0 + t] = ys[t];
 }
@@ -3713,22 +3713,22 @@ static_assert(64 * WIN_OFFR_RING <= 1024, "the ring variant's window offsets exc
 int ilu_window_stream_pad() { return 0; }
 int ilu_window_max_entries() { return WIN_KP; }
 
-template <int KPW>
+template <int KL, int KU>
 static void window_launch(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                           const int64_t *Lwoff, const int32_t *Lrec, const double *Ltinv, const int64_t *Uwoff,
                           const int32_t *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
                           hipStream_t st, int depth, bool ring, int tri) {
     static bool configured = false;
     if (!configured) {
-        for (const void *k : {(const void *)k_ilu_blocks_window<2, false, KPW>,
-                              (const void *)k_ilu_blocks_window<3, false, KPW>,
-                              (const void *)k_ilu_blocks_window<2, true, KPW>})
+        for (const void *k : {(const void *)k_ilu_blocks_window<2, false, KL, KU>,
+                              (const void *)k_ilu_blocks_window<3, false, KL, KU>,
+                              (const void *)k_ilu_blocks_window<2, true, KL, KU>})
             (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)163840);
         configured = true;
     }
     if (ring) {  // (x may be y: a window's input rows are read before its solution is stored)
         const size_t bytes = (size_t)(1600 + WIN_RING + 64) * 8;
-        k_ilu_blocks_window<2, true, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
+        k_ilu_blocks_window<2, true, KL, KU><<<(unsigned)nblocks, 256, bytes, st>>>(
             n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, tri, 0);
         return;
     }
@@ -3737,22 +3737,44 @@ static void window_launch(int64_t n, int64_t nblocks, const int64_t *bstart, con
     const int lwo_ok = bytes + obytes <= 163840 ? 1 : 0;
     if (lwo_ok) bytes += obytes;
     if (depth == 3)
-        k_ilu_blocks_window<3, false, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
+        k_ilu_blocks_window<3, false, KL, KU><<<(unsigned)nblocks, 256, bytes, st>>>(
             n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3, lwo_ok);
     else
-        k_ilu_blocks_window<2, false, KPW><<<(unsigned)nblocks, 256, bytes, st>>>(
+        k_ilu_blocks_window<2, false, KL, KU><<<(unsigned)nblocks, 256, bytes, st>>>(
             n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, 3, lwo_ok);
+}
+int window_records(int max_entries) {  // stream records per wave and window: 4, 6 or 8
+    return max_entries <= 4 * WIN_NW ? 4 : max_entries <= 6 * WIN_NW ? 6 : WIN_KPW;
+}
+template <int KL>
+static void window_launch_u(int ku, int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
+                            const int64_t *Lwoff, const int32_t *Lrec, const double *Ltinv, const int64_t *Uwoff,
+                            const int32_t *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
+                            hipStream_t st, int depth, bool ring, int tri) {
+    if (ku == 4)
+        window_launch<KL, 4>(n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st,
+                             depth, ring, tri);
+    else if (ku == 6)
+        window_launch<KL, 6>(n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st,
+                             depth, ring, tri);
+    else
+        window_launch<KL, WIN_KPW>(n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len,
+                                   st, depth, ring, tri);
 }
 void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart, const int64_t *wstart,
                               const int64_t *Lwoff, const int32_t *Lrec, const double *Ltinv, const int64_t *Uwoff,
                               const int32_t *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
-                              hipStream_t st, int depth, bool ring, int tri, int max_entries) {
-    if (max_entries <= 4 * WIN_NW)
-        window_launch<4>(n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st, depth,
-                         ring, tri);
+                              hipStream_t st, int depth, bool ring, int tri, int max_entries_L, int max_entries_U) {
+    const int kl = window_records(max_entries_L), ku = window_records(max_entries_U);
+    if (kl == 4)
+        window_launch_u<4>(ku, n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st,
+                           depth, ring, tri);
+    else if (kl == 6)
+        window_launch_u<6>(ku, n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st,
+                           depth, ring, tri);
     else
-        window_launch<WIN_KPW>(n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len, st,
-                               depth, ring, tri);
+        window_launch_u<WIN_KPW>(ku, n, nblocks, bstart, wstart, Lwoff, Lrec, Ltinv, Uwoff, Urec, Utinv, x, y, max_len,
+                                 st, depth, ring, tri);
 }
 
 // ======================================================= super-window sweep ==

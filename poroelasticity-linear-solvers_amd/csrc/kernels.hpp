@@ -269,7 +269,8 @@ void launch_ilu_blocks_window(int64_t n, int64_t nblocks, const int64_t *bstart,
                               const int64_t *Lwoff, const int32_t *Lrec, const double *Ltinv, const int64_t *Uwoff,
                               const int32_t *Urec, const double *Utinv, const double *x, double *y, int64_t max_len,
                               hipStream_t st, int depth = 2, bool ring = false, int tri = 3,
-                              int max_entries = 32);  // (the rows' most off-window entries, <= 32)
+                              int max_entries_L = 32, int max_entries_U = 32);  // (rows' most off-window entries)
+int window_records(int max_entries);  // stream records per wave and window (4, 6, 8) for that many entries
 // (depth: windows of data in flight, 2 or 3; pls.window_depth; the ring variant: 2;
 // tri (ring variant): 1 the L sweep, 2 the U sweep on y (holding L's solution), 3 both)
 // The ring sweep (kernels.hip, k_ilu_blocks_ring): blocks of narrow levels whose

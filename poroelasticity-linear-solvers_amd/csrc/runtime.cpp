@@ -1219,9 +1219,9 @@ static void ring_tables(int64_t n, int64_t nb, const std::vector<int32_t> &order
 // unit lower (I + L_ww) or upper with the diagonal (U_ww) -- by row-wise
 // substitution in double precision without contraction, stored [k][lane].
 // Largest number of off-window entries of a row (the kernel's limit: ilu_window_max_entries())
-static int64_t window_max_entries(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
-                                  const std::vector<int32_t> &ci, const std::vector<int64_t> &dg) {
-    int64_t kmax = 0;
+static void window_max_entries_lu(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
+                                  const std::vector<int32_t> &ci, const std::vector<int64_t> &dg, int &eL, int &eU) {
+    int64_t kml = 0, kmu = 0;
     for (int64_t b = 0; b < nblk; ++b)
         for (int64_t i = bst[b]; i < bst[b + 1]; ++i) {
             const int64_t w0 = bst[b] + (i - bst[b]) / 64 * 64, w1 = std::min<int64_t>(w0 + 64, bst[b + 1]);
@@ -1230,9 +1230,17 @@ static int64_t window_max_entries(int64_t nblk, const std::vector<int64_t> &bst,
                 kl += ci[k] < w0;
                 ku += ci[k] >= w1;
             }
-            kmax = std::max(kmax, std::max(kl, ku));
+            kml = std::max(kml, kl);
+            kmu = std::max(kmu, ku);
         }
-    return kmax;
+    eL = (int)kml;
+    eU = (int)kmu;
+}
+static int64_t window_max_entries(int64_t nblk, const std::vector<int64_t> &bst, const std::vector<int64_t> &rp,
+                                  const std::vector<int32_t> &ci, const std::vector<int64_t> &dg) {
+    int eL = 0, eU = 0;
+    window_max_entries_lu(nblk, bst, rp, ci, dg, eL, eU);
+    return std::max(eL, eU);
 }
 // Farthest dependency of a row in rows (|i - c| over the off-diagonal entries;
 // the ring variant's limit: ilu_window_ring_rows() - 64)
@@ -1782,7 +1790,9 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
             mark("super-window tables");
         }
         auto build_windows = [&](const std::vector<int64_t> &bst) {
-            window_entries = c.window_kpw == 8 ? 32 : (int)window_max_entries(nblocks, bst, rp, ci, dg);
+            window_max_entries_lu(nblocks, bst, rp, ci, dg, window_entries_L, window_entries_U);
+            if (c.window_kpw == 8) window_entries_L = window_entries_U = 32;
+            window_entries = std::max(window_entries_L, window_entries_U);
             std::vector<double> fv(F.nnz);
             if (F.nnz) HIPCHK(hipMemcpyAsync(fv.data(), F.val.p, sizeof(double) * F.nnz, hipMemcpyDeviceToHost, c.st));
             c.sync();
@@ -1966,7 +1976,10 @@ PCILU::PCILU(const DevCSR &M, int64_t nb, Ctx &c, bool exact_lu, bool lds, int f
     if (c.ilu_view)
         fprintf(stderr, "[pls ilu] type %s n %lld blocks %lld max_len %lld levels %lld/%lld sweep %s%s\n", type.c_str(),
                 (long long)n, (long long)nblocks, (long long)max_len, (long long)nlev_L, (long long)nlev_U,
-                sweep_kind(), window ? (window_entries <= 16 ? " (4 records)" : " (8 records)") : "");
+                sweep_kind(),
+                window ? (" (records " + std::to_string(window_records(window_entries_L)) + "/" +
+                          std::to_string(window_records(window_entries_U)) + ")").c_str()
+                       : "");
 }
 
 void PCILU::apply_blocks(const double *x, double *y, Ctx &c, int64_t b_lo, int64_t b_hi, int rr_group, int tpb,
@@ -2015,13 +2028,13 @@ void PCILU::apply(const double *x, double *y, Ctx &c) {
                               0, bstart_h.empty() ? nullptr : bstart.p, max_len, -1, -1, 2);
         launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.rec.p,
                                  Lw.tinv.p, Uw.woff.p, Uw.rec.p, Uw.tinv.p, y, y, max_len, c.st,
-                                 c.window_depth, true, 2, window_entries);
+                                 c.window_depth, true, 2, window_entries_L, window_entries_U);
         return;
     }
     if (use_lds && window) {
         launch_ilu_blocks_window(n, nblocks, bstart_h.empty() ? nullptr : bstart.p, wstart.p, Lw.woff.p, Lw.rec.p,
                                  Lw.tinv.p, Uw.woff.p, Uw.rec.p, Uw.tinv.p, x, y, max_len, c.st,
-                                 c.window_depth, window_ring, 3, window_entries);
+                                 c.window_depth, window_ring, 3, window_entries_L, window_entries_U);
         return;
     }
     if (use_lds && chain) {

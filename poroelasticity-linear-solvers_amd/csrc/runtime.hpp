@@ -397,6 +397,7 @@ struct PCILU : PC {
     bool window = false;
     bool window_ring = false;  // (the ring variant: y-resident, an LDS ring of the recent rows)
     int window_entries = 32;   // (the rows' most off-window entries: <= 16 loads 4 stream records per wave)
+    int window_entries_L = 32, window_entries_U = 32;  // (per triangle: 4, 6 or 8 records per wave)
     bool window_mixed = false; // (ring variant: L by the y-resident level sweep, U by windows)
     DBuf<int64_t> zgoff;       // (no levels: the mixed sweep's empty U for the level launch)
     WinTri Lw, Uw;

@@ -121,16 +121,16 @@ def test_window_ring_matches_window_sweep(gpu, capfd, depth):
 @pytest.mark.parametrize("ring", ["0", "1"])
 def test_window_records_per_wave(gpu, capfd, ring):
     """The window sweep loads 4 stream records per wave and window where no row
-    has more than 16 off-window entries (these 5-point blocks: 1), else 8
-    (pls.window_kpw 8 forces it): the same sums, bitwise."""
+    of the triangle has more than 16 off-window entries (these 5-point blocks:
+    1), 6 up to 24, else 8 (pls.window_kpw 8 forces 8): the same sums, bitwise."""
     A, is_s, is_f, is_p = _system()
     x = np.random.default_rng(3).standard_normal(A.shape[0])
     capfd.readouterr()
     base = {"pls.sweep_window": "1", "pls.window_ring": ring}
     y4 = _apply(A, is_s, is_f, is_p, x, base)
-    assert any("n 19880 " in ln and "(4 records)" in ln for ln in _sweeps(capfd.readouterr().err))
+    assert any("n 19880 " in ln and "(records 4/4)" in ln for ln in _sweeps(capfd.readouterr().err))
     y8 = _apply(A, is_s, is_f, is_p, x, dict(base, **{"pls.window_kpw": "8"}))
-    assert any("n 19880 " in ln and "(8 records)" in ln for ln in _sweeps(capfd.readouterr().err))
+    assert any("n 19880 " in ln and "(records 8/8)" in ln for ln in _sweeps(capfd.readouterr().err))
     assert np.array_equal(y4, y8)
 
 
